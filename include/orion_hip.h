@@ -1,0 +1,192 @@
+/*
+ * orion_hip.h -- C-ABI of liborion_hip.so, the MI355X (gfx950) RNS-CKKS
+ * backend for Orion.
+ *
+ * Part 1 is the drop-in boundary: exactly the symbol set Orion's Python layer
+ * binds for its Lattigo backend (/root/reference/orion/backend/lattigo/
+ * bindings.py:141-746, cgo exports in orion/backend/lattigo/<file>.go), with the
+ * same argument meaning and int-handle semantics (lowest-free-id reuse,
+ * minheap.go:46-64; *New ops allocate, in-place ops return their input id).
+ * Each entry cites the Go export it replaces.  Plus the two symbols the fork's
+ * Python layer calls that only its HEonGPU binding defines
+ * (GenerateConsolidatedRotationKeys, lt_evaluator.py:77; CloneCiphertext,
+ * tensors.py:229).
+ *
+ * Error behaviour: Lattigo panics (aborts the process).  This library never
+ * aborts: handle-returning calls return -1, void calls record the error, and
+ * OrionHipLastError() returns the message (the Python binding raises
+ * RuntimeError).  Scalars and diagonals cross the ABI as 32-bit float, scales
+ * as unsigned long, exactly like the Lattigo binding.
+ *
+ * Part 2 (OrionHip* and *Batch symbols) is new: batch ciphertexts (one handle
+ * = B independent images, one kernel launch per op for the whole batch),
+ * host/device import/export for parity tests and the RCCL key broadcast,
+ * stream control and kernel timing.
+ *
+ * Every call is asynchronous on the library stream unless it returns data to
+ * the host (Decode, Export*, Get*Scale never need to sync; Decode/Export do).
+ */
+#ifndef ORION_HIP_H
+#define ORION_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct { int *Data; unsigned long Length; } ArrayResultInt;          /* bindings.py:749-751 */
+typedef struct { float *Data; unsigned long Length; } ArrayResultFloat;      /* bindings.py:753-754 */
+typedef struct { double *Data; unsigned long Length; } ArrayResultDouble;    /* bindings.py:756-757 */
+typedef struct { unsigned long *Data; unsigned long Length; } ArrayResultUInt64; /* bindings.py:759-760 */
+typedef struct { char *Data; unsigned long Length; } ArrayResultByte;        /* bindings.py:762 */
+
+/* ---------------- scheme (scheme.go:34-100, utils.go:93-95) ---------------- */
+void NewScheme(int logN, int *logQ, int lenQ, int *logP, int lenP, int logScale, int h,
+               char *ringType, char *keysPath, char *ioMode);                 /* scheme.go:35 */
+void DeleteScheme(void);                                                   /* scheme.go:89 */
+void FreeCArray(void *ptr);                                                /* utils.go:93 */
+
+/* ---------------- tensors (tensors.go:36-123) ---------------- */
+void DeletePlaintext(int id);                                              /* tensors.go:35 */
+void DeleteCiphertext(int id);                                             /* tensors.go:40 */
+unsigned long GetPlaintextScale(int id);                                   /* tensors.go:45 */
+unsigned long GetCiphertextScale(int id);                                  /* tensors.go:53 */
+void SetPlaintextScale(int id, unsigned long scale);                       /* tensors.go:61 */
+void SetCiphertextScale(int id, unsigned long scale);                      /* tensors.go:67 */
+int GetPlaintextLevel(int id);                                             /* tensors.go:73 */
+int GetCiphertextLevel(int id);                                            /* tensors.go:79 */
+int GetPlaintextSlots(int id);                                             /* tensors.go:85 */
+int GetCiphertextSlots(int id);                                            /* tensors.go:92 */
+int GetCiphertextDegree(int id);                                           /* tensors.go:99 */
+ArrayResultUInt64 GetModuliChain(void);                                    /* tensors.go:105 */
+ArrayResultInt GetLivePlaintexts(void);                                    /* tensors.go:112 */
+ArrayResultInt GetLiveCiphertexts(void);                                   /* tensors.go:119 */
+int CloneCiphertext(int id);                                               /* fork: tensors.py:229 */
+
+/* ---------------- key generator (keygenerator.go:13-58) ---------------- */
+void NewKeyGenerator(void);                                                /* keygenerator.go:13 */
+void GenerateSecretKey(void);                                              /* keygenerator.go:18 */
+void GeneratePublicKey(void);                                              /* keygenerator.go:23 */
+void GenerateRelinearizationKey(void);                                     /* keygenerator.go:28 */
+void GenerateEvaluationKeys(void);                                         /* keygenerator.go:33 */
+ArrayResultByte SerializeSecretKey(void);                                  /* keygenerator.go:38 */
+void LoadSecretKey(char *data, unsigned long len);                         /* keygenerator.go:49 */
+
+/* ---------------- encoder / encryptor (encoder.go, encryptor.go) ---------------- */
+void NewEncoder(void);                                                     /* encoder.go:11 */
+int Encode(float *values, int lenValues, int level, unsigned long scale);  /* encoder.go:16 */
+ArrayResultFloat Decode(int ptId);                                         /* encoder.go:33 */
+void NewEncryptor(void);                                                   /* encryptor.go:10 */
+void NewDecryptor(void);                                                   /* encryptor.go:15 */
+int Encrypt(int ptId);                                                     /* encryptor.go:20 */
+int Decrypt(int ctId);                                                     /* encryptor.go:30 */
+
+/* ---------------- evaluator (evaluator.go:13-317) ---------------- */
+void NewEvaluator(void);                                                   /* evaluator.go:14 */
+void AddRotationKey(int rotation);                                         /* evaluator.go:34 */
+int Negate(int ct);                                                        /* evaluator.go:49 */
+int Rotate(int ct, int amount);                                            /* evaluator.go:61 */
+int RotateNew(int ct, int amount);                                         /* evaluator.go:70 */
+int Rescale(int ct);                                                       /* evaluator.go:84 */
+int RescaleNew(int ct);                                                    /* evaluator.go:92 */
+int AddScalar(int ct, float scalar);                                       /* evaluator.go:102 */
+int AddScalarNew(int ct, float scalar);                                    /* evaluator.go:110 */
+int SubScalar(int ct, float scalar);                                       /* evaluator.go:122 */
+int SubScalarNew(int ct, float scalar);                                    /* evaluator.go:130 */
+int MulScalarInt(int ct, int scalar);                                      /* evaluator.go:142 */
+int MulScalarIntNew(int ct, int scalar);                                   /* evaluator.go:150 */
+int MulScalarFloat(int ct, float scalar);                                  /* evaluator.go:162 */
+int MulScalarFloatNew(int ct, float scalar);                               /* evaluator.go:170 */
+int AddPlaintext(int ct, int pt);                                          /* evaluator.go:182 */
+int AddPlaintextNew(int ct, int pt);                                       /* evaluator.go:191 */
+int SubPlaintext(int ct, int pt);                                          /* evaluator.go:205 */
+int SubPlaintextNew(int ct, int pt);                                       /* evaluator.go:214 */
+int MulPlaintext(int ct, int pt);                                          /* evaluator.go:228 */
+int MulPlaintextNew(int ct, int pt);                                       /* evaluator.go:237 */
+int AddCiphertext(int ct0, int ct1);                                       /* evaluator.go:251 */
+int AddCiphertextNew(int ct0, int ct1);                                    /* evaluator.go:260 */
+int SubCiphertext(int ct0, int ct1);                                       /* evaluator.go:274 */
+int SubCiphertextNew(int ct0, int ct1);                                    /* evaluator.go:283 */
+int MulRelinCiphertext(int ct0, int ct1);                                  /* evaluator.go:297 */
+int MulRelinCiphertextNew(int ct0, int ct1);                               /* evaluator.go:306 */
+
+/* ---------------- linear transforms (lineartransform.go:26-211) ---------------- */
+void NewLinearTransformEvaluator(void);                                    /* lineartransform.go:31 */
+int GenerateLinearTransform(int *diagIdx, int nIdx, float *diagData, int nData, int level,
+                            float bsgsRatio, char *ioMode);                /* lineartransform.go:37 */
+int EvaluateLinearTransform(int transformId, int ctId);                    /* lineartransform.go:96 */
+void DeleteLinearTransform(int id);                                        /* lineartransform.go:26 */
+ArrayResultInt GetLinearTransformRotationKeys(int transformId);            /* lineartransform.go:116 */
+void GenerateLinearTransformRotationKey(int galEl);                        /* lineartransform.go:125 */
+void GenerateConsolidatedRotationKeys(int *galEls, int n);                 /* fork: lt_evaluator.py:77 */
+ArrayResultByte GenerateAndSerializeRotationKey(int galEl);                /* lineartransform.go:131 */
+void LoadRotationKey(char *data, unsigned long len, unsigned long galEl);  /* lineartransform.go:143 */
+ArrayResultByte SerializeDiagonal(int transformId, int diagIdx);           /* lineartransform.go:162 */
+void LoadPlaintextDiagonal(char *data, unsigned long len, int transformId,
+                           unsigned long diagIdx);                         /* lineartransform.go:180 */
+void RemovePlaintextDiagonals(int transformId);                            /* lineartransform.go:196 */
+void RemoveRotationKeys(void);                                             /* lineartransform.go:204 */
+
+/* ---------------- polynomial evaluator / bootstrapping (next) ----------------
+ * Exported so the binding resolves; they fail with an error in this round.  */
+void NewPolynomialEvaluator(void);                                         /* polyeval.go:33 */
+int GenerateMonomial(float *coeffs, int n);                                /* polyeval.go:38 */
+int GenerateChebyshev(float *coeffs, int n);                               /* polyeval.go:50 */
+int EvaluatePolynomial(int ct, int poly, unsigned long outScale);          /* polyeval.go:63 */
+ArrayResultDouble GenerateMinimaxSignCoeffs(int *degrees, int n, int prec, int logalpha,
+                                            int logerr, int debug);        /* polyeval.go:91 */
+void NewBootstrapper(int *logPs, int n, int slots);                        /* bootstrapper.go:19 */
+int Bootstrap(int ct, int slots);                                          /* bootstrapper.go:61 */
+void DeleteBootstrappers(void);                                            /* bootstrapper.go:91 */
+
+/* ================= Part 2: MI355X extensions ================= */
+const char *OrionHipLastError(void);
+void OrionHipClearError(void);
+int OrionHipSetDevice(int device);
+void OrionHipSetSeed(unsigned long seed);                /* keygen / encryption PRNG seed */
+void OrionHipSetStream(void *hipStream);                  /* NULL = library-owned stream */
+void *OrionHipGetStream(void);
+int OrionHipSynchronize(void);
+int OrionHipLogN(void);
+int OrionHipNumQ(void);
+int OrionHipNumP(void);
+unsigned long OrionHipModulus(int idx);                   /* QP index space */
+
+/* batch ciphertexts: one handle holds B images; ops act on the whole batch */
+int EncodeBatch(float *values, int lenPerImage, int batch, int level, unsigned long scale);
+int GetCiphertextBatch(int ct);
+int GetPlaintextBatch(int pt);
+double GetCiphertextScaleF(int ct);                       /* exact-ish scale (long double -> double) */
+
+/* host import/export, canonical host layout [batch][comp][limb][N] (NTT) */
+int ImportCiphertext(const unsigned long *data, int batch, int level, double scale);
+int ExportCiphertext(int ct, unsigned long *out, unsigned long n);
+int ImportPlaintext(const unsigned long *data, int batch, int level, double scale);
+int ExportPlaintext(int pt, unsigned long *out, unsigned long n);
+int ExportSecretKey(unsigned long *out, unsigned long n);                  /* [L+K][N]           */
+int ExportRelinKey(unsigned long *out, unsigned long n);                   /* [dnum][2][L+K][N]  */
+int ExportGaloisKey(unsigned long galEl, unsigned long *out, unsigned long n);
+int ExportLinearTransformDiagonal(int lt, int diagIdx, unsigned long *out, unsigned long n); /* [lvl+1+K][N] */
+int GetLinearTransformN1(int lt);
+unsigned long GaloisElement(int rotation);
+
+/* key bundle (public + evaluation keys [+ secret]) as one device buffer, for
+ * RCCL broadcast over xGMI; dptr is device memory owned by the caller */
+unsigned long KeyBundleBytes(int withSecret);
+int ExportKeyBundle(void *dptr, int withSecret);
+int ImportKeyBundle(const void *dptr, unsigned long bytes);
+
+/* kernel timing with HIP events on the library stream */
+void OrionHipProfile(int enable);
+/* fills up to max entries: name (32 chars each), launches, total ms, algorithmic bytes */
+int OrionHipProfileRead(char *names, long *launches, double *ms, double *bytes, int max);
+void OrionHipProfileReset(void);
+
+/* raw kernel entry for the roofline microbenchmark and parity tests:
+ * in-place NTT/INTT of `nlimb` limbs x `batch` images at device pointer
+ * (layout [limb][batch][N]), limb l under QP modulus index mods[l] */
+int OrionHipNTT(unsigned long *dptr, int nlimb, int batch, const int *mods, int inverse);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

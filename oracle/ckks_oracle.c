@@ -1,0 +1,1063 @@
+/*
+ * ckks_oracle.c -- CPU restatement of Lattigo-v6 RNS-CKKS arithmetic used by
+ * Orion's backend (TEST INFRASTRUCTURE: parity oracle + CPU baseline only).
+ * See ckks_oracle.h for the scope statement and reference citations.
+ * "parity unpinned" w.r.t. Lattigo itself: no golden vectors exist upstream.
+ *
+ * Built with -O2 -ffp-contract=off so that the float64 quotient inside the
+ * exact basis extension and the encoder FFT round exactly as written.
+ */
+#include "ckks_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef unsigned __int128 u128;
+typedef uint64_t u64;
+
+#define MAXMOD 80
+
+struct oracle_ctx {
+  int logN, N, L, K;
+  u64 mod[MAXMOD];
+  u64 psi[MAXMOD];
+  u64 *fw[MAXMOD];  /* fw[bitrev(j)] = psi^j            */
+  u64 *fws[MAXMOD]; /* Shoup companions floor(w 2^64/q)  */
+  u64 *iw[MAXMOD];  /* iw[bitrev(j)] = psi^-j           */
+  u64 *iws[MAXMOD];
+  u64 ninv[MAXMOD], ninvs[MAXMOD];
+};
+
+/* ------------------------------------------------------------------ */
+/* modular helpers                                                     */
+/* ------------------------------------------------------------------ */
+static inline u64 mulmod(u64 a, u64 b, u64 q) { return (u64)(((u128)a * b) % q); }
+static inline u64 addmod(u64 a, u64 b, u64 q) { u64 c = a + b; return c >= q ? c - q : c; }
+static inline u64 submod(u64 a, u64 b, u64 q) { return a >= b ? a - b : a + q - b; }
+static u64 powmod(u64 b, u64 e, u64 q) {
+  u64 r = 1 % q;
+  b %= q;
+  while (e) {
+    if (e & 1) r = mulmod(r, b, q);
+    b = mulmod(b, b, q);
+    e >>= 1;
+  }
+  return r;
+}
+static u64 invmod(u64 a, u64 q) { return powmod(a % q, q - 2, q); }
+static inline u64 shoup(u64 w, u64 q) { return (u64)(((u128)w << 64) / q); }
+/* Shoup product, result in [0, 2q) for any a < 2^64 */
+static inline u64 mul_shoup_lazy(u64 a, u64 w, u64 ws, u64 q) {
+  u64 hi = (u64)(((u128)a * ws) >> 64);
+  return a * w - hi * q;
+}
+
+static u64 bitrev(u64 x, int bits) {
+  u64 r = 0;
+  for (int i = 0; i < bits; i++) {
+    r = (r << 1) | (x & 1);
+    x >>= 1;
+  }
+  return r;
+}
+
+/* ------------------------------------------------------------------ */
+/* primes (Lattigo GenModuli / NTTFriendlyPrimesGenerator) */
+/* ------------------------------------------------------------------ */
+static int is_prime_u64(u64 n) {
+  if (n < 2) return 0;
+  static const u64 small[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
+  for (int i = 0; i < 12; i++) {
+    if (n % small[i] == 0) return n == small[i];
+  }
+  u64 d = n - 1;
+  int s = 0;
+  while ((d & 1) == 0) {
+    d >>= 1;
+    s++;
+  }
+  for (int i = 0; i < 12; i++) {
+    u64 x = powmod(small[i], d, n);
+    if (x == 1 || x == n - 1) continue;
+    int comp = 1;
+    for (int r = 1; r < s; r++) {
+      x = mulmod(x, x, n);
+      if (x == n - 1) {
+        comp = 0;
+        break;
+      }
+    }
+    if (comp) return 0;
+  }
+  return 1;
+}
+
+typedef struct {
+  double size;
+  u64 nthroot, next, prev;
+  int check_next, check_prev;
+} primegen;
+
+static void pg_init(primegen *g, int bitlen, u64 nthroot) {
+  g->size = (double)bitlen;
+  g->nthroot = nthroot;
+  g->next = ((u64)1 << bitlen) + 1;
+  g->prev = ((u64)1 << bitlen) + 1;
+  g->check_next = g->check_prev = 1;
+}
+
+static u64 pg_next_downstream(primegen *g) {
+  for (;;) {
+    if (g->prev < g->nthroot) return 0;
+    g->prev -= g->nthroot;
+    if (g->size - log2((double)g->prev) >= 0.5) return 0;
+    if (is_prime_u64(g->prev)) return g->prev;
+  }
+}
+
+static u64 pg_next_alternating(primegen *g) {
+  for (;;) {
+    if (!(g->check_next || g->check_prev)) return 0;
+    if (g->check_next) {
+      if (g->next > UINT64_MAX - g->nthroot || log2((double)g->next) - g->size >= 0.5) {
+        g->check_next = 0;
+      } else {
+        g->next += g->nthroot;
+        if (is_prime_u64(g->next)) return g->next;
+      }
+    }
+    if (g->check_prev) {
+      if (g->prev < g->nthroot || g->size - log2((double)g->prev) >= 0.5) {
+        g->check_prev = 0;
+      } else {
+        g->prev -= g->nthroot;
+        if (is_prime_u64(g->prev)) return g->prev;
+      }
+    }
+  }
+}
+
+int oracle_gen_moduli(int logN, const int *logQ, int lenQ, const int *logP, int lenP,
+                      u64 *out) {
+  /* Standard ring: NthRoot = 2N.  Primes of each distinct bit size are drawn
+   * in one stream and handed out first to Q (in order), then to P. */
+  u64 nthroot = (u64)2 << logN;
+  int sizes[MAXMOD], counts[MAXMOD], nsz = 0;
+  for (int i = 0; i < lenQ + lenP; i++) {
+    int b = i < lenQ ? logQ[i] : logP[i - lenQ];
+    int k;
+    for (k = 0; k < nsz; k++)
+      if (sizes[k] == b) break;
+    if (k == nsz) {
+      sizes[nsz] = b;
+      counts[nsz++] = 0;
+    }
+    counts[k]++;
+  }
+  u64 pool[MAXMOD][MAXMOD];
+  int used[MAXMOD] = {0};
+  for (int k = 0; k < nsz; k++) {
+    primegen g;
+    pg_init(&g, sizes[k], nthroot);
+    for (int c = 0; c < counts[k]; c++) {
+      u64 p = sizes[k] == 61 ? pg_next_downstream(&g) : pg_next_alternating(&g);
+      if (!p) return -1;
+      pool[k][c] = p;
+    }
+  }
+  for (int i = 0; i < lenQ + lenP; i++) {
+    int b = i < lenQ ? logQ[i] : logP[i - lenQ];
+    int k;
+    for (k = 0; k < nsz; k++)
+      if (sizes[k] == b) break;
+    out[i] = pool[k][used[k]++];
+  }
+  return 0;
+}
+
+/* smallest primitive root, candidates 3, 4, 5, ... (Lattigo PrimitiveRoot:
+ * g starts at 2 and is incremented before the first test) */
+u64 oracle_primitive_root(u64 q) {
+  u64 factors[64];
+  int nf = 0;
+  u64 m = q - 1;
+  for (u64 f = 2; f * f <= m; f += (f == 2 ? 1 : 2)) {
+    if (m % f == 0) {
+      factors[nf++] = f;
+      while (m % f == 0) m /= f;
+    }
+  }
+  if (m > 1) factors[nf++] = m;
+  for (u64 g = 3;; g++) {
+    int ok = 1;
+    for (int i = 0; i < nf; i++) {
+      if (powmod(g, (q - 1) / factors[i], q) == 1) {
+        ok = 0;
+        break;
+      }
+    }
+    if (ok) return g;
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* context                                                             */
+/* ------------------------------------------------------------------ */
+oracle_ctx *oracle_new(int logN, const u64 *moduli, int L, int K) {
+  if (L + K > MAXMOD) return NULL;
+  oracle_ctx *c = (oracle_ctx *)calloc(1, sizeof(oracle_ctx));
+  c->logN = logN;
+  c->N = 1 << logN;
+  c->L = L;
+  c->K = K;
+  int N = c->N;
+  for (int m = 0; m < L + K; m++) {
+    u64 q = moduli[m];
+    c->mod[m] = q;
+    u64 g = oracle_primitive_root(q);
+    u64 psi = powmod(g, (q - 1) / (2 * (u64)N), q);
+    u64 psii = invmod(psi, q);
+    c->psi[m] = psi;
+    c->fw[m] = (u64 *)malloc(sizeof(u64) * N);
+    c->fws[m] = (u64 *)malloc(sizeof(u64) * N);
+    c->iw[m] = (u64 *)malloc(sizeof(u64) * N);
+    c->iws[m] = (u64 *)malloc(sizeof(u64) * N);
+    u64 a = 1, b = 1;
+    for (int j = 0; j < N; j++) {
+      u64 r = bitrev(j, logN);
+      c->fw[m][r] = a;
+      c->fws[m][r] = shoup(a, q);
+      c->iw[m][r] = b;
+      c->iws[m][r] = shoup(b, q);
+      a = mulmod(a, psi, q);
+      b = mulmod(b, psii, q);
+    }
+    c->ninv[m] = invmod((u64)N, q);
+    c->ninvs[m] = shoup(c->ninv[m], q);
+  }
+  return c;
+}
+
+void oracle_free(oracle_ctx *c) {
+  if (!c) return;
+  for (int m = 0; m < c->L + c->K; m++) {
+    free(c->fw[m]);
+    free(c->fws[m]);
+    free(c->iw[m]);
+    free(c->iws[m]);
+  }
+  free(c);
+}
+
+int oracle_N(const oracle_ctx *c) { return c->N; }
+u64 oracle_psi(const oracle_ctx *c, int m) { return c->psi[m]; }
+
+/* ------------------------------------------------------------------ */
+/* NTT (Cooley-Tukey, natural -> bit-reversed; Harvey lazy butterflies) */
+/* ------------------------------------------------------------------ */
+void oracle_ntt(const oracle_ctx *c, int mi, u64 *a) {
+  const int N = c->N;
+  const u64 q = c->mod[mi], q2 = 2 * q;
+  const u64 *w = c->fw[mi], *ws = c->fws[mi];
+  int t = N;
+  for (int m = 1; m < N; m <<= 1) {
+    t >>= 1;
+    for (int i = 0; i < m; i++) {
+      const u64 W = w[m + i], Ws = ws[m + i];
+      u64 *x = a + 2 * i * t, *y = x + t;
+      for (int j = 0; j < t; j++) {
+        u64 X = x[j];
+        if (X >= q2) X -= q2;
+        u64 T = mul_shoup_lazy(y[j], W, Ws, q);
+        x[j] = X + T;
+        y[j] = X - T + q2;
+      }
+    }
+  }
+  for (int j = 0; j < N; j++) {
+    u64 X = a[j];
+    if (X >= q2) X -= q2;
+    if (X >= q) X -= q;
+    a[j] = X;
+  }
+}
+
+void oracle_intt(const oracle_ctx *c, int mi, u64 *a) {
+  const int N = c->N;
+  const u64 q = c->mod[mi], q2 = 2 * q;
+  const u64 *w = c->iw[mi], *ws = c->iws[mi];
+  int t = 1;
+  for (int m = N >> 1; m >= 1; m >>= 1) {
+    for (int i = 0; i < m; i++) {
+      const u64 W = w[m + i], Ws = ws[m + i];
+      u64 *x = a + 2 * i * t, *y = x + t;
+      for (int j = 0; j < t; j++) {
+        u64 U = x[j], V = y[j];
+        u64 S = U + V;
+        if (S >= q2) S -= q2;
+        x[j] = S;
+        y[j] = mul_shoup_lazy(U - V + q2, W, Ws, q);
+      }
+    }
+    t <<= 1;
+  }
+  for (int j = 0; j < N; j++) {
+    u64 X = mul_shoup_lazy(a[j], c->ninv[mi], c->ninvs[mi], q);
+    if (X >= q) X -= q;
+    a[j] = X;
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* exact basis extension (Lattigo ModUpExact restated, App. A.5)        */
+/*   y_i = x_i * (S/s_i)^-1 mod s_i                                     */
+/*   v   = (u64) sum_i (double)y_i * (1.0/(double)s_i)   (ordered, no FMA) */
+/*   out_t = sum_i y_i * (S/s_i mod t) - v * (S mod t)   mod t          */
+/* ------------------------------------------------------------------ */
+void oracle_basis_extend(const oracle_ctx *c, const u64 *x, const int *src, int ns,
+                         u64 *out, const int *dst, int nt) {
+  const int N = c->N;
+  u64 qhatinv[MAXMOD];
+  double qinvf[MAXMOD];
+  u64 qhat_t[MAXMOD][MAXMOD]; /* [t][i] */
+  u64 S_t[MAXMOD];
+  for (int i = 0; i < ns; i++) {
+    u64 si = c->mod[src[i]];
+    u64 prod = 1;
+    for (int k = 0; k < ns; k++)
+      if (k != i) prod = mulmod(prod, c->mod[src[k]] % si, si);
+    qhatinv[i] = invmod(prod, si);
+    qinvf[i] = 1.0 / (double)si;
+  }
+  for (int t = 0; t < nt; t++) {
+    u64 tm = c->mod[dst[t]];
+    u64 S = 1;
+    for (int k = 0; k < ns; k++) S = mulmod(S, c->mod[src[k]] % tm, tm);
+    S_t[t] = S;
+    for (int i = 0; i < ns; i++) {
+      u64 p = 1;
+      for (int k = 0; k < ns; k++)
+        if (k != i) p = mulmod(p, c->mod[src[k]] % tm, tm);
+      qhat_t[t][i] = p;
+    }
+  }
+  u64 y[MAXMOD];
+  for (int n = 0; n < N; n++) {
+    double vf = 0.0;
+    for (int i = 0; i < ns; i++) {
+      u64 si = c->mod[src[i]];
+      y[i] = mulmod(x[(size_t)i * N + n] % si, qhatinv[i], si);
+      volatile double prod = (double)y[i] * qinvf[i];
+      vf = vf + prod;
+    }
+    u64 v = (u64)vf;
+    for (int t = 0; t < nt; t++) {
+      u64 tm = c->mod[dst[t]];
+      u128 acc = 0;
+      for (int i = 0; i < ns; i++) acc += (u128)y[i] * qhat_t[t][i];
+      u64 r = (u64)(acc % tm);
+      u64 vs = mulmod(v % tm, S_t[t], tm);
+      out[(size_t)t * N + n] = submod(r, vs, tm);
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* rescale: round(x / q_l)  (DivRoundByLastModulusNTT, App. A.4)        */
+/* ------------------------------------------------------------------ */
+void oracle_rescale(const oracle_ctx *c, int level, int ncomp, const u64 *ct, u64 *out) {
+  const int N = c->N;
+  const u64 ql = c->mod[level];
+  const u64 half = ql >> 1;
+  u64 *last = (u64 *)malloc(sizeof(u64) * N);
+  u64 *t = (u64 *)malloc(sizeof(u64) * N);
+  for (int comp = 0; comp < ncomp; comp++) {
+    const u64 *in = ct + (size_t)comp * (level + 1) * N;
+    u64 *o = out + (size_t)comp * level * N;
+    memcpy(last, in + (size_t)level * N, sizeof(u64) * N);
+    oracle_intt(c, level, last);
+    for (int n = 0; n < N; n++) last[n] = addmod(last[n], half, ql);
+    for (int i = 0; i < level; i++) {
+      u64 qi = c->mod[i];
+      u64 hmod = half % qi;
+      for (int n = 0; n < N; n++) t[n] = submod(last[n] % qi, hmod, qi);
+      oracle_ntt(c, i, t);
+      u64 qlinv = invmod(ql % qi, qi);
+      for (int n = 0; n < N; n++) o[(size_t)i * N + n] = mulmod(submod(in[(size_t)i * N + n], t[n], qi), qlinv, qi);
+    }
+  }
+  free(last);
+  free(t);
+}
+
+/* ------------------------------------------------------------------ */
+/* ModDown QP -> Q: (x_Q - ext_{P->Q}(x_P)) * P^-1                      */
+/* ------------------------------------------------------------------ */
+void oracle_moddown(const oracle_ctx *c, int level, const u64 *x, u64 *out) {
+  const int N = c->N, L = c->L, K = c->K;
+  int src[MAXMOD], dst[MAXMOD];
+  u64 *xp = (u64 *)malloc(sizeof(u64) * N * K);
+  u64 *ext = (u64 *)malloc(sizeof(u64) * N * (level + 1));
+  memcpy(xp, x + (size_t)(level + 1) * N, sizeof(u64) * N * K);
+  for (int k = 0; k < K; k++) {
+    src[k] = L + k;
+    oracle_intt(c, L + k, xp + (size_t)k * N);
+  }
+  for (int j = 0; j <= level; j++) dst[j] = j;
+  oracle_basis_extend(c, xp, src, K, ext, dst, level + 1);
+  for (int j = 0; j <= level; j++) {
+    u64 qj = c->mod[j];
+    oracle_ntt(c, j, ext + (size_t)j * N);
+    u64 P = 1;
+    for (int k = 0; k < K; k++) P = mulmod(P, c->mod[L + k] % qj, qj);
+    u64 pinv = invmod(P, qj);
+    for (int n = 0; n < N; n++)
+      out[(size_t)j * N + n] = mulmod(submod(x[(size_t)j * N + n], ext[(size_t)j * N + n], qj), pinv, qj);
+  }
+  free(xp);
+  free(ext);
+}
+
+/* ------------------------------------------------------------------ */
+/* gadget product (hybrid key switching, App. A.5)                      */
+/* digit i covers Q limbs [i*K, min((i+1)*K, level+1))                  */
+/* ------------------------------------------------------------------ */
+void oracle_gadget_product_lazy(const oracle_ctx *c, int level, const u64 *cx,
+                                const u64 *evk, u64 *out0, u64 *out1) {
+  const int N = c->N, L = c->L, K = c->K;
+  const int nqp = level + 1 + K;
+  const int dnum_full = (L + K - 1) / K;
+  const int beta = (level + 1 + K - 1) / K;
+  (void)dnum_full;
+  u64 *cinv = (u64 *)malloc(sizeof(u64) * N * (level + 1));
+  u64 *d = (u64 *)malloc(sizeof(u64) * N * nqp);
+  memcpy(cinv, cx, sizeof(u64) * N * (level + 1));
+  for (int j = 0; j <= level; j++) oracle_intt(c, j, cinv + (size_t)j * N);
+  memset(out0, 0, sizeof(u64) * N * nqp);
+  memset(out1, 0, sizeof(u64) * N * nqp);
+  for (int i = 0; i < beta; i++) {
+    int lo = i * K, hi = (i + 1) * K;
+    if (hi > level + 1) hi = level + 1;
+    int src[MAXMOD], dst[MAXMOD], pos[MAXMOD], nt = 0;
+    for (int j = lo; j < hi; j++) src[j - lo] = j;
+    for (int j = 0; j < nqp; j++) {
+      int mi = j <= level ? j : L + (j - level - 1);
+      if (j >= lo && j < hi) continue;
+      dst[nt] = mi;
+      pos[nt++] = j;
+    }
+    u64 *ext = (u64 *)malloc(sizeof(u64) * N * (nt ? nt : 1));
+    oracle_basis_extend(c, cinv + (size_t)lo * N, src, hi - lo, ext, dst, nt);
+    for (int t = 0; t < nt; t++) {
+      oracle_ntt(c, dst[t], ext + (size_t)t * N);
+      memcpy(d + (size_t)pos[t] * N, ext + (size_t)t * N, sizeof(u64) * N);
+    }
+    for (int j = lo; j < hi; j++) memcpy(d + (size_t)j * N, cx + (size_t)j * N, sizeof(u64) * N);
+    free(ext);
+    /* MAC with key digit i: key limb index for QP position j */
+    const u64 *b = evk + (size_t)i * 2 * (L + K) * N;
+    const u64 *a = b + (size_t)(L + K) * N;
+    for (int j = 0; j < nqp; j++) {
+      int mi = j <= level ? j : L + (j - level - 1);
+      u64 q = c->mod[mi];
+      const u64 *bj = b + (size_t)mi * N, *aj = a + (size_t)mi * N, *dj = d + (size_t)j * N;
+      u64 *o0 = out0 + (size_t)j * N, *o1 = out1 + (size_t)j * N;
+      for (int n = 0; n < N; n++) {
+        o0[n] = addmod(o0[n], mulmod(dj[n], bj[n], q), q);
+        o1[n] = addmod(o1[n], mulmod(dj[n], aj[n], q), q);
+      }
+    }
+  }
+  free(cinv);
+  free(d);
+}
+
+void oracle_keyswitch(const oracle_ctx *c, int level, const u64 *cx, const u64 *evk,
+                      u64 *out0, u64 *out1) {
+  const int N = c->N, K = c->K;
+  size_t sz = sizeof(u64) * N * (level + 1 + K);
+  u64 *t0 = (u64 *)malloc(sz), *t1 = (u64 *)malloc(sz);
+  oracle_gadget_product_lazy(c, level, cx, evk, t0, t1);
+  oracle_moddown(c, level, t0, out0);
+  oracle_moddown(c, level, t1, out1);
+  free(t0);
+  free(t1);
+}
+
+/* ------------------------------------------------------------------ */
+/* automorphisms                                                         */
+/* ------------------------------------------------------------------ */
+uint64_t oracle_galois_element(const oracle_ctx *c, int k) {
+  u64 M = 2 * (u64)c->N;
+  u64 e = (u64)((int64_t)k) & (M - 1);
+  return powmod(5, e, M);
+}
+
+static void automorphism_index(const oracle_ctx *c, u64 g, uint32_t *idx) {
+  const int N = c->N, logN = c->logN;
+  const u64 mask = 2 * (u64)N - 1;
+  for (int j = 0; j < N; j++) {
+    u64 t1 = 2 * bitrev(j, logN) + 1;
+    u64 t2 = (((g * t1) & mask) - 1) >> 1;
+    idx[j] = (uint32_t)bitrev(t2, logN);
+  }
+}
+
+void oracle_automorphism_ntt(const oracle_ctx *c, u64 g, const u64 *in, u64 *out, int nl) {
+  const int N = c->N;
+  uint32_t *idx = (uint32_t *)malloc(sizeof(uint32_t) * N);
+  automorphism_index(c, g, idx);
+  for (int l = 0; l < nl; l++)
+    for (int j = 0; j < N; j++) out[(size_t)l * N + j] = in[(size_t)l * N + idx[j]];
+  free(idx);
+}
+
+/* ------------------------------------------------------------------ */
+/* ciphertext ops                                                        */
+/* ------------------------------------------------------------------ */
+void oracle_mul_coeffs(const oracle_ctx *c, const int *mods, int nl, const u64 *a,
+                       const u64 *b, u64 *out) {
+  const int N = c->N;
+  for (int l = 0; l < nl; l++) {
+    u64 q = c->mod[mods[l]];
+    for (int n = 0; n < N; n++) out[(size_t)l * N + n] = mulmod(a[(size_t)l * N + n], b[(size_t)l * N + n], q);
+  }
+}
+
+void oracle_mul_relin(const oracle_ctx *c, int level, const u64 *a, const u64 *b,
+                      const u64 *rlk, u64 *out) {
+  const int N = c->N;
+  const size_t P = (size_t)(level + 1) * N;
+  u64 *d2 = (u64 *)malloc(sizeof(u64) * P);
+  u64 *k0 = (u64 *)malloc(sizeof(u64) * P), *k1 = (u64 *)malloc(sizeof(u64) * P);
+  const u64 *a0 = a, *a1 = a + P, *b0 = b, *b1 = b + P;
+  for (int j = 0; j <= level; j++) {
+    u64 q = c->mod[j];
+    for (int n = 0; n < N; n++) {
+      size_t x = (size_t)j * N + n;
+      out[x] = mulmod(a0[x], b0[x], q);
+      out[P + x] = addmod(mulmod(a0[x], b1[x], q), mulmod(a1[x], b0[x], q), q);
+      d2[x] = mulmod(a1[x], b1[x], q);
+    }
+  }
+  oracle_keyswitch(c, level, d2, rlk, k0, k1);
+  for (int j = 0; j <= level; j++) {
+    u64 q = c->mod[j];
+    for (int n = 0; n < N; n++) {
+      size_t x = (size_t)j * N + n;
+      out[x] = addmod(out[x], k0[x], q);
+      out[P + x] = addmod(out[P + x], k1[x], q);
+    }
+  }
+  free(d2);
+  free(k0);
+  free(k1);
+}
+
+void oracle_rotate(const oracle_ctx *c, int level, const u64 *ct, u64 g, const u64 *gk,
+                   u64 *out) {
+  const int N = c->N;
+  const size_t P = (size_t)(level + 1) * N;
+  u64 *k = (u64 *)malloc(sizeof(u64) * 2 * P);
+  oracle_keyswitch(c, level, ct + P, gk, k, k + P);
+  for (int j = 0; j <= level; j++) {
+    u64 q = c->mod[j];
+    for (int n = 0; n < N; n++) {
+      size_t x = (size_t)j * N + n;
+      k[x] = addmod(k[x], ct[x], q);
+    }
+  }
+  oracle_automorphism_ntt(c, g, k, out, level + 1);
+  oracle_automorphism_ntt(c, g, k + P, out + P, level + 1);
+  free(k);
+}
+
+/* ------------------------------------------------------------------ */
+/* BSGS linear transform (lintrans MultiplyByDiagMatrixBSGS restated)   */
+/* ------------------------------------------------------------------ */
+static void bsgs_split(int rot, int slots, int N1, int *giant, int *baby) {
+  rot &= (slots - 1);
+  *giant = ((rot / N1) * N1) & (slots - 1);
+  *baby = rot & (N1 - 1);
+}
+
+int oracle_find_best_bsgs_n1(const int *diag_idx, int nd, int slots, int logMaxRatio) {
+  double maxRatio = (double)(1 << logMaxRatio);
+  for (int N1 = 1; N1 < slots; N1 <<= 1) {
+    /* count distinct giant / baby indices */
+    int *g = (int *)malloc(sizeof(int) * nd), *b = (int *)malloc(sizeof(int) * nd);
+    int ng = 0, nb = 0;
+    for (int d = 0; d < nd; d++) {
+      int gi, bi, k;
+      bsgs_split(diag_idx[d], slots, N1, &gi, &bi);
+      for (k = 0; k < ng; k++)
+        if (g[k] == gi) break;
+      if (k == ng) g[ng++] = gi;
+      for (k = 0; k < nb; k++)
+        if (b[k] == bi) break;
+      if (k == nb) b[nb++] = bi;
+    }
+    free(g);
+    free(b);
+    double r = (double)(nb - 1) / (double)(ng - 1);
+    if (r == maxRatio) return N1;
+    if (r > maxRatio) return N1 / 2;
+  }
+  return 1;
+}
+
+static const u64 *find_key(u64 g, int ngk, const u64 *gels, const u64 *const *gks) {
+  for (int i = 0; i < ngk; i++)
+    if (gels[i] == g) return gks[i];
+  return NULL;
+}
+
+static int cmp_int(const void *a, const void *b) { return (*(const int *)a > *(const int *)b) - (*(const int *)a < *(const int *)b); }
+
+void oracle_lt_bsgs(const oracle_ctx *c, int level, const u64 *ct, int nd, const int *diag_idx,
+                    const u64 *const *pts, int N1, int ngk, const u64 *gels,
+                    const u64 *const *gks, u64 *out) {
+  const int N = c->N, L = c->L, K = c->K, slots = N / 2;
+  const int nq = level + 1, nqp = nq + K;
+  const size_t PQ = (size_t)nq * N, PQP = (size_t)nqp * N;
+  int mods[MAXMOD];
+  for (int j = 0; j < nqp; j++) mods[j] = j < nq ? j : L + (j - nq);
+
+  /* giant/baby decomposition */
+  int *gi = (int *)malloc(sizeof(int) * nd), *bi = (int *)malloc(sizeof(int) * nd);
+  int *giants = (int *)malloc(sizeof(int) * nd), *babies = (int *)malloc(sizeof(int) * nd);
+  int ng = 0, nb = 0;
+  for (int d = 0; d < nd; d++) {
+    int k;
+    bsgs_split(diag_idx[d], slots, N1, &gi[d], &bi[d]);
+    for (k = 0; k < ng; k++)
+      if (giants[k] == gi[d]) break;
+    if (k == ng) giants[ng++] = gi[d];
+    for (k = 0; k < nb; k++)
+      if (babies[k] == bi[d]) break;
+    if (k == nb) babies[nb++] = bi[d];
+  }
+  qsort(giants, ng, sizeof(int), cmp_int);
+
+  /* hoisted baby-step rotations in QP: rot_i = phi_i((c0*P + u0, u1)) */
+  u64 **rot0 = (u64 **)calloc(nb, sizeof(u64 *)), **rot1 = (u64 **)calloc(nb, sizeof(u64 *));
+  u64 *u0 = (u64 *)malloc(sizeof(u64) * PQP), *u1 = (u64 *)malloc(sizeof(u64) * PQP);
+  for (int b = 0; b < nb; b++) {
+    rot0[b] = (u64 *)malloc(sizeof(u64) * PQP);
+    rot1[b] = (u64 *)malloc(sizeof(u64) * PQP);
+    if (babies[b] == 0) {
+      /* (c0*P, c1*P) in Q, zero P part */
+      for (int j = 0; j < nq; j++) {
+        u64 q = c->mod[j], Pm = 1;
+        for (int k = 0; k < K; k++) Pm = mulmod(Pm, c->mod[L + k] % q, q);
+        for (int n = 0; n < N; n++) {
+          rot0[b][(size_t)j * N + n] = mulmod(ct[(size_t)j * N + n], Pm, q);
+          rot1[b][(size_t)j * N + n] = mulmod(ct[PQ + (size_t)j * N + n], Pm, q);
+        }
+      }
+      memset(rot0[b] + PQ, 0, sizeof(u64) * K * N);
+      memset(rot1[b] + PQ, 0, sizeof(u64) * K * N);
+      continue;
+    }
+    u64 g = oracle_galois_element(c, babies[b]);
+    const u64 *key = find_key(g, ngk, gels, gks);
+    if (!key) abort();
+    oracle_gadget_product_lazy(c, level, ct + PQ, key, u0, u1);
+    for (int j = 0; j < nq; j++) {
+      u64 q = c->mod[j], Pm = 1;
+      for (int k = 0; k < K; k++) Pm = mulmod(Pm, c->mod[L + k] % q, q);
+      for (int n = 0; n < N; n++)
+        u0[(size_t)j * N + n] = addmod(u0[(size_t)j * N + n], mulmod(ct[(size_t)j * N + n], Pm, q), q);
+    }
+    oracle_automorphism_ntt(c, g, u0, rot0[b], nqp);
+    oracle_automorphism_ntt(c, g, u1, rot1[b], nqp);
+  }
+
+  u64 *acc0 = (u64 *)calloc(PQP, sizeof(u64)), *acc1 = (u64 *)calloc(PQP, sizeof(u64));
+  u64 *t0 = (u64 *)malloc(sizeof(u64) * PQP), *t1 = (u64 *)malloc(sizeof(u64) * PQP);
+  u64 *t1q = (u64 *)malloc(sizeof(u64) * PQ);
+  u64 *c0 = (u64 *)malloc(sizeof(u64) * PQP), *c1 = (u64 *)malloc(sizeof(u64) * PQP);
+  u64 *r0 = (u64 *)malloc(sizeof(u64) * PQP), *r1 = (u64 *)malloc(sizeof(u64) * PQP);
+  for (int G = 0; G < ng; G++) {
+    int j = giants[G];
+    memset(t0, 0, sizeof(u64) * PQP);
+    memset(t1, 0, sizeof(u64) * PQP);
+    for (int d = 0; d < nd; d++) {
+      if (gi[d] != j) continue;
+      int b;
+      for (b = 0; b < nb; b++)
+        if (babies[b] == bi[d]) break;
+      for (int l = 0; l < nqp; l++) {
+        u64 q = c->mod[mods[l]];
+        for (int n = 0; n < N; n++) {
+          size_t x = (size_t)l * N + n;
+          t0[x] = addmod(t0[x], mulmod(pts[d][x], rot0[b][x], q), q);
+          t1[x] = addmod(t1[x], mulmod(pts[d][x], rot1[b][x], q), q);
+        }
+      }
+    }
+    if (j != 0) {
+      u64 g = oracle_galois_element(c, j);
+      const u64 *key = find_key(g, ngk, gels, gks);
+      if (!key) abort();
+      oracle_moddown(c, level, t1, t1q);
+      oracle_gadget_product_lazy(c, level, t1q, key, c0, c1);
+      for (int l = 0; l < nqp; l++) {
+        u64 q = c->mod[mods[l]];
+        for (int n = 0; n < N; n++) {
+          size_t x = (size_t)l * N + n;
+          c0[x] = addmod(c0[x], t0[x], q);
+        }
+      }
+      oracle_automorphism_ntt(c, g, c0, r0, nqp);
+      oracle_automorphism_ntt(c, g, c1, r1, nqp);
+    } else {
+      memcpy(r0, t0, sizeof(u64) * PQP);
+      memcpy(r1, t1, sizeof(u64) * PQP);
+    }
+    for (int l = 0; l < nqp; l++) {
+      u64 q = c->mod[mods[l]];
+      for (int n = 0; n < N; n++) {
+        size_t x = (size_t)l * N + n;
+        acc0[x] = addmod(acc0[x], r0[x], q);
+        acc1[x] = addmod(acc1[x], r1[x], q);
+      }
+    }
+  }
+  oracle_moddown(c, level, acc0, out);
+  oracle_moddown(c, level, acc1, out + PQ);
+
+  for (int b = 0; b < nb; b++) {
+    free(rot0[b]);
+    free(rot1[b]);
+  }
+  free(rot0); free(rot1); free(u0); free(u1);
+  free(acc0); free(acc1); free(t0); free(t1); free(t1q);
+  free(c0); free(c1); free(r0); free(r1);
+  free(gi); free(bi); free(giants); free(babies);
+}
+
+/* ------------------------------------------------------------------ */
+/* encoder (Standard ring, n = N/2 slots; HEAAN/Lattigo special FFT)    */
+/* ------------------------------------------------------------------ */
+typedef struct {
+  double re, im;
+} cplx;
+
+static void special_tables(int n, int M, int **rot, cplx **roots) {
+  *rot = (int *)malloc(sizeof(int) * n);
+  *roots = (cplx *)malloc(sizeof(cplx) * (M + 1));
+  int r = 1;
+  for (int i = 0; i < n; i++) {
+    (*rot)[i] = r;
+    r = (int)(((long)r * 5) % M);
+  }
+  for (int i = 0; i <= M; i++) {
+    double ang = 2.0 * M_PI * (double)i / (double)M;
+    (*roots)[i].re = cos(ang);
+    (*roots)[i].im = sin(ang);
+  }
+}
+
+static void bitrev_cplx(cplx *v, int n) {
+  int logn = 0;
+  while ((1 << logn) < n) logn++;
+  for (int i = 0; i < n; i++) {
+    int j = (int)bitrev(i, logn);
+    if (i < j) {
+      cplx t = v[i];
+      v[i] = v[j];
+      v[j] = t;
+    }
+  }
+}
+
+static inline cplx cmul(cplx a, cplx b) {
+  cplx r;
+  double ac = a.re * b.re, bd = a.im * b.im, ad = a.re * b.im, bc = a.im * b.re;
+  r.re = ac - bd;
+  r.im = ad + bc;
+  return r;
+}
+
+static void special_ifft(cplx *v, int n, int M, const int *rot, const cplx *roots) {
+  for (int len = n; len >= 2; len >>= 1) {
+    int lenh = len >> 1, lenq = len << 2;
+    for (int i = 0; i < n; i += len) {
+      for (int j = 0; j < lenh; j++) {
+        int idx = (lenq - (rot[j] % lenq)) * (M / lenq);
+        cplx u, w;
+        u.re = v[i + j].re + v[i + j + lenh].re;
+        u.im = v[i + j].im + v[i + j + lenh].im;
+        w.re = v[i + j].re - v[i + j + lenh].re;
+        w.im = v[i + j].im - v[i + j + lenh].im;
+        v[i + j] = u;
+        v[i + j + lenh] = cmul(w, roots[idx]);
+      }
+    }
+  }
+  bitrev_cplx(v, n);
+  double inv = 1.0 / (double)n;
+  for (int i = 0; i < n; i++) {
+    v[i].re *= inv;
+    v[i].im *= inv;
+  }
+}
+
+static void special_fft(cplx *v, int n, int M, const int *rot, const cplx *roots) {
+  bitrev_cplx(v, n);
+  for (int len = 2; len <= n; len <<= 1) {
+    int lenh = len >> 1, lenq = len << 2;
+    for (int i = 0; i < n; i += len) {
+      for (int j = 0; j < lenh; j++) {
+        int idx = (rot[j] % lenq) * (M / lenq);
+        cplx u = v[i + j];
+        cplx w = cmul(v[i + j + lenh], roots[idx]);
+        v[i + j].re = u.re + w.re;
+        v[i + j].im = u.im + w.im;
+        v[i + j + lenh].re = u.re - w.re;
+        v[i + j + lenh].im = u.im - w.im;
+      }
+    }
+  }
+}
+
+/* Lattigo SingleFloat64ToFixedPointCRT restated: c = floor(|v|*scale + 0.5),
+ * negative values map to q - (c mod q) (fully reduced here). */
+static void to_crt(double v, double scale, const oracle_ctx *c, const int *mods, int nm,
+                   u64 *out, size_t stride) {
+  if (v == 0.0) {
+    for (int m = 0; m < nm; m++) out[m * stride] = 0;
+    return;
+  }
+  int neg = v < 0;
+  double x = neg ? v * (-scale) : v * scale;
+  u64 cval = (u64)(x + 0.5);
+  for (int m = 0; m < nm; m++) {
+    u64 q = c->mod[mods[m]];
+    u64 r = cval % q;
+    out[m * stride] = neg ? (r ? q - r : 0) : r;
+  }
+}
+
+void oracle_encode(const oracle_ctx *c, const double *values, int nvals, double scale,
+                   const int *mods, int nm, u64 *out) {
+  const int N = c->N, n = N / 2, M = 2 * N;
+  int *rot;
+  cplx *roots;
+  special_tables(n, M, &rot, &roots);
+  cplx *v = (cplx *)calloc(n, sizeof(cplx));
+  for (int i = 0; i < nvals && i < n; i++) v[i].re = values[i];
+  special_ifft(v, n, M, rot, roots);
+  for (int i = 0; i < n; i++) {
+    to_crt(v[i].re, scale, c, mods, nm, out + i, (size_t)N);
+    to_crt(v[i].im, scale, c, mods, nm, out + i + n, (size_t)N);
+  }
+  for (int m = 0; m < nm; m++) oracle_ntt(c, mods[m], out + (size_t)m * N);
+  free(v);
+  free(rot);
+  free(roots);
+}
+
+/* centered CRT reconstruction of one coefficient -> double (tests only) */
+static double crt_centered_double(const oracle_ctx *c, int level, const u64 *res) {
+  /* mixed-radix (Garner) digits, then evaluate in long double with the
+   * centered correction x - Q when x > Q/2 (decided on the top digit). */
+  int nl = level + 1;
+  u64 d[MAXMOD];
+  for (int i = 0; i < nl; i++) {
+    u64 qi = c->mod[i];
+    u64 x = res[i] % qi;
+    for (int k = 0; k < i; k++) {
+      u64 qk = c->mod[k] % qi;
+      x = mulmod(submod(x, d[k] % qi, qi), invmod(qk, qi), qi);
+    }
+    d[i] = x;
+  }
+  /* value = d0 + d1 q0 + d2 q0 q1 + ...; compare with Q/2 via the mixed-radix
+   * digits of Q-1 halved: x > Q/2  <=>  x >= ceil(Q/2).  Use long double for
+   * the magnitude, exact sign decision through digit comparison. */
+  /* half digits of (Q-1)/2 in mixed radix */
+  u64 h[MAXMOD];
+  {
+    /* (Q-1) digits are (q_i - 1); divide by 2 from the top */
+    u64 rem = 0;
+    for (int i = nl - 1; i >= 0; i--) {
+      u128 cur = (u128)rem * c->mod[i] + (c->mod[i] - 1);
+      h[i] = (u64)(cur / 2);
+      rem = (u64)(cur % 2);
+    }
+  }
+  int greater = 0;
+  for (int i = nl - 1; i >= 0; i--) {
+    if (d[i] != h[i]) {
+      greater = d[i] > h[i];
+      break;
+    }
+  }
+  long double val = 0.0L, base = 1.0L;
+  if (!greater) {
+    for (int i = 0; i < nl; i++) {
+      val += (long double)d[i] * base;
+      base *= (long double)c->mod[i];
+    }
+  } else {
+    /* Q - x with mixed radix borrow arithmetic: digits of (Q-1-x) + 1 */
+    u64 e[MAXMOD];
+    for (int i = 0; i < nl; i++) e[i] = c->mod[i] - 1 - d[i];
+    for (int i = 0; i < nl; i++) {
+      if (e[i] + 1 < c->mod[i]) {
+        e[i] += 1;
+        break;
+      }
+      e[i] = 0;
+    }
+    for (int i = 0; i < nl; i++) {
+      val += (long double)e[i] * base;
+      base *= (long double)c->mod[i];
+    }
+    val = -val;
+  }
+  return (double)val;
+}
+
+void oracle_decode(const oracle_ctx *c, int level, const u64 *pt, double scale,
+                   double *values) {
+  const int N = c->N, n = N / 2, M = 2 * N, nl = level + 1;
+  u64 *x = (u64 *)malloc(sizeof(u64) * N * nl);
+  memcpy(x, pt, sizeof(u64) * N * nl);
+  for (int j = 0; j < nl; j++) oracle_intt(c, j, x + (size_t)j * N);
+  int *rot;
+  cplx *roots;
+  special_tables(n, M, &rot, &roots);
+  cplx *v = (cplx *)calloc(n, sizeof(cplx));
+  u64 res[MAXMOD];
+  for (int i = 0; i < N; i++) {
+    for (int j = 0; j < nl; j++) res[j] = x[(size_t)j * N + i];
+    double f = crt_centered_double(c, level, res) / scale;
+    if (i < n)
+      v[i].re = f;
+    else
+      v[i - n].im = f;
+  }
+  special_fft(v, n, M, rot, roots);
+  for (int i = 0; i < n; i++) values[i] = v[i].re;
+  free(x);
+  free(v);
+  free(rot);
+  free(roots);
+}
+
+/* ------------------------------------------------------------------ */
+/* test-only keygen / encryption (seeded SplitMix64)                    */
+/* ------------------------------------------------------------------ */
+static u64 sm64(u64 *s) {
+  u64 z = (*s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static u64 uniform_mod(u64 *s, u64 q) {
+  int bits = 64 - __builtin_clzll(q);
+  u64 mask = bits == 64 ? ~0ull : (((u64)1 << bits) - 1);
+  for (;;) {
+    u64 r = sm64(s) & mask;
+    if (r < q) return r;
+  }
+}
+static int64_t gauss(u64 *s) {
+  for (;;) {
+    double u1 = ((double)(sm64(s) >> 11) + 1.0) / 9007199254740993.0;
+    double u2 = (double)(sm64(s) >> 11) / 9007199254740992.0;
+    double z = sqrt(-2.0 * log(u1)) * cos(2.0 * M_PI * u2) * 3.2;
+    if (fabs(z) <= 19.2) return (int64_t)llround(z);
+  }
+}
+static void small_to_ntt(const oracle_ctx *c, const int64_t *v, int m, u64 *out) {
+  u64 q = c->mod[m];
+  for (int n = 0; n < c->N; n++) out[n] = v[n] >= 0 ? (u64)v[n] % q : q - ((u64)(-v[n]) % q);
+  oracle_ntt(c, m, out);
+}
+
+void oracle_gen_secret(const oracle_ctx *c, u64 seed, int h, u64 *sk) {
+  const int N = c->N;
+  u64 s = seed;
+  int64_t *v = (int64_t *)calloc(N, sizeof(int64_t));
+  int *perm = (int *)malloc(sizeof(int) * N);
+  for (int i = 0; i < N; i++) perm[i] = i;
+  if (h > N) h = N;
+  for (int i = 0; i < h; i++) {
+    int j = i + (int)(sm64(&s) % (u64)(N - i));
+    int t = perm[i];
+    perm[i] = perm[j];
+    perm[j] = t;
+    v[perm[i]] = (sm64(&s) & 1) ? 1 : -1;
+  }
+  for (int m = 0; m < c->L + c->K; m++) small_to_ntt(c, v, m, sk + (size_t)m * N);
+  free(v);
+  free(perm);
+}
+
+void oracle_gen_evk(const oracle_ctx *c, u64 seed, const u64 *s_in, const u64 *s_out, u64 *evk) {
+  const int N = c->N, L = c->L, K = c->K, nm = L + K;
+  const int dnum = (L + K - 1) / K;
+  u64 s = seed;
+  int64_t *e = (int64_t *)malloc(sizeof(int64_t) * N);
+  u64 *et = (u64 *)malloc(sizeof(u64) * N);
+  for (int i = 0; i < dnum; i++) {
+    u64 *b = evk + (size_t)i * 2 * nm * N;
+    u64 *a = b + (size_t)nm * N;
+    for (int n = 0; n < N; n++) e[n] = gauss(&s);
+    for (int m = 0; m < nm; m++) {
+      u64 q = c->mod[m];
+      small_to_ntt(c, e, m, et);
+      u64 Pm = 1;
+      for (int k = 0; k < K; k++) Pm = mulmod(Pm, c->mod[L + k] % q, q);
+      int in_digit = m < L && m >= i * K && m < (i + 1) * K;
+      for (int n = 0; n < N; n++) {
+        size_t x = (size_t)m * N + n;
+        a[x] = uniform_mod(&s, q);
+        u64 v = submod(et[n], mulmod(a[x], s_out[x], q), q);
+        if (in_digit) v = addmod(v, mulmod(Pm, s_in[x], q), q);
+        b[x] = v;
+      }
+    }
+  }
+  free(e);
+  free(et);
+}
+
+void oracle_encrypt_sk(const oracle_ctx *c, u64 seed, int level, const u64 *sk, const u64 *pt,
+                       u64 *ct) {
+  const int N = c->N;
+  const size_t P = (size_t)(level + 1) * N;
+  u64 s = seed;
+  int64_t *e = (int64_t *)malloc(sizeof(int64_t) * N);
+  u64 *et = (u64 *)malloc(sizeof(u64) * N);
+  for (int n = 0; n < N; n++) e[n] = gauss(&s);
+  for (int j = 0; j <= level; j++) {
+    u64 q = c->mod[j];
+    small_to_ntt(c, e, j, et);
+    for (int n = 0; n < N; n++) {
+      size_t x = (size_t)j * N + n;
+      u64 a = uniform_mod(&s, q);
+      ct[P + x] = a;
+      ct[x] = addmod(submod(et[n], mulmod(a, sk[x], q), q), pt[x], q);
+    }
+  }
+  free(e);
+  free(et);
+}
+
+void oracle_decrypt(const oracle_ctx *c, int level, const u64 *sk, const u64 *ct, u64 *pt) {
+  const int N = c->N;
+  const size_t P = (size_t)(level + 1) * N;
+  for (int j = 0; j <= level; j++) {
+    u64 q = c->mod[j];
+    for (int n = 0; n < N; n++) {
+      size_t x = (size_t)j * N + n;
+      pt[x] = addmod(ct[x], mulmod(ct[P + x], sk[x], q), q);
+    }
+  }
+}

@@ -1,0 +1,140 @@
+/*
+ * ckks_oracle.h -- CPU restatement of the RNS-CKKS arithmetic that Orion's
+ * Lattigo backend reaches (TEST INFRASTRUCTURE ONLY).
+ *
+ * This library is the parity oracle for the HIP backend in orion_amd/.  Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ * It is never linked into liborion_hip.so and never used as a fallback.
+ *
+ * Reference call sites it restates (all under /root/reference):
+ *   orion/backend/lattigo/scheme.go:57-65     ckks.NewParametersFromLiteral (primes, NTT tables)
+ *   orion/backend/lattigo/evaluator.go:61-99  Rotate/RotateNew/Rescale/RescaleNew
+ *   orion/backend/lattigo/evaluator.go:101-294 scalar / plaintext / ciphertext add, sub, mul
+ *   orion/backend/lattigo/evaluator.go:297-317 MulRelinCiphertext(New)
+ *   orion/backend/lattigo/lineartransform.go:37-113 Generate/EvaluateLinearTransform (BSGS)
+ *   orion/backend/lattigo/encoder.go:16-42    Encode/Decode
+ * The algorithms themselves live in github.com/baahl-nyu/lattigo/v6 v6.2.0
+ * (go.mod:5), which is NOT vendored in the reference and cannot be built here
+ * (no Go toolchain).  This file restates Lattigo v6's published algorithms
+ * (SURVEY.md Appendix A).  PARITY WITH LATTIGO ITSELF IS UNPINNED: the
+ * reference holds no golden vectors for this path.  The
+ * oracle is pinned by first-principles big-integer KATs (tests/golden/).
+ *
+ * Conventions shared with the HIP backend:
+ *   - a polynomial is limb-major u64[nlimbs][N], every residue fully reduced;
+ *   - NTT domain = Lattigo's: natural-order input, bit-reversed output,
+ *     out[j] = a(psi^(2*brv(j)+1)) mod q, psi = g^((q-1)/2N), g the smallest
+ *     primitive root of q;
+ *   - QP moduli array = [q_0 .. q_{L-1}, p_0 .. p_{K-1}].
+ */
+#ifndef CKKS_ORACLE_H
+#define CKKS_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_ctx oracle_ctx;
+
+/* Prime chain generation (Lattigo ckks GenModuli restated).
+ * out must hold lenQ+lenP entries.  Returns 0 on success. */
+int oracle_gen_moduli(int logN, const int *logQ, int lenQ, const int *logP,
+                      int lenP, uint64_t *out);
+
+oracle_ctx *oracle_new(int logN, const uint64_t *moduli, int L, int K);
+void oracle_free(oracle_ctx *ctx);
+int oracle_N(const oracle_ctx *ctx);
+
+/* NTT tables (for KATs): psi of modulus m, and the bit-reversed root table. */
+uint64_t oracle_psi(const oracle_ctx *ctx, int m);
+uint64_t oracle_primitive_root(uint64_t q);
+
+/* In-place NTT / INTT of one limb under modulus index m. */
+void oracle_ntt(const oracle_ctx *ctx, int m, uint64_t *a);
+void oracle_intt(const oracle_ctx *ctx, int m, uint64_t *a);
+
+/* Exact basis extension (Lattigo ModUpExact): x holds ns coefficient-domain
+ * limbs (moduli src[0..ns)); writes nt limbs (moduli dst[0..nt)) to out. */
+void oracle_basis_extend(const oracle_ctx *ctx, const uint64_t *x,
+                         const int *src, int ns, uint64_t *out,
+                         const int *dst, int nt);
+
+/* Rescale (DivRoundByLastModulusNTT): ct has ncomp components, each
+ * [level+1][N] (NTT).  out gets [level][N] per component. */
+void oracle_rescale(const oracle_ctx *ctx, int level, int ncomp,
+                    const uint64_t *ct, uint64_t *out);
+
+/* ModDown QP->Q of one poly: x is [level+1 + K][N] (Q limbs then P limbs,
+ * NTT).  out is [level+1][N] = floor(x / P). */
+void oracle_moddown(const oracle_ctx *ctx, int level, const uint64_t *x,
+                    uint64_t *out);
+
+/* Hybrid gadget product, lazy (no ModDown).  c: [level+1][N] NTT.
+ * evk: [dnum][2][L+K][N] (NTT), dnum = ceil(L/K).
+ * out0/out1: [level+1+K][N] in QP. */
+void oracle_gadget_product_lazy(const oracle_ctx *ctx, int level,
+                                const uint64_t *c, const uint64_t *evk,
+                                uint64_t *out0, uint64_t *out1);
+/* Same, followed by ModDown -> out0/out1 [level+1][N]. */
+void oracle_keyswitch(const oracle_ctx *ctx, int level, const uint64_t *c,
+                      const uint64_t *evk, uint64_t *out0, uint64_t *out1);
+
+/* Galois element for a rotation by k slots (Standard ring): 5^k mod 2N. */
+uint64_t oracle_galois_element(const oracle_ctx *ctx, int k);
+/* NTT-domain automorphism: out[j] = in[index_g[j]] for nlimbs limbs. */
+void oracle_automorphism_ntt(const oracle_ctx *ctx, uint64_t galEl,
+                             const uint64_t *in, uint64_t *out, int nlimbs);
+
+/* ct x ct with relinearisation (tensor + gadget product with rlk). a, b, out
+ * are [2][level+1][N].  rlk layout as evk. */
+void oracle_mul_relin(const oracle_ctx *ctx, int level, const uint64_t *a,
+                      const uint64_t *b, const uint64_t *rlk, uint64_t *out);
+/* Rotation: keyswitch c1 with gk, add c0, then automorphism. */
+void oracle_rotate(const oracle_ctx *ctx, int level, const uint64_t *ct,
+                   uint64_t galEl, const uint64_t *gk, uint64_t *out);
+
+/* BSGS linear transform (lintrans MultiplyByDiagMatrixBSGS restated).
+ *   ndiag diagonals, diag_idx[d] in [0, slots), pts[d] = [level+1+K][N]
+ *   pre-rotated QP plaintexts (NTT), N1 baby-step size.
+ *   gk_for(galEl) resolved through the (galEls, gks) table of ngk keys.
+ * out: [2][level+1][N]. */
+void oracle_lt_bsgs(const oracle_ctx *ctx, int level, const uint64_t *ct,
+                    int ndiag, const int *diag_idx, const uint64_t *const *pts,
+                    int N1, int ngk, const uint64_t *galEls,
+                    const uint64_t *const *gks, uint64_t *out);
+/* Lattigo FindBestBSGSRatio / BSGSIndex helpers. */
+int oracle_find_best_bsgs_n1(const int *diag_idx, int ndiag, int slots,
+                             int logMaxRatio);
+
+/* ---- encoder (Standard ring, slots = N/2) ---- */
+/* values: nvals <= N/2 reals (zero padded).  Encodes at scale into the limbs
+ * listed in mods (NTT domain). */
+void oracle_encode(const oracle_ctx *ctx, const double *values, int nvals,
+                   double scale, const int *mods, int nmods, uint64_t *out);
+/* Decode a [level+1][N] NTT plaintext at scale: writes N/2 reals. */
+void oracle_decode(const oracle_ctx *ctx, int level, const uint64_t *pt,
+                   double scale, double *values);
+
+/* ---- test-only key generation (seeded, NOT the product keygen) ---- */
+/* sk: [L+K][N] NTT ternary secret with Hamming weight h. */
+void oracle_gen_secret(const oracle_ctx *ctx, uint64_t seed, int h,
+                       uint64_t *sk);
+/* evk switching s_in -> s_out: [dnum][2][L+K][N]. */
+void oracle_gen_evk(const oracle_ctx *ctx, uint64_t seed, const uint64_t *s_in,
+                    const uint64_t *s_out, uint64_t *evk);
+/* Encrypt (secret key) a [level+1][N] NTT plaintext. */
+void oracle_encrypt_sk(const oracle_ctx *ctx, uint64_t seed, int level,
+                       const uint64_t *sk, const uint64_t *pt, uint64_t *ct);
+void oracle_decrypt(const oracle_ctx *ctx, int level, const uint64_t *sk,
+                    const uint64_t *ct, uint64_t *pt);
+
+/* coefficient-wise helpers used by tests */
+void oracle_mul_coeffs(const oracle_ctx *ctx, const int *mods, int nl,
+                       const uint64_t *a, const uint64_t *b, uint64_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

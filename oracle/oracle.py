@@ -1,0 +1,249 @@
+"""ctypes wrapper of the CPU parity oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module.  The product path (orion_amd/) never does.
+
+Restates Lattigo-v6 RNS-CKKS arithmetic reached from
+/root/reference/orion/backend/lattigo/*.go (see ckks_oracle.h for the
+function-by-function citations).  Parity with Lattigo itself is unpinned.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libckks_oracle.so")
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_intp = ctypes.POINTER(ctypes.c_int)
+_dblp = ctypes.POINTER(ctypes.c_double)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def _load():
+    if not os.path.exists(_LIB_PATH):
+        build()
+    lib = ctypes.CDLL(_LIB_PATH)
+    vp = ctypes.c_void_p
+    sig = {
+        "oracle_gen_moduli": (ctypes.c_int, [ctypes.c_int, _intp, ctypes.c_int, _intp, ctypes.c_int, _u64p]),
+        "oracle_new": (vp, [ctypes.c_int, _u64p, ctypes.c_int, ctypes.c_int]),
+        "oracle_free": (None, [vp]),
+        "oracle_psi": (ctypes.c_uint64, [vp, ctypes.c_int]),
+        "oracle_primitive_root": (ctypes.c_uint64, [ctypes.c_uint64]),
+        "oracle_ntt": (None, [vp, ctypes.c_int, _u64p]),
+        "oracle_intt": (None, [vp, ctypes.c_int, _u64p]),
+        "oracle_basis_extend": (None, [vp, _u64p, _intp, ctypes.c_int, _u64p, _intp, ctypes.c_int]),
+        "oracle_rescale": (None, [vp, ctypes.c_int, ctypes.c_int, _u64p, _u64p]),
+        "oracle_moddown": (None, [vp, ctypes.c_int, _u64p, _u64p]),
+        "oracle_gadget_product_lazy": (None, [vp, ctypes.c_int, _u64p, _u64p, _u64p, _u64p]),
+        "oracle_keyswitch": (None, [vp, ctypes.c_int, _u64p, _u64p, _u64p, _u64p]),
+        "oracle_galois_element": (ctypes.c_uint64, [vp, ctypes.c_int]),
+        "oracle_automorphism_ntt": (None, [vp, ctypes.c_uint64, _u64p, _u64p, ctypes.c_int]),
+        "oracle_mul_relin": (None, [vp, ctypes.c_int, _u64p, _u64p, _u64p, _u64p]),
+        "oracle_rotate": (None, [vp, ctypes.c_int, _u64p, ctypes.c_uint64, _u64p, _u64p]),
+        "oracle_lt_bsgs": (None, [vp, ctypes.c_int, _u64p, ctypes.c_int, _intp,
+                                  ctypes.POINTER(_u64p), ctypes.c_int, ctypes.c_int, _u64p,
+                                  ctypes.POINTER(_u64p), _u64p]),
+        "oracle_find_best_bsgs_n1": (ctypes.c_int, [_intp, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+        "oracle_encode": (None, [vp, _dblp, ctypes.c_int, ctypes.c_double, _intp, ctypes.c_int, _u64p]),
+        "oracle_decode": (None, [vp, ctypes.c_int, _u64p, ctypes.c_double, _dblp]),
+        "oracle_gen_secret": (None, [vp, ctypes.c_uint64, ctypes.c_int, _u64p]),
+        "oracle_gen_evk": (None, [vp, ctypes.c_uint64, _u64p, _u64p, _u64p]),
+        "oracle_encrypt_sk": (None, [vp, ctypes.c_uint64, ctypes.c_int, _u64p, _u64p, _u64p]),
+        "oracle_decrypt": (None, [vp, ctypes.c_int, _u64p, _u64p, _u64p]),
+        "oracle_mul_coeffs": (None, [vp, _intp, ctypes.c_int, _u64p, _u64p, _u64p]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = _load()
+    return _lib
+
+
+def _p(a):
+    assert a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"], (a.dtype, a.flags)
+    return a.ctypes.data_as(_u64p)
+
+
+def _ip(lst):
+    arr = (ctypes.c_int * max(1, len(lst)))(*lst)
+    return arr
+
+
+def gen_moduli(logN, logQ, logP):
+    out = np.zeros(len(logQ) + len(logP), dtype=np.uint64)
+    rc = lib().oracle_gen_moduli(logN, _ip(logQ), len(logQ), _ip(logP), len(logP), _p(out))
+    if rc != 0:
+        raise ValueError("prime generation exhausted")
+    return [int(x) for x in out]
+
+
+class Oracle:
+    """One parameter set.  Arrays are numpy uint64, limb-major [limbs][N]."""
+
+    def __init__(self, logN, moduli, L, K):
+        self.logN, self.N, self.L, self.K = logN, 1 << logN, L, K
+        self.moduli = [int(m) for m in moduli]
+        arr = np.array(self.moduli, dtype=np.uint64)
+        self._h = lib().oracle_new(logN, _p(arr), L, K)
+        self.dnum = (L + K - 1) // K
+
+    @classmethod
+    def from_logs(cls, logN, logQ, logP):
+        return cls(logN, gen_moduli(logN, logQ, logP), len(logQ), len(logP))
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.oracle_free(self._h)
+            self._h = None
+
+    # -- single limb ------------------------------------------------------
+    def ntt(self, m, a):
+        a = np.ascontiguousarray(a, dtype=np.uint64).copy()
+        lib().oracle_ntt(self._h, m, _p(a))
+        return a
+
+    def intt(self, m, a):
+        a = np.ascontiguousarray(a, dtype=np.uint64).copy()
+        lib().oracle_intt(self._h, m, _p(a))
+        return a
+
+    def psi(self, m):
+        return int(lib().oracle_psi(self._h, m))
+
+    def qp_mods(self, level):
+        return list(range(level + 1)) + [self.L + k for k in range(self.K)]
+
+    # -- polynomial ops ---------------------------------------------------
+    def basis_extend(self, x, src, dst):
+        x = np.ascontiguousarray(x, dtype=np.uint64)
+        out = np.zeros((len(dst), self.N), dtype=np.uint64)
+        lib().oracle_basis_extend(self._h, _p(x), _ip(src), len(src), _p(out), _ip(dst), len(dst))
+        return out
+
+    def rescale(self, ct, level):
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        ncomp = ct.shape[0]
+        out = np.zeros((ncomp, level, self.N), dtype=np.uint64)
+        lib().oracle_rescale(self._h, level, ncomp, _p(ct), _p(out))
+        return out
+
+    def moddown(self, x, level):
+        x = np.ascontiguousarray(x, dtype=np.uint64)
+        out = np.zeros((level + 1, self.N), dtype=np.uint64)
+        lib().oracle_moddown(self._h, level, _p(x), _p(out))
+        return out
+
+    def gadget_product_lazy(self, c, evk, level):
+        c = np.ascontiguousarray(c, dtype=np.uint64)
+        evk = np.ascontiguousarray(evk, dtype=np.uint64)
+        o0 = np.zeros((level + 1 + self.K, self.N), dtype=np.uint64)
+        o1 = np.zeros_like(o0)
+        lib().oracle_gadget_product_lazy(self._h, level, _p(c), _p(evk), _p(o0), _p(o1))
+        return o0, o1
+
+    def keyswitch(self, c, evk, level):
+        c = np.ascontiguousarray(c, dtype=np.uint64)
+        evk = np.ascontiguousarray(evk, dtype=np.uint64)
+        o0 = np.zeros((level + 1, self.N), dtype=np.uint64)
+        o1 = np.zeros_like(o0)
+        lib().oracle_keyswitch(self._h, level, _p(c), _p(evk), _p(o0), _p(o1))
+        return o0, o1
+
+    def galois_element(self, k):
+        return int(lib().oracle_galois_element(self._h, k))
+
+    def automorphism_ntt(self, x, galEl):
+        x = np.ascontiguousarray(x, dtype=np.uint64)
+        out = np.zeros_like(x)
+        lib().oracle_automorphism_ntt(self._h, galEl, _p(x), _p(out), x.shape[0])
+        return out
+
+    def mul_relin(self, a, b, rlk, level):
+        a = np.ascontiguousarray(a, dtype=np.uint64)
+        b = np.ascontiguousarray(b, dtype=np.uint64)
+        out = np.zeros((2, level + 1, self.N), dtype=np.uint64)
+        lib().oracle_mul_relin(self._h, level, _p(a), _p(b), _p(np.ascontiguousarray(rlk)), _p(out))
+        return out
+
+    def rotate(self, ct, galEl, gk, level):
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        out = np.zeros((2, level + 1, self.N), dtype=np.uint64)
+        lib().oracle_rotate(self._h, level, _p(ct), galEl, _p(np.ascontiguousarray(gk)), _p(out))
+        return out
+
+    def lt_bsgs(self, ct, level, diag_idx, pts, N1, gkeys):
+        """gkeys: dict galEl -> evk array."""
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        out = np.zeros((2, level + 1, self.N), dtype=np.uint64)
+        pts = [np.ascontiguousarray(p, dtype=np.uint64) for p in pts]
+        ptarr = (_u64p * len(pts))(*[_p(p) for p in pts])
+        gels = list(gkeys.keys())
+        garr = np.array(gels if gels else [0], dtype=np.uint64)
+        karrs = [np.ascontiguousarray(gkeys[g]) for g in gels]
+        karr = (_u64p * max(1, len(karrs)))(*[_p(k) for k in karrs])
+        lib().oracle_lt_bsgs(self._h, level, _p(ct), len(diag_idx), _ip(diag_idx), ptarr, N1,
+                             len(gels), _p(garr), karr, _p(out))
+        return out
+
+    def find_best_bsgs_n1(self, diag_idx, log_ratio=0):
+        return int(lib().oracle_find_best_bsgs_n1(_ip(diag_idx), len(diag_idx), self.N // 2, log_ratio))
+
+    def encode(self, values, scale, mods):
+        v = np.ascontiguousarray(values, dtype=np.float64)
+        out = np.zeros((len(mods), self.N), dtype=np.uint64)
+        lib().oracle_encode(self._h, v.ctypes.data_as(_dblp), len(v), float(scale), _ip(mods),
+                            len(mods), _p(out))
+        return out
+
+    def decode(self, pt, level, scale):
+        pt = np.ascontiguousarray(pt, dtype=np.uint64)
+        out = np.zeros(self.N // 2, dtype=np.float64)
+        lib().oracle_decode(self._h, level, _p(pt), float(scale), out.ctypes.data_as(_dblp))
+        return out
+
+    def gen_secret(self, seed, h):
+        sk = np.zeros((self.L + self.K, self.N), dtype=np.uint64)
+        lib().oracle_gen_secret(self._h, seed, h, _p(sk))
+        return sk
+
+    def gen_evk(self, seed, s_in, s_out):
+        evk = np.zeros((self.dnum, 2, self.L + self.K, self.N), dtype=np.uint64)
+        lib().oracle_gen_evk(self._h, seed, _p(np.ascontiguousarray(s_in)),
+                             _p(np.ascontiguousarray(s_out)), _p(evk))
+        return evk
+
+    def encrypt_sk(self, seed, sk, pt, level):
+        ct = np.zeros((2, level + 1, self.N), dtype=np.uint64)
+        lib().oracle_encrypt_sk(self._h, seed, level, _p(np.ascontiguousarray(sk)),
+                                _p(np.ascontiguousarray(pt)), _p(ct))
+        return ct
+
+    def decrypt(self, ct, sk, level):
+        pt = np.zeros((level + 1, self.N), dtype=np.uint64)
+        lib().oracle_decrypt(self._h, level, _p(np.ascontiguousarray(sk)),
+                             _p(np.ascontiguousarray(ct)), _p(pt))
+        return pt
+
+    def mul_coeffs(self, a, b, mods):
+        a = np.ascontiguousarray(a, dtype=np.uint64)
+        b = np.ascontiguousarray(b, dtype=np.uint64)
+        out = np.zeros_like(a)
+        lib().oracle_mul_coeffs(self._h, _ip(mods), len(mods), _p(a), _p(b), _p(out))
+        return out

@@ -1,0 +1,358 @@
+"""Python binding of liborion_hip.so -- the MI355X backend behind Orion's
+backend-plugin API.
+
+`HipLibrary` mirrors the reference's `LattigoLibrary`
+(/root/reference/orion/backend/lattigo/bindings.py:94-746): same method names,
+argument meaning (handles are ints, scalars/diagonals cross as C float,
+scales as unsigned long) and list conversions, so Orion's L1 wrappers
+(orion/backend/python/*.py) can drive it unchanged.  A maintainer selects it
+in `Scheme.setup_backend` (orion/core/orion.py:90-106) -- see INTEGRATION.md.
+
+Error behaviour: the library never aborts; failed calls raise RuntimeError
+with the library's message (Lattigo would panic and abort the process).
+
+This module never falls back to a CPU implementation: if the HIP extension
+cannot be loaded, or no GPU is visible when the scheme is created, it raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liborion_hip.so")
+
+c_int, c_float, c_ulong, c_double, c_char_p, c_void_p = (
+    ctypes.c_int, ctypes.c_float, ctypes.c_ulong, ctypes.c_double, ctypes.c_char_p, ctypes.c_void_p)
+P = ctypes.POINTER
+
+
+class ArrayResultInt(ctypes.Structure):
+    _fields_ = [("Data", P(ctypes.c_int)), ("Length", ctypes.c_ulong)]
+
+
+class ArrayResultFloat(ctypes.Structure):
+    _fields_ = [("Data", P(ctypes.c_float)), ("Length", ctypes.c_ulong)]
+
+
+class ArrayResultDouble(ctypes.Structure):
+    _fields_ = [("Data", P(ctypes.c_double)), ("Length", ctypes.c_ulong)]
+
+
+class ArrayResultUInt64(ctypes.Structure):
+    _fields_ = [("Data", P(ctypes.c_ulong)), ("Length", ctypes.c_ulong)]
+
+
+class ArrayResultByte(ctypes.Structure):
+    _fields_ = [("Data", P(ctypes.c_ubyte)), ("Length", ctypes.c_ulong)]
+
+
+# name -> (argtypes, restype); the Lattigo-compatible set first
+SIGNATURES = {
+    "NewScheme": ([c_int, P(c_int), c_int, P(c_int), c_int, c_int, c_int, c_char_p, c_char_p, c_char_p], None),
+    "DeleteScheme": ([], None),
+    "FreeCArray": ([c_void_p], None),
+    "DeletePlaintext": ([c_int], None),
+    "DeleteCiphertext": ([c_int], None),
+    "GetPlaintextScale": ([c_int], c_ulong),
+    "GetCiphertextScale": ([c_int], c_ulong),
+    "SetPlaintextScale": ([c_int, c_ulong], None),
+    "SetCiphertextScale": ([c_int, c_ulong], None),
+    "GetPlaintextLevel": ([c_int], c_int),
+    "GetCiphertextLevel": ([c_int], c_int),
+    "GetPlaintextSlots": ([c_int], c_int),
+    "GetCiphertextSlots": ([c_int], c_int),
+    "GetCiphertextDegree": ([c_int], c_int),
+    "GetModuliChain": ([], ArrayResultUInt64),
+    "GetLivePlaintexts": ([], ArrayResultInt),
+    "GetLiveCiphertexts": ([], ArrayResultInt),
+    "CloneCiphertext": ([c_int], c_int),
+    "NewKeyGenerator": ([], None),
+    "GenerateSecretKey": ([], None),
+    "GeneratePublicKey": ([], None),
+    "GenerateRelinearizationKey": ([], None),
+    "GenerateEvaluationKeys": ([], None),
+    "SerializeSecretKey": ([], ArrayResultByte),
+    "LoadSecretKey": ([P(ctypes.c_ubyte), c_ulong], None),
+    "NewEncoder": ([], None),
+    "Encode": ([P(c_float), c_int, c_int, c_ulong], c_int),
+    "Decode": ([c_int], ArrayResultFloat),
+    "NewEncryptor": ([], None),
+    "NewDecryptor": ([], None),
+    "Encrypt": ([c_int], c_int),
+    "Decrypt": ([c_int], c_int),
+    "NewEvaluator": ([], None),
+    "AddRotationKey": ([c_int], None),
+    "Negate": ([c_int], c_int),
+    "Rotate": ([c_int, c_int], c_int),
+    "RotateNew": ([c_int, c_int], c_int),
+    "Rescale": ([c_int], c_int),
+    "RescaleNew": ([c_int], c_int),
+    "AddScalar": ([c_int, c_float], c_int),
+    "AddScalarNew": ([c_int, c_float], c_int),
+    "SubScalar": ([c_int, c_float], c_int),
+    "SubScalarNew": ([c_int, c_float], c_int),
+    "MulScalarInt": ([c_int, c_int], c_int),
+    "MulScalarIntNew": ([c_int, c_int], c_int),
+    "MulScalarFloat": ([c_int, c_float], c_int),
+    "MulScalarFloatNew": ([c_int, c_float], c_int),
+    "AddPlaintext": ([c_int, c_int], c_int),
+    "AddPlaintextNew": ([c_int, c_int], c_int),
+    "SubPlaintext": ([c_int, c_int], c_int),
+    "SubPlaintextNew": ([c_int, c_int], c_int),
+    "MulPlaintext": ([c_int, c_int], c_int),
+    "MulPlaintextNew": ([c_int, c_int], c_int),
+    "AddCiphertext": ([c_int, c_int], c_int),
+    "AddCiphertextNew": ([c_int, c_int], c_int),
+    "SubCiphertext": ([c_int, c_int], c_int),
+    "SubCiphertextNew": ([c_int, c_int], c_int),
+    "MulRelinCiphertext": ([c_int, c_int], c_int),
+    "MulRelinCiphertextNew": ([c_int, c_int], c_int),
+    "NewPolynomialEvaluator": ([], None),
+    "GenerateMonomial": ([P(c_float), c_int], c_int),
+    "GenerateChebyshev": ([P(c_float), c_int], c_int),
+    "EvaluatePolynomial": ([c_int, c_int, c_ulong], c_int),
+    "GenerateMinimaxSignCoeffs": ([P(c_int), c_int, c_int, c_int, c_int, c_int], ArrayResultDouble),
+    "NewLinearTransformEvaluator": ([], None),
+    "GenerateLinearTransform": ([P(c_int), c_int, P(c_float), c_int, c_int, c_float, c_char_p], c_int),
+    "EvaluateLinearTransform": ([c_int, c_int], c_int),
+    "DeleteLinearTransform": ([c_int], None),
+    "GetLinearTransformRotationKeys": ([c_int], ArrayResultInt),
+    "GenerateLinearTransformRotationKey": ([c_int], None),
+    "GenerateConsolidatedRotationKeys": ([P(c_int), c_int], None),
+    "GenerateAndSerializeRotationKey": ([c_int], ArrayResultByte),
+    "LoadRotationKey": ([P(ctypes.c_ubyte), c_ulong, c_ulong], None),
+    "SerializeDiagonal": ([c_int, c_int], ArrayResultByte),
+    "LoadPlaintextDiagonal": ([P(ctypes.c_ubyte), c_ulong, c_int, c_ulong], None),
+    "RemovePlaintextDiagonals": ([c_int], None),
+    "RemoveRotationKeys": ([], None),
+    "NewBootstrapper": ([P(c_int), c_int, c_int], None),
+    "Bootstrap": ([c_int, c_int], c_int),
+    "DeleteBootstrappers": ([], None),
+    # ---- MI355X extensions ----
+    "OrionHipLastError": ([], c_char_p),
+    "OrionHipClearError": ([], None),
+    "OrionHipSetDevice": ([c_int], c_int),
+    "OrionHipSetSeed": ([c_ulong], None),
+    "OrionHipSetStream": ([c_void_p], None),
+    "OrionHipGetStream": ([], c_void_p),
+    "OrionHipSynchronize": ([], c_int),
+    "OrionHipLogN": ([], c_int),
+    "OrionHipNumQ": ([], c_int),
+    "OrionHipNumP": ([], c_int),
+    "OrionHipModulus": ([c_int], c_ulong),
+    "EncodeBatch": ([P(c_float), c_int, c_int, c_int, c_ulong], c_int),
+    "GetCiphertextBatch": ([c_int], c_int),
+    "GetPlaintextBatch": ([c_int], c_int),
+    "GetCiphertextScaleF": ([c_int], c_double),
+    "ImportCiphertext": ([P(c_ulong), c_int, c_int, c_double], c_int),
+    "ExportCiphertext": ([c_int, P(c_ulong), c_ulong], c_int),
+    "ImportPlaintext": ([P(c_ulong), c_int, c_int, c_double], c_int),
+    "ExportPlaintext": ([c_int, P(c_ulong), c_ulong], c_int),
+    "ExportSecretKey": ([P(c_ulong), c_ulong], c_int),
+    "ExportRelinKey": ([P(c_ulong), c_ulong], c_int),
+    "ExportGaloisKey": ([c_ulong, P(c_ulong), c_ulong], c_int),
+    "ExportLinearTransformDiagonal": ([c_int, c_int, P(c_ulong), c_ulong], c_int),
+    "GetLinearTransformN1": ([c_int], c_int),
+    "GaloisElement": ([c_int], c_ulong),
+    "KeyBundleBytes": ([c_int], c_ulong),
+    "ExportKeyBundle": ([c_void_p, c_int], c_int),
+    "ImportKeyBundle": ([c_void_p, c_ulong], c_int),
+    "OrionHipProfile": ([c_int], None),
+    "OrionHipProfileRead": ([c_char_p, P(ctypes.c_long), P(c_double), P(c_double), c_int], c_int),
+    "OrionHipProfileReset": ([], None),
+    "OrionHipNTT": ([P(c_ulong), c_int, c_int, P(c_int), c_int], c_int),
+}
+
+# the symbols a binding of the reference's Lattigo backend resolves (bindings.py:141-746 + fork extras)
+LATTIGO_SYMBOLS = [n for n in SIGNATURES if not n.startswith("OrionHip") and n not in (
+    "EncodeBatch", "GetCiphertextBatch", "GetPlaintextBatch", "GetCiphertextScaleF", "ImportCiphertext",
+    "ExportCiphertext", "ImportPlaintext", "ExportPlaintext", "ExportSecretKey", "ExportRelinKey",
+    "ExportGaloisKey", "ExportLinearTransformDiagonal", "GetLinearTransformN1", "GaloisElement",
+    "KeyBundleBytes", "ExportKeyBundle", "ImportKeyBundle")]
+
+
+def load_library(path=LIB_PATH):
+    """Load liborion_hip.so and declare every symbol; raises if missing."""
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"HIP backend library not found at {path}: build it with "
+            "`python orion_amd/build.py` (no CPU fallback exists)")
+    lib = ctypes.CDLL(path)
+    for name, (args, res) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+    return lib
+
+
+class HipFunction:
+    """Mirror of LattigoFunction (bindings.py:10-66): converts Python lists to
+    C arrays (floats -> C float), ArrayResult structs to lists (freed with
+    FreeCArray), and raises on library errors."""
+
+    def __init__(self, lib, name):
+        self.lib = lib
+        self.name = name
+        self.func = getattr(lib, name)
+        self.argtypes = self.func.argtypes or []
+
+    def _convert(self, arg, typ):
+        if isinstance(arg, bool):
+            arg = int(arg)
+        if isinstance(arg, (int, np.integer)) and typ in (c_int, c_ulong, c_float):
+            return typ(float(arg)) if typ is c_float else typ(int(arg))
+        if isinstance(arg, (float, np.floating)):
+            return c_float(float(arg)) if typ is c_float else typ(arg)
+        if isinstance(arg, str):
+            return arg.encode("utf-8")
+        if isinstance(arg, np.ndarray) and arg.dtype == np.uint8:
+            arg = np.ascontiguousarray(arg)
+            return (arg.ctypes.data_as(P(ctypes.c_ubyte)), len(arg))
+        if isinstance(arg, (list, tuple, np.ndarray)):
+            if typ == P(c_int):
+                return ((c_int * len(arg))(*[int(x) for x in arg]), len(arg))
+            if typ == P(c_float):
+                a = np.ascontiguousarray(arg, dtype=np.float32)
+                return (a.ctypes.data_as(P(c_float)), len(a), a)
+            if typ == P(c_ulong):
+                return ((c_ulong * len(arg))(*[int(x) for x in arg]), len(arg))
+            raise ValueError(f"{self.name}: unexpected list argument for {typ}")
+        return arg
+
+    def __call__(self, *args):
+        c_args, keep = [], []
+        for arg in args:
+            typ = self.argtypes[len(c_args)] if len(c_args) < len(self.argtypes) else None
+            c = self._convert(arg, typ)
+            if isinstance(c, tuple):
+                c_args.extend(c[:2])
+                keep.append(c)
+            else:
+                c_args.append(c)
+        self.lib.OrionHipClearError()
+        res = self.func(*c_args)
+        err = self.lib.OrionHipLastError()
+        if err:
+            raise RuntimeError(f"{self.name}: {err.decode()}")
+        if isinstance(res, (ArrayResultFloat, ArrayResultDouble)):
+            out = [float(res.Data[i]) for i in range(res.Length)]
+            self.lib.FreeCArray(ctypes.cast(res.Data, c_void_p))
+            return out
+        if isinstance(res, (ArrayResultInt, ArrayResultUInt64)):
+            out = [int(res.Data[i]) for i in range(res.Length)]
+            self.lib.FreeCArray(ctypes.cast(res.Data, c_void_p))
+            return out
+        if isinstance(res, ArrayResultByte):
+            buf = ctypes.cast(res.Data, P(ctypes.c_ubyte * res.Length)).contents if res.Length else b""
+            arr = np.frombuffer(bytes(buf), dtype=np.uint8).copy()
+            self.lib.FreeCArray(ctypes.cast(res.Data, c_void_p))
+            return arr, None
+        return res
+
+
+class HipLibrary:
+    """Drop-in replacement for LattigoLibrary (bindings.py:94-139)."""
+
+    def __init__(self, path=LIB_PATH):
+        self.lib = load_library(path)
+        for name in SIGNATURES:
+            setattr(self, name, HipFunction(self.lib, name))
+
+    def setup_bindings(self, orion_params):
+        """Same flow as LattigoLibrary.setup_bindings -> NewScheme (bindings.py:126-179)."""
+        self.NewScheme(
+            orion_params.get_logn(), orion_params.get_logq(), orion_params.get_logp(),
+            orion_params.get_logscale(), orion_params.get_hamming_weight(), orion_params.get_ringtype(),
+            orion_params.get_keys_path(), orion_params.get_io_mode())
+
+    # ---- numpy helpers for tests / bench (extension API) ----------------
+    def new_scheme(self, logn, logq, logp, logscale=None, h=192, ringtype="standard", seed=None, device=None):
+        if device is not None:
+            if self.OrionHipSetDevice(device) != 0:
+                raise RuntimeError("OrionHipSetDevice failed")
+        if seed is not None:
+            self.OrionHipSetSeed(seed)
+        self.NewScheme(logn, list(logq), list(logp), logscale or logq[-1], h, ringtype, "", "none")
+        self.N = 1 << logn
+        self.L, self.K = len(logq), len(logp)
+        return self
+
+    def moduli(self):
+        return [int(self.OrionHipModulus(i)) for i in range(self.L + self.K)]
+
+    def export_ciphertext(self, ct):
+        B, lvl = self.GetCiphertextBatch(ct), self.GetCiphertextLevel(ct)
+        out = np.zeros((B, 2, lvl + 1, self.N), dtype=np.uint64)
+        self._chk(self.lib.ExportCiphertext(ct, out.ctypes.data_as(P(c_ulong)), out.size), "ExportCiphertext")
+        return out
+
+    def import_ciphertext(self, arr, scale):
+        arr = np.ascontiguousarray(arr, dtype=np.uint64)
+        if arr.ndim == 3:
+            arr = arr[None]
+        B, _, nl, _ = arr.shape
+        h = self.lib.ImportCiphertext(arr.ctypes.data_as(P(c_ulong)), B, nl - 1, float(scale))
+        return self._chk(h, "ImportCiphertext")
+
+    def export_plaintext(self, pt):
+        B = self.GetPlaintextBatch(pt)
+        lvl = self.GetPlaintextLevel(pt)
+        out = np.zeros((B, lvl + 1, self.N), dtype=np.uint64)
+        self._chk(self.lib.ExportPlaintext(pt, out.ctypes.data_as(P(c_ulong)), out.size), "ExportPlaintext")
+        return out
+
+    def import_plaintext(self, arr, scale):
+        arr = np.ascontiguousarray(arr, dtype=np.uint64)
+        if arr.ndim == 2:
+            arr = arr[None]
+        B, nl, _ = arr.shape
+        return self._chk(self.lib.ImportPlaintext(arr.ctypes.data_as(P(c_ulong)), B, nl - 1, float(scale)),
+                         "ImportPlaintext")
+
+    def export_secret_key(self):
+        out = np.zeros((self.L + self.K, self.N), dtype=np.uint64)
+        self._chk(self.lib.ExportSecretKey(out.ctypes.data_as(P(c_ulong)), out.size), "ExportSecretKey")
+        return out
+
+    def _evk_shape(self):
+        return ((self.L + self.K - 1) // self.K, 2, self.L + self.K, self.N)
+
+    def export_relin_key(self):
+        out = np.zeros(self._evk_shape(), dtype=np.uint64)
+        self._chk(self.lib.ExportRelinKey(out.ctypes.data_as(P(c_ulong)), out.size), "ExportRelinKey")
+        return out
+
+    def export_galois_key(self, galEl):
+        out = np.zeros(self._evk_shape(), dtype=np.uint64)
+        self._chk(self.lib.ExportGaloisKey(galEl, out.ctypes.data_as(P(c_ulong)), out.size), "ExportGaloisKey")
+        return out
+
+    def export_lt_diagonal(self, lt, idx, level):
+        out = np.zeros((level + 1 + self.K, self.N), dtype=np.uint64)
+        self._chk(self.lib.ExportLinearTransformDiagonal(lt, idx, out.ctypes.data_as(P(c_ulong)), out.size),
+                  "ExportLinearTransformDiagonal")
+        return out
+
+    def encode_batch(self, values, level, scale):
+        v = np.ascontiguousarray(values, dtype=np.float32)
+        B, n = v.shape
+        return self._chk(self.lib.EncodeBatch(v.ctypes.data_as(P(c_float)), n, B, level, int(scale)), "EncodeBatch")
+
+    def profile_read(self):
+        n = 16
+        names = ctypes.create_string_buffer(32 * n)
+        launches = (ctypes.c_long * n)()
+        ms = (c_double * n)()
+        byts = (c_double * n)()
+        k = self.lib.OrionHipProfileRead(names, launches, ms, byts, n)
+        out = {}
+        for i in range(max(k, 0)):
+            nm = names.raw[32 * i:32 * i + 32].split(b"\0")[0].decode()
+            out[nm] = dict(launches=int(launches[i]), ms=float(ms[i]), bytes=float(byts[i]))
+        return out
+
+    def _chk(self, rc, name):
+        if rc is None or (isinstance(rc, int) and rc < 0):
+            raise RuntimeError(f"{name}: {self.lib.OrionHipLastError().decode()}")
+        return rc

@@ -1,0 +1,56 @@
+"""Build liborion_hip.so in-tree for gfx950 (hipcc, no JIT cache)."""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "liborion_hip.so")
+ARCH = os.environ.get("ORION_HIP_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# -ffp-contract=off: the float64 quotient of the exact basis extension and the
+# encoder FFT must round exactly as written (bit parity with the CPU oracle).
+FLAGS = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result"]
+SOURCES = ["ntt.hip", "kernels.hip", "backend.hip", "hostmath.cpp"]
+
+
+def _needs(obj, deps):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose=False):
+    os.makedirs(BUILD, exist_ok=True)
+    headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
+    headers.append(os.path.join(HERE, "..", "include", "orion_hip.h"))
+    objs, jobs = [], []
+    for src in SOURCES:
+        path = os.path.join(CSRC, src)
+        obj = os.path.join(BUILD, src + ".o")
+        objs.append(obj)
+        if _needs(obj, [path] + headers):
+            cmd = [HIPCC] + FLAGS + ["-c", path, "-o", obj]
+            if src.endswith(".hip"):
+                cmd.insert(1, f"--offload-arch={ARCH}")
+            jobs.append(cmd)
+
+    def run(cmd):
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("compile failed: " + " ".join(cmd) + "\n" + r.stderr)
+        if verbose and r.stderr:
+            print(r.stderr, file=sys.stderr)
+
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        list(ex.map(run, jobs))
+    if jobs or not os.path.exists(LIB):
+        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True))

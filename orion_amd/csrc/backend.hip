@@ -1,0 +1,2025 @@
+// backend.hip -- context, device memory, keys, CKKS operators and the
+// Lattigo-compatible C-ABI of liborion_hip.so (include/orion_hip.h).
+//
+// Operator algorithms follow Lattigo v6 as reached from
+// /root/reference/orion/backend/lattigo/*.go; the CPU
+// restatement they are checked against lives in oracle/ (tests only).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/orion_hip.h"
+#include "common.h"
+#include "hostmath.h"
+
+int orion_launch_ntt(int logN, const LimbSet& s, const DeviceTables* tb, bool inverse, hipStream_t st);
+int orion_ntt_init();
+int orion_launch_ew(int op, const LimbSet& o, const LimbSet& a, const LimbSet& b, const u64* s, const u64* ss,
+                    const DeviceTables* tb, int N, hipStream_t st);
+int orion_launch_tensor(const LimbSet& d, const LimbSet& a, const LimbSet& b, const DeviceTables* tb, int N,
+                        hipStream_t st);
+int orion_launch_rescale_prep(const LimbSet& dst, const u64* src, long long src_comp_stride,
+                              long long src_batch_stride, int modL, const DeviceTables* tb, int N, hipStream_t st);
+int orion_launch_basis_ext(const LimbSet& out, const LimbSet& in, const BasisExtTable* T, const DeviceTables* tb,
+                           int N, hipStream_t st);
+int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const u64* key, int beta, int nmod_key,
+                        const DeviceTables* tb, int N, int accumulate, hipStream_t st);
+int orion_launch_automorph(const LimbSet& o, const LimbSet& a, const u32* idx, const DeviceTables* tb, int N,
+                           int accumulate, hipStream_t st);
+
+namespace orion {
+
+enum { EW_ADD = 0, EW_SUB, EW_MUL, EW_MULADD, EW_NEG, EW_SCALE, EW_ADDC, EW_SUBSCALE, EW_COPY, EW_ADDSCALE };
+
+#define HIPCHK(x)                                                                                  \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e_) + \
+                                                   " at " + #x);                                   \
+  } while (0)
+
+static thread_local std::string g_last_error;
+
+// ---------------------------------------------------------------------------
+// device memory: size-class cache (no hipMalloc/hipFree on the op path)
+// ---------------------------------------------------------------------------
+class DevicePool {
+ public:
+  void* alloc(size_t bytes) {
+    auto it = free_.find(bytes);
+    if (it != free_.end() && !it->second.empty()) {
+      void* p = it->second.back();
+      it->second.pop_back();
+      return p;
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {  // release the cache once and retry
+      trim();
+      HIPCHK(hipMalloc(&p, bytes));
+    }
+    return p;
+  }
+  void release(void* p, size_t bytes) { free_[bytes].push_back(p); }
+  void trim() {
+    hipDeviceSynchronize();
+    for (auto& kv : free_)
+      for (void* p : kv.second) hipFree(p);
+    free_.clear();
+  }
+  ~DevicePool() { trim(); }
+
+ private:
+  std::unordered_map<size_t, std::vector<void*>> free_;
+};
+
+struct Buffer {
+  DevicePool* pool;
+  u64* p;
+  size_t bytes;
+  Buffer(DevicePool* pl, size_t b) : pool(pl), p((u64*)pl->alloc(b)), bytes(b) {}
+  ~Buffer() { pool->release(p, bytes); }
+};
+
+// [ncomp][nlimb][B][N]
+struct Poly {
+  std::shared_ptr<Buffer> buf;
+  int ncomp = 0, nlimb = 0, B = 0, N = 0;
+  u64* ptr() const { return buf ? buf->p : nullptr; }
+  long long batch_stride() const { return N; }
+  long long limb_stride() const { return (long long)B * N; }
+  long long comp_stride() const { return (long long)nlimb * B * N; }
+};
+
+struct Ciphertext {
+  Poly poly;
+  int level = 0;
+  long double scale = 1;
+};
+
+struct Plaintext {
+  Poly poly;
+  int level = 0;
+  long double scale = 1;
+  bool qp = false;  // limbs: Q 0..level then P (LT diagonals)
+};
+
+struct LinTrans {
+  int level = 0, N1 = 1;
+  float ratio = 1;
+  std::vector<int> idx;                 // diagonal indices, as given
+  std::map<int, Plaintext> diags;       // keyed by idx & (slots-1)
+  std::vector<int> giants, babies;      // sorted giants; babies in first-seen order
+  std::map<int, std::vector<int>> index;  // giant -> sorted babies
+};
+
+template <class T>
+class HandlePool {  // lowest-free-id reuse (minheap.go:46-64)
+ public:
+  int add(T&& v) {
+    int id;
+    if (!free_.empty()) {
+      id = *free_.begin();
+      free_.erase(free_.begin());
+    } else {
+      id = next_++;
+    }
+    map_[id] = std::make_unique<T>(std::move(v));
+    return id;
+  }
+  T& get(int id) {
+    auto it = map_.find(id);
+    if (it == map_.end()) throw std::runtime_error("handle not found: " + std::to_string(id));
+    return *it->second;
+  }
+  bool has(int id) const { return map_.count(id) != 0; }
+  void del(int id) {
+    if (map_.erase(id)) free_.insert(id);
+  }
+  void reset() {
+    map_.clear();
+    free_.clear();
+    next_ = 0;
+  }
+  std::vector<int> live() const {
+    std::vector<int> v;
+    for (auto& kv : map_) v.push_back(kv.first);
+    return v;
+  }
+
+ private:
+  std::map<int, std::unique_ptr<T>> map_;
+  std::set<int> free_;
+  int next_ = 0;
+};
+
+struct ProfRec {
+  int cat;
+  hipEvent_t e0, e1;
+  double bytes;
+};
+static const char* kProfNames[] = {"ntt_fwd", "ntt_inv", "elementwise", "basis_ext", "ks_mac", "automorph",
+                                   "tensor", "rescale_prep"};
+enum { P_NTT_FWD = 0, P_NTT_INV, P_EW, P_BEXT, P_MAC, P_AUT, P_TENSOR, P_RSPREP, P_NCAT };
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+struct Context {
+  int logN = 0, N = 0, L = 0, K = 0, dnum = 0, logScale = 0, h = 0;
+  std::vector<u64> mods;  // QP
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  DevicePool pool;
+  DeviceTables host_tb;
+  DeviceTables* d_tb = nullptr;
+  std::vector<void*> static_bufs;
+  std::unique_ptr<SpecialFFT> fft;
+  Prng prng{0x0123456789abcdefull};
+
+  Poly sk, pk, rlk;
+  bool have_sk = false, have_pk = false, have_rlk = false;
+  std::map<u64, Poly> gks;
+  std::map<u64, u32*> autidx;
+  std::map<std::pair<int, int>, BasisExtTable*> betab;
+  std::map<std::pair<int, int>, std::vector<int>> betab_pos;  // target positions (QP order)
+
+  HandlePool<Plaintext> pts;
+  HandlePool<Ciphertext> cts;
+  HandlePool<LinTrans> lts;
+
+  bool prof = false;
+  std::vector<ProfRec> prof_recs;
+  std::vector<hipEvent_t> ev_free;
+  double prof_launch[P_NCAT] = {0}, prof_ms[P_NCAT] = {0}, prof_bytes[P_NCAT] = {0};
+
+  ~Context() {
+    hipDeviceSynchronize();
+    gks.clear();
+    sk = pk = rlk = Poly();
+    pts.reset();
+    cts.reset();
+    lts.reset();
+    for (auto& kv : autidx) hipFree(kv.second);
+    for (auto& kv : betab) hipFree(kv.second);
+    for (void* p : static_bufs) hipFree(p);
+    if (d_tb) hipFree(d_tb);
+    for (auto& r : prof_recs) {
+      hipEventDestroy(r.e0);
+      hipEventDestroy(r.e1);
+    }
+    for (auto e : ev_free) hipEventDestroy(e);
+    if (own_stream && stream) hipStreamDestroy(stream);
+  }
+
+  // -- profiling -----------------------------------------------------------
+  hipEvent_t ev() {
+    if (!ev_free.empty()) {
+      hipEvent_t e = ev_free.back();
+      ev_free.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    return e;
+  }
+  struct Scope {
+    Context* c;
+    int cat;
+    double bytes;
+    hipEvent_t e0 = nullptr;
+    Scope(Context* ctx, int k, double b) : c(ctx), cat(k), bytes(b) {
+      if (c->prof) {
+        e0 = c->ev();
+        hipEventRecord(e0, c->stream);
+      }
+    }
+    ~Scope() {
+      if (e0) {
+        hipEvent_t e1 = c->ev();
+        hipEventRecord(e1, c->stream);
+        c->prof_recs.push_back(ProfRec{cat, e0, e1, bytes});
+        if (c->prof_recs.size() > 20000) c->prof_flush();
+      }
+    }
+  };
+  void prof_flush() {
+    if (prof_recs.empty()) return;
+    hipStreamSynchronize(stream);
+    for (auto& r : prof_recs) {
+      float ms = 0;
+      hipEventElapsedTime(&ms, r.e0, r.e1);
+      prof_launch[r.cat] += 1;
+      prof_ms[r.cat] += ms;
+      prof_bytes[r.cat] += r.bytes;
+      ev_free.push_back(r.e0);
+      ev_free.push_back(r.e1);
+    }
+    prof_recs.clear();
+  }
+
+  // -- allocation --------------------------------------------------------------
+  Poly alloc(int ncomp, int nlimb, int B) {
+    Poly p;
+    p.ncomp = ncomp;
+    p.nlimb = nlimb;
+    p.B = B;
+    p.N = N;
+    p.buf = std::make_shared<Buffer>(&pool, (size_t)ncomp * nlimb * B * N * sizeof(u64) + 16);
+    return p;
+  }
+
+  int qp_mod(int level, int pos) const { return pos <= level ? pos : L + (pos - level - 1); }
+
+  // LimbSet over components [c0, c0+nc) and limb positions/moduli
+  LimbSet ls(const Poly& P, int c0, int nc, const std::vector<int>& pos, const std::vector<int>& md,
+             int nbatch = -1) const {
+    LimbSet s;
+    memset(&s, 0, sizeof(s));
+    s.p = P.ptr() + c0 * P.comp_stride();
+    s.comp_stride = P.comp_stride();
+    s.limb_stride = P.limb_stride();
+    s.batch_stride = P.batch_stride();
+    s.ncomp = nc;
+    s.nlimb = (int)pos.size();
+    s.nbatch = nbatch < 0 ? P.B : nbatch;
+    if (P.B == 1 && s.nbatch > 1) s.batch_stride = 0;  // broadcast
+    if (pos.size() > ORION_MAXLIMB) throw std::runtime_error("too many limbs in one launch");
+    for (size_t i = 0; i < pos.size(); ++i) {
+      s.pos[i] = (unsigned char)pos[i];
+      s.mod[i] = (unsigned char)md[i];
+    }
+    return s;
+  }
+  static std::vector<int> iota(int a, int b) {
+    std::vector<int> v;
+    for (int i = a; i < b; ++i) v.push_back(i);
+    return v;
+  }
+  LimbSet lsq(const Poly& P, int c0, int nc, int level, int nbatch = -1) const {
+    auto v = iota(0, level + 1);
+    return ls(P, c0, nc, v, v, nbatch);
+  }
+  // QP limbs of a poly laid out [Q 0..lvl_alloc][P], used at `level` <= lvl_alloc
+  LimbSet lsqp(const Poly& P, int c0, int nc, int level, int lvl_alloc, int nbatch = -1) const {
+    std::vector<int> pos, md;
+    for (int j = 0; j <= level; ++j) pos.push_back(j), md.push_back(j);
+    for (int k = 0; k < K; ++k) pos.push_back(lvl_alloc + 1 + k), md.push_back(L + k);
+    return ls(P, c0, nc, pos, md, nbatch);
+  }
+  LimbSet lsp(const Poly& P, int c0, int nc, int lvl_alloc) const {
+    std::vector<int> pos, md;
+    for (int k = 0; k < K; ++k) pos.push_back(lvl_alloc + 1 + k), md.push_back(L + k);
+    return ls(P, c0, nc, pos, md);
+  }
+
+  // -- kernel wrappers ------------------------------------------------------------
+  void ntt(const LimbSet& s, bool inv) {
+    Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, 16.0 * N * s.ncomp * s.nlimb * s.nbatch);
+    if (orion_launch_ntt(logN, s, d_tb, inv, stream)) throw std::runtime_error("unsupported logN for NTT");
+  }
+  void ew(int op, const LimbSet& o, const LimbSet& a, const LimbSet& b, const std::vector<u64>* sc = nullptr) {
+    std::vector<u64> s, ss;
+    if (sc) {
+      s = *sc;
+      for (int l = 0; l < o.nlimb; ++l) ss.push_back(hm_shoup(s[l], mods[o.mod[l]]));
+    }
+    int nin = (op == EW_NEG || op == EW_SCALE || op == EW_ADDC || op == EW_COPY) ? 1 : 2;
+    if (op == EW_MULADD || op == EW_ADDSCALE) nin += 1;
+    Scope scp(this, P_EW, 8.0 * N * o.ncomp * o.nlimb * o.nbatch * (nin + 1));
+    orion_launch_ew(op, o, a, b, sc ? s.data() : nullptr, sc ? ss.data() : nullptr, d_tb, N, stream);
+  }
+  void ew1(int op, const LimbSet& o, const LimbSet& a, const std::vector<u64>* sc = nullptr) { ew(op, o, a, a, sc); }
+  void copy(const LimbSet& o, const LimbSet& a) { ew(EW_COPY, o, a, a); }
+
+  // -- tables ---------------------------------------------------------------------
+  void setup(int logN_, const std::vector<int>& logQ, const std::vector<int>& logP, int logScale_, int h_) {
+    logN = logN_;
+    N = 1 << logN;
+    L = (int)logQ.size();
+    K = (int)logP.size();
+    if (K < 1) throw std::runtime_error("at least one P prime is required (hybrid key switching)");
+    dnum = (L + K - 1) / K;
+    logScale = logScale_;
+    h = h_;
+    if (logN < 13 || logN > 15) throw std::runtime_error("logN must be 13..15 in this build");
+    if (L + K > ORION_MAXMOD) throw std::runtime_error("too many moduli");
+    for (int b : logQ)
+      if (b > 61) throw std::runtime_error("moduli must be <= 61 bits");
+    for (int b : logP)
+      if (b > 61) throw std::runtime_error("moduli must be <= 61 bits");
+    mods = gen_moduli(logN, logQ, logP);
+    fft.reset(new SpecialFFT(logN));
+    if (!stream) {
+      HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+      own_stream = true;
+    }
+    orion_ntt_init();
+    memset(&host_tb, 0, sizeof(host_tb));
+    std::vector<ulonglong2> fw(N), iv(N);
+    for (int m = 0; m < L + K; ++m) {
+      const u64 q = mods[m];
+      ModConst& mc = host_tb.mc[m];
+      mc.q = q;
+      mc.bar_k = 64 - __builtin_clzll(q);
+      mc.bar_mu = (u64)(((u128)1 << (2 * mc.bar_k)) / q);
+      mc.ninv = hm_invmod((u64)N, q);
+      mc.ninv_s = hm_shoup(mc.ninv, q);
+      const u64 g = primitive_root(q);
+      const u64 psi = hm_powmod(g, (q - 1) / (2 * (u64)N), q);
+      const u64 psii = hm_invmod(psi, q);
+      u64 a = 1, b = 1;
+      for (int j = 0; j < N; ++j) {
+        const u64 r = hm_bitrev(j, logN);
+        fw[r] = make_ulonglong2(a, hm_shoup(a, q));
+        iv[r] = make_ulonglong2(b, hm_shoup(b, q));
+        a = hm_mulmod(a, psi, q);
+        b = hm_mulmod(b, psii, q);
+      }
+      void *dfw, *div;
+      HIPCHK(hipMalloc(&dfw, N * sizeof(ulonglong2)));
+      HIPCHK(hipMalloc(&div, N * sizeof(ulonglong2)));
+      HIPCHK(hipMemcpy(dfw, fw.data(), N * sizeof(ulonglong2), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(div, iv.data(), N * sizeof(ulonglong2), hipMemcpyHostToDevice));
+      static_bufs.push_back(dfw);
+      static_bufs.push_back(div);
+      host_tb.fwd[m] = (const ulonglong2*)dfw;
+      host_tb.inv[m] = (const ulonglong2*)div;
+    }
+    HIPCHK(hipMalloc(&d_tb, sizeof(DeviceTables)));
+    HIPCHK(hipMemcpy(d_tb, &host_tb, sizeof(DeviceTables), hipMemcpyHostToDevice));
+  }
+
+  u64 prod_mod(const std::vector<int>& src, int skip, u64 t) const {
+    u64 r = 1 % t;
+    for (int i = 0; i < (int)src.size(); ++i)
+      if (i != skip) r = hm_mulmod(r, mods[src[i]] % t, t);
+    return r;
+  }
+
+  BasisExtTable* make_betab(const std::vector<int>& src, const std::vector<int>& dst) {
+    BasisExtTable T;
+    memset(&T, 0, sizeof(T));
+    T.ns = (int)src.size();
+    T.nt = (int)dst.size();
+    if (T.ns > ORION_MAXSRC || T.nt > ORION_MAXLIMB) throw std::runtime_error("basis extension too large");
+    for (int i = 0; i < T.ns; ++i) {
+      const u64 si = mods[src[i]];
+      T.src_mod[i] = src[i];
+      T.qhatinv[i] = hm_invmod(prod_mod(src, i, si), si);
+      T.qhatinv_s[i] = hm_shoup(T.qhatinv[i], si);
+      T.qinv_f[i] = 1.0 / (double)si;
+    }
+    for (int t = 0; t < T.nt; ++t) {
+      const u64 tm = mods[dst[t]];
+      T.dst_mod[t] = dst[t];
+      T.S_t[t] = prod_mod(src, -1, tm);
+      for (int i = 0; i < T.ns; ++i) T.qhat_t[t][i] = prod_mod(src, i, tm);
+    }
+    BasisExtTable* d;
+    HIPCHK(hipMalloc(&d, sizeof(T)));
+    HIPCHK(hipMemcpy(d, &T, sizeof(T), hipMemcpyHostToDevice));
+    return d;
+  }
+  // ModUp of digit i at level: sources Q[lo,hi), targets = rest of QP in QP-position order
+  BasisExtTable* modup_tab(int level, int digit, std::vector<int>& tpos) {
+    auto key = std::make_pair(level, digit);
+    auto it = betab.find(key);
+    if (it != betab.end()) {
+      tpos = betab_pos[key];
+      return it->second;
+    }
+    const int lo = digit * K, hi = std::min((digit + 1) * K, level + 1);
+    std::vector<int> src = iota(lo, hi), dst;
+    tpos.clear();
+    for (int j = 0; j <= level + K; ++j) {
+      if (j >= lo && j < hi) continue;
+      tpos.push_back(j);
+      dst.push_back(qp_mod(level, j));
+    }
+    BasisExtTable* d = make_betab(src, dst);
+    betab[key] = d;
+    betab_pos[key] = tpos;
+    return d;
+  }
+  BasisExtTable* moddown_tab(int level) {
+    auto key = std::make_pair(level, -1);
+    auto it = betab.find(key);
+    if (it != betab.end()) return it->second;
+    std::vector<int> src;
+    for (int k = 0; k < K; ++k) src.push_back(L + k);
+    BasisExtTable* d = make_betab(src, iota(0, level + 1));
+    betab[key] = d;
+    return d;
+  }
+
+  u64 galois_element(int k) const {
+    const u64 M = 2 * (u64)N;
+    return hm_powmod(5, (u64)(long long)k & (M - 1), M);
+  }
+  const u32* aut_index(u64 g) {
+    auto it = autidx.find(g);
+    if (it != autidx.end()) return it->second;
+    std::vector<u32> idx(N);
+    const u64 mask = 2 * (u64)N - 1;
+    for (int j = 0; j < N; ++j) {
+      const u64 t1 = 2 * hm_bitrev(j, logN) + 1;
+      const u64 t2 = (((g * t1) & mask) - 1) >> 1;
+      idx[j] = (u32)hm_bitrev(t2, logN);
+    }
+    u32* d;
+    HIPCHK(hipMalloc(&d, N * sizeof(u32)));
+    HIPCHK(hipMemcpy(d, idx.data(), N * sizeof(u32), hipMemcpyHostToDevice));
+    autidx[g] = d;
+    return d;
+  }
+  void automorph(const LimbSet& o, const LimbSet& a, u64 g, bool acc) {
+    const u32* idx = aut_index(g);
+    Scope sc(this, P_AUT, 8.0 * N * o.ncomp * o.nlimb * o.nbatch * (acc ? 3 : 2));
+    orion_launch_automorph(o, a, idx, d_tb, N, acc ? 1 : 0, stream);
+  }
+
+  // -- upload of host residues (coefficient domain) + NTT -------------------------------
+  void upload(const Poly& P, const std::vector<u64>& host) {
+    HIPCHK(hipMemcpyAsync(P.ptr(), host.data(), host.size() * sizeof(u64), hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+  }
+  void download(const Poly& P, std::vector<u64>& host) {
+    host.resize((size_t)P.ncomp * P.nlimb * P.B * N);
+    HIPCHK(hipMemcpyAsync(host.data(), P.ptr(), host.size() * sizeof(u64), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+  }
+  // small signed coefficients -> residues for moduli md, into host[l*N + n] of a [nl][N] block
+  void small_residues(const std::vector<int64_t>& v, const std::vector<int>& md, u64* out) const {
+    for (size_t l = 0; l < md.size(); ++l) {
+      const u64 q = mods[md[l]];
+      for (int n = 0; n < N; ++n) {
+        const int64_t x = v[n];
+        out[l * N + n] = x >= 0 ? (u64)x % q : (q - ((u64)(-x) % q)) % q;
+      }
+    }
+  }
+  std::vector<int64_t> sample_gauss() {
+    std::vector<int64_t> e(N);
+    for (auto& x : e) x = prng.gaussian(3.2, 19.2);
+    return e;
+  }
+  std::vector<int64_t> sample_ternary_h(int hw) {
+    std::vector<int64_t> s(N, 0);
+    std::vector<int> perm(N);
+    for (int i = 0; i < N; ++i) perm[i] = i;
+    hw = std::min(hw, N);
+    for (int i = 0; i < hw; ++i) {
+      const int j = i + (int)(prng.next() % (u64)(N - i));
+      std::swap(perm[i], perm[j]);
+      s[perm[i]] = (prng.next() & 1) ? 1 : -1;
+    }
+    return s;
+  }
+  std::vector<int64_t> sample_ternary_uniform() {
+    std::vector<int64_t> s(N);
+    for (auto& x : s) x = (int64_t)(prng.next() % 3) - 1;
+    return s;
+  }
+  std::vector<u64> qp_mod_list() const {
+    std::vector<u64> v;
+    for (int j = 0; j < L + K; ++j) v.push_back(mods[j]);
+    return v;
+  }
+
+  // ---------------------------------------------------------------------------
+  // keys
+  // ---------------------------------------------------------------------------
+  void gen_secret() {
+    auto s = sample_ternary_h(h);
+    sk = alloc(1, L + K, 1);
+    std::vector<u64> host((size_t)(L + K) * N);
+    small_residues(s, iota(0, L + K), host.data());
+    upload(sk, host);
+    ntt(ls(sk, 0, 1, iota(0, L + K), iota(0, L + K)), false);
+    have_sk = true;
+  }
+  LimbSet full(const Poly& P, int c0, int nc) const { return ls(P, c0, nc, iota(0, L + K), iota(0, L + K)); }
+
+  void gen_public() {
+    if (!have_sk) throw std::runtime_error("secret key not generated");
+    pk = alloc(2, L + K, 1);
+    std::vector<u64> a((size_t)(L + K) * N), e((size_t)(L + K) * N);
+    for (int m = 0; m < L + K; ++m)
+      for (int n = 0; n < N; ++n) a[(size_t)m * N + n] = prng.uniform(mods[m]);
+    small_residues(sample_gauss(), iota(0, L + K), e.data());
+    Poly tmp = alloc(1, L + K, 1);
+    HIPCHK(hipMemcpyAsync(pk.ptr() + pk.comp_stride(), a.data(), a.size() * 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(pk.ptr(), e.data(), e.size() * 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    ntt(full(pk, 0, 1), false);
+    ew(EW_MUL, full(tmp, 0, 1), full(pk, 1, 1), full(sk, 0, 1));
+    ew(EW_SUB, full(pk, 0, 1), full(pk, 0, 1), full(tmp, 0, 1));
+    have_pk = true;
+  }
+
+  // evaluation key switching s_in -> s_out, layout [dnum][2][L+K][N]
+  Poly gen_evk(const Poly& s_in, const Poly& s_out) {
+    Poly k = alloc(2 * dnum, L + K, 1);
+    Poly tmp = alloc(1, L + K, 1);
+    std::vector<u64> a((size_t)(L + K) * N), e((size_t)(L + K) * N);
+    for (int i = 0; i < dnum; ++i) {
+      for (int m = 0; m < L + K; ++m)
+        for (int n = 0; n < N; ++n) a[(size_t)m * N + n] = prng.uniform(mods[m]);
+      small_residues(sample_gauss(), iota(0, L + K), e.data());
+      HIPCHK(hipMemcpyAsync(k.ptr() + (2 * i + 1) * k.comp_stride(), a.data(), a.size() * 8,
+                            hipMemcpyHostToDevice, stream));
+      HIPCHK(hipMemcpyAsync(k.ptr() + (2 * i) * k.comp_stride(), e.data(), e.size() * 8, hipMemcpyHostToDevice,
+                            stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      ntt(full(k, 2 * i, 1), false);
+      ew(EW_MUL, full(tmp, 0, 1), full(k, 2 * i + 1, 1), full(s_out, 0, 1));
+      ew(EW_SUB, full(k, 2 * i, 1), full(k, 2 * i, 1), full(tmp, 0, 1));
+      // + P * s_in on the Q limbs of digit i
+      const int lo = i * K, hi = std::min((i + 1) * K, L);
+      std::vector<int> dl = iota(lo, hi);
+      std::vector<u64> pm;
+      for (int j : dl) {
+        u64 P = 1;
+        for (int kk = 0; kk < K; ++kk) P = hm_mulmod(P, mods[L + kk] % mods[j], mods[j]);
+        pm.push_back(P);
+      }
+      ew(EW_ADDSCALE, ls(k, 2 * i, 1, dl, dl), ls(s_in, 0, 1, dl, dl), ls(s_in, 0, 1, dl, dl), &pm);
+    }
+    return k;
+  }
+  void gen_relin() {
+    if (!have_sk) throw std::runtime_error("secret key not generated");
+    Poly s2 = alloc(1, L + K, 1);
+    ew(EW_MUL, full(s2, 0, 1), full(sk, 0, 1), full(sk, 0, 1));
+    rlk = gen_evk(s2, sk);
+    have_rlk = true;
+  }
+  void gen_galois(u64 g) {
+    if (gks.count(g)) return;
+    if (!have_sk) throw std::runtime_error("secret key not generated");
+    const u64 M = 2 * (u64)N;
+    u64 ginv = hm_powmod(g, M / 2 - 1, M);  // g^-1 mod 2N (group order N/2 divides M/2)
+    if ((g * ginv) % M != 1) {
+      for (ginv = 1; ginv < M; ginv += 2)
+        if ((g * ginv) % M == 1) break;
+    }
+    Poly s_out = alloc(1, L + K, 1);
+    automorph(full(s_out, 0, 1), full(sk, 0, 1), ginv, false);
+    gks[g] = gen_evk(sk, s_out);
+  }
+  const Poly& galois_key(u64 g) {
+    auto it = gks.find(g);
+    if (it == gks.end()) {
+      gen_galois(g);  // Lattigo AddRotationKey semantics: generate on first use
+      it = gks.find(g);
+    }
+    return it->second;
+  }
+
+  // ---------------------------------------------------------------------------
+  // key switching building blocks
+  // ---------------------------------------------------------------------------
+  // decompose a Q poly (1 comp, limbs 0..level) into beta digits extended to QP (NTT)
+  Poly decompose(const LimbSet& c, int level, int B) {
+    const int beta = (level + 1 + K - 1) / K;
+    const int nqp = level + 1 + K;
+    Poly cinv = alloc(1, level + 1, B);
+    copy(lsq(cinv, 0, 1, level), c);
+    ntt(lsq(cinv, 0, 1, level), true);
+    Poly D = alloc(beta, nqp, B);
+    for (int i = 0; i < beta; ++i) {
+      const int lo = i * K, hi = std::min((i + 1) * K, level + 1);
+      std::vector<int> tpos;
+      BasisExtTable* T = modup_tab(level, i, tpos);
+      std::vector<int> tmod;
+      for (int p : tpos) tmod.push_back(qp_mod(level, p));
+      LimbSet in = ls(cinv, 0, 1, iota(lo, hi), iota(lo, hi));
+      LimbSet out = ls(D, i, 1, tpos, tmod);
+      {
+        Scope sc(this, P_BEXT, 8.0 * N * B * (in.nlimb + out.nlimb));
+        orion_launch_basis_ext(out, in, T, d_tb, N, stream);
+      }
+      ntt(out, false);
+      LimbSet own = ls(D, i, 1, iota(lo, hi), iota(lo, hi));
+      LimbSet src = c;
+      src.nlimb = hi - lo;
+      for (int j = lo; j < hi; ++j) {
+        src.pos[j - lo] = c.pos[j];
+        src.mod[j - lo] = c.mod[j];
+      }
+      copy(own, src);
+    }
+    return D;
+  }
+  // out (2 comps, QP at level) [+]= sum_i D_i * key_i
+  void mac(const Poly& out, const Poly& D, const Poly& key, int level, bool acc) {
+    const int beta = (level + 1 + K - 1) / K;
+    LimbSet o = lsqp(out, 0, 2, level, level);
+    LimbSet d = lsqp(D, 0, beta, level, level);
+    Scope sc(this, P_MAC, 8.0 * N * o.nlimb * (o.nbatch * (beta + 2 + (acc ? 2 : 0)) + 2 * beta));
+    orion_launch_ks_mac(o, d, key.ptr(), beta, L + K, d_tb, N, acc ? 1 : 0, stream);
+  }
+  // x: poly with comps [c0, c0+nc) in QP layout (alloc level lvl_alloc); clobbers x's P limbs
+  void moddown(const Poly& x, int c0, int nc, int level, int lvl_alloc, const LimbSet& out) {
+    const int B = x.B;
+    LimbSet xp = ls(x, c0, nc, iota(lvl_alloc + 1, lvl_alloc + 1 + K), iota(L, L + K));
+    ntt(xp, true);
+    Poly ext = alloc(nc, level + 1, B);
+    LimbSet le = lsq(ext, 0, nc, level);
+    {
+      Scope sc(this, P_BEXT, 8.0 * N * B * nc * (K + level + 1));
+      orion_launch_basis_ext(le, xp, moddown_tab(level), d_tb, N, stream);
+    }
+    ntt(le, false);
+    std::vector<u64> pinv;
+    for (int j = 0; j <= level; ++j) {
+      u64 P = 1;
+      for (int k = 0; k < K; ++k) P = hm_mulmod(P, mods[L + k] % mods[j], mods[j]);
+      pinv.push_back(hm_invmod(P, mods[j]));
+    }
+    LimbSet xq = ls(x, c0, nc, iota(0, level + 1), iota(0, level + 1));
+    ew(EW_SUBSCALE, out, xq, le, &pinv);
+  }
+  // full key switch of c (Q, level) -> (k0, k1) written to out comps 0/1 (Q, level)
+  void keyswitch(const LimbSet& c, int level, int B, const Poly& key, const Poly& out) {
+    Poly D = decompose(c, level, B);
+    Poly u = alloc(2, level + 1 + K, B);
+    mac(u, D, key, level, false);
+    moddown(u, 0, 2, level, level, lsq(out, 0, 2, level));
+  }
+  std::vector<u64> p_mod_q(int level) const {
+    std::vector<u64> v;
+    for (int j = 0; j <= level; ++j) {
+      u64 P = 1;
+      for (int k = 0; k < K; ++k) P = hm_mulmod(P, mods[L + k] % mods[j], mods[j]);
+      v.push_back(P);
+    }
+    return v;
+  }
+
+  // ---------------------------------------------------------------------------
+  // ciphertext operators
+  // ---------------------------------------------------------------------------
+  Ciphertext new_ct(int level, int B, long double scale) {
+    Ciphertext c;
+    c.poly = alloc(2, level + 1, B);
+    c.level = level;
+    c.scale = scale;
+    return c;
+  }
+  Ciphertext clone(const Ciphertext& a) {
+    Ciphertext c = new_ct(a.level, a.poly.B, a.scale);
+    copy(lsq(c.poly, 0, 2, a.level), lsq(a.poly, 0, 2, a.level));
+    return c;
+  }
+
+  void rescale_inplace(Ciphertext& ct) {
+    const int l = ct.level;
+    if (l < 1) throw std::runtime_error("cannot rescale a level-0 ciphertext");
+    const int B = ct.poly.B;
+    ntt(ls(ct.poly, 0, 2, {l}, {l}), true);
+    Poly T = alloc(2, l, B);
+    LimbSet lt = lsq(T, 0, 2, l - 1);
+    {
+      Scope sc(this, P_RSPREP, 8.0 * N * B * 2 * (1 + l));
+      orion_launch_rescale_prep(lt, ct.poly.ptr() + l * ct.poly.limb_stride(), ct.poly.comp_stride(),
+                                ct.poly.batch_stride(), l, d_tb, N, stream);
+    }
+    ntt(lt, false);
+    std::vector<u64> inv;
+    for (int j = 0; j < l; ++j) inv.push_back(hm_invmod(mods[l] % mods[j], mods[j]));
+    LimbSet cq = lsq(ct.poly, 0, 2, l - 1);
+    ew(EW_SUBSCALE, cq, cq, lt, &inv);
+    ct.level = l - 1;
+    ct.scale /= (long double)mods[l];
+  }
+
+  int batch_of(int a, int b) const {
+    if (a == b || b == 1) return a;
+    if (a == 1) return b;
+    throw std::runtime_error("batch size mismatch");
+  }
+
+  Ciphertext mul_relin(const Ciphertext& a, const Ciphertext& b) {
+    if (!have_rlk) throw std::runtime_error("relinearization key not generated");
+    const int level = std::min(a.level, b.level);
+    const int B = batch_of(a.poly.B, b.poly.B);
+    Poly d = alloc(3, level + 1, B);
+    {
+      LimbSet ld = lsq(d, 0, 3, level);
+      Scope sc(this, P_TENSOR, 8.0 * N * (level + 1) * B * 7);
+      orion_launch_tensor(ld, lsq(a.poly, 0, 2, level, B), lsq(b.poly, 0, 2, level, B), d_tb, N, stream);
+    }
+    Ciphertext out = new_ct(level, B, a.scale * b.scale);
+    keyswitch(lsq(d, 2, 1, level), level, B, rlk, out.poly);
+    LimbSet o = lsq(out.poly, 0, 2, level);
+    ew(EW_ADD, o, o, lsq(d, 0, 2, level));
+    return out;
+  }
+
+  Ciphertext rotate(const Ciphertext& a, int k) {
+    const int level = a.level, B = a.poly.B;
+    const u64 g = galois_element(k);
+    const Poly& key = galois_key(g);
+    Poly t = alloc(2, level + 1, B);
+    keyswitch(lsq(a.poly, 1, 1, level), level, B, key, t);
+    ew(EW_ADD, lsq(t, 0, 1, level), lsq(t, 0, 1, level), lsq(a.poly, 0, 1, level));
+    Ciphertext out = new_ct(level, B, a.scale);
+    automorph(lsq(out.poly, 0, 2, level), lsq(t, 0, 2, level), g, false);
+    return out;
+  }
+
+  // scale matching for additions (Lattigo evaluateInPlace: the lower-scale
+  // operand is multiplied by the rounded integer ratio when it is > 1)
+  void add_like(Ciphertext& out, const Ciphertext& a, const LimbSet& b, long double bscale, int op) {
+    const int level = out.level;
+    LimbSet o = lsq(out.poly, 0, 2, level);
+    LimbSet la = lsq(a.poly, 0, 2, level, out.poly.B);
+    long double ratio = a.scale > bscale ? a.scale / bscale : bscale / a.scale;
+    long long r = llroundl(ratio);
+    if (r > 1) {
+      std::vector<u64> sc;
+      for (int j = 0; j <= level; ++j) sc.push_back((u64)r % mods[j]);
+      if (a.scale > bscale) {
+        Poly tb = alloc(b.ncomp, level + 1, out.poly.B);
+        LimbSet lt = lsq(tb, 0, b.ncomp, level);
+        ew1(EW_SCALE, lt, b, &sc);
+        ew(op, lsq(out.poly, 0, b.ncomp, level), lsq(a.poly, 0, b.ncomp, level, out.poly.B), lt);
+        if (b.ncomp == 1 && &out != &a) copy(lsq(out.poly, 1, 1, level), lsq(a.poly, 1, 1, level, out.poly.B));
+        out.scale = a.scale;
+        return;
+      }
+      ew1(EW_SCALE, o, la, &sc);
+      ew(op, lsq(out.poly, 0, b.ncomp, level), lsq(out.poly, 0, b.ncomp, level), b);
+      out.scale = bscale;
+      return;
+    }
+    ew(op, lsq(out.poly, 0, b.ncomp, level), lsq(a.poly, 0, b.ncomp, level, out.poly.B), b);
+    if (b.ncomp == 1 && &out != &a) copy(lsq(out.poly, 1, 1, level), lsq(a.poly, 1, 1, level, out.poly.B));
+    out.scale = a.scale;
+  }
+
+  // BSGS linear transform (lintrans MultiplyByDiagMatrixBSGS restated; oracle_lt_bsgs)
+  Ciphertext eval_lt(const LinTrans& T, const Ciphertext& ct) {
+    const int level = std::min(ct.level, T.level);
+    const int B = ct.poly.B, nqp = level + 1 + K;
+    const std::vector<u64> pq = p_mod_q(level);
+    Poly D = decompose(lsq(ct.poly, 1, 1, level), level, B);
+    std::map<int, Poly> rot;  // baby -> [2][QP][B]
+    for (int b : T.babies) {
+      Poly r = alloc(2, nqp, B);
+      if (b == 0) {
+        ew1(EW_SCALE, lsq(r, 0, 2, level), lsq(ct.poly, 0, 2, level), &pq);
+        std::vector<u64> zero(K, 0);
+        LimbSet rp = lsp(r, 0, 2, level);
+        ew1(EW_SCALE, rp, rp, &zero);  // P part = 0 (c * P mod p)
+        rot[b] = r;
+        continue;
+      }
+      const u64 g = galois_element(b);
+      const Poly& key = galois_key(g);
+      Poly u = alloc(2, nqp, B);
+      mac(u, D, key, level, false);
+      ew(EW_ADDSCALE, lsq(u, 0, 1, level), lsq(ct.poly, 0, 1, level), lsq(ct.poly, 0, 1, level), &pq);
+      automorph(lsqp(r, 0, 2, level, level), lsqp(u, 0, 2, level, level), g, false);
+      rot[b] = r;
+    }
+    Poly acc = alloc(2, nqp, B);
+    bool acc_init = false;
+    Poly t = alloc(2, nqp, B);
+    Poly c = alloc(2, nqp, B);
+    Poly t1q = alloc(1, level + 1, B);
+    for (int j : T.giants) {
+      const std::vector<int>& bl = T.index.at(j);
+      bool first = true;
+      for (int b : bl) {
+        const int d = (j + b) & (N / 2 - 1);
+        const Plaintext& pt = T.diags.at(d);
+        LimbSet lp = lsqp(pt.poly, 0, 1, level, T.level, B);
+        lp.ncomp = 2;
+        lp.comp_stride = 0;  // same diagonal for both components
+        LimbSet lt = lsqp(t, 0, 2, level, level);
+        ew(first ? EW_MUL : EW_MULADD, lt, lp, lsqp(rot.at(b), 0, 2, level, level));
+        first = false;
+      }
+      LimbSet la = lsqp(acc, 0, 2, level, level);
+      if (j != 0) {
+        const u64 g = galois_element(j);
+        const Poly& key = galois_key(g);
+        moddown(t, 1, 1, level, level, lsq(t1q, 0, 1, level));
+        Poly Dj = decompose(lsq(t1q, 0, 1, level), level, B);
+        mac(c, Dj, key, level, false);
+        LimbSet c0 = lsqp(c, 0, 1, level, level);
+        ew(EW_ADD, c0, c0, lsqp(t, 0, 1, level, level));
+        automorph(la, lsqp(c, 0, 2, level, level), g, acc_init);
+      } else {
+        if (acc_init)
+          ew(EW_ADD, la, la, lsqp(t, 0, 2, level, level));
+        else
+          copy(la, lsqp(t, 0, 2, level, level));
+      }
+      acc_init = true;
+    }
+    Ciphertext out = new_ct(level, B, ct.scale * (long double)mods[T.level]);
+    if (!acc_init) throw std::runtime_error("linear transform without diagonals");
+    moddown(acc, 0, 2, level, level, lsq(out.poly, 0, 2, level));
+    return out;
+  }
+
+  // ---------------------------------------------------------------------------
+  // encoder / encryptor
+  // ---------------------------------------------------------------------------
+  // values: B images x nvals; mods: QP modulus index of each limb
+  Plaintext encode(const float* values, int nvals, int B, int level, long double scale, bool qp) {
+    const int n = N / 2;
+    if (nvals > n) throw std::runtime_error("too many values for the slot count");
+    std::vector<int> md = iota(0, level + 1);
+    if (qp)
+      for (int k = 0; k < K; ++k) md.push_back(L + k);
+    std::vector<u64> mv;
+    for (int m : md) mv.push_back(mods[m]);
+    const int nl = (int)md.size();
+    Plaintext pt;
+    pt.level = level;
+    pt.scale = scale;
+    pt.qp = qp;
+    pt.poly = alloc(1, nl, B);
+    std::vector<u64> host((size_t)nl * B * N);
+    std::vector<Cplx> v(n);
+    for (int b = 0; b < B; ++b) {
+      for (int i = 0; i < n; ++i) v[i] = Cplx{i < nvals ? (double)values[(size_t)b * nvals + i] : 0.0, 0.0};
+      fft->inverse(v);
+      for (int i = 0; i < n; ++i) {
+        fixed_point_crt(v[i].re, (double)scale, mv.data(), nl, host.data() + (size_t)b * N + i, (size_t)B * N);
+        fixed_point_crt(v[i].im, (double)scale, mv.data(), nl, host.data() + (size_t)b * N + i + n, (size_t)B * N);
+      }
+    }
+    upload(pt.poly, host);
+    ntt(ls(pt.poly, 0, 1, iota(0, nl), md), false);
+    return pt;
+  }
+
+  std::vector<float> decode(const Plaintext& pt) {
+    const int level = pt.level, B = pt.poly.B, n = N / 2, nl = level + 1;
+    Poly t = alloc(1, nl, B);
+    copy(lsq(t, 0, 1, level), lsq(pt.poly, 0, 1, level));
+    ntt(lsq(t, 0, 1, level), true);
+    std::vector<u64> host;
+    download(t, host);
+    // Garner constants
+    std::vector<std::vector<u64>> inv(nl, std::vector<u64>(nl));
+    for (int i = 0; i < nl; ++i)
+      for (int k = 0; k < i; ++k) inv[i][k] = hm_invmod(mods[k] % mods[i], mods[i]);
+    std::vector<u64> half(nl);
+    {
+      u64 rem = 0;
+      for (int i = nl - 1; i >= 0; --i) {
+        u128 cur = (u128)rem * mods[i] + (mods[i] - 1);
+        half[i] = (u64)(cur / 2);
+        rem = (u64)(cur % 2);
+      }
+    }
+    std::vector<float> out((size_t)B * n);
+    std::vector<Cplx> v(n);
+    std::vector<u64> d(nl), e(nl);
+    for (int b = 0; b < B; ++b) {
+      for (int i = 0; i < N; ++i) {
+        for (int j = 0; j < nl; ++j) {
+          u64 x = host[((size_t)j * B + b) * N + i];
+          for (int k = 0; k < j; ++k) {
+            const u64 qj = mods[j];
+            x = hm_mulmod((x + qj - d[k] % qj) % qj, inv[j][k], qj);
+          }
+          d[j] = x;
+        }
+        bool greater = false;
+        for (int j = nl - 1; j >= 0; --j)
+          if (d[j] != half[j]) {
+            greater = d[j] > half[j];
+            break;
+          }
+        long double val = 0, base = 1;
+        if (!greater) {
+          for (int j = 0; j < nl; ++j) val += (long double)d[j] * base, base *= (long double)mods[j];
+        } else {
+          for (int j = 0; j < nl; ++j) e[j] = mods[j] - 1 - d[j];
+          for (int j = 0; j < nl; ++j) {
+            if (e[j] + 1 < mods[j]) {
+              e[j] += 1;
+              break;
+            }
+            e[j] = 0;
+          }
+          for (int j = 0; j < nl; ++j) val += (long double)e[j] * base, base *= (long double)mods[j];
+          val = -val;
+        }
+        const double f = (double)(val / pt.scale);
+        if (i < n)
+          v[i].re = f;
+        else
+          v[i - n].im = f;
+      }
+      fft->forward(v);
+      for (int i = 0; i < n; ++i) out[(size_t)b * n + i] = (float)v[i].re;
+    }
+    return out;
+  }
+
+  Ciphertext encrypt(const Plaintext& pt) {
+    if (!have_pk) throw std::runtime_error("public key not generated");
+    const int level = pt.level, B = pt.poly.B, nl = level + 1;
+    // u (ternary), e0, e1 per image, coefficient domain -> NTT
+    Poly r = alloc(3, nl, B);
+    std::vector<u64> host((size_t)3 * nl * B * N);
+    std::vector<int> md = iota(0, nl);
+    std::vector<u64> blk((size_t)nl * N);
+    for (int c = 0; c < 3; ++c) {
+      for (int b = 0; b < B; ++b) {
+        auto v = c == 0 ? sample_ternary_uniform() : sample_gauss();
+        small_residues(v, md, blk.data());
+        for (int j = 0; j < nl; ++j)
+          memcpy(&host[(((size_t)c * nl + j) * B + b) * N], &blk[(size_t)j * N], N * 8);
+      }
+    }
+    upload(r, host);
+    ntt(lsq(r, 0, 3, level), false);
+    Ciphertext ct = new_ct(level, B, pt.scale);
+    LimbSet c0 = lsq(ct.poly, 0, 1, level), c1 = lsq(ct.poly, 1, 1, level);
+    ew(EW_MUL, c0, lsq(r, 0, 1, level), lsq(pk, 0, 1, level, B));
+    ew(EW_ADD, c0, c0, lsq(r, 1, 1, level));
+    ew(EW_ADD, c0, c0, lsq(pt.poly, 0, 1, level, B));
+    ew(EW_MUL, c1, lsq(r, 0, 1, level), lsq(pk, 1, 1, level, B));
+    ew(EW_ADD, c1, c1, lsq(r, 2, 1, level));
+    return ct;
+  }
+
+  Plaintext decrypt(const Ciphertext& ct) {
+    if (!have_sk) throw std::runtime_error("secret key not generated");
+    const int level = ct.level, B = ct.poly.B;
+    Plaintext pt;
+    pt.level = level;
+    pt.scale = ct.scale;
+    pt.poly = alloc(1, level + 1, B);
+    LimbSet p = lsq(pt.poly, 0, 1, level);
+    ew(EW_MUL, p, lsq(ct.poly, 1, 1, level), lsq(sk, 0, 1, level, B));
+    ew(EW_ADD, p, p, lsq(ct.poly, 0, 1, level));
+    return pt;
+  }
+
+  // rounded integer constant c -> residues at `level`
+  std::vector<u64> const_residues(long double c, int level) const {
+    std::vector<u64> r;
+    const bool neg = c < 0;
+    long double a = neg ? -c : c;
+    // a < 2^64 required
+    if (a >= 18446744073709551615.0L) throw std::runtime_error("scalar constant too large");
+    const u64 v = (u64)a;
+    for (int j = 0; j <= level; ++j) {
+      const u64 x = v % mods[j];
+      r.push_back(neg ? (x ? mods[j] - x : 0) : x);
+    }
+    return r;
+  }
+};
+
+static std::unique_ptr<Context> g;
+static std::recursive_mutex g_mu;
+
+static Context& ctx() {
+  if (!g) throw std::runtime_error("scheme not initialised: call NewScheme first");
+  return *g;
+}
+
+}  // namespace orion
+
+using namespace orion;
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+#define API_BEGIN                                  \
+  std::lock_guard<std::recursive_mutex> lk_(g_mu); \
+  try {
+#define API_END(errval)          \
+  }                              \
+  catch (const std::exception& e) { \
+    g_last_error = e.what();     \
+    return errval;               \
+  }
+#define API_END_VOID                \
+  }                                 \
+  catch (const std::exception& e) { \
+    g_last_error = e.what();        \
+  }
+
+template <class T, class U>
+static U* to_c_array(const std::vector<T>& v, unsigned long* len) {
+  *len = v.size();
+  if (v.empty()) return nullptr;
+  U* p = (U*)malloc(sizeof(U) * v.size());
+  for (size_t i = 0; i < v.size(); ++i) p[i] = (U)v[i];
+  return p;
+}
+
+extern "C" {
+
+const char* OrionHipLastError(void) { return g_last_error.c_str(); }
+void OrionHipClearError(void) { g_last_error.clear(); }
+
+static hipStream_t g_user_stream = nullptr;
+static unsigned long g_seed = 0x0123456789abcdefull;
+
+int OrionHipSetDevice(int device) {
+  API_BEGIN
+  HIPCHK(hipSetDevice(device));
+  return 0;
+  API_END(-1)
+}
+
+void OrionHipSetSeed(unsigned long seed) {
+  API_BEGIN
+  g_seed = seed;
+  if (g) g->prng = Prng(seed);
+  API_END_VOID
+}
+
+void OrionHipSetStream(void* s) {
+  API_BEGIN
+  g_user_stream = (hipStream_t)s;
+  if (g) {
+    if (g->own_stream && g->stream) hipStreamDestroy(g->stream);
+    g->own_stream = false;
+    g->stream = (hipStream_t)s;
+    if (!s) {
+      HIPCHK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+      g->own_stream = true;
+    }
+  }
+  API_END_VOID
+}
+
+void* OrionHipGetStream(void) { return g ? (void*)g->stream : nullptr; }
+
+int OrionHipSynchronize(void) {
+  API_BEGIN
+  HIPCHK(hipStreamSynchronize(ctx().stream));
+  return 0;
+  API_END(-1)
+}
+
+int OrionHipLogN(void) { return g ? g->logN : -1; }
+int OrionHipNumQ(void) { return g ? g->L : -1; }
+int OrionHipNumP(void) { return g ? g->K : -1; }
+unsigned long OrionHipModulus(int i) { return (g && i >= 0 && i < (int)g->mods.size()) ? g->mods[i] : 0; }
+
+void NewScheme(int logN, int* logQ, int lenQ, int* logP, int lenP, int logScale, int h, char* ringType,
+               char* keysPath, char* ioMode) {
+  API_BEGIN
+  (void)keysPath;
+  (void)ioMode;
+  std::string rt = ringType ? ringType : "standard";
+  for (auto& ch : rt) ch = (char)tolower(ch);
+  if (rt != "standard")
+    throw std::runtime_error("ring type '" + rt + "' not supported by the HIP backend (Standard ring only)");
+  g.reset();
+  g.reset(new Context());
+  g->stream = g_user_stream;
+  g->prng = Prng(g_seed);
+  g->setup(logN, std::vector<int>(logQ, logQ + lenQ), std::vector<int>(logP, logP + lenP), logScale, h);
+  API_END_VOID
+}
+
+void DeleteScheme(void) {
+  API_BEGIN
+  g.reset();
+  API_END_VOID
+}
+
+void FreeCArray(void* p) { free(p); }
+
+void DeletePlaintext(int id) {
+  API_BEGIN
+  ctx().pts.del(id);
+  API_END_VOID
+}
+void DeleteCiphertext(int id) {
+  API_BEGIN
+  ctx().cts.del(id);
+  API_END_VOID
+}
+
+static unsigned long scale_u64(long double s) {
+  if (s >= 18446744073709551615.0L) return ~0ul;
+  return (unsigned long)s;
+}
+unsigned long GetPlaintextScale(int id) {
+  API_BEGIN
+  return scale_u64(ctx().pts.get(id).scale);
+  API_END(0)
+}
+unsigned long GetCiphertextScale(int id) {
+  API_BEGIN
+  return scale_u64(ctx().cts.get(id).scale);
+  API_END(0)
+}
+double GetCiphertextScaleF(int id) {
+  API_BEGIN
+  return (double)ctx().cts.get(id).scale;
+  API_END(0)
+}
+void SetPlaintextScale(int id, unsigned long s) {
+  API_BEGIN
+  ctx().pts.get(id).scale = (long double)s;
+  API_END_VOID
+}
+void SetCiphertextScale(int id, unsigned long s) {
+  API_BEGIN
+  ctx().cts.get(id).scale = (long double)s;
+  API_END_VOID
+}
+int GetPlaintextLevel(int id) {
+  API_BEGIN
+  return ctx().pts.get(id).level;
+  API_END(-1)
+}
+int GetCiphertextLevel(int id) {
+  API_BEGIN
+  return ctx().cts.get(id).level;
+  API_END(-1)
+}
+int GetPlaintextSlots(int id) {
+  API_BEGIN
+  ctx().pts.get(id);
+  return ctx().N / 2;
+  API_END(-1)
+}
+int GetCiphertextSlots(int id) {
+  API_BEGIN
+  ctx().cts.get(id);
+  return ctx().N / 2;
+  API_END(-1)
+}
+int GetCiphertextDegree(int id) {
+  API_BEGIN
+  ctx().cts.get(id);
+  return 1;
+  API_END(-1)
+}
+int GetCiphertextBatch(int id) {
+  API_BEGIN
+  return ctx().cts.get(id).poly.B;
+  API_END(-1)
+}
+int GetPlaintextBatch(int id) {
+  API_BEGIN
+  return ctx().pts.get(id).poly.B;
+  API_END(-1)
+}
+ArrayResultUInt64 GetModuliChain(void) {
+  ArrayResultUInt64 r{nullptr, 0};
+  API_BEGIN
+  std::vector<u64> q(ctx().mods.begin(), ctx().mods.begin() + ctx().L);
+  r.Data = to_c_array<u64, unsigned long>(q, &r.Length);
+  return r;
+  API_END(r)
+}
+ArrayResultInt GetLivePlaintexts(void) {
+  ArrayResultInt r{nullptr, 0};
+  API_BEGIN
+  r.Data = to_c_array<int, int>(ctx().pts.live(), &r.Length);
+  return r;
+  API_END(r)
+}
+ArrayResultInt GetLiveCiphertexts(void) {
+  ArrayResultInt r{nullptr, 0};
+  API_BEGIN
+  r.Data = to_c_array<int, int>(ctx().cts.live(), &r.Length);
+  return r;
+  API_END(r)
+}
+int CloneCiphertext(int id) {
+  API_BEGIN
+  Context& c = ctx();
+  return c.cts.add(c.clone(c.cts.get(id)));
+  API_END(-1)
+}
+
+// ---- keys ----
+void NewKeyGenerator(void) {}
+void GenerateSecretKey(void) {
+  API_BEGIN
+  ctx().gen_secret();
+  API_END_VOID
+}
+void GeneratePublicKey(void) {
+  API_BEGIN
+  ctx().gen_public();
+  API_END_VOID
+}
+void GenerateRelinearizationKey(void) {
+  API_BEGIN
+  ctx().gen_relin();
+  API_END_VOID
+}
+void GenerateEvaluationKeys(void) {}
+
+ArrayResultByte SerializeSecretKey(void) {
+  ArrayResultByte r{nullptr, 0};
+  API_BEGIN
+  Context& c = ctx();
+  if (!c.have_sk) throw std::runtime_error("secret key not generated");
+  std::vector<u64> host;
+  c.download(c.sk, host);
+  std::vector<char> bytes(16 + host.size() * 8);
+  const u64 hdr[2] = {0x4f52494f4e534b31ull /* "ORIONSK1" */, (u64)host.size()};
+  memcpy(bytes.data(), hdr, 16);
+  memcpy(bytes.data() + 16, host.data(), host.size() * 8);
+  r.Data = to_c_array<char, char>(bytes, &r.Length);
+  return r;
+  API_END(r)
+}
+void LoadSecretKey(char* data, unsigned long len) {
+  API_BEGIN
+  Context& c = ctx();
+  u64 hdr[2];
+  if (len < 16) throw std::runtime_error("secret key blob too short");
+  memcpy(hdr, data, 16);
+  const size_t n = (size_t)(c.L + c.K) * c.N;
+  if (hdr[0] != 0x4f52494f4e534b31ull || hdr[1] != n || len != 16 + n * 8)
+    throw std::runtime_error("secret key blob does not match the scheme");
+  std::vector<u64> host(n);
+  memcpy(host.data(), data + 16, n * 8);
+  c.sk = c.alloc(1, c.L + c.K, 1);
+  c.upload(c.sk, host);
+  c.have_sk = true;
+  API_END_VOID
+}
+
+// ---- encoder / encryptor ----
+void NewEncoder(void) {}
+int Encode(float* values, int n, int level, unsigned long scale) {
+  API_BEGIN
+  Context& c = ctx();
+  if (level < 0 || level >= c.L) throw std::runtime_error("invalid level");
+  return c.pts.add(c.encode(values, n, 1, level, (long double)scale, false));
+  API_END(-1)
+}
+int EncodeBatch(float* values, int n, int B, int level, unsigned long scale) {
+  API_BEGIN
+  Context& c = ctx();
+  if (level < 0 || level >= c.L || B < 1) throw std::runtime_error("invalid level/batch");
+  return c.pts.add(c.encode(values, n, B, level, (long double)scale, false));
+  API_END(-1)
+}
+ArrayResultFloat Decode(int id) {
+  ArrayResultFloat r{nullptr, 0};
+  API_BEGIN
+  Context& c = ctx();
+  std::vector<float> v = c.decode(c.pts.get(id));
+  r.Data = to_c_array<float, float>(v, &r.Length);
+  return r;
+  API_END(r)
+}
+void NewEncryptor(void) {}
+void NewDecryptor(void) {}
+int Encrypt(int pt) {
+  API_BEGIN
+  Context& c = ctx();
+  return c.cts.add(c.encrypt(c.pts.get(pt)));
+  API_END(-1)
+}
+int Decrypt(int ct) {
+  API_BEGIN
+  Context& c = ctx();
+  return c.pts.add(c.decrypt(c.cts.get(ct)));
+  API_END(-1)
+}
+
+// ---- evaluator ----
+void NewEvaluator(void) {
+  API_BEGIN
+  Context& c = ctx();
+  for (int i = 1; i < c.N / 2; i *= 2) c.gen_galois(c.galois_element(i));  // evaluator.go:25-31
+  API_END_VOID
+}
+void AddRotationKey(int k) {
+  API_BEGIN
+  Context& c = ctx();
+  c.gen_galois(c.galois_element(k));
+  API_END_VOID
+}
+unsigned long GaloisElement(int k) {
+  API_BEGIN
+  return ctx().galois_element(k);
+  API_END(0)
+}
+
+int Negate(int id) {
+  API_BEGIN
+  Context& c = ctx();
+  Ciphertext& a = c.cts.get(id);
+  Ciphertext o = c.new_ct(a.level, a.poly.B, a.scale);
+  c.ew1(EW_NEG, c.lsq(o.poly, 0, 2, a.level), c.lsq(a.poly, 0, 2, a.level));
+  return c.cts.add(std::move(o));
+  API_END(-1)
+}
+int Rotate(int id, int k) {
+  API_BEGIN
+  Context& c = ctx();
+  Ciphertext& a = c.cts.get(id);
+  a = c.rotate(a, k);
+  return id;
+  API_END(-1)
+}
+int RotateNew(int id, int k) {
+  API_BEGIN
+  Context& c = ctx();
+  return c.cts.add(c.rotate(c.cts.get(id), k));
+  API_END(-1)
+}
+int Rescale(int id) {
+  API_BEGIN
+  Context& c = ctx();
+  c.rescale_inplace(c.cts.get(id));
+  return id;
+  API_END(-1)
+}
+int RescaleNew(int id) {  // evaluator.go:92-99: rescales the input in place, returns a copy
+  API_BEGIN
+  Context& c = ctx();
+  Ciphertext& a = c.cts.get(id);
+  c.rescale_inplace(a);
+  return c.cts.add(c.clone(a));
+  API_END(-1)
+}
+
+static Ciphertext add_scalar(Context& c, const Ciphertext& a, float v, bool inplace_target, Ciphertext* dst) {
+  (void)inplace_target;
+  long double x = (long double)v * a.scale;
+  long double r = x < 0 ? -floorl(-x + 0.5L) : floorl(x + 0.5L);
+  std::vector<u64> k = c.const_residues(r, a.level);
+  Ciphertext o = dst ? Ciphertext() : c.new_ct(a.level, a.poly.B, a.scale);
+  Ciphertext& out = dst ? *dst : o;
+  c.ew1(EW_ADDC, c.lsq(out.poly, 0, 1, a.level), c.lsq(a.poly, 0, 1, a.level), &k);
+  if (!dst) c.copy(c.lsq(out.poly, 1, 1, a.level), c.lsq(a.poly, 1, 1, a.level));
+  return o;
+}
+int AddScalar(int id, float v) {
+  API_BEGIN
+  Context& c = ctx();
+  Ciphertext& a = c.cts.get(id);
+  add_scalar(c, a, v, true, &a);
+  return id;
+  API_END(-1)
+}
+int AddScalarNew(int id, float v) {
+  API_BEGIN
+  Context& c = ctx();
+  return c.cts.add(add_scalar(c, c.cts.get(id), v, false, nullptr));
+  API_END(-1)
+}
+int SubScalar(int id, float v) { return AddScalar(id, -v); }
+int SubScalarNew(int id, float v) { return AddScalarNew(id, -v); }
+
+static void mul_const(Context& c, const Ciphertext& a, Ciphertext& out, const std::vector<u64>& k) {
+  c.ew1(EW_SCALE, c.lsq(out.poly, 0, 2, a.level), c.lsq(a.poly, 0, 2, a.level), &k);
+}
+int MulScalarInt(int id, int v) {
+  API_BEGIN
+  Context& c = ctx();
+  Ciphertext& a = c.cts.get(id);
+  mul_const(c, a, a, c.const_residues((long double)v, a.level));
+  return id;
+  API_END(-1)
+}
+int MulScalarIntNew(int id, int v) {
+  API_BEGIN
+  Context& c = ctx();
+  Ciphertext& a = c.cts.get(id);
+  Ciphertext o = c.new_ct(a.level, a.poly.B, a.scale);
+  mul_const(c, a, o, c.const_residues((long double)v, a.level));
+  return c.cts.add(std::move(o));
+  API_END(-1)
+}
+// non-integral constants are scaled by q_level (Lattigo getConstantAndScale)
+static void mul_float(Context& c, const Ciphertext& a, Ciphertext& out, float v) {
+  const double dv = (double)v;
+  if (dv == floor(dv)) {
+    mul_const(c, a, out, c.const_residues((long double)dv, a.level));
+    out.scale = a.scale;
+    return;
+  }
+  const long double ql = (long double)c.mods[a.level];
+  long double x = (long double)dv * ql;
+  long double r = x < 0 ? -floorl(-x + 0.5L) : floorl(x + 0.5L);
+  mul_const(c, a, out, c.const_residues(r, a.level));
+  out.scale = a.scale * ql;
+}
+int MulScalarFloat(int id, float v) {
+  API_BEGIN
+  Context& c = ctx();
+  Ciphertext& a = c.cts.get(id);
+  mul_float(c, a, a, v);
+  return id;
+  API_END(-1)
+}
+int MulScalarFloatNew(int id, float v) {
+  API_BEGIN
+  Context& c = ctx();
+  Ciphertext& a = c.cts.get(id);
+  Ciphertext o = c.new_ct(a.level, a.poly.B, a.scale);
+  mul_float(c, a, o, v);
+  return c.cts.add(std::move(o));
+  API_END(-1)
+}
+
+// ct (+/-) pt
+static int ct_pt_op(int id, int pid, int op, bool inplace) {
+  Context& c = ctx();
+  Ciphertext& a = c.cts.get(id);
+  const Plaintext& p = c.pts.get(pid);
+  const int level = std::min(a.level, p.level);
+  const int B = c.batch_of(a.poly.B, p.poly.B);
+  if (inplace && B != a.poly.B) throw std::runtime_error("in-place op cannot grow the batch");
+  Ciphertext o;
+  Ciphertext* out = &a;
+  if (!inplace) {
+    o = c.new_ct(level, B, a.scale);
+    out = &o;
+  }
+  out->level = level;
+  c.add_like(*out, a, c.lsq(p.poly, 0, 1, level, B), p.scale, op);
+  return inplace ? id : c.cts.add(std::move(o));
+}
+int AddPlaintext(int id, int pt) {
+  API_BEGIN
+  return ct_pt_op(id, pt, EW_ADD, true);
+  API_END(-1)
+}
+int AddPlaintextNew(int id, int pt) {
+  API_BEGIN
+  return ct_pt_op(id, pt, EW_ADD, false);
+  API_END(-1)
+}
+int SubPlaintext(int id, int pt) {
+  API_BEGIN
+  return ct_pt_op(id, pt, EW_SUB, true);
+  API_END(-1)
+}
+int SubPlaintextNew(int id, int pt) {
+  API_BEGIN
+  return ct_pt_op(id, pt, EW_SUB, false);
+  API_END(-1)
+}
+static int ct_pt_mul(int id, int pid, bool inplace) {
+  Context& c = ctx();
+  Ciphertext& a = c.cts.get(id);
+  const Plaintext& p = c.pts.get(pid);
+  const int level = std::min(a.level, p.level);
+  const int B = c.batch_of(a.poly.B, p.poly.B);
+  if (inplace && B != a.poly.B) throw std::runtime_error("in-place op cannot grow the batch");
+  Ciphertext o;
+  Ciphertext* out = &a;
+  if (!inplace) {
+    o = c.new_ct(level, B, a.scale);
+    out = &o;
+  }
+  LimbSet lp = c.lsq(p.poly, 0, 1, level, B);
+  lp.ncomp = 2;
+  lp.comp_stride = 0;
+  c.ew(EW_MUL, c.lsq(out->poly, 0, 2, level), c.lsq(a.poly, 0, 2, level, B), lp);
+  out->level = level;
+  out->scale = a.scale * p.scale;
+  return inplace ? id : c.cts.add(std::move(o));
+}
+int MulPlaintext(int id, int pt) {
+  API_BEGIN
+  return ct_pt_mul(id, pt, true);
+  API_END(-1)
+}
+int MulPlaintextNew(int id, int pt) {
+  API_BEGIN
+  return ct_pt_mul(id, pt, false);
+  API_END(-1)
+}
+static int ct_ct_op(int i0, int i1, int op, bool inplace) {
+  Context& c = ctx();
+  Ciphertext& a = c.cts.get(i0);
+  const Ciphertext& b = c.cts.get(i1);
+  const int level = std::min(a.level, b.level);
+  const int B = c.batch_of(a.poly.B, b.poly.B);
+  if (inplace && B != a.poly.B) throw std::runtime_error("in-place op cannot grow the batch");
+  Ciphertext o;
+  Ciphertext* out = &a;
+  if (!inplace) {
+    o = c.new_ct(level, B, a.scale);
+    out = &o;
+  }
+  out->level = level;
+  c.add_like(*out, a, c.lsq(b.poly, 0, 2, level, B), b.scale, op);
+  return inplace ? i0 : c.cts.add(std::move(o));
+}
+int AddCiphertext(int a, int b) {
+  API_BEGIN
+  return ct_ct_op(a, b, EW_ADD, true);
+  API_END(-1)
+}
+int AddCiphertextNew(int a, int b) {
+  API_BEGIN
+  return ct_ct_op(a, b, EW_ADD, false);
+  API_END(-1)
+}
+int SubCiphertext(int a, int b) {
+  API_BEGIN
+  return ct_ct_op(a, b, EW_SUB, true);
+  API_END(-1)
+}
+int SubCiphertextNew(int a, int b) {
+  API_BEGIN
+  return ct_ct_op(a, b, EW_SUB, false);
+  API_END(-1)
+}
+int MulRelinCiphertext(int a, int b) {
+  API_BEGIN
+  Context& c = ctx();
+  Ciphertext r = c.mul_relin(c.cts.get(a), c.cts.get(b));
+  if (r.poly.B != c.cts.get(a).poly.B) throw std::runtime_error("in-place op cannot grow the batch");
+  c.cts.get(a) = std::move(r);
+  return a;
+  API_END(-1)
+}
+int MulRelinCiphertextNew(int a, int b) {
+  API_BEGIN
+  Context& c = ctx();
+  return c.cts.add(c.mul_relin(c.cts.get(a), c.cts.get(b)));
+  API_END(-1)
+}
+
+// ---- linear transforms ----
+void NewLinearTransformEvaluator(void) {}
+
+static void bsgs_split(int rot, int slots, int N1, int* giant, int* baby) {
+  rot &= (slots - 1);
+  *giant = ((rot / N1) * N1) & (slots - 1);
+  *baby = rot & (N1 - 1);
+}
+// Lattigo lintrans FindBestBSGSRatio
+static int find_best_n1(const std::vector<int>& idx, int slots, int logMaxRatio) {
+  const double maxRatio = (double)(1 << logMaxRatio);
+  for (int N1 = 1; N1 < slots; N1 <<= 1) {
+    std::set<int> gs, bs;
+    for (int d : idx) {
+      int gi, bi;
+      bsgs_split(d, slots, N1, &gi, &bi);
+      gs.insert(gi);
+      bs.insert(bi);
+    }
+    const double r = (double)((int)bs.size() - 1) / (double)((int)gs.size() - 1);
+    if (r == maxRatio) return N1;
+    if (r > maxRatio) return N1 / 2;
+  }
+  return 1;
+}
+
+int GenerateLinearTransform(int* diagIdx, int nIdx, float* data, int nData, int level, float ratio,
+                            char* ioMode) {
+  API_BEGIN
+  Context& c = ctx();
+  (void)ioMode;
+  const int slots = c.N / 2;
+  if ((long)nIdx * slots != (long)nData) throw std::runtime_error("diagonal data length != nIdx * slots");
+  if (level < 0 || level >= c.L) throw std::runtime_error("invalid level");
+  LinTrans T;
+  T.level = level;
+  T.ratio = ratio;
+  T.idx.assign(diagIdx, diagIdx + nIdx);
+  const int logRatio = (int)log((double)ratio);  // lineartransform.go:67 (natural log)
+  if (logRatio < 0) throw std::runtime_error("naive (non-BSGS) linear transforms are not supported");
+  T.N1 = find_best_n1(T.idx, slots, logRatio);
+  std::set<int> seenb;
+  for (int d : T.idx) {
+    int gi, bi;
+    bsgs_split(d, slots, T.N1, &gi, &bi);
+    T.index[gi].push_back(bi);
+    if (!seenb.count(bi)) {
+      seenb.insert(bi);
+      T.babies.push_back(bi);
+    }
+  }
+  for (auto& kv : T.index) {
+    std::sort(kv.second.begin(), kv.second.end());
+    T.giants.push_back(kv.first);
+  }
+  std::vector<float> vec(slots);
+  for (int i = 0; i < nIdx; ++i) {
+    int gi, bi;
+    bsgs_split(diagIdx[i], slots, T.N1, &gi, &bi);
+    const float* v = data + (size_t)i * slots;
+    for (int s = 0; s < slots; ++s) vec[s] = v[((s - gi) % slots + slots) % slots];  // rotate right by giant
+    T.diags[diagIdx[i] & (slots - 1)] = c.encode(vec.data(), slots, 1, level, (long double)c.mods[level], true);
+  }
+  return c.lts.add(std::move(T));
+  API_END(-1)
+}
+
+int GetLinearTransformN1(int id) {
+  API_BEGIN
+  return ctx().lts.get(id).N1;
+  API_END(-1)
+}
+
+int EvaluateLinearTransform(int tid, int cid) {
+  API_BEGIN
+  Context& c = ctx();
+  return c.cts.add(c.eval_lt(c.lts.get(tid), c.cts.get(cid)));
+  API_END(-1)
+}
+void DeleteLinearTransform(int id) {
+  API_BEGIN
+  ctx().lts.del(id);
+  API_END_VOID
+}
+ArrayResultInt GetLinearTransformRotationKeys(int id) {
+  ArrayResultInt r{nullptr, 0};
+  API_BEGIN
+  Context& c = ctx();
+  const LinTrans& T = c.lts.get(id);
+  std::vector<int> rots(T.giants.begin(), T.giants.end());
+  for (int b : T.babies)
+    if (std::find(rots.begin(), rots.end(), b) == rots.end()) rots.push_back(b);
+  std::vector<int> gels;
+  for (int k : rots) gels.push_back((int)c.galois_element(k));
+  r.Data = to_c_array<int, int>(gels, &r.Length);
+  return r;
+  API_END(r)
+}
+void GenerateLinearTransformRotationKey(int galEl) {
+  API_BEGIN
+  ctx().gen_galois((u64)(unsigned)galEl);
+  API_END_VOID
+}
+void GenerateConsolidatedRotationKeys(int* galEls, int n) {
+  API_BEGIN
+  for (int i = 0; i < n; ++i) ctx().gen_galois((u64)(unsigned)galEls[i]);
+  API_END_VOID
+}
+ArrayResultByte GenerateAndSerializeRotationKey(int galEl) {
+  ArrayResultByte r{nullptr, 0};
+  API_BEGIN
+  Context& c = ctx();
+  c.gen_galois((u64)(unsigned)galEl);
+  std::vector<u64> host;
+  c.download(c.gks.at((u64)(unsigned)galEl), host);
+  std::vector<char> bytes(host.size() * 8);
+  memcpy(bytes.data(), host.data(), bytes.size());
+  r.Data = to_c_array<char, char>(bytes, &r.Length);
+  return r;
+  API_END(r)
+}
+void LoadRotationKey(char* data, unsigned long len, unsigned long galEl) {
+  API_BEGIN
+  Context& c = ctx();
+  Poly k = c.alloc(2 * c.dnum, c.L + c.K, 1);
+  if (len != (unsigned long)k.ncomp * k.nlimb * c.N * 8) throw std::runtime_error("rotation key blob size mismatch");
+  std::vector<u64> host(len / 8);
+  memcpy(host.data(), data, len);
+  c.upload(k, host);
+  c.gks[galEl] = k;
+  API_END_VOID
+}
+ArrayResultByte SerializeDiagonal(int tid, int diagIdx) {
+  ArrayResultByte r{nullptr, 0};
+  API_BEGIN
+  Context& c = ctx();
+  const Plaintext& p = c.lts.get(tid).diags.at(diagIdx & (c.N / 2 - 1));
+  std::vector<u64> host;
+  c.download(p.poly, host);
+  std::vector<char> bytes(host.size() * 8);
+  memcpy(bytes.data(), host.data(), bytes.size());
+  r.Data = to_c_array<char, char>(bytes, &r.Length);
+  return r;
+  API_END(r)
+}
+void LoadPlaintextDiagonal(char* data, unsigned long len, int tid, unsigned long diagIdx) {
+  API_BEGIN
+  Context& c = ctx();
+  LinTrans& T = c.lts.get(tid);
+  Plaintext p;
+  p.level = T.level;
+  p.qp = true;
+  p.scale = (long double)c.mods[T.level];
+  p.poly = c.alloc(1, T.level + 1 + c.K, 1);
+  if (len != (unsigned long)p.poly.nlimb * c.N * 8) throw std::runtime_error("diagonal blob size mismatch");
+  std::vector<u64> host(len / 8);
+  memcpy(host.data(), data, len);
+  c.upload(p.poly, host);
+  T.diags[(int)diagIdx & (c.N / 2 - 1)] = p;
+  API_END_VOID
+}
+void RemovePlaintextDiagonals(int tid) {
+  API_BEGIN
+  ctx().lts.get(tid).diags.clear();
+  API_END_VOID
+}
+void RemoveRotationKeys(void) {
+  API_BEGIN
+  ctx().gks.clear();
+  API_END_VOID
+}
+
+// ---- SURVEY §8f "next": polynomial evaluation, minimax, bootstrapping ----
+void NewPolynomialEvaluator(void) {}
+int GenerateMonomial(float*, int) {
+  g_last_error = "GenerateMonomial: polynomial evaluation is not implemented in the HIP backend yet";
+  return -1;
+}
+int GenerateChebyshev(float*, int) {
+  g_last_error = "GenerateChebyshev: polynomial evaluation is not implemented in the HIP backend yet";
+  return -1;
+}
+int EvaluatePolynomial(int, int, unsigned long) {
+  g_last_error = "EvaluatePolynomial: not implemented in the HIP backend yet";
+  return -1;
+}
+ArrayResultDouble GenerateMinimaxSignCoeffs(int*, int, int, int, int, int) {
+  g_last_error = "GenerateMinimaxSignCoeffs: not implemented in the HIP backend yet";
+  return ArrayResultDouble{nullptr, 0};
+}
+void NewBootstrapper(int*, int, int) { g_last_error = "NewBootstrapper: bootstrapping is not implemented yet"; }
+int Bootstrap(int, int) {
+  g_last_error = "Bootstrap: bootstrapping is not implemented in the HIP backend yet";
+  return -1;
+}
+void DeleteBootstrappers(void) {}
+
+// ---- import / export ----
+static void to_canonical(const std::vector<u64>& dev, int ncomp, int nl, int B, int N, unsigned long* out) {
+  // device [c][l][b][n] -> host [b][c][l][n]
+  for (int c = 0; c < ncomp; ++c)
+    for (int l = 0; l < nl; ++l)
+      for (int b = 0; b < B; ++b)
+        memcpy(out + (((size_t)b * ncomp + c) * nl + l) * N, dev.data() + (((size_t)c * nl + l) * B + b) * N, N * 8);
+}
+static std::vector<u64> from_canonical(const unsigned long* in, int ncomp, int nl, int B, int N) {
+  std::vector<u64> dev((size_t)ncomp * nl * B * N);
+  for (int c = 0; c < ncomp; ++c)
+    for (int l = 0; l < nl; ++l)
+      for (int b = 0; b < B; ++b)
+        memcpy(dev.data() + (((size_t)c * nl + l) * B + b) * N, in + (((size_t)b * ncomp + c) * nl + l) * N, N * 8);
+  return dev;
+}
+int ImportCiphertext(const unsigned long* data, int B, int level, double scale) {
+  API_BEGIN
+  Context& c = ctx();
+  Ciphertext ct = c.new_ct(level, B, (long double)scale);
+  c.upload(ct.poly, from_canonical(data, 2, level + 1, B, c.N));
+  return c.cts.add(std::move(ct));
+  API_END(-1)
+}
+int ExportCiphertext(int id, unsigned long* out, unsigned long n) {
+  API_BEGIN
+  Context& c = ctx();
+  const Ciphertext& ct = c.cts.get(id);
+  const int nl = ct.level + 1, B = ct.poly.B;
+  if (n != (unsigned long)B * 2 * nl * c.N) throw std::runtime_error("export buffer size mismatch");
+  Poly t = c.alloc(2, nl, B);
+  c.copy(c.lsq(t, 0, 2, ct.level), c.lsq(ct.poly, 0, 2, ct.level));
+  std::vector<u64> host;
+  c.download(t, host);
+  to_canonical(host, 2, nl, B, c.N, out);
+  return 0;
+  API_END(-1)
+}
+int ImportPlaintext(const unsigned long* data, int B, int level, double scale) {
+  API_BEGIN
+  Context& c = ctx();
+  Plaintext p;
+  p.level = level;
+  p.scale = (long double)scale;
+  p.poly = c.alloc(1, level + 1, B);
+  c.upload(p.poly, from_canonical(data, 1, level + 1, B, c.N));
+  return c.pts.add(std::move(p));
+  API_END(-1)
+}
+int ExportPlaintext(int id, unsigned long* out, unsigned long n) {
+  API_BEGIN
+  Context& c = ctx();
+  const Plaintext& p = c.pts.get(id);
+  const int nl = p.poly.nlimb, B = p.poly.B;
+  if (n != (unsigned long)B * nl * c.N) throw std::runtime_error("export buffer size mismatch");
+  std::vector<u64> host;
+  c.download(p.poly, host);
+  to_canonical(host, 1, nl, B, c.N, out);
+  return 0;
+  API_END(-1)
+}
+static int export_poly(const Poly& p, unsigned long* out, unsigned long n) {
+  Context& c = ctx();
+  std::vector<u64> host;
+  c.download(p, host);
+  if (n != host.size()) throw std::runtime_error("export buffer size mismatch");
+  memcpy(out, host.data(), n * 8);
+  return 0;
+}
+int ExportSecretKey(unsigned long* out, unsigned long n) {
+  API_BEGIN
+  if (!ctx().have_sk) throw std::runtime_error("no secret key");
+  return export_poly(ctx().sk, out, n);
+  API_END(-1)
+}
+int ExportRelinKey(unsigned long* out, unsigned long n) {
+  API_BEGIN
+  if (!ctx().have_rlk) throw std::runtime_error("no relinearization key");
+  return export_poly(ctx().rlk, out, n);
+  API_END(-1)
+}
+int ExportGaloisKey(unsigned long galEl, unsigned long* out, unsigned long n) {
+  API_BEGIN
+  Context& c = ctx();
+  auto it = c.gks.find(galEl);
+  if (it == c.gks.end()) throw std::runtime_error("no galois key for element " + std::to_string(galEl));
+  return export_poly(it->second, out, n);
+  API_END(-1)
+}
+int ExportLinearTransformDiagonal(int tid, int diagIdx, unsigned long* out, unsigned long n) {
+  API_BEGIN
+  Context& c = ctx();
+  return export_poly(c.lts.get(tid).diags.at(diagIdx & (c.N / 2 - 1)).poly, out, n);
+  API_END(-1)
+}
+
+// ---- key bundle for RCCL broadcast ----
+// layout: header u64[4] {magic, ngk, withSecret, haveRlk}, galEls[ngk], then
+// pk, rlk, gk_0..gk_{ngk-1}, [sk] as raw device polys
+unsigned long KeyBundleBytes(int withSecret) {
+  API_BEGIN
+  Context& c = ctx();
+  const size_t key = (size_t)2 * c.dnum * (c.L + c.K) * c.N * 8, pk = (size_t)2 * (c.L + c.K) * c.N * 8,
+               sk = (size_t)(c.L + c.K) * c.N * 8;
+  size_t hdr = (4 + c.gks.size()) * 8;
+  hdr = (hdr + 255) & ~(size_t)255;
+  return hdr + pk + (c.have_rlk ? key : 0) + c.gks.size() * key + (withSecret ? sk : 0);
+  API_END(0)
+}
+int ExportKeyBundle(void* dptr, int withSecret) {
+  API_BEGIN
+  Context& c = ctx();
+  if (!c.have_pk) throw std::runtime_error("no public key");
+  if (withSecret && !c.have_sk) throw std::runtime_error("no secret key");
+  std::vector<u64> hdr = {0x4f52494f4e4b4231ull, (u64)c.gks.size(), (u64)(withSecret ? 1 : 0), (u64)c.have_rlk};
+  for (auto& kv : c.gks) hdr.push_back(kv.first);
+  size_t off = ((hdr.size() * 8) + 255) & ~(size_t)255;
+  char* d = (char*)dptr;
+  HIPCHK(hipMemcpyAsync(d, hdr.data(), hdr.size() * 8, hipMemcpyHostToDevice, c.stream));
+  auto put = [&](const Poly& p) {
+    const size_t b = (size_t)p.ncomp * p.nlimb * p.B * c.N * 8;
+    HIPCHK(hipMemcpyAsync(d + off, p.ptr(), b, hipMemcpyDeviceToDevice, c.stream));
+    off += b;
+  };
+  put(c.pk);
+  if (c.have_rlk) put(c.rlk);
+  for (auto& kv : c.gks) put(kv.second);
+  if (withSecret) put(c.sk);
+  HIPCHK(hipStreamSynchronize(c.stream));
+  return 0;
+  API_END(-1)
+}
+int ImportKeyBundle(const void* dptr, unsigned long bytes) {
+  API_BEGIN
+  Context& c = ctx();
+  u64 h4[4];
+  HIPCHK(hipMemcpy(h4, dptr, 32, hipMemcpyDeviceToHost));
+  if (h4[0] != 0x4f52494f4e4b4231ull) throw std::runtime_error("not a key bundle");
+  std::vector<u64> gels(h4[1]);
+  if (h4[1]) HIPCHK(hipMemcpy(gels.data(), (const char*)dptr + 32, h4[1] * 8, hipMemcpyDeviceToHost));
+  size_t off = ((4 + h4[1]) * 8 + 255) & ~(size_t)255;
+  const char* d = (const char*)dptr;
+  auto get = [&](int ncomp, int nlimb) {
+    Poly p = c.alloc(ncomp, nlimb, 1);
+    const size_t b = (size_t)ncomp * nlimb * c.N * 8;
+    if (off + b > bytes) throw std::runtime_error("key bundle truncated");
+    HIPCHK(hipMemcpyAsync(p.ptr(), d + off, b, hipMemcpyDeviceToDevice, c.stream));
+    off += b;
+    return p;
+  };
+  c.pk = get(2, c.L + c.K);
+  c.have_pk = true;
+  if (h4[3]) {
+    c.rlk = get(2 * c.dnum, c.L + c.K);
+    c.have_rlk = true;
+  }
+  for (u64 ge : gels) c.gks[ge] = get(2 * c.dnum, c.L + c.K);
+  if (h4[2]) {
+    c.sk = get(1, c.L + c.K);
+    c.have_sk = true;
+  }
+  HIPCHK(hipStreamSynchronize(c.stream));
+  return 0;
+  API_END(-1)
+}
+
+// ---- profiling ----
+void OrionHipProfile(int enable) {
+  API_BEGIN
+  Context& c = ctx();
+  if (!enable) c.prof_flush();
+  c.prof = enable != 0;
+  API_END_VOID
+}
+void OrionHipProfileReset(void) {
+  API_BEGIN
+  Context& c = ctx();
+  c.prof_flush();
+  for (int i = 0; i < P_NCAT; ++i) c.prof_launch[i] = c.prof_ms[i] = c.prof_bytes[i] = 0;
+  API_END_VOID
+}
+int OrionHipProfileRead(char* names, long* launches, double* ms, double* bytes, int max) {
+  API_BEGIN
+  Context& c = ctx();
+  c.prof_flush();
+  int n = std::min(max, (int)P_NCAT);
+  for (int i = 0; i < n; ++i) {
+    strncpy(names + 32 * i, kProfNames[i], 31);
+    names[32 * i + 31] = 0;
+    launches[i] = (long)c.prof_launch[i];
+    ms[i] = c.prof_ms[i];
+    bytes[i] = c.prof_bytes[i];
+  }
+  return n;
+  API_END(-1)
+}
+
+int OrionHipNTT(unsigned long* dptr, int nlimb, int batch, const int* mods, int inverse) {
+  API_BEGIN
+  Context& c = ctx();
+  LimbSet s;
+  memset(&s, 0, sizeof(s));
+  s.p = (u64*)dptr;
+  s.ncomp = 1;
+  s.nlimb = nlimb;
+  s.nbatch = batch;
+  s.batch_stride = c.N;
+  s.limb_stride = (long long)batch * c.N;
+  if (nlimb > ORION_MAXLIMB) throw std::runtime_error("too many limbs");
+  for (int l = 0; l < nlimb; ++l) {
+    if (mods[l] < 0 || mods[l] >= c.L + c.K) throw std::runtime_error("bad modulus index");
+    s.mod[l] = (unsigned char)mods[l];
+    s.pos[l] = (unsigned char)l;
+  }
+  c.ntt(s, inverse != 0);
+  return 0;
+  API_END(-1)
+}
+
+}  // extern "C"

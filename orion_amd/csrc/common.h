@@ -1,0 +1,109 @@
+// common.h -- shared types and 64-bit modular arithmetic for the MI355X
+// (gfx950) RNS-CKKS backend.  Device and host.
+//
+// Layout conventions:
+//   * a residue polynomial limb is N u64 words, NTT domain unless stated,
+//     fully reduced in [0, q) at every kernel boundary;
+//   * a ciphertext batch is [comp][limb][batch][N]: one limb-plane per
+//     (comp, limb) holds the B independent images contiguously, so kernels
+//     index (comp, limb, image) -> one workgroup (NTT) or one grid row;
+//   * QP moduli index space = [q_0 .. q_{L-1}, p_0 .. p_{K-1}].
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+
+#define ORION_MAXMOD 80   // max |Q| + |P|
+#define ORION_MAXLIMB 48  // max limbs touched by one kernel launch (QP at one level)
+
+// ---------------------------------------------------------------------------
+// per-modulus constants (device-resident table, indexed by QP modulus index)
+// ---------------------------------------------------------------------------
+struct ModConst {
+  u64 q;        // modulus
+  u64 bar_mu;   // floor(2^(2k) / q), k = bitlen(q)   (Barrett)
+  int bar_k;    // bitlen(q)
+  int pad;
+  u64 ninv, ninv_s;  // N^-1 and its Shoup companion
+};
+
+struct DeviceTables {
+  ModConst mc[ORION_MAXMOD];
+  // twiddles, interleaved {w, floor(w*2^64/q)} : fwd[m][k] = psi^bitrev(k), inv = psi^-bitrev(k)
+  const ulonglong2* fwd[ORION_MAXMOD];
+  const ulonglong2* inv[ORION_MAXMOD];
+};
+
+// ---------------------------------------------------------------------------
+// a batch of limbs: element (c, l, b, n) at p[c*comp_stride + pos[l]*limb_stride + b*batch_stride + n]
+// ---------------------------------------------------------------------------
+struct LimbSet {
+  u64* p;
+  long long comp_stride, limb_stride, batch_stride;
+  int ncomp, nlimb, nbatch;
+  int pad;
+  unsigned char mod[ORION_MAXLIMB];  // QP modulus index of limb l
+  unsigned char pos[ORION_MAXLIMB];  // limb l lives at p + pos[l]*limb_stride
+};
+
+// ---------------------------------------------------------------------------
+// modular arithmetic (q < 2^62)
+// ---------------------------------------------------------------------------
+__host__ __device__ static inline u64 mulhi64(u64 a, u64 b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(a, b);
+#else
+  return (u64)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+__host__ __device__ static inline u64 add_mod(u64 a, u64 b, u64 q) {
+  u64 c = a + b;
+  return c >= q ? c - q : c;
+}
+__host__ __device__ static inline u64 sub_mod(u64 a, u64 b, u64 q) {
+  return a >= b ? a - b : a + q - b;
+}
+// Shoup: a*w mod q in [0, 2q), ws = floor(w*2^64/q), any a < 2^64
+__host__ __device__ static inline u64 shoup_lazy(u64 a, u64 w, u64 ws, u64 q) {
+  return a * w - mulhi64(a, ws) * q;
+}
+__host__ __device__ static inline u64 shoup_mul(u64 a, u64 w, u64 ws, u64 q) {
+  u64 r = shoup_lazy(a, w, ws, q);
+  return r >= q ? r - q : r;
+}
+// Barrett reduction of the 128-bit value hi:lo < q^2 (q < 2^62)
+__host__ __device__ static inline u64 barrett128(u64 hi, u64 lo, const ModConst& m) {
+  const int k = m.bar_k;
+  // t1 = x >> (k-1)  (< 2^(k+1))
+  u64 t1 = (lo >> (k - 1)) | (hi << (65 - k));
+  // t2 = (t1 * mu) >> (k+1)
+  u64 ph = mulhi64(t1, m.bar_mu), pl = t1 * m.bar_mu;
+  u64 t2 = (pl >> (k + 1)) | (ph << (63 - k));
+  u64 r = lo - t2 * m.q;
+  if (r >= m.q) r -= m.q;
+  if (r >= m.q) r -= m.q;
+  return r;
+}
+__host__ __device__ static inline u64 mul_mod(u64 a, u64 b, const ModConst& m) {
+  return barrett128(mulhi64(a, b), a * b, m);
+}
+
+// ---------------------------------------------------------------------------
+// host-side tables for basis extension (ModUp / ModDown), device-resident
+//   y_i  = x_i * qhatinv[i] mod s_i
+//   v    = (u64) sum_i (double)y_i * qinv_f[i]       (ordered, no FMA)
+//   out_t = sum_i y_i * qhat_t[t][i] - v * S_t[t]   mod t
+// ---------------------------------------------------------------------------
+#define ORION_MAXSRC 8
+struct BasisExtTable {
+  int ns, nt;
+  int src_mod[ORION_MAXSRC];
+  int dst_mod[ORION_MAXLIMB];
+  u64 qhatinv[ORION_MAXSRC], qhatinv_s[ORION_MAXSRC];
+  double qinv_f[ORION_MAXSRC];
+  u64 qhat_t[ORION_MAXLIMB][ORION_MAXSRC];
+  u64 S_t[ORION_MAXLIMB];
+};

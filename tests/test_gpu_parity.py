@@ -1,0 +1,159 @@
+"""GPU parity tests: the HIP backend (through the C-ABI) vs the CPU oracle on
+the same inputs.  Integer ring arithmetic must match bit for bit."""
+import numpy as np
+import pytest
+
+from tests.helpers import SMALL, rand_ct
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def small(torch_cuda, oracle_mod):
+    from orion_amd.backend import HipLibrary
+    lib = HipLibrary().new_scheme(SMALL["logn"], SMALL["logq"], SMALL["logp"], 40, h=192, seed=1234)
+    mods = lib.moduli()
+    orc = oracle_mod.Oracle(SMALL["logn"], mods, len(SMALL["logq"]), len(SMALL["logp"]))
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    return lib, orc
+
+
+@pytest.mark.parametrize("logn", [13, 14, 15])
+def test_ntt_roundtrip_and_parity(torch_cuda, oracle_mod, logn):
+    torch = torch_cuda
+    from orion_amd.backend import HipLibrary
+    import ctypes
+    logq = [60] + [40] * 3
+    lib = HipLibrary().new_scheme(logn, logq, [60, 60], 40)
+    mods = lib.moduli()
+    assert mods == oracle_mod.gen_moduli(logn, logq, [60, 60])
+    orc = oracle_mod.Oracle(logn, mods, len(logq), 2)
+    N, B = 1 << logn, 3
+    nl = len(mods)
+    rng = np.random.default_rng(logn)
+    host = np.stack([rng.integers(0, mods[m], (B, N), dtype=np.uint64) for m in range(nl)])  # [limb][b][N]
+    dev = torch.from_numpy(host.view(np.int64).copy()).cuda()
+    mods_c = (ctypes.c_int * nl)(*range(nl))
+    ptr = ctypes.cast(dev.data_ptr(), ctypes.POINTER(ctypes.c_ulong))
+    assert lib.lib.OrionHipNTT(ptr, nl, B, mods_c, 0) == 0
+    lib.OrionHipSynchronize()
+    fwd = dev.cpu().numpy().view(np.uint64)
+    for m in range(nl):
+        for b in range(B):
+            assert np.array_equal(fwd[m, b], orc.ntt(m, host[m, b])), (m, b)
+    assert lib.lib.OrionHipNTT(ptr, nl, B, mods_c, 1) == 0
+    lib.OrionHipSynchronize()
+    back = dev.cpu().numpy().view(np.uint64)
+    assert np.array_equal(back, host)
+    lib.DeleteScheme()
+
+
+def test_encode_parity(small):
+    lib, orc = small
+    rng = np.random.default_rng(1)
+    vals = rng.standard_normal(orc.N // 2).astype(np.float32)
+    level = 4
+    pt = lib.Encode(list(vals), level, 1 << 40)
+    got = lib.export_plaintext(pt)[0]
+    ref = orc.encode(vals.astype(np.float64), 2.0 ** 40, list(range(level + 1)))
+    assert np.array_equal(got, ref)
+
+
+def test_encrypt_decrypt(small):
+    lib, orc = small
+    rng = np.random.default_rng(2)
+    vals = rng.standard_normal(orc.N // 2).astype(np.float32)
+    pt = lib.Encode(list(vals), 5, 1 << 40)
+    ct = lib.Encrypt(pt)
+    dec = np.array(lib.Decode(lib.Decrypt(ct)))
+    assert np.abs(dec - vals).max() < 1e-4
+
+
+def test_rescale_parity(small):
+    lib, orc = small
+    rng = np.random.default_rng(3)
+    level = 5
+    x = rand_ct(rng, orc.moduli, level, orc.N, B=2)
+    ct = lib.import_ciphertext(x, 2.0 ** 80)
+    lib.Rescale(ct)
+    got = lib.export_ciphertext(ct)
+    for b in range(2):
+        assert np.array_equal(got[b], orc.rescale(x[b], level))
+    assert lib.GetCiphertextLevel(ct) == level - 1
+
+
+def test_mul_relin_parity(small):
+    lib, orc = small
+    rng = np.random.default_rng(4)
+    level = 4
+    a = rand_ct(rng, orc.moduli, level, orc.N, B=2)
+    b = rand_ct(rng, orc.moduli, level, orc.N, B=2)
+    ca, cb = lib.import_ciphertext(a, 2.0 ** 40), lib.import_ciphertext(b, 2.0 ** 40)
+    cc = lib.MulRelinCiphertextNew(ca, cb)
+    got = lib.export_ciphertext(cc)
+    rlk = lib.export_relin_key()
+    for i in range(2):
+        assert np.array_equal(got[i], orc.mul_relin(a[i], b[i], rlk, level)), i
+
+
+def test_rotate_parity(small):
+    lib, orc = small
+    rng = np.random.default_rng(5)
+    level = 3
+    a = rand_ct(rng, orc.moduli, level, orc.N, B=1)
+    ca = lib.import_ciphertext(a, 2.0 ** 40)
+    for k in [1, 5, -3, 1000]:
+        cr = lib.RotateNew(ca, k)
+        g = int(lib.GaloisElement(k))
+        assert g == orc.galois_element(k)
+        gk = lib.export_galois_key(g)
+        got = lib.export_ciphertext(cr)[0]
+        assert np.array_equal(got, orc.rotate(a[0], g, gk, level)), k
+
+
+def test_rotate_decrypts(small):
+    lib, orc = small
+    rng = np.random.default_rng(6)
+    vals = rng.standard_normal(orc.N // 2).astype(np.float32)
+    ct = lib.Encrypt(lib.Encode(list(vals), 5, 1 << 40))
+    r = lib.RotateNew(ct, 7)
+    dec = np.array(lib.Decode(lib.Decrypt(r)))
+    assert np.abs(dec - np.roll(vals, -7)).max() < 1e-3
+
+
+def test_linear_transform_parity(small):
+    lib, orc = small
+    rng = np.random.default_rng(7)
+    slots = orc.N // 2
+    level = 4
+    idx = [0, 1, 2, 3, 17, 64, 65, 300, slots - 1]
+    diags = rng.uniform(-1, 1, (len(idx), slots)).astype(np.float32)
+    lt = lib.GenerateLinearTransform(idx, list(diags.reshape(-1)), level, 2.0, "none")
+    gels = lib.GetLinearTransformRotationKeys(lt)
+    lib.GenerateConsolidatedRotationKeys(gels)
+    vals = rng.standard_normal(slots).astype(np.float32)
+    ct = lib.Encrypt(lib.Encode(list(vals), level, 1 << 40))
+    x = lib.export_ciphertext(ct)[0]
+    out = lib.EvaluateLinearTransform(lt, ct)
+    got = lib.export_ciphertext(out)[0]
+    N1 = lib.GetLinearTransformN1(lt)
+    assert N1 == orc.find_best_bsgs_n1(idx, 0)
+    pts = [lib.export_lt_diagonal(lt, d, level) for d in idx]
+    gkeys = {g: lib.export_galois_key(g) for g in gels}
+    ref = orc.lt_bsgs(x, level, idx, pts, N1, gkeys)
+    assert np.array_equal(got, ref)
+    # functional: y[k] = sum_d diag_d[k] * x[k+d]
+    lib.Rescale(out)
+    dec = np.array(lib.Decode(lib.Decrypt(out)))
+    exp = sum(diags[i].astype(np.float64) * np.roll(vals, -d) for i, d in enumerate(idx))
+    assert np.abs(dec - exp).max() < 1e-3
