@@ -1,0 +1,210 @@
+"""Encrypted-inference throughput of Orion's LoLA on the MI355X HIP backend.
+
+Metric (BASELINE.json): encrypted images/sec (LoLA, N=2^15) + NTT achieved
+HBM GB/s vs peak.  A "step" is one FHE forward pass `net(ct)` of the LoLA op
+stream (the exact backend-call sequence the reference frontend emits, see
+orion_amd/replay.py) over one batch of B images per GPU, every ciphertext
+already resident in HBM.  Multi-GPU: one process per GPU, independent image
+shards (weak scaling), evaluation keys generated on rank 0 and broadcast over
+RCCL/xGMI once before timing; no collective inside the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("ORION_BENCH_BATCH", 64)))
+    ap.add_argument("--workload", default="lola_n15")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-images", type=int, default=1)
+    return ap.parse_args()
+
+
+def cpu_baseline(name, n_images):
+    """The CPU parity oracle (single-threaded C restatement) running the same
+    op stream on this host: bounded sample of n_images images."""
+    from oracle.replay_cpu import CpuStream
+    s = CpuStream(name)
+    s.keygen()
+    s.compile()
+    imgs = [s.arrays["input"]] * n_images
+    cts = [s.encrypt(im) for im in imgs]
+    t0 = time.perf_counter()
+    for ct in cts:
+        s.forward(ct)
+    dt = time.perf_counter() - t0
+    return dict(value=n_images / dt, unit="images/s", cores=1, kind="port",
+                sample=f"{n_images} image(s) of {name}, oracle/ckks_oracle.c single thread, "
+                       f"{dt:.1f} s; host nproc={os.cpu_count()}")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from orion_amd.replay import OrionStream
+    lib_seed = 2024
+    st = OrionStream(args.workload, seed=lib_seed + rank, device=local)
+    lib = st.lib
+    torch_stream = torch.cuda.Stream()
+    lib.OrionHipSetStream(torch_stream.cuda_stream)
+
+    t_setup = time.perf_counter()
+    if rank == 0:
+        st.keygen(with_po2=True)
+        st.compile(gen_keys=True)
+    else:
+        st.compile(gen_keys=False)
+    if world > 1:
+        # RCCL broadcast of public + evaluation keys (+ secret for output checks)
+        nbytes = torch.zeros(1, dtype=torch.int64, device="cuda")
+        if rank == 0:
+            nbytes[0] = int(lib.KeyBundleBytes(1))
+        dist.broadcast(nbytes, 0)
+        buf = torch.empty(int(nbytes.item()), dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            lib.OrionHipSynchronize()
+            if lib.lib.ExportKeyBundle(buf.data_ptr(), 1) != 0:
+                raise RuntimeError(lib.lib.OrionHipLastError().decode())
+        torch.cuda.synchronize()
+        dist.broadcast(buf, 0)
+        torch.cuda.synchronize()
+        if rank != 0:
+            if lib.lib.ImportKeyBundle(buf.data_ptr(), buf.numel()) != 0:
+                raise RuntimeError(lib.lib.OrionHipLastError().decode())
+        del buf
+    t_setup = time.perf_counter() - t_setup
+
+    # this rank's shard of synthetic images (MNIST-shaped, N(0,1), seed 42 + rank)
+    g = torch.Generator().manual_seed(42 + rank)
+    imgs = torch.randn(args.batch, 1, 28, 28, generator=g).numpy()
+    imgs[0] = st.reference_input().reshape(1, 28, 28)
+    ct = st.encrypt_batch(imgs)
+    lib.OrionHipSynchronize()
+
+    def step():
+        out = st.forward(ct)
+        return out
+
+    for _ in range(args.warmup):
+        lib.DeleteCiphertext(step())
+    lib.OrionHipSynchronize()
+
+    lib.OrionHipProfileReset()
+    lib.OrionHipProfile(0b11)  # HIP events around the NTT launches only (the roofline kernel)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    lib.OrionHipSynchronize()
+    t0 = time.perf_counter()
+    outs = []
+    for _ in range(args.steps):
+        outs.append(step())
+    lib.OrionHipSynchronize()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    lib.OrionHipProfile(0)
+    prof = lib.profile_read()
+    if dist:
+        dist.barrier()
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # correctness of the timed output (image 0 is the fixture's reference input)
+    res = st.decrypt_output(outs[-1])
+    exp = st.arrays["expected_output"].reshape(-1)
+    mae = float(np.abs(res[0] - exp).mean())
+    for o in outs:
+        lib.DeleteCiphertext(o)
+    # one extra, fully profiled step (outside the timed region) for the per-kernel breakdown
+    lib.OrionHipProfileReset()
+    lib.OrionHipProfile(1)
+    lib.DeleteCiphertext(step())
+    lib.OrionHipProfile(0)
+    breakdown = lib.profile_read()
+
+    images = args.batch * world * args.steps
+    value = images / dt
+    ntt = [prof.get("ntt_fwd", {}), prof.get("ntt_inv", {})]
+    n_launch = sum(p.get("launches", 0) for p in ntt)
+    n_ms = sum(p.get("ms", 0.0) for p in ntt)
+    n_bytes = sum(p.get("bytes", 0.0) for p in ntt)
+    achieved = (n_bytes / (n_ms / 1e3)) / 1e9 if n_ms > 0 else 0.0
+    total_prof_ms = sum(p["ms"] for p in breakdown.values())
+    bd_ntt_ms = breakdown.get("ntt_fwd", {}).get("ms", 0) + breakdown.get("ntt_inv", {}).get("ms", 0)
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "ntt_traffic.json")
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            tj = json.load(f)
+        if tj.get("workload") == args.workload and tj.get("batch") == args.batch:
+            traffic = tj.get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                cpu = cpu_baseline(args.workload, args.cpu_images)
+            except Exception as e:  # the baseline must never break the GPU line
+                cpu = dict(value=None, unit="images/s", cores=1, kind="port", sample=f"failed: {e}")
+        line = {
+            "metric": "encrypted images/sec (LoLa N=2^15) + NTT HBM GB/s vs peak",
+            "value": round(value, 3),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic: N(0,1) 1x28x28 images (image 0 = fixture input), LoLA diagonals from the "
+                    "reference frontend's compile of seeded random-init weights",
+            "config": {"workload": f"LoLA (models/lola.py) {args.workload}: N=2^15, LogQ=[60]+[40]x11, "
+                                   f"LogP=[60,60], input level {st.input_level}, Standard ring",
+                       "batch_per_gpu": args.batch, "global_batch": args.batch * world,
+                       "parallelism": f"replicas x{world} (image shards), keys RCCL-broadcast"},
+            "roofline": {"bound": "hbm", "kernel": "ntt (fwd+inv, 1 limb per workgroup)",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "launches": n_launch, "avg_launch_us": round(n_ms / max(n_launch, 1) * 1e3, 2),
+                         "algorithmic_bytes_per_launch": round(n_bytes / max(n_launch, 1)),
+                         "ntt_share_of_kernel_time": round(bd_ntt_ms / total_prof_ms, 3) if total_prof_ms else None},
+            "cpu_baseline": cpu,
+            "check": {"mae_image0_vs_cleartext": mae, "setup_s": round(t_setup, 1)},
+            "kernel_ms_per_step": {k: round(v["ms"], 3) for k, v in breakdown.items()},
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -175,7 +175,10 @@ unsigned long KeyBundleBytes(int withSecret);
 int ExportKeyBundle(void *dptr, int withSecret);
 int ImportKeyBundle(const void *dptr, unsigned long bytes);
 
-/* kernel timing with HIP events on the library stream */
+/* kernel timing with HIP events on the library stream; enable: 0 = off,
+ * 1 = every category, otherwise a bit mask of categories (bit 0 ntt_fwd,
+ * 1 ntt_inv, 2 elementwise, 3 basis_ext, 4 ks_mac, 5 automorph, 6 tensor,
+ * 7 rescale_prep) */
 void OrionHipProfile(int enable);
 /* fills up to max entries: name (32 chars each), launches, total ms, algorithmic bytes */
 int OrionHipProfileRead(char *names, long *launches, double *ms, double *bytes, int max);

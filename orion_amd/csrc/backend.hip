@@ -198,7 +198,7 @@ struct Context {
   HandlePool<Ciphertext> cts;
   HandlePool<LinTrans> lts;
 
-  bool prof = false;
+  unsigned prof = 0;  // bit mask of profiled kernel categories
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> ev_free;
   double prof_launch[P_NCAT] = {0}, prof_ms[P_NCAT] = {0}, prof_bytes[P_NCAT] = {0};
@@ -239,7 +239,7 @@ struct Context {
     double bytes;
     hipEvent_t e0 = nullptr;
     Scope(Context* ctx, int k, double b) : c(ctx), cat(k), bytes(b) {
-      if (c->prof) {
+      if (c->prof & (1u << cat)) {
         e0 = c->ev();
         hipEventRecord(e0, c->stream);
       }
@@ -1974,7 +1974,7 @@ void OrionHipProfile(int enable) {
   API_BEGIN
   Context& c = ctx();
   if (!enable) c.prof_flush();
-  c.prof = enable != 0;
+  c.prof = enable == 1 ? 0xffffffffu : (unsigned)enable;  // 1 = all categories, else a bit mask
   API_END_VOID
 }
 void OrionHipProfileReset(void) {

@@ -1,0 +1,201 @@
+"""Replay an Orion op stream through the HIP backend's Lattigo-compatible API.
+
+The stream (tests/golden/<name>_trace.json + _arrays.npz) is the exact
+sequence of backend calls the reference frontend makes for a model
+(orion/nn/*.py -> orion/backend/python/*.py -> backend), recorded by
+tools/gen_fixtures.py.  Replaying it here reproduces `net(ct)` of
+/root/reference/examples/run_lola.py:45-47 call for call, with two
+deliberate differences:
+
+* the fork's debug decryptions inside the forward pass
+  (lt_evaluator.py:156-158,194-196; activation.py:51-62) are skipped -- they
+  need the secret key and are not part of the operator semantics;
+* one ciphertext handle carries a batch of B images (EncodeBatch), so every
+  call of the stream runs once for the whole batch.
+
+Handles recorded in the trace are mapped to the library's own handles at the
+events that create them, so deletes and lowest-free-id reuse replay exactly.
+"""
+import json
+import os
+
+import numpy as np
+
+from .backend import HipLibrary
+
+GOLDEN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+
+
+def load_stream(name, root=GOLDEN):
+    with open(os.path.join(root, f"{name}_trace.json")) as f:
+        trace = json.load(f)
+    arrays = dict(np.load(os.path.join(root, f"{name}_arrays.npz"), allow_pickle=False))
+    return trace, arrays
+
+
+# ops whose trace args are (ct, ct|pt|scalar) and that return a ciphertext
+_CT_OPS = {
+    "RotateNew": ("ct", "int"), "Rotate": ("ct", "int"),
+    "RescaleNew": ("ct",), "Rescale": ("ct",),
+    "AddCiphertext": ("ct", "ct"), "AddCiphertextNew": ("ct", "ct"),
+    "SubCiphertext": ("ct", "ct"), "SubCiphertextNew": ("ct", "ct"),
+    "MulRelinCiphertext": ("ct", "ct"), "MulRelinCiphertextNew": ("ct", "ct"),
+    "AddPlaintext": ("ct", "pt"), "AddPlaintextNew": ("ct", "pt"),
+    "SubPlaintext": ("ct", "pt"), "SubPlaintextNew": ("ct", "pt"),
+    "MulPlaintext": ("ct", "pt"), "MulPlaintextNew": ("ct", "pt"),
+    "AddScalar": ("ct", "float"), "AddScalarNew": ("ct", "float"),
+    "SubScalar": ("ct", "float"), "SubScalarNew": ("ct", "float"),
+    "MulScalarInt": ("ct", "int"), "MulScalarIntNew": ("ct", "int"),
+    "MulScalarFloat": ("ct", "float"), "MulScalarFloatNew": ("ct", "float"),
+    "Negate": ("ct",),
+    "EvaluateLinearTransform": ("lt", "ct"),
+}
+
+
+class OrionStream:
+    """A compiled Orion model as an op stream bound to one HipLibrary."""
+
+    def __init__(self, name, lib=None, seed=2024, device=None, root=GOLDEN, synthetic_diagonals=False):
+        self.name = name
+        self.trace, self.arrays = load_stream(name, root)
+        self.meta = self.trace["meta"]
+        cfg = self.meta["config"]
+        self.lib = lib or HipLibrary()
+        self.lib.new_scheme(cfg["logn"], cfg["logq"], cfg["logp"], cfg["logscale"], h=cfg["h"], seed=seed,
+                            device=device)
+        self.slots = self.meta["slots"]
+        self.synthetic = synthetic_diagonals
+        self.pt_map, self.ct_map, self.lt_map = {}, {}, {}
+        self.input_level = self.meta["input_level"]
+        self._events = self.trace["events"]
+
+    # -- setup: keys + evaluator (key_generator.py:10-15, evaluator.py:2-6) ---
+    def keygen(self, with_po2=True):
+        lib = self.lib
+        lib.NewKeyGenerator()
+        lib.GenerateSecretKey()
+        lib.GeneratePublicKey()
+        lib.GenerateRelinearizationKey()
+        lib.GenerateEvaluationKeys()
+        lib.NewEncoder()
+        lib.NewEncryptor()
+        lib.NewDecryptor()
+        if with_po2:
+            lib.NewEvaluator()  # power-of-two rotation keys (evaluator.go:25-31)
+        lib.NewPolynomialEvaluator()
+        lib.NewLinearTransformEvaluator()
+
+    # -- compile phase: bias plaintexts + linear transforms + their keys --------
+    def compile(self, gen_keys=True):
+        lib = self.lib
+        rng = np.random.default_rng(7)
+        for ev in self._events:
+            if ev["phase"] != "compile":
+                continue
+            op, args, ret = ev["op"], ev["args"], ev["ret"]
+            if op == "Encode":
+                vals = self.arrays[ev["arrays"] + "_values"]
+                self.pt_map[ret] = lib.Encode(vals, args[1], args[2])
+            elif op == "GenerateLinearTransform":
+                idx, _, level, ratio, io = args
+                diags = self.arrays[ev["arrays"] + "_diags"]
+                if self.synthetic:
+                    diags = rng.uniform(-1, 1, diags.shape).astype(np.float32)
+                h = lib.GenerateLinearTransform(idx, diags.reshape(-1), level, ratio, "none")
+                self.lt_map[ret] = h
+                if gen_keys:
+                    lib.GenerateConsolidatedRotationKeys(lib.GetLinearTransformRotationKeys(h))
+            elif op == "DeletePlaintext" and args[0] in self.pt_map:
+                lib.DeletePlaintext(self.pt_map.pop(args[0]))
+        # rotation amounts used by the forward pass (hybrid output rotations)
+        if gen_keys:
+            for ev in self._events:
+                if ev["phase"] == "forward" and ev["op"] in ("RotateNew", "Rotate"):
+                    lib.AddRotationKey(ev["args"][1])
+
+    def input_events(self):
+        return [e for e in self._events if e["phase"] == "input"]
+
+    # -- input phase: encode + encrypt a batch of images -------------------------
+    def encrypt_batch(self, images):
+        """images: (B, ...) array; each image flattened into the slots the way
+        orion's encoder pads it (encoder.py:29-42)."""
+        imgs = np.asarray(images, dtype=np.float32).reshape(len(images), -1)
+        enc = [e for e in self.input_events() if e["op"] == "Encode"][0]
+        level, scale = enc["args"][1], enc["args"][2]
+        vals = np.zeros((imgs.shape[0], self.slots), dtype=np.float32)
+        vals[:, :imgs.shape[1]] = imgs
+        pt = self.lib.encode_batch(vals, level, scale)
+        ct = self.lib.Encrypt(pt)
+        self.lib.DeletePlaintext(pt)
+        return ct
+
+    def reference_input(self):
+        return self.arrays["input"]
+
+    # -- forward: the timed net(ct) ------------------------------------------------
+    def forward(self, ct_in):
+        lib = self.lib
+        in_ids = self.meta["input_ids"]
+        ct_map = {in_ids[0]: ct_in}
+        skipped_pts = set()
+        owned = set()
+        for ev in self._events:
+            if ev["phase"] != "forward":
+                continue
+            op, args, ret = ev["op"], ev["args"], ev["ret"]
+            if op in ("Decrypt", "Decode"):  # debug decryptions of the fork: not operator semantics
+                if op == "Decrypt":
+                    skipped_pts.add(ret)
+                continue
+            if op == "DeletePlaintext":
+                if args[0] in skipped_pts:
+                    skipped_pts.discard(args[0])
+                elif args[0] in self.pt_map:
+                    lib.DeletePlaintext(self.pt_map.pop(args[0]))
+                continue
+            if op == "DeleteCiphertext":
+                h = ct_map.pop(args[0], None)
+                if h is not None and h in owned:
+                    lib.DeleteCiphertext(h)
+                    owned.discard(h)
+                continue
+            if op == "SetCiphertextScale":
+                lib.SetCiphertextScale(ct_map[args[0]], args[1])
+                continue
+            kinds = _CT_OPS.get(op)
+            if kinds is None:
+                raise RuntimeError(f"replay: unsupported op {op} in forward phase")
+            cargs = []
+            for k, a in zip(kinds, args):
+                cargs.append(ct_map[a] if k == "ct" else self.pt_map[a] if k == "pt" else
+                             self.lt_map[a] if k == "lt" else a)
+            h = getattr(lib, op)(*cargs)
+            if ret is not None:
+                if op.endswith("New") or op == "EvaluateLinearTransform":
+                    owned.add(h)
+                ct_map[ret] = h
+        out_ids = self.meta["output_ids"]
+        out = ct_map[out_ids[0]]
+        for rid, h in ct_map.items():
+            if h != out and h in owned:
+                lib.DeleteCiphertext(h)
+        return out
+
+    def decrypt_output(self, ct, n_out=None):
+        """Decrypt + decode a batch output; returns (B, n_out) floats."""
+        lib = self.lib
+        B = lib.GetCiphertextBatch(ct)
+        pt = lib.Decrypt(ct)
+        vals = np.array(lib.Decode(pt), dtype=np.float64).reshape(B, self.slots)
+        lib.DeletePlaintext(pt)
+        n = n_out or int(np.prod(self.meta["output_shape"]))
+        return vals[:, :n]
+
+    def forward_op_counts(self):
+        c = {}
+        for e in self._events:
+            if e["phase"] == "forward" and e["op"] not in ("Decrypt", "Decode", "DeletePlaintext",
+                                                          "DeleteCiphertext"):
+                c[e["op"]] = c.get(e["op"], 0) + 1
+        return c

@@ -157,3 +157,60 @@ def test_linear_transform_parity(small):
     dec = np.array(lib.Decode(lib.Decrypt(out)))
     exp = sum(diags[i].astype(np.float64) * np.roll(vals, -d) for i, d in enumerate(idx))
     assert np.abs(dec - exp).max() < 1e-3
+
+
+def test_lola_n13_end_to_end(torch_cuda):
+    """The reference frontend's LoLA op stream (tests/golden/lola_n13_*) replayed
+    through the C-ABI: decrypted output vs the cleartext PyTorch model, the
+    reference's own numeric gate (tests/models/test_mlp.py:45-48, MAE < 0.005)."""
+    from orion_amd.replay import OrionStream
+    st = OrionStream("lola_n13", seed=11)
+    st.keygen()
+    st.compile()
+    imgs = np.stack([st.reference_input().reshape(1, 28, 28)] * 3)
+    ct = st.encrypt_batch(imgs)
+    out = st.forward(ct)
+    res = st.decrypt_output(out)
+    exp = st.arrays["expected_output"].reshape(-1)
+    for b in range(3):
+        assert np.abs(res[b] - exp).mean() < 0.005
+    # replaying twice gives the same ciphertext (deterministic kernels)
+    out2 = st.forward(ct)
+    assert np.array_equal(st.lib.export_ciphertext(out), st.lib.export_ciphertext(out2))
+
+
+def test_lola_n13_matches_cpu_oracle_replay(torch_cuda):
+    """Whole-network ciphertext parity: the GPU replay and the CPU-oracle replay
+    of the same op stream, same keys and same input ciphertext, bit for bit."""
+    from orion_amd.replay import OrionStream
+    from oracle.replay_cpu import CpuStream
+    st = OrionStream("lola_n13", seed=12)
+    st.keygen()
+    st.compile()
+    lib = st.lib
+    cpu = CpuStream("lola_n13")
+    # share the GPU's keys with the oracle
+    cpu.sk = lib.export_secret_key()
+    cpu.rlk = lib.export_relin_key()
+    cpu.compile_keys = False
+    cpu.gks = {}
+    for g in _galois_elements(st):
+        cpu.gks[g] = lib.export_galois_key(g)
+    cpu.compile()
+    ct = st.encrypt_batch(st.reference_input()[None])
+    x = lib.export_ciphertext(ct)[0]
+    out = lib.export_ciphertext(st.forward(ct))[0]
+    enc = [e for e in cpu.trace["events"] if e["phase"] == "input" and e["op"] == "Encode"][0]
+    ref = cpu.forward((x, x.shape[1] - 1, float(enc["args"][2])))
+    assert np.array_equal(out, ref[0])
+
+
+def _galois_elements(st):
+    lib = st.lib
+    gels = set()
+    for rid, h in st.lt_map.items():
+        gels.update(lib.GetLinearTransformRotationKeys(h))
+    for ev in st.trace["events"]:
+        if ev["phase"] == "forward" and ev["op"] in ("RotateNew", "Rotate"):
+            gels.add(int(lib.GaloisElement(ev["args"][1])))
+    return sorted(gels)
