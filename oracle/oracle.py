@@ -102,7 +102,7 @@ class Oracle:
         self.moduli = [int(m) for m in moduli]
         arr = np.array(self.moduli, dtype=np.uint64)
         self._h = lib().oracle_new(logN, _p(arr), L, K)
-        self.dnum = (L + K - 1) // K
+        self.dnum = (L + K - 1) // K if K else 0
 
     @classmethod
     def from_logs(cls, logN, logQ, logP):

@@ -23,17 +23,19 @@ def _needs(obj, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose=False):
-    os.makedirs(BUILD, exist_ok=True)
+def build(verbose=False, extra_flags=(), lib=LIB, build_dir=BUILD):
+    """Compile liborion_hip.so (extra_flags/lib/build_dir: timing-only variants)."""
+    BUILD_, LIB_ = build_dir, lib
+    os.makedirs(BUILD_, exist_ok=True)
     headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     headers.append(os.path.join(HERE, "..", "include", "orion_hip.h"))
     objs, jobs = [], []
     for src in SOURCES:
         path = os.path.join(CSRC, src)
-        obj = os.path.join(BUILD, src + ".o")
+        obj = os.path.join(BUILD_, src + ".o")
         objs.append(obj)
         if _needs(obj, [path] + headers):
-            cmd = [HIPCC] + FLAGS + ["-c", path, "-o", obj]
+            cmd = [HIPCC] + FLAGS + list(extra_flags) + ["-c", path, "-o", obj]
             if src.endswith(".hip"):
                 cmd.insert(1, f"--offload-arch={ARCH}")
             jobs.append(cmd)
@@ -47,9 +49,9 @@ def build(verbose=False):
 
     with ThreadPoolExecutor(max_workers=4) as ex:
         list(ex.map(run, jobs))
-    if jobs or not os.path.exists(LIB):
-        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs)
-    return LIB
+    if jobs or not os.path.exists(LIB_):
+        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_] + objs)
+    return LIB_
 
 
 if __name__ == "__main__":

@@ -36,6 +36,8 @@ int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const u64* key, in
                         const DeviceTables* tb, int N, int accumulate, hipStream_t st);
 int orion_launch_automorph(const LimbSet& o, const LimbSet& a, const u32* idx, const DeviceTables* tb, int N,
                            int accumulate, hipStream_t st);
+int orion_launch_lt_mac(const LimbSet& t, const u64* const* rot, const u64* const* pt, int m, const LimbSet& ptl,
+                        const DeviceTables* tb, int N, hipStream_t st);
 
 namespace orion {
 
@@ -169,8 +171,8 @@ struct ProfRec {
   double bytes;
 };
 static const char* kProfNames[] = {"ntt_fwd", "ntt_inv", "elementwise", "basis_ext", "ks_mac", "automorph",
-                                   "tensor", "rescale_prep"};
-enum { P_NTT_FWD = 0, P_NTT_INV, P_EW, P_BEXT, P_MAC, P_AUT, P_TENSOR, P_RSPREP, P_NCAT };
+                                   "tensor", "rescale_prep", "lt_mac"};
+enum { P_NTT_FWD = 0, P_NTT_INV, P_EW, P_BEXT, P_MAC, P_AUT, P_TENSOR, P_RSPREP, P_LTMAC, P_NCAT };
 
 // ---------------------------------------------------------------------------
 // context
@@ -386,6 +388,28 @@ struct Context {
         a = hm_mulmod(a, psi, q);
         b = hm_mulmod(b, psii, q);
       }
+      // float64-path constants and centered twiddles for small moduli
+      mc.f64 = mc.bar_k <= ORION_F64_BITS ? 1 : 0;
+      mc.qd = (double)q;
+      mc.qinv_d = 1.0 / (double)q;
+      mc.ninv_d = (double)(mc.ninv > q / 2 ? (long long)mc.ninv - (long long)q : (long long)mc.ninv);
+      if (mc.f64) {
+        std::vector<double> fd(N), id(N);
+        for (int j = 0; j < N; ++j) {
+          const u64 a1 = fw[j].x, b1 = iv[j].x;
+          fd[j] = (double)(a1 > q / 2 ? (long long)a1 - (long long)q : (long long)a1);
+          id[j] = (double)(b1 > q / 2 ? (long long)b1 - (long long)q : (long long)b1);
+        }
+        void *dfd, *did;
+        HIPCHK(hipMalloc(&dfd, N * sizeof(double)));
+        HIPCHK(hipMalloc(&did, N * sizeof(double)));
+        HIPCHK(hipMemcpy(dfd, fd.data(), N * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(did, id.data(), N * sizeof(double), hipMemcpyHostToDevice));
+        static_bufs.push_back(dfd);
+        static_bufs.push_back(did);
+        host_tb.fwd_d[m] = (const double*)dfd;
+        host_tb.inv_d[m] = (const double*)did;
+      }
       void *dfw, *div;
       HIPCHK(hipMalloc(&dfw, N * sizeof(ulonglong2)));
       HIPCHK(hipMalloc(&div, N * sizeof(ulonglong2)));
@@ -424,7 +448,14 @@ struct Context {
       const u64 tm = mods[dst[t]];
       T.dst_mod[t] = dst[t];
       T.S_t[t] = prod_mod(src, -1, tm);
-      for (int i = 0; i < T.ns; ++i) T.qhat_t[t][i] = prod_mod(src, i, tm);
+      for (int i = 0; i < T.ns; ++i) {
+        T.qhat_t[t][i] = prod_mod(src, i, tm);
+        T.qhat_ts[t][i] = hm_shoup(T.qhat_t[t][i], tm);
+      }
+      for (int v = 0; v <= T.ns; ++v) {
+        const u64 vs = hm_mulmod((u64)v, T.S_t[t], tm);
+        T.vS_t[t][v] = vs ? tm - vs : 0;
+      }
     }
     BasisExtTable* d;
     HIPCHK(hipMalloc(&d, sizeof(T)));
@@ -842,16 +873,31 @@ struct Context {
     Poly t1q = alloc(1, level + 1, B);
     for (int j : T.giants) {
       const std::vector<int>& bl = T.index.at(j);
-      bool first = true;
-      for (int b : bl) {
-        const int d = (j + b) & (N / 2 - 1);
-        const Plaintext& pt = T.diags.at(d);
-        LimbSet lp = lsqp(pt.poly, 0, 1, level, T.level, B);
-        lp.ncomp = 2;
-        lp.comp_stride = 0;  // same diagonal for both components
+      {
+        // fused sum over this giant step's babies: t = sum_i pt[j+i] * rot_i
+        std::vector<const u64*> rp, pp;
+        const Plaintext* pt0 = nullptr;
+        for (int b : bl) {
+          const int d = (j + b) & (N / 2 - 1);
+          const Plaintext& pt = T.diags.at(d);
+          pt0 = &pt;
+          rp.push_back(rot.at(b).ptr());
+          pp.push_back(pt.poly.ptr());
+        }
         LimbSet lt = lsqp(t, 0, 2, level, level);
-        ew(first ? EW_MUL : EW_MULADD, lt, lp, lsqp(rot.at(b), 0, 2, level, level));
-        first = false;
+        LimbSet lp = lsqp(pt0->poly, 0, 1, level, T.level, 1);
+        for (size_t c0 = 0; c0 < rp.size(); c0 += ORION_MAXBABY) {
+          const int m = (int)std::min<size_t>(ORION_MAXBABY, rp.size() - c0);
+          Scope sc(this, P_LTMAC, 8.0 * N * lt.nlimb * (2.0 * B * (m + 1) + m));
+          if (c0 == 0) {
+            orion_launch_lt_mac(lt, rp.data(), pp.data(), m, lp, d_tb, N, stream);
+          } else {  // > ORION_MAXBABY babies: accumulate chunk results
+            Poly t2 = alloc(2, nqp, B);
+            LimbSet l2 = lsqp(t2, 0, 2, level, level);
+            orion_launch_lt_mac(l2, rp.data() + c0, pp.data() + c0, m, lp, d_tb, N, stream);
+            ew(EW_ADD, lt, lt, l2);
+          }
+        }
       }
       LimbSet la = lsqp(acc, 0, 2, level, level);
       if (j != 0) {

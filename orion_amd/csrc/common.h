@@ -25,15 +25,20 @@ struct ModConst {
   u64 q;        // modulus
   u64 bar_mu;   // floor(2^(2k) / q), k = bitlen(q)   (Barrett)
   int bar_k;    // bitlen(q)
-  int pad;
+  int f64;      // 1: NTT in float64 arithmetic (q < 2^ORION_F64_BITS)
   u64 ninv, ninv_s;  // N^-1 and its Shoup companion
+  double qd, qinv_d, ninv_d;  // float64 path: q, 1/q, centered N^-1
 };
+#define ORION_F64_BITS 46
 
 struct DeviceTables {
   ModConst mc[ORION_MAXMOD];
   // twiddles, interleaved {w, floor(w*2^64/q)} : fwd[m][k] = psi^bitrev(k), inv = psi^-bitrev(k)
   const ulonglong2* fwd[ORION_MAXMOD];
   const ulonglong2* inv[ORION_MAXMOD];
+  // float64 path: centered twiddles (|w| <= q/2) as doubles, same indexing
+  const double* fwd_d[ORION_MAXMOD];
+  const double* inv_d[ORION_MAXMOD];
 };
 
 // ---------------------------------------------------------------------------
@@ -90,6 +95,29 @@ __host__ __device__ static inline u64 barrett128(u64 hi, u64 lo, const ModConst&
 __host__ __device__ static inline u64 mul_mod(u64 a, u64 b, const ModConst& m) {
   return barrett128(mulhi64(a, b), a * b, m);
 }
+// Barrett reduction of a 128-bit sum of up to 4 products, x < 4 q^2 (q < 2^61):
+// t1 = x >> (k-1) < 2^(k+3) still fits 64 bits; the quotient estimate is low
+// by at most 4, so r < 5q < 2^64.
+__host__ __device__ static inline u64 barrett128_4(u64 hi, u64 lo, const ModConst& m) {
+  const int k = m.bar_k;
+  u64 t1 = (lo >> (k - 1)) | (hi << (65 - k));
+  u64 ph = mulhi64(t1, m.bar_mu), pl = t1 * m.bar_mu;
+  u64 t2 = (pl >> (k + 1)) | (ph << (63 - k));
+  u64 r = lo - t2 * m.q;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r = r >= m.q ? r - m.q : r;
+  return r;
+}
+// 128-bit accumulator helpers
+struct Acc128 {
+  u64 hi, lo;
+};
+__host__ __device__ static inline void mac128(Acc128& a, u64 x, u64 y) {
+  const u64 l = x * y, h = mulhi64(x, y);
+  const u64 nl = a.lo + l;
+  a.hi += h + (nl < l);
+  a.lo = nl;
+}
 
 // ---------------------------------------------------------------------------
 // host-side tables for basis extension (ModUp / ModDown), device-resident
@@ -98,12 +126,15 @@ __host__ __device__ static inline u64 mul_mod(u64 a, u64 b, const ModConst& m) {
 //   out_t = sum_i y_i * qhat_t[t][i] - v * S_t[t]   mod t
 // ---------------------------------------------------------------------------
 #define ORION_MAXSRC 8
+#define ORION_MAXBABY 64  // baby steps fused into one BSGS giant-step MAC launch
 struct BasisExtTable {
   int ns, nt;
   int src_mod[ORION_MAXSRC];
   int dst_mod[ORION_MAXLIMB];
   u64 qhatinv[ORION_MAXSRC], qhatinv_s[ORION_MAXSRC];
   double qinv_f[ORION_MAXSRC];
-  u64 qhat_t[ORION_MAXLIMB][ORION_MAXSRC];
+  u64 qhat_t[ORION_MAXLIMB][ORION_MAXSRC];    // (S/s_i) mod t
+  u64 qhat_ts[ORION_MAXLIMB][ORION_MAXSRC];   // its Shoup companion
   u64 S_t[ORION_MAXLIMB];
+  u64 vS_t[ORION_MAXLIMB][ORION_MAXSRC + 1];  // (t - v*S mod t) mod t, v = 0..ns (Lattigo vtimesqmodp)
 };

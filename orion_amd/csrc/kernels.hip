@@ -146,14 +146,16 @@ __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in,
     vf = __dadd_rn(vf, __dmul_rn((double)y[i], T->qinv_f[i]));
   }
   const u64 v = (u64)vf;
+  // out_t = sum_i y_i * (S/s_i mod t) - v*S  (mod t); y_i < s_i may exceed t, the
+  // Shoup product accepts any 64-bit multiplicand and returns [0, 2t)
   for (int t = 0; t < nt; ++t) {
-    const ModConst mc = tb->mc[T->dst_mod[t]];
-    u64 acc = 0;
+    const u64 q = tb->mc[T->dst_mod[t]].q;
+    u64 acc = T->vS_t[t][v];
     for (int i = 0; i < ns; ++i) {
-      const u64 yi = barrett128(0, y[i], mc);
-      acc = add_mod(acc, mul_mod(yi, T->qhat_t[t][i], mc), mc.q);
+      u64 r = shoup_lazy(y[i], T->qhat_t[t][i], T->qhat_ts[t][i], q);
+      r = r >= q ? r - q : r;
+      acc = add_mod(acc, r, q);
     }
-    acc = sub_mod(acc, mul_mod(v, T->S_t[t], mc), mc.q);
     out.p[row_off(out, c, t, bi) + n] = acc;
   }
 }
@@ -176,16 +178,25 @@ __global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, con
     r0 = *(const ulonglong2*)(out.p + row_off(out, 0, l, bi) + n);
     r1 = *(const ulonglong2*)(out.p + row_off(out, 1, l, bi) + n);
   }
+  // d, key < q: each product < q^2; sum 4 of them in 128 bits, reduce once
+  Acc128 s0x = {0, 0}, s0y = {0, 0}, s1x = {0, 0}, s1y = {0, 0};
   for (int i = 0; i < beta; ++i) {
     const ulonglong2 d = *(const ulonglong2*)(D.p + row_off(D, i, l, bi) + n);
     const u64* kb = key + ((long long)(i * 2 + 0) * nmod_key + m) * N + n;
     const u64* ka = key + ((long long)(i * 2 + 1) * nmod_key + m) * N + n;
     const ulonglong2 b = *(const ulonglong2*)kb;
     const ulonglong2 a = *(const ulonglong2*)ka;
-    r0.x = add_mod(r0.x, mul_mod(d.x, b.x, mc), q);
-    r0.y = add_mod(r0.y, mul_mod(d.y, b.y, mc), q);
-    r1.x = add_mod(r1.x, mul_mod(d.x, a.x, mc), q);
-    r1.y = add_mod(r1.y, mul_mod(d.y, a.y, mc), q);
+    mac128(s0x, d.x, b.x);
+    mac128(s0y, d.y, b.y);
+    mac128(s1x, d.x, a.x);
+    mac128(s1y, d.y, a.y);
+    if ((i & 3) == 3 || i == beta - 1) {
+      r0.x = add_mod(r0.x, barrett128_4(s0x.hi, s0x.lo, mc), q);
+      r0.y = add_mod(r0.y, barrett128_4(s0y.hi, s0y.lo, mc), q);
+      r1.x = add_mod(r1.x, barrett128_4(s1x.hi, s1x.lo, mc), q);
+      r1.y = add_mod(r1.y, barrett128_4(s1y.hi, s1y.lo, mc), q);
+      s0x = s0y = s1x = s1y = Acc128{0, 0};
+    }
   }
   *(ulonglong2*)(out.p + row_off(out, 0, l, bi) + n) = r0;
   *(ulonglong2*)(out.p + row_off(out, 1, l, bi) + n) = r1;
@@ -212,6 +223,47 @@ __global__ void __launch_bounds__(256) automorph_kernel(LimbSet o, LimbSet a, co
     z.y = add_mod(z.y, w.y, q);
   }
   *(ulonglong2*)dst = z;
+}
+
+// BSGS giant-step MAC (lintrans MultiplyByDiagMatrixBSGS inner loop, fused):
+//   t[c][l][b] = sum_i pt_i[l] * rot_i[c][l][b]   for c = 0, 1
+// rot_i share t's layout; pt_i is one limb plane per QP position (pt_pos[l]).
+// Grid: x = image (fastest, so the blocks that reuse a pt chunk run together),
+// y = coefficient chunk, z = limb.  Products are summed in 128 bits and
+// reduced once per 4 terms.
+struct LtMacArgs {
+  const u64* rot[ORION_MAXBABY];
+  const u64* pt[ORION_MAXBABY];
+};
+__global__ void __launch_bounds__(256) lt_mac_kernel(LimbSet t, LtMacArgs A, int m, const unsigned char* __restrict__ pt_pos_unused,
+                                                     LimbSet ptl, const DeviceTables* __restrict__ tb, int N) {
+  const int bi = blockIdx.x;
+  const int n = (blockIdx.y * blockDim.x + threadIdx.x) * 2;
+  const int l = blockIdx.z;
+  if (n >= N) return;
+  const ModConst mc = tb->mc[t.mod[l]];
+  const long long ro0 = row_off(t, 0, l, bi) + n, ro1 = row_off(t, 1, l, bi) + n;
+  const long long po = (long long)ptl.pos[l] * ptl.limb_stride + n;
+  Acc128 a0x = {0, 0}, a0y = {0, 0}, a1x = {0, 0}, a1y = {0, 0};
+  u64 r0x = 0, r0y = 0, r1x = 0, r1y = 0;
+  for (int i = 0; i < m; ++i) {
+    const ulonglong2 p = *(const ulonglong2*)(A.pt[i] + po);
+    const ulonglong2 x0 = *(const ulonglong2*)(A.rot[i] + ro0);
+    const ulonglong2 x1 = *(const ulonglong2*)(A.rot[i] + ro1);
+    mac128(a0x, p.x, x0.x);
+    mac128(a0y, p.y, x0.y);
+    mac128(a1x, p.x, x1.x);
+    mac128(a1y, p.y, x1.y);
+    if ((i & 3) == 3 || i == m - 1) {
+      r0x = add_mod(r0x, barrett128_4(a0x.hi, a0x.lo, mc), mc.q);
+      r0y = add_mod(r0y, barrett128_4(a0y.hi, a0y.lo, mc), mc.q);
+      r1x = add_mod(r1x, barrett128_4(a1x.hi, a1x.lo, mc), mc.q);
+      r1y = add_mod(r1y, barrett128_4(a1y.hi, a1y.lo, mc), mc.q);
+      a0x = a0y = a1x = a1y = Acc128{0, 0};
+    }
+  }
+  *(ulonglong2*)(t.p + ro0) = make_ulonglong2(r0x, r0y);
+  *(ulonglong2*)(t.p + ro1) = make_ulonglong2(r1x, r1y);
 }
 
 inline dim3 ew_grid(int N, int rows) { return dim3((N / 2 + 255) / 256, rows); }
@@ -270,6 +322,19 @@ int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const u64* key, in
   const int rows = out.nlimb * out.nbatch;
   hipLaunchKernelGGL(ks_mac_kernel, ew_grid(N, rows), dim3(256), 0, st, out, D, key, beta, nmod_key, tb, N,
                      accumulate);
+  return 0;
+}
+
+int orion_launch_lt_mac(const LimbSet& t, const u64* const* rot, const u64* const* pt, int m, const LimbSet& ptl,
+                        const DeviceTables* tb, int N, hipStream_t st) {
+  if (m < 1 || m > ORION_MAXBABY) return -1;
+  LtMacArgs A;
+  for (int i = 0; i < m; ++i) {
+    A.rot[i] = rot[i];
+    A.pt[i] = pt[i];
+  }
+  dim3 g(t.nbatch, (N / 2 + 255) / 256, t.nlimb);
+  hipLaunchKernelGGL(lt_mac_kernel, g, dim3(256), 0, st, t, A, m, (const unsigned char*)nullptr, ptl, tb, N);
   return 0;
 }
 

@@ -4,7 +4,8 @@
 // /root/reference/orion/backend/lattigo/evaluator.go:
 // forward = Cooley-Tukey, natural order in, bit-reversed out, twiddle for the
 // butterfly group i of the stage with m groups = psi^bitrev(m+i); inverse =
-// Gentleman-Sande with psi^-1 and a final N^-1.
+// Gentleman-Sande with psi^-1 and a final N^-1.  Outputs are fully reduced,
+// so they are bit-identical to any exact NTT with the same psi.
 //
 // MI355X design (one limb per workgroup, register resident):
 //   * N/32 threads per workgroup, 32 u64 per thread held in VGPRs (64 VGPRs);
@@ -14,10 +15,30 @@
 //     butterfly network); between rounds the limb is re-distributed through
 //     LDS in two 32-bit halves (N*4 B + padding = 132 KiB for N = 2^15), with
 //     a one-word-per-32 pad that makes every exchange bank-conflict free.
-//   * Harvey lazy butterflies with Shoup twiddles: values stay in [0, 4q)
-//     (forward) / [0, 2q) (inverse) between stages; one u64 x u64 -> hi
-//     product per butterfly.  Twiddles are {w, w'} pairs, 16-B loads.
+//     The last (forward) / first (inverse) round is the one whose thread
+//     holds 32 consecutive elements, accessed with 16-byte loads/stores.
+//   * Two arithmetic paths, chosen per limb (block-uniform):
+//       - integer (q >= 2^46): Harvey lazy butterflies with Shoup twiddles,
+//         values in [0, 4q);
+//       - float64 (q < 2^46, i.e. the 40-bit Q primes): values are signed
+//         integers held exactly in doubles, a*w mod q = fma residuals
+//         (h = a*w, l = fma(a, w, -h), k = rint(h/q), r = fma(-k, q, h) + l).
+//         On gfx950 one FP64 op issues at the rate of one 32-bit integer
+//         multiply piece (tools/ubench/valu_rates.hip), and the float path
+//         needs ~9 of them per butterfly instead of ~30 integer instructions.
 #include "common.h"
+
+// timing-only ablation builds (tools/ntt_ablate.sh); 0 in the product:
+// bit 0 skips the butterfly rounds, bit 1 skips the LDS exchanges
+#ifndef NTT_ABLATE
+#define NTT_ABLATE 0
+#endif
+// forward store strategy: 0 = 16-byte stores straight from window 0 (lane
+// stride 256 B); 1 = one more LDS exchange back to window B0, then fully
+// coalesced 8-byte stores
+#ifndef NTT_FWD_COAL
+#define NTT_FWD_COAL 1
+#endif
 
 namespace {
 
@@ -25,48 +46,11 @@ template <int LOGN>
 struct NttGeom {
   static constexpr int N = 1 << LOGN;
   static constexpr int T = N / 32;  // threads
-  static constexpr int B0 = LOGN - 5;
 };
 
-__device__ __forceinline__ int lds_pad(int e) { return e + (e >> 5); }
-
-// One limb is addressed through a buffer descriptor built from wave-uniform
-// values: element k*2^B0 + t is voffset t*8 plus a per-k SGPR/immediate
-// offset, so the 32 loads/stores need no per-element VGPR addresses (hipcc
-// otherwise keeps 32 64-bit addresses live from the load to the store and
-// spills them).  The descriptor's range check also confines the kernel to
-// its limb.
-__device__ __forceinline__ u64 buf_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  return __builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
-}
-__device__ __forceinline__ void buf_ld2(__amdgpu_buffer_rsrc_t r, u64& x, u64& y, int voff, int soff) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
-  x = ((u64)v[1] << 32) | v[0];
-  y = ((u64)v[3] << 32) | v[2];
-}
-__device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, u64 x, u64 y, int voff, int soff) {
-  __attribute__((ext_vector_type(4))) unsigned v = {(unsigned)x, (unsigned)(x >> 32), (unsigned)y,
-                                                   (unsigned)(y >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
-}
-__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, u64 v, int voff, int soff) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), r,
-                                        voff, soff, 0);
-}
-
-// element index held in slot k of thread t for the round whose 5 k-bits start at bit B
-template <int B>
-__device__ __forceinline__ int elem(int t, int k) {
-  return ((t >> B) << (B + 5)) | (k << B) | (t & ((1 << B) - 1));
-}
-
-// Redistribute a[] from window BOLD to window BNEW through LDS, one 32-bit
-// half at a time (the whole limb does not fit in 160 KiB of LDS as u64).
-// The halves live in two u32 arrays so the exchange never needs more than
-// the 64 VGPRs of the data itself.
 // LDS word of element e is pad(e) = e + (e >> 5).  With e = T | (k << B) (disjoint
-// fields) this splits into a per-thread base and a compile-time per-slot offset,
-// so every ds_read/ds_write is base VGPR + immediate.
+// fields: T = thread part, k = slot) this splits into a per-thread base and a
+// compile-time per-slot offset, so every ds_read/ds_write is base VGPR + immediate.
 template <int B>
 __device__ __forceinline__ int lds_base(int t) {
   const int T = ((t >> B) << (B + 5)) | (t & ((1 << B) - 1));
@@ -77,15 +61,142 @@ __host__ __device__ constexpr int lds_off(int k) {
   return (k << B) + ((k << B) >> 5);
 }
 
-template <int BOLD, int BNEW>
-__device__ __forceinline__ void exchange(u64 (&a)[32], u32* lds, int t) {
+// The limb is addressed through a buffer descriptor built from wave-uniform
+// values: every access is a lane offset plus an immediate/SGPR offset, so no
+// per-element VGPR addresses stay live (hipcc otherwise spills them), and the
+// descriptor's range check confines the kernel to its limb.
+__device__ __forceinline__ void buf_ld2(__amdgpu_buffer_rsrc_t r, u64& x, u64& y, int voff, int soff) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  x = ((u64)v[1] << 32) | v[0];
+  y = ((u64)v[3] << 32) | v[2];
+}
+__device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, u64 x, u64 y, int voff, int soff) {
+  __attribute__((ext_vector_type(4))) unsigned v = {(unsigned)x, (unsigned)(x >> 32), (unsigned)y,
+                                                   (unsigned)(y >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+}
+__device__ __forceinline__ u64 buf_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, u64 v, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), r,
+                                        voff, soff, 0);
+}
+
+#define NTT_FENCE() __builtin_amdgcn_sched_barrier(0)
+// An empty volatile asm that "redefines" a butterfly's two inputs: volatile
+// asm statements stay in program order, so no butterfly can be hoisted above
+// its predecessors by IR-level code motion (which sched_barrier cannot stop)
+// -- this is what keeps the kernel at <= 128 VGPRs (1024 threads/CU).
+#define PIN(x, y) asm volatile("" : "+v"(x), "+v"(y))
+
+// ---------------------------------------------------------------------------
+// arithmetic policies
+// ---------------------------------------------------------------------------
+struct IntArith {
+  typedef u64 T;
+  typedef ulonglong2 W;
+  u64 q, q2, ninv, ninv_s;
+  __device__ IntArith(const ModConst& m) : q(m.q), q2(m.q << 1), ninv(m.ninv), ninv_s(m.ninv_s) {}
+  __device__ __forceinline__ W tw(__amdgpu_buffer_rsrc_t r, int vidx, int sidx) const {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, vidx * 16, sidx * 16, 0);
+    return make_ulonglong2(((u64)v[1] << 32) | v[0], ((u64)v[3] << 32) | v[2]);
+  }
+  __device__ __forceinline__ T from_u64(u64 x) const { return x; }
+  // Harvey CT butterfly, values in [0, 4q)
+  __device__ __forceinline__ void ct(T& X, T& Y, const W& w) const {
+    const u64 x = X >= q2 ? X - q2 : X;
+    const u64 t = shoup_lazy(Y, w.x, w.y, q);
+    X = x + t;
+    Y = x - t + q2;
+  }
+  // Harvey GS butterfly, values in [0, 2q)
+  __device__ __forceinline__ void gs(T& X, T& Y, const W& w, bool) const {
+    const u64 x = X, y = Y;
+    const u64 s = x + y;
+    X = s >= q2 ? s - q2 : s;
+    Y = shoup_lazy(x - y + q2, w.x, w.y, q);
+  }
+  __device__ __forceinline__ T reduce_round(T x) const { return x; }  // lazy range is invariant
+  __device__ __forceinline__ u64 final_fwd(T x) const {
+    x = x >= q2 ? x - q2 : x;
+    return x >= q ? x - q : x;
+  }
+  __device__ __forceinline__ u64 final_inv(T x) const {
+    x = shoup_lazy(x, ninv, ninv_s, q);
+    return x >= q ? x - q : x;
+  }
+};
+
+struct F64Arith {
+  typedef double T;
+  typedef double W;
+  double q, qinv, ninv;
+  __device__ F64Arith(const ModConst& m) : q(m.qd), qinv(m.qinv_d), ninv(m.ninv_d) {}
+  __device__ __forceinline__ W tw(__amdgpu_buffer_rsrc_t r, int vidx, int sidx) const {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vidx * 8, sidx * 8, 0));
+  }
+  __device__ __forceinline__ T from_u64(u64 x) const { return (double)x; }
+  // a*w mod q for exact integer doubles (|a| < 16q, |w| <= q/2, q < 2^46):
+  // h + l == a*w exactly, k*q within 1.5q of h, so the result is exact and
+  // |result| < 1.5q + ulp(h)/2 < 2q
+  __device__ __forceinline__ double mulmod(double a, double w) const {
+    const double h = a * w;
+    const double l = __builtin_fma(a, w, -h);
+    const double k = __builtin_rint(h * qinv);
+    return __builtin_fma(-k, q, h) + l;
+  }
+  __device__ __forceinline__ double red(double x) const { return __builtin_fma(-__builtin_rint(x * qinv), q, x); }
+  // CT: |x|, |y| stay below ~12q inside a round (reduced at round boundaries)
+  __device__ __forceinline__ void ct(T& X, T& Y, const W& w) const {
+    const double t = mulmod(Y, w);
+    const double x = X;
+    X = x + t;
+    Y = x - t;
+  }
+  // GS: the sum is reduced every other stage
+  __device__ __forceinline__ void gs(T& X, T& Y, const W& w, bool reduce_sum) const {
+    const double x = X, y = Y;
+    const double s = x + y;
+    X = reduce_sum ? red(s) : s;
+    Y = mulmod(x - y, w);
+  }
+  __device__ __forceinline__ T reduce_round(T x) const { return red(x); }
+  __device__ __forceinline__ u64 to_u64(double x) const {
+    x = red(x);
+    x = x < 0 ? x + q : x;
+    x = x >= q ? x - q : x;
+    x = x < 0 ? x + q : x;
+    return (u64)x;
+  }
+  __device__ __forceinline__ u64 final_fwd(T x) const { return to_u64(x); }
+  __device__ __forceinline__ u64 final_inv(T x) const { return to_u64(mulmod(x, ninv)); }
+};
+
+template <class T>
+__device__ __forceinline__ u64 to_bits(T x) {
+  return __builtin_bit_cast(u64, x);
+}
+template <class T>
+__device__ __forceinline__ T from_bits(u64 x) {
+  return __builtin_bit_cast(T, x);
+}
+
+// Redistribute a[] from window BOLD to window BNEW through LDS, one 32-bit
+// half at a time (the whole limb does not fit in 160 KiB of LDS as u64).
+// The halves live in two u32 arrays so the exchange needs no VGPRs beyond the
+// data's own 64.
+template <class T, int BOLD, int BNEW>
+__device__ __forceinline__ void exchange(T (&a)[32], u32* lds, int t) {
+  if (NTT_ABLATE & 2) return;
   u32 lo[32], hi[32];
   u32* const wr = lds + lds_base<BOLD>(t);
   u32* const rd = lds + lds_base<BNEW>(t);
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
-    lo[k] = (u32)a[k];
-    hi[k] = (u32)(a[k] >> 32);
+    const u64 b = to_bits(a[k]);
+    lo[k] = (u32)b;
+    hi[k] = (u32)(b >> 32);
   }
 #pragma unroll
   for (int k = 0; k < 32; ++k) wr[lds_off<BOLD>(k)] = lo[k];
@@ -100,83 +211,114 @@ __device__ __forceinline__ void exchange(u64 (&a)[32], u32* lds, int t) {
   for (int k = 0; k < 32; ++k) hi[k] = rd[lds_off<BNEW>(k)];
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < 32; ++k) a[k] = ((u64)hi[k] << 32) | lo[k];
+  for (int k = 0; k < 32; ++k) a[k] = from_bits<T>(((u64)hi[k] << 32) | lo[k]);
 }
 
-// keeps the scheduler from hoisting every twiddle load of a round (which
-// would need 124 extra VGPRs and spill): twiddles are loaded group by group.
-#define NTT_FENCE() __builtin_amdgcn_sched_barrier(0)
-// An empty volatile asm that "redefines" a butterfly's two inputs: volatile
-// asm statements stay in program order, so no butterfly can be hoisted above
-// its predecessors by IR-level code motion (which sched_barrier cannot stop).
-#define PIN(x, y) asm volatile("" : "+v"(x), "+v"(y))
+// Twiddle schedule of one round: its stages in execution order, each with
+// 2^(4-dk) distinct twiddles (dk = stage bit - window base B).  Twiddles are
+// software-prefetched TW_PF groups ahead through a compile-time ring, so the
+// L2 latency of a per-thread twiddle load is hidden behind earlier butterflies.
+#define TW_PF 4
+template <int B, int DFIRST, int DLAST>
+struct RoundPlan {
+  static constexpr int DIR = DLAST >= DFIRST ? 1 : -1;
+  static constexpr int nstage = (DLAST - DFIRST) * DIR + 1;
+  static constexpr int d_of(int s) { return DFIRST + s * DIR; }
+  static constexpr int g_of(int s) { return 1 << (4 - (d_of(s) - B)); }
+  static constexpr int first(int s) { return s == 0 ? 0 : first(s - 1) + g_of(s - 1); }
+  static constexpr int total() { return first(nstage - 1) + g_of(nstage - 1); }
+  static constexpr int stage_of(int i, int s = 0) { return i < first(s) + g_of(s) ? s : stage_of(i, s + 1); }
+};
 
-#if defined(__HIP_DEVICE_COMPILE__)
-typedef const __attribute__((address_space(1))) ulonglong2* gtw_ptr;  // global (not flat) twiddle loads
-#else
-typedef const ulonglong2* gtw_ptr;
-#endif
-
-// Forward CT stages for bits DHI..DLO (all inside the window starting at B).
-// The 16 butterflies of a stage are issued in fenced groups of 4 so that at
-// most 4 are in flight per thread (64 VGPRs hold the data, the rest must
-// cover temporaries: the kernel has to fit 128 VGPRs at 1024 threads).
-__device__ __forceinline__ ulonglong2 tw_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
-  return make_ulonglong2(((u64)v[1] << 32) | v[0], ((u64)v[3] << 32) | v[2]);
+template <class A, int LOGN, int B, class Plan, int I>
+__device__ __forceinline__ typename A::W tw_load(const A& ar, __amdgpu_buffer_rsrc_t w, int thigh) {
+  constexpr int s = Plan::stage_of(I);
+  constexpr int d = Plan::d_of(s), dk = d - B, khi = I - Plan::first(s);
+  constexpr int m = (1 << LOGN) >> (d + 1);
+  return ar.tw(w, thigh << (4 - dk), m + khi);
 }
 
-template <int LOGN, int B, int DHI, int DLO>
-__device__ __forceinline__ void fwd_round(u64 (&a)[32], __amdgpu_buffer_rsrc_t w, u64 q, int t) {
-  const u64 q2 = q << 1;
-  const int thigh = t >> B;
+template <class A, int LOGN, int B, class Plan, int I>
+__device__ __forceinline__ void tw_prefetch(typename A::W (&ring)[TW_PF], const A& ar, __amdgpu_buffer_rsrc_t w,
+                                            int thigh) {
+  if constexpr (I < Plan::total()) ring[I % TW_PF] = tw_load<A, LOGN, B, Plan, I>(ar, w, thigh);
+}
+
+// One stage's 16 butterflies.  Twiddle of the butterfly group i = e >> (d+1)
+// of stage d is w[m + i], m = N >> (d+1); with e = T | (k << B) that is
+// m + ((t>>B) << (4-dk) | khi).
+template <class A, int LOGN, int B, class Plan, int S, bool FWD>
+__device__ __forceinline__ void run_stage(typename A::T (&a)[32], typename A::W (&ring)[TW_PF], const A& ar,
+                                          __amdgpu_buffer_rsrc_t w, int thigh) {
+  constexpr int d = Plan::d_of(S), dk = d - B;
+  typename A::W W;
 #pragma unroll
-  for (int d = DHI; d >= DLO; --d) {
-    const int dk = d - B;
-    const int m = (1 << LOGN) >> (d + 1);
-    ulonglong2 W;
-#pragma unroll
-    for (int pr = 0; pr < 16; ++pr) {
-      const int khi = pr >> dk, klo = pr & ((1 << dk) - 1);
-      if (klo == 0) W = tw_ld(w, (thigh << (4 - dk)) * 16, (m + khi) * 16);
-      const int k0 = (khi << (dk + 1)) | klo;
-      const int k1 = k0 | (1 << dk);
-      PIN(a[k0], a[k1]);
-      u64 X = a[k0];
-      X = X >= q2 ? X - q2 : X;
-      const u64 T = shoup_lazy(a[k1], W.x, W.y, q);
-      a[k0] = X + T;
-      a[k1] = X - T + q2;
-      if ((pr & 3) == 3) NTT_FENCE();
+  for (int pr = 0; pr < 16; ++pr) {
+    const int khi = pr >> dk, klo = pr & ((1 << dk) - 1);
+    if (klo == 0) {
+      const int i = Plan::first(S) + khi;
+      W = ring[i % TW_PF];
+      // refill the slot just consumed with the twiddle TW_PF groups ahead
+      switch (i) {
+#define TWC(J) case J: tw_prefetch<A, LOGN, B, Plan, J + TW_PF>(ring, ar, w, thigh); break;
+        TWC(0) TWC(1) TWC(2) TWC(3) TWC(4) TWC(5) TWC(6) TWC(7) TWC(8) TWC(9) TWC(10) TWC(11) TWC(12)
+        TWC(13) TWC(14) TWC(15) TWC(16) TWC(17) TWC(18) TWC(19) TWC(20) TWC(21) TWC(22) TWC(23) TWC(24)
+        TWC(25) TWC(26) TWC(27) TWC(28) TWC(29) TWC(30) TWC(31)
+#undef TWC
+        default: break;
+      }
     }
-  }
-}
-
-// Inverse GS stages for bits DLO..DHI.
-template <int LOGN, int B, int DLO, int DHI>
-__device__ __forceinline__ void inv_round(u64 (&a)[32], __amdgpu_buffer_rsrc_t w, u64 q, int t) {
-  const u64 q2 = q << 1;
-  const int thigh = t >> B;
-#pragma unroll
-  for (int d = DLO; d <= DHI; ++d) {
-    const int dk = d - B;
-    const int m = (1 << LOGN) >> (d + 1);
-    ulonglong2 W;
-#pragma unroll
-    for (int pr = 0; pr < 16; ++pr) {
-      const int khi = pr >> dk, klo = pr & ((1 << dk) - 1);
-      if (klo == 0) W = tw_ld(w, (thigh << (4 - dk)) * 16, (m + khi) * 16);
-      const int k0 = (khi << (dk + 1)) | klo;
-      const int k1 = k0 | (1 << dk);
-      PIN(a[k0], a[k1]);
-      const u64 X = a[k0], Y = a[k1];
-      u64 S = X + Y;
-      S = S >= q2 ? S - q2 : S;
-      a[k0] = S;
-      a[k1] = shoup_lazy(X - Y + q2, W.x, W.y, q);
+    const int k0 = (khi << (dk + 1)) | klo;
+    const int k1 = k0 | (1 << dk);
+    PIN(a[k0], a[k1]);
+    if constexpr (FWD) {
+      ar.ct(a[k0], a[k1], W);
+      if ((pr & 3) == 3) NTT_FENCE();
+    } else {
+      ar.gs(a[k0], a[k1], W, (S & 1) == 1);
       if ((pr & 1) == 1) NTT_FENCE();
     }
   }
+}
+
+template <class A, int LOGN, int B, class Plan, bool FWD, int S>
+__device__ __forceinline__ void run_stages(typename A::T (&a)[32], typename A::W (&ring)[TW_PF], const A& ar,
+                                           __amdgpu_buffer_rsrc_t w, int thigh) {
+  if constexpr (S < Plan::nstage) {
+    run_stage<A, LOGN, B, Plan, S, FWD>(a, ring, ar, w, thigh);
+    run_stages<A, LOGN, B, Plan, FWD, S + 1>(a, ring, ar, w, thigh);
+  }
+}
+
+template <class A, int LOGN, int B, int DFIRST, int DLAST, bool FWD>
+__device__ __forceinline__ void do_round(typename A::T (&a)[32], const A& ar, __amdgpu_buffer_rsrc_t w, int t) {
+  if (NTT_ABLATE & 1) return;
+  typedef RoundPlan<B, DFIRST, DLAST> Plan;
+  const int thigh = t >> B;
+  typename A::W ring[TW_PF];
+  tw_prefetch<A, LOGN, B, Plan, 0>(ring, ar, w, thigh);
+  tw_prefetch<A, LOGN, B, Plan, 1>(ring, ar, w, thigh);
+  tw_prefetch<A, LOGN, B, Plan, 2>(ring, ar, w, thigh);
+  tw_prefetch<A, LOGN, B, Plan, 3>(ring, ar, w, thigh);
+  run_stages<A, LOGN, B, Plan, FWD, 0>(a, ring, ar, w, thigh);
+}
+
+// Forward CT stages for bits DHI..DLO (all inside the window starting at B).
+template <class A, int LOGN, int B, int DHI, int DLO>
+__device__ __forceinline__ void fwd_round(typename A::T (&a)[32], const A& ar, __amdgpu_buffer_rsrc_t w, int t) {
+  do_round<A, LOGN, B, DHI, DLO, true>(a, ar, w, t);
+}
+
+// Inverse GS stages for bits DLO..DHI.
+template <class A, int LOGN, int B, int DLO, int DHI>
+__device__ __forceinline__ void inv_round(typename A::T (&a)[32], const A& ar, __amdgpu_buffer_rsrc_t w, int t) {
+  do_round<A, LOGN, B, DLO, DHI, false>(a, ar, w, t);
+}
+
+template <class A>
+__device__ __forceinline__ void reduce_all(typename A::T (&a)[32], const A& ar) {
+#pragma unroll
+  for (int k = 0; k < 32; ++k) a[k] = ar.reduce_round(a[k]);
 }
 
 __device__ __forceinline__ u64* job_ptr(const LimbSet& s, int job, int& mod) {
@@ -196,60 +338,98 @@ __device__ __forceinline__ u64* job_ptr(const LimbSet& s, int job, int& mod) {
 
 // Round windows: LOGN=15 -> bits [10,15), [5,10), [0,5); LOGN=14 -> [9,14),[4,9),[0,5)
 // (last round only bits 3..0); LOGN=13 -> [8,13),[3,8),[0,5) (bits 2..0).
-template <int LOGN>
-__global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_fwd_kernel(LimbSet s, const DeviceTables* __restrict__ tb) {
+template <class A, int LOGN>
+__device__ __forceinline__ void ntt_fwd_body(u64* p, const A& ar, __amdgpu_buffer_rsrc_t w, u32* lds) {
   constexpr int N = 1 << LOGN, B0 = LOGN - 5, B1 = LOGN - 10;
-  extern __shared__ u32 lds[];
   const int t = threadIdx.x;
-  int mod;
-  u64* __restrict__ p = job_ptr(s, blockIdx.x, mod);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p, 0, N * 8, 0x00020000);
-  const u64 q = tb->mc[mod].q;
-  const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd[mod], 0, (1 << LOGN) * 16, 0x00020000);
-  u64 a[32];
+  typename A::T a[32];
 #pragma unroll
-  for (int k = 0; k < 32; ++k) a[k] = buf_ld(rs, t * 8, (k << B0) * 8);
-  fwd_round<LOGN, B0, LOGN - 1, B0>(a, w, q, t);
-  exchange<B0, B1>(a, lds, t);
-  fwd_round<LOGN, B1, B0 - 1, B1>(a, w, q, t);
-  exchange<B1, 0>(a, lds, t);
-  fwd_round<LOGN, 0, B1 - 1, 0>(a, w, q, t);
-  const u64 q2 = q << 1;
+  for (int k = 0; k < 32; ++k) a[k] = ar.from_u64(buf_ld(rs, t * 8, (k << B0) * 8));
+  fwd_round<A, LOGN, B0, LOGN - 1, B0>(a, ar, w, t);
+  reduce_all<A>(a, ar);
+  exchange<typename A::T, B0, B1>(a, lds, t);
+  fwd_round<A, LOGN, B1, B0 - 1, B1>(a, ar, w, t);
+  reduce_all<A>(a, ar);
+  exchange<typename A::T, B1, 0>(a, lds, t);
+  fwd_round<A, LOGN, 0, B1 - 1, 0>(a, ar, w, t);
+  if constexpr (NTT_FWD_COAL) {
+    u64 r[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) r[k] = ar.final_fwd(a[k]);
+    exchange<u64, 0, B0>(r, lds, t);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      buf_st(rs, r[k], t * 8, (k << B0) * 8);
+      if ((k & 3) == 3) NTT_FENCE();
+    }
+  } else {
+    // window 0: thread t holds elements 32t .. 32t+31 -> 16-byte stores
+#pragma unroll
+    for (int k = 0; k < 32; k += 2) {
+      const u64 x = ar.final_fwd(a[k]), y = ar.final_fwd(a[k + 1]);
+      buf_st2(rs, x, y, t * 256, k * 8);
+      if ((k & 7) == 6) NTT_FENCE();
+    }
+  }
+}
+
+template <class A, int LOGN>
+__device__ __forceinline__ void ntt_inv_body(u64* p, const A& ar, __amdgpu_buffer_rsrc_t w, u32* lds) {
+  constexpr int N = 1 << LOGN, B0 = LOGN - 5, B1 = LOGN - 10;
+  const int t = threadIdx.x;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p, 0, N * 8, 0x00020000);
+  typename A::T a[32];
+#pragma unroll
+  for (int k = 0; k < 32; k += 2) {
+    u64 x, y;
+    buf_ld2(rs, x, y, t * 256, k * 8);
+    a[k] = ar.from_u64(x);
+    a[k + 1] = ar.from_u64(y);
+  }
+  inv_round<A, LOGN, 0, 0, B1 - 1>(a, ar, w, t);
+  reduce_all<A>(a, ar);
+  exchange<typename A::T, 0, B1>(a, lds, t);
+  inv_round<A, LOGN, B1, B1, B0 - 1>(a, ar, w, t);
+  reduce_all<A>(a, ar);
+  exchange<typename A::T, B1, B0>(a, lds, t);
+  inv_round<A, LOGN, B0, B0, LOGN - 1>(a, ar, w, t);
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
-    u64 x = a[k];
-    x = x >= q2 ? x - q2 : x;
-    a[k] = x >= q ? x - q : x;
+    buf_st(rs, ar.final_inv(a[k]), t * 8, (k << B0) * 8);
+    if ((k & 3) == 3) NTT_FENCE();
   }
-  // window 0: thread t holds elements 32t .. 32t+31 -> 16-byte stores
-#pragma unroll
-  for (int k = 0; k < 32; k += 2) buf_st2(rs, a[k], a[k + 1], t * 256, k * 8);
+}
+
+template <int LOGN>
+__global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_fwd_kernel(LimbSet s, const DeviceTables* __restrict__ tb) {
+  constexpr int N = 1 << LOGN;
+  extern __shared__ u32 lds[];
+  int mod;
+  u64* p = job_ptr(s, blockIdx.x, mod);
+  const ModConst mc = tb->mc[mod];
+  if (mc.f64) {
+    const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd_d[mod], 0, N * 8, 0x00020000);
+    ntt_fwd_body<F64Arith, LOGN>(p, F64Arith(mc), w, lds);
+  } else {
+    const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd[mod], 0, N * 16, 0x00020000);
+    ntt_fwd_body<IntArith, LOGN>(p, IntArith(mc), w, lds);
+  }
 }
 
 template <int LOGN>
 __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_inv_kernel(LimbSet s, const DeviceTables* __restrict__ tb) {
-  constexpr int B0 = LOGN - 5, B1 = LOGN - 10;
+  constexpr int N = 1 << LOGN;
   extern __shared__ u32 lds[];
-  const int t = threadIdx.x;
   int mod;
-  u64* __restrict__ p = job_ptr(s, blockIdx.x, mod);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p, 0, (1 << LOGN) * 8, 0x00020000);
+  u64* p = job_ptr(s, blockIdx.x, mod);
   const ModConst mc = tb->mc[mod];
-  const u64 q = mc.q;
-  const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->inv[mod], 0, (1 << LOGN) * 16, 0x00020000);
-  u64 a[32];
-#pragma unroll
-  for (int k = 0; k < 32; k += 2) buf_ld2(rs, a[k], a[k + 1], t * 256, k * 8);
-  inv_round<LOGN, 0, 0, B1 - 1>(a, w, q, t);
-  exchange<0, B1>(a, lds, t);
-  inv_round<LOGN, B1, B1, B0 - 1>(a, w, q, t);
-  exchange<B1, B0>(a, lds, t);
-  inv_round<LOGN, B0, B0, LOGN - 1>(a, w, q, t);
-#pragma unroll
-  for (int k = 0; k < 32; ++k) {
-    u64 x = shoup_lazy(a[k], mc.ninv, mc.ninv_s, q);
-    buf_st(rs, x >= q ? x - q : x, t * 8, (k << B0) * 8);
-    if ((k & 3) == 3) NTT_FENCE();
+  if (mc.f64) {
+    const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->inv_d[mod], 0, N * 8, 0x00020000);
+    ntt_inv_body<F64Arith, LOGN>(p, F64Arith(mc), w, lds);
+  } else {
+    const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->inv[mod], 0, N * 16, 0x00020000);
+    ntt_inv_body<IntArith, LOGN>(p, IntArith(mc), w, lds);
   }
 }
 

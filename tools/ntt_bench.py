@@ -1,0 +1,58 @@
+"""NTT kernel microbenchmark (GPU): per-launch time and algorithmic GB/s for
+the float64 path (40-bit moduli) and the integer path (60-bit moduli) at
+several job counts.  Usage: python tools/ntt_bench.py"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from orion_amd.backend import HipLibrary  # noqa: E402
+
+
+def main():
+    logn = int(os.environ.get("LOGN", 15))
+    N = 1 << logn
+    path = os.environ.get("ORION_LIB")
+    lib = (HipLibrary(path) if path else HipLibrary()).new_scheme(logn, [40] * 8 + [60] * 8, [60], 40)
+    mods = lib.moduli()
+    res = []
+    for kind, mset in [("f64(40-bit)", list(range(0, 8))), ("int(60-bit)", list(range(8, 16)))]:
+        for jobs in [int(j) for j in os.environ.get("JOBS", "256,512,1024,2048").split(",")]:
+            nl = len(mset)
+            B = jobs // nl
+            rng = np.random.default_rng(0)
+            host = np.stack([rng.integers(0, mods[m], (B, N), dtype=np.uint64) for m in mset])
+            dev = torch.from_numpy(host.view(np.int64)).cuda()
+            ptr = ctypes.cast(dev.data_ptr(), ctypes.POINTER(ctypes.c_ulong))
+            mc = (ctypes.c_int * nl)(*mset)
+            for inv in (0, 1):
+                for _ in range(3):
+                    lib.lib.OrionHipNTT(ptr, nl, B, mc, inv)
+                lib.OrionHipSynchronize()
+                s = torch.cuda.Stream(device=0)
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                lib.OrionHipSetStream(s.cuda_stream)
+                reps = 10
+                with torch.cuda.stream(s):
+                    e0.record(s)
+                    for _ in range(reps):
+                        lib.lib.OrionHipNTT(ptr, nl, B, mc, inv)
+                    e1.record(s)
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / reps
+                gbs = 16 * N * jobs / (ms * 1e-3) / 1e9
+                line = f"{kind:12s} {'inv' if inv else 'fwd'} jobs={jobs:5d}  {ms*1e3:8.1f} us/launch  {gbs:7.1f} GB/s  {ms*1e3/ (jobs/256):6.1f} us per 256 limbs"
+                print(line, flush=True)
+                res.append(line)
+            del dev
+    tag = os.environ.get("TAG", "")
+    with open(os.path.join("gpurun_out", f"ntt_bench_{logn}{tag}.txt"), "w") as f:
+        f.write("\n".join(res) + "\n")
+
+
+if __name__ == "__main__":
+    main()
