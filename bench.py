@@ -32,7 +32,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=int(os.environ.get("ORION_BENCH_BATCH", 64)))
     ap.add_argument("--workload", default="lola_n15")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-images", type=int, default=1)
+    ap.add_argument("--cpu-images", type=int, default=12)
     return ap.parse_args()
 
 
@@ -56,10 +56,9 @@ def cpu_baseline(name, n_images):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
+    from orion_amd import dist as odist
+    world, rank, local = odist.env_ranks()
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -81,22 +80,18 @@ def main():
         st.compile(gen_keys=False)
     if world > 1:
         # RCCL broadcast of public + evaluation keys (+ secret for output checks)
-        nbytes = torch.zeros(1, dtype=torch.int64, device="cuda")
-        if rank == 0:
-            nbytes[0] = int(lib.KeyBundleBytes(1))
-        dist.broadcast(nbytes, 0)
-        buf = torch.empty(int(nbytes.item()), dtype=torch.uint8, device="cuda")
-        if rank == 0:
+        def export(buf):
             lib.OrionHipSynchronize()
             if lib.lib.ExportKeyBundle(buf.data_ptr(), 1) != 0:
                 raise RuntimeError(lib.lib.OrionHipLastError().decode())
-        torch.cuda.synchronize()
-        dist.broadcast(buf, 0)
-        torch.cuda.synchronize()
-        if rank != 0:
+            lib.OrionHipSynchronize()
+
+        def load(buf):
             if lib.lib.ImportKeyBundle(buf.data_ptr(), buf.numel()) != 0:
                 raise RuntimeError(lib.lib.OrionHipLastError().decode())
-        del buf
+            lib.OrionHipSynchronize()
+
+        odist.broadcast_bundle(dist, lambda: lib.KeyBundleBytes(1), export, load, torch.device("cuda", local))
     t_setup = time.perf_counter() - t_setup
 
     # this rank's shard of synthetic images (MNIST-shaped, N(0,1), seed 42 + rank)
@@ -131,9 +126,7 @@ def main():
     prof = lib.profile_read()
     if dist:
         dist.barrier()
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt = odist.max_over_ranks(dist, dt, torch.device("cuda", local))
 
     # correctness of the timed output (image 0 is the fixture's reference input)
     res = st.decrypt_output(outs[-1])
@@ -162,8 +155,10 @@ def main():
     if os.path.exists(tfile):
         with open(tfile) as f:
             tj = json.load(f)
-        if tj.get("workload") == args.workload and tj.get("batch") == args.batch:
-            traffic = tj.get("hbm_bytes_per_launch")
+        # HBM bytes per algorithmic byte of the NTT launches, from the committed
+        # rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/pmc_summary.py)
+        if tj.get("workload") == args.workload and tj.get("batch") == args.batch and n_launch:
+            traffic = round(tj["hbm_bytes_per_algorithmic_byte"] * n_bytes / n_launch)
 
     if rank == 0:
         cpu = None

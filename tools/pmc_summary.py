@@ -1,0 +1,68 @@
+"""Summarise one rocprofv3 profiling round (tools/gpu_prof.sh) into profiles/.
+
+Reads gpurun_out/prof_<tag>/ (kernel-trace stats + the FETCH_SIZE, WRITE_SIZE
+and SQ counter passes) and writes
+  profiles/<tag>_kernel_stats.csv   the rocprofv3 --stats summary, verbatim
+  profiles/<tag>_pmc_summary.json   per-kernel counter totals and the NTT HBM
+                                    traffic per algorithmic byte
+  profiles/ntt_traffic.json         HBM bytes per NTT launch for bench.py
+
+HBM bytes follow MI355X_MICROARCH.md (HBM/rocprofv3): FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide
+coalesced reads, so it is doubled.  Algorithmic bytes of an NTT launch =
+16 N per limb-transform (one workgroup of N/32 threads per limb).
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def rows(path):
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+def main(tag, workload="lola_n15", batch=64, logn=15):
+    d = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    shutil.copy(os.path.join(d, "kt_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
+    N = 1 << logn
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    ntt_alg = ntt_fetch = ntt_write = 0.0
+    for name in ("pmc_fetch", "pmc_write", "pmc_sq"):
+        p = os.path.join(d, f"{name}_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        for r in rows(p):
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+            v = float(r["Counter_Value"])
+            per[k][r["Counter_Name"]] += v
+            per[k]["_dispatches_" + name] += 1
+            if "ntt_" in k and int(r["Grid_Size"]) >= N // 32 * 64:  # the batched launches, not keygen
+                wgs = int(r["Grid_Size"]) // (N // 32)
+                if r["Counter_Name"] == "FETCH_SIZE":
+                    ntt_fetch += 2 * v * 1024
+                    ntt_alg += wgs * 16.0 * N
+                elif r["Counter_Name"] == "WRITE_SIZE":
+                    ntt_write += v * 1024
+    ratio = (ntt_fetch + ntt_write) / ntt_alg if ntt_alg else None
+    summary = {"tag": tag, "ntt_hbm_bytes_per_algorithmic_byte": ratio,
+               "ntt_fetch_bytes_per_algorithmic_byte": ntt_fetch / ntt_alg if ntt_alg else None,
+               "kernels": {k: dict(v) for k, v in per.items()}}
+    with open(os.path.join(out, f"{tag}_pmc_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    if ratio:
+        with open(os.path.join(out, "ntt_traffic.json"), "w") as f:
+            json.dump({"tag": tag, "workload": workload, "batch": batch,
+                       "hbm_bytes_per_algorithmic_byte": round(ratio, 4)}, f, indent=1)
+    print(json.dumps({"tag": tag, "ntt_hbm_bytes_per_algorithmic_byte": ratio}))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
