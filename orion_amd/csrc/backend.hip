@@ -32,12 +32,15 @@ int orion_launch_rescale_prep(const LimbSet& dst, const u64* src, long long src_
                               long long src_batch_stride, int modL, const DeviceTables* tb, int N, hipStream_t st);
 int orion_launch_basis_ext(const LimbSet& out, const LimbSet& in, const BasisExtTable* T, const DeviceTables* tb,
                            int N, hipStream_t st);
-int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const u64* key, int beta, int nmod_key,
-                        const DeviceTables* tb, int N, int accumulate, hipStream_t st);
+int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const LimbSet& own, const MacGroups& G, int ngroup,
+                        int beta, int nmod_key, const DeviceTables* tb, int N, hipStream_t st);
 int orion_launch_automorph(const LimbSet& o, const LimbSet& a, const u32* idx, const DeviceTables* tb, int N,
                            int accumulate, hipStream_t st);
-int orion_launch_lt_mac(const LimbSet& t, const u64* const* rot, const u64* const* pt, int m, const LimbSet& ptl,
-                        const DeviceTables* tb, int N, hipStream_t st);
+int orion_launch_lt_bsgs(const LimbSet& t0, const LimbSet& t1, const LimbSet& D, const LimbSet& ct,
+                         const LtBabies& Bb, const LtPlan* plan, int g0, int g1, int accumulate, const LimbSet& ptl,
+                         const DeviceTables* tb, int N, hipStream_t st);
+int orion_launch_lt_giant(const LimbSet& acc, const LimbSet& D, const LimbSet& own, const LimbSet& t0,
+                          const LimbSet& z, const LtGiants& G, const DeviceTables* tb, int N, hipStream_t st);
 
 namespace orion {
 
@@ -123,6 +126,27 @@ struct LinTrans {
   std::map<int, Plaintext> diags;       // keyed by idx & (slots-1)
   std::vector<int> giants, babies;      // sorted giants; babies in first-seen order
   std::map<int, std::vector<int>> index;  // giant -> sorted babies
+  // device BSGS plan (built at first evaluation, rebuilt when diagonals change)
+  std::vector<int> slots;   // baby of each register slot: nonzero babies, then 0
+  std::vector<int> gorder;  // giants in evaluation order: nonzero giants, then 0
+  LtPlan* d_plan = nullptr;
+  int n_plan = 0;
+  bool plan_dirty = true;
+  LinTrans() = default;
+  LinTrans(const LinTrans&) = delete;
+  LinTrans& operator=(const LinTrans&) = delete;
+  LinTrans(LinTrans&& o) noexcept { *this = std::move(o); }
+  LinTrans& operator=(LinTrans&& o) noexcept {
+    level = o.level, N1 = o.N1, ratio = o.ratio;
+    idx = std::move(o.idx), diags = std::move(o.diags), giants = std::move(o.giants), babies = std::move(o.babies);
+    index = std::move(o.index), slots = std::move(o.slots), gorder = std::move(o.gorder);
+    std::swap(d_plan, o.d_plan), std::swap(n_plan, o.n_plan);
+    plan_dirty = o.plan_dirty;
+    return *this;
+  }
+  ~LinTrans() {
+    if (d_plan) hipFree(d_plan);
+  }
 };
 
 template <class T>
@@ -171,7 +195,7 @@ struct ProfRec {
   double bytes;
 };
 static const char* kProfNames[] = {"ntt_fwd", "ntt_inv", "elementwise", "basis_ext", "ks_mac", "automorph",
-                                   "tensor", "rescale_prep", "lt_mac"};
+                                   "tensor", "rescale_prep", "lt_bsgs"};
 enum { P_NTT_FWD = 0, P_NTT_INV, P_EW, P_BEXT, P_MAC, P_AUT, P_TENSOR, P_RSPREP, P_LTMAC, P_NCAT };
 
 // ---------------------------------------------------------------------------
@@ -375,6 +399,7 @@ struct Context {
       mc.q = q;
       mc.bar_k = 64 - __builtin_clzll(q);
       mc.bar_mu = (u64)(((u128)1 << (2 * mc.bar_k)) / q);
+      mc.bar_mu2 = (u64)(((u128)1 << (2 * mc.bar_k + 2)) / q);
       mc.ninv = hm_invmod((u64)N, q);
       mc.ninv_s = hm_shoup(mc.ninv, q);
       const u64 g = primitive_root(q);
@@ -661,50 +686,82 @@ struct Context {
   // ---------------------------------------------------------------------------
   // key switching building blocks
   // ---------------------------------------------------------------------------
-  // decompose a Q poly (1 comp, limbs 0..level) into beta digits extended to QP (NTT)
+  // sub-range [first, first+count) of a LimbSet's limbs
+  static LimbSet limbs(const LimbSet& x, int first, int count) {
+    LimbSet s = x;
+    s.nlimb = count;
+    for (int i = 0; i < count; ++i) {
+      s.pos[i] = x.pos[first + i];
+      s.mod[i] = x.mod[first + i];
+    }
+    return s;
+  }
+  // decompose c.ncomp Q polys (limbs 0..level of c) into beta digits each,
+  // extended to QP and in the NTT domain.  D layout [comp][digit][QP][B], QP
+  // positions at lvl_alloc = level.  Digit i's own Q limbs (l / K == i) equal
+  // c's and are not written: every consumer (ks_mac, lt_bsgs, lt_giant) reads
+  // them from c.
   Poly decompose(const LimbSet& c, int level, int B) {
+    const int nc = c.ncomp;
     const int beta = (level + 1 + K - 1) / K;
     const int nqp = level + 1 + K;
-    Poly cinv = alloc(1, level + 1, B);
-    copy(lsq(cinv, 0, 1, level), c);
-    ntt(lsq(cinv, 0, 1, level), true);
-    Poly D = alloc(beta, nqp, B);
+    Poly cinv = alloc(nc, level + 1, B);
+    copy(lsq(cinv, 0, nc, level), c);
+    ntt(lsq(cinv, 0, nc, level), true);
+    Poly D = alloc(nc * beta, nqp, B);
+    const long long dstride = (long long)beta * D.comp_stride();
     for (int i = 0; i < beta; ++i) {
       const int lo = i * K, hi = std::min((i + 1) * K, level + 1);
       std::vector<int> tpos;
       BasisExtTable* T = modup_tab(level, i, tpos);
       std::vector<int> tmod;
       for (int p : tpos) tmod.push_back(qp_mod(level, p));
-      LimbSet in = ls(cinv, 0, 1, iota(lo, hi), iota(lo, hi));
-      LimbSet out = ls(D, i, 1, tpos, tmod);
+      LimbSet in = ls(cinv, 0, nc, iota(lo, hi), iota(lo, hi));
+      LimbSet out = ls(D, i, nc, tpos, tmod);
+      out.comp_stride = dstride;
       {
-        Scope sc(this, P_BEXT, 8.0 * N * B * (in.nlimb + out.nlimb));
+        Scope sc(this, P_BEXT, 8.0 * N * B * nc * (in.nlimb + out.nlimb));
         orion_launch_basis_ext(out, in, T, d_tb, N, stream);
       }
       ntt(out, false);
-      LimbSet own = ls(D, i, 1, iota(lo, hi), iota(lo, hi));
-      LimbSet src = c;
-      src.nlimb = hi - lo;
-      for (int j = lo; j < hi; ++j) {
-        src.pos[j - lo] = c.pos[j];
-        src.mod[j - lo] = c.mod[j];
-      }
-      copy(own, src);
     }
-    return D;
+    return D;  // the own Q limbs of each digit are left unset: consumers read them from c
+
   }
-  // out (2 comps, QP at level) [+]= sum_i D_i * key_i
-  void mac(const Poly& out, const Poly& D, const Poly& key, int level, bool acc) {
-    const int beta = (level + 1 + K - 1) / K;
-    LimbSet o = lsqp(out, 0, 2, level, level);
-    LimbSet d = lsqp(D, 0, beta, level, level);
-    Scope sc(this, P_MAC, 8.0 * N * o.nlimb * (o.nbatch * (beta + 2 + (acc ? 2 : 0)) + 2 * beta));
-    orion_launch_ks_mac(o, d, key.ptr(), beta, L + K, d_tb, N, acc ? 1 : 0, stream);
+  // grouped gadget products: out_g (comps 0/1 at o.p + g*out_gstride) =
+  //   [add0_g on comp 0] + sum_i D_g,i * keys[g]_i,   D_g at d.p + g*d_gstride,
+  // own Q limbs of each digit read from own (group stride own_gstride)
+  void mac_groups(const LimbSet& o, long long out_gstride, const LimbSet& d, long long d_gstride,
+                  const LimbSet& own, long long own_gstride, const std::vector<const u64*>& keys, int beta,
+                  const u64* add0 = nullptr, long long add_gstride = 0) {
+    const int G = (int)keys.size();
+    for (int g0 = 0; g0 < G; g0 += ORION_MAXGROUP) {
+      const int ng = std::min(ORION_MAXGROUP, G - g0);
+      MacGroups mg;
+      memset(&mg, 0, sizeof(mg));
+      for (int g = 0; g < ng; ++g) mg.key[g] = keys[g0 + g];
+      mg.out_gstride = out_gstride;
+      mg.d_gstride = d_gstride;
+      mg.add_gstride = add_gstride;
+      mg.own_gstride = own_gstride;
+      mg.K = K;
+      mg.add0 = add0 ? add0 + g0 * add_gstride : nullptr;
+      LimbSet oo = o, dd = d, ow = own;
+      oo.p += g0 * out_gstride;
+      dd.p += g0 * d_gstride;
+      ow.p += g0 * own_gstride;
+      const double rows = (double)o.nlimb * o.nbatch;
+      const double dreads = d_gstride ? rows * ng * beta : rows * beta;
+      Scope sc(this, P_MAC, 8.0 * N * (dreads + rows * ng * (2 + (add0 ? 1 : 0)) + 2.0 * beta * ng * o.nlimb));
+      if (orion_launch_ks_mac(oo, dd, ow, mg, ng, beta, L + K, d_tb, N, stream))
+        throw std::runtime_error("ks_mac launch failed");
+    }
   }
-  // x: poly with comps [c0, c0+nc) in QP layout (alloc level lvl_alloc); clobbers x's P limbs
-  void moddown(const Poly& x, int c0, int nc, int level, int lvl_alloc, const LimbSet& out) {
-    const int B = x.B;
-    LimbSet xp = ls(x, c0, nc, iota(lvl_alloc + 1, lvl_alloc + 1 + K), iota(L, L + K));
+  // x: x.ncomp polys, QP limbs in the order [Q 0..level][P 0..K-1] (any strides);
+  // out = (x_Q - ModUp(INTT(x_P))) * P^-1.  Clobbers x's P limbs.
+  void moddown(const LimbSet& x, int level, const LimbSet& out) {
+    const int nc = x.ncomp, B = x.nbatch;
+    LimbSet xp = limbs(x, level + 1, K);
     ntt(xp, true);
     Poly ext = alloc(nc, level + 1, B);
     LimbSet le = lsq(ext, 0, nc, level);
@@ -719,15 +776,15 @@ struct Context {
       for (int k = 0; k < K; ++k) P = hm_mulmod(P, mods[L + k] % mods[j], mods[j]);
       pinv.push_back(hm_invmod(P, mods[j]));
     }
-    LimbSet xq = ls(x, c0, nc, iota(0, level + 1), iota(0, level + 1));
-    ew(EW_SUBSCALE, out, xq, le, &pinv);
+    ew(EW_SUBSCALE, out, limbs(x, 0, level + 1), le, &pinv);
   }
   // full key switch of c (Q, level) -> (k0, k1) written to out comps 0/1 (Q, level)
   void keyswitch(const LimbSet& c, int level, int B, const Poly& key, const Poly& out) {
     Poly D = decompose(c, level, B);
     Poly u = alloc(2, level + 1 + K, B);
-    mac(u, D, key, level, false);
-    moddown(u, 0, 2, level, level, lsq(out, 0, 2, level));
+    const int beta = (level + 1 + K - 1) / K;
+    mac_groups(lsqp(u, 0, 2, level, level), 0, lsqp(D, 0, beta, level, level), 0, c, 0, {key.ptr()}, beta);
+    moddown(lsqp(u, 0, 2, level, level), level, lsq(out, 0, 2, level));
   }
   std::vector<u64> p_mod_q(int level) const {
     std::vector<u64> v;
@@ -841,85 +898,154 @@ struct Context {
     out.scale = a.scale;
   }
 
-  // BSGS linear transform (lintrans MultiplyByDiagMatrixBSGS restated; oracle_lt_bsgs)
-  Ciphertext eval_lt(const LinTrans& T, const Ciphertext& ct) {
+  // device plan of a BSGS transform: register slot of each baby, giant order,
+  // and the diagonal plane of every (giant, slot) term
+  void build_plan(LinTrans& T) {
+    T.slots.clear();
+    T.gorder.clear();
+    bool b0 = false, g0 = false;
+    for (int b : T.babies) (b == 0 ? b0 = true : (T.slots.push_back(b), false));
+    if (b0) T.slots.push_back(0);
+    for (int j : T.giants) (j == 0 ? g0 = true : (T.gorder.push_back(j), false));
+    if (g0) T.gorder.push_back(0);
+    if ((int)T.slots.size() > LT_MAXSLOT)
+      throw std::runtime_error("linear transform with more than 64 baby steps");
+    std::map<int, int> slot_of;
+    for (size_t s = 0; s < T.slots.size(); ++s) slot_of[T.slots[s]] = (int)s;
+    const int ng = (int)T.gorder.size();
+    const int nplan = (ng + LT_MAXG - 1) / LT_MAXG;
+    std::vector<LtPlan> plans(nplan);
+    memset(plans.data(), 0, plans.size() * sizeof(LtPlan));
+    for (int gi = 0; gi < ng; ++gi) {
+      LtPlan& P = plans[gi / LT_MAXG];
+      const int j = T.gorder[gi], gg = gi % LT_MAXG;
+      for (int b : T.index.at(j)) {
+        const int sl = slot_of.at(b);
+        P.mask[gg] |= 1ull << sl;
+        P.pt[gg][sl] = T.diags.at((j + b) & (N / 2 - 1)).poly.ptr();
+      }
+    }
+    if (T.d_plan && T.n_plan != nplan) {
+      HIPCHK(hipFree(T.d_plan));
+      T.d_plan = nullptr;
+    }
+    if (!T.d_plan) HIPCHK(hipMalloc(&T.d_plan, nplan * sizeof(LtPlan)));
+    HIPCHK(hipMemcpy(T.d_plan, plans.data(), nplan * sizeof(LtPlan), hipMemcpyHostToDevice));
+    T.n_plan = nplan;
+    T.plan_dirty = false;
+  }
+
+  // BSGS linear transform (lintrans MultiplyByDiagMatrixBSGS restated; oracle_lt_bsgs).
+  // Every phase runs as one grouped launch over all babies / all giants:
+  //   1. one hoisted decomposition of ct1;
+  //   2. all baby key switches (one MAC, decomposition shared) and their
+  //      automorphisms with the + P*ct0 term (one launch);
+  //   3. all giant inner products sum_s pt * rot_s (lt_bsgs: each baby read once);
+  //   4. all giant key switches: ModDown of c1, decomposition, MAC with each
+  //      giant's key (+ c0 folded in), then the automorphism-accumulate;
+  //   5. ModDown of the accumulator.
+  Ciphertext eval_lt(LinTrans& T, const Ciphertext& ct) {
     const int level = std::min(ct.level, T.level);
     const int B = ct.poly.B, nqp = level + 1 + K;
+    const int beta = (level + 1 + K - 1) / K;
+    if (T.giants.empty()) throw std::runtime_error("linear transform without diagonals");
+    if (T.plan_dirty) build_plan(T);
     const std::vector<u64> pq = p_mod_q(level);
-    Poly D = decompose(lsq(ct.poly, 1, 1, level), level, B);
-    std::map<int, Poly> rot;  // baby -> [2][QP][B]
-    for (int b : T.babies) {
-      Poly r = alloc(2, nqp, B);
-      if (b == 0) {
-        ew1(EW_SCALE, lsq(r, 0, 2, level), lsq(ct.poly, 0, 2, level), &pq);
-        std::vector<u64> zero(K, 0);
-        LimbSet rp = lsp(r, 0, 2, level);
-        ew1(EW_SCALE, rp, rp, &zero);  // P part = 0 (c * P mod p)
-        rot[b] = r;
-        continue;
+    const int nb = (int)T.slots.size();
+    const int nzb = nb - (T.slots.back() == 0 ? 1 : 0);
+
+    // 1. hoisted decomposition of ct1 (only needed when some baby rotates)
+    Poly D = nzb > 0 ? decompose(lsq(ct.poly, 1, 1, level), level, B) : alloc(1, 1, 1);
+    LimbSet dl = lsqp(D, 0, 1, level, level);
+    if (nzb == 0) dl.p = nullptr;
+    LimbSet ctl = lsq(ct.poly, 0, 2, level);
+
+    // 2-3. baby rotations + giant inner products (lt_bsgs): Tt comps [0, ng) =
+    // c0 of giant slot gi, [ng, 2ng) = its c1
+    const int ng = (int)T.gorder.size();
+    const bool has_g0 = T.gorder.back() == 0;
+    const int nzg = ng - (has_g0 ? 1 : 0);
+    Poly Tt = alloc(2 * ng, nqp, B);
+    {
+      const Poly& pt0 = T.diags.begin()->second.poly;
+      LimbSet ptl = lsqp(pt0, 0, 1, level, T.level, 1);
+      for (int s0 = 0; s0 < nb; s0 += LT_MAXB) {
+        LtBabies Bb;
+        memset(&Bb, 0, sizeof(Bb));
+        Bb.nb = std::min(LT_MAXB, nb - s0);
+        Bb.s0 = s0;
+        Bb.beta = beta;
+        Bb.K = K;
+        Bb.level = level;
+        Bb.nmod_key = L + K;
+        for (int j = 0; j <= level; ++j) Bb.pq[j] = pq[j], Bb.pqs[j] = hm_shoup(pq[j], mods[j]);
+        int nrot = 0;
+        for (int s = 0; s < Bb.nb; ++s) {
+          const int b = T.slots[s0 + s];
+          if (b == 0) continue;
+          const u64 g = galois_element(b);
+          Bb.key[s] = galois_key(g).ptr();
+          Bb.idx[s] = aut_index(g);
+          ++nrot;
+        }
+        for (int p = 0; p < T.n_plan; ++p) {
+          const int gcount = std::min(LT_MAXG, ng - p * LT_MAXG);
+          LimbSet t0 = lsqp(Tt, p * LT_MAXG, 1, level, level), t1 = lsqp(Tt, ng + p * LT_MAXG, 1, level, level);
+          const double rows = (double)nqp * B;
+          Scope sc(this, P_LTMAC, 8.0 * N * rows * (nrot * beta + 2.0 + 2.0 * gcount * (s0 ? 2 : 1)));
+          if (orion_launch_lt_bsgs(t0, t1, dl, ctl, Bb, T.d_plan + p, 0, gcount, s0 > 0, ptl, d_tb, N, stream))
+            throw std::runtime_error("lt_bsgs launch failed");
+        }
       }
-      const u64 g = galois_element(b);
-      const Poly& key = galois_key(g);
-      Poly u = alloc(2, nqp, B);
-      mac(u, D, key, level, false);
-      ew(EW_ADDSCALE, lsq(u, 0, 1, level), lsq(ct.poly, 0, 1, level), lsq(ct.poly, 0, 1, level), &pq);
-      automorph(lsqp(r, 0, 2, level, level), lsqp(u, 0, 2, level, level), g, false);
-      rot[b] = r;
     }
+
+    // 4. giant key switches and the automorphism-accumulation (lt_giant)
     Poly acc = alloc(2, nqp, B);
-    bool acc_init = false;
-    Poly t = alloc(2, nqp, B);
-    Poly c = alloc(2, nqp, B);
-    Poly t1q = alloc(1, level + 1, B);
-    for (int j : T.giants) {
-      const std::vector<int>& bl = T.index.at(j);
-      {
-        // fused sum over this giant step's babies: t = sum_i pt[j+i] * rot_i
-        std::vector<const u64*> rp, pp;
-        const Plaintext* pt0 = nullptr;
-        for (int b : bl) {
-          const int d = (j + b) & (N / 2 - 1);
-          const Plaintext& pt = T.diags.at(d);
-          pt0 = &pt;
-          rp.push_back(rot.at(b).ptr());
-          pp.push_back(pt.poly.ptr());
+    LimbSet la = lsqp(acc, 0, 2, level, level);
+    LimbSet z = lsqp(Tt, ng - 1, 2, level, level);  // the zero giant: (c0, c1) at comps ng-1, 2ng-1
+    z.comp_stride = (long long)ng * Tt.comp_stride();
+    if (nzg > 0) {
+      Poly T1q = alloc(nzg, level + 1, B);
+      moddown(lsqp(Tt, ng, nzg, level, level), level, lsq(T1q, 0, nzg, level));
+      Poly Dg = decompose(lsq(T1q, 0, nzg, level), level, B);
+      for (int g0 = 0; g0 < nzg; g0 += ORION_MAXGROUP) {
+        LtGiants G;
+        memset(&G, 0, sizeof(G));
+        G.ng = std::min(ORION_MAXGROUP, nzg - g0);
+        G.beta = beta;
+        G.K = K;
+        G.level = level;
+        G.nmod_key = L + K;
+        G.has_zero = (has_g0 && g0 == 0) ? 1 : 0;
+        G.d_gstride = (long long)beta * Dg.comp_stride();
+        G.own_gstride = T1q.comp_stride();
+        G.t0_gstride = Tt.comp_stride();
+        for (int k = 0; k < G.ng; ++k) {
+          const u64 g = galois_element(T.gorder[g0 + k]);
+          G.key[k] = galois_key(g).ptr();
+          G.idx[k] = aut_index(g);
         }
-        LimbSet lt = lsqp(t, 0, 2, level, level);
-        LimbSet lp = lsqp(pt0->poly, 0, 1, level, T.level, 1);
-        for (size_t c0 = 0; c0 < rp.size(); c0 += ORION_MAXBABY) {
-          const int m = (int)std::min<size_t>(ORION_MAXBABY, rp.size() - c0);
-          Scope sc(this, P_LTMAC, 8.0 * N * lt.nlimb * (2.0 * B * (m + 1) + m));
-          if (c0 == 0) {
-            orion_launch_lt_mac(lt, rp.data(), pp.data(), m, lp, d_tb, N, stream);
-          } else {  // > ORION_MAXBABY babies: accumulate chunk results
-            Poly t2 = alloc(2, nqp, B);
-            LimbSet l2 = lsqp(t2, 0, 2, level, level);
-            orion_launch_lt_mac(l2, rp.data() + c0, pp.data() + c0, m, lp, d_tb, N, stream);
-            ew(EW_ADD, lt, lt, l2);
-          }
+        LimbSet dg = lsqp(Dg, g0 * beta, 1, level, level);
+        LimbSet own = lsq(T1q, g0, 1, level);
+        LimbSet t0 = lsqp(Tt, g0, 1, level, level);
+        LimbSet a = la;
+        Poly part;
+        if (g0 > 0) {  // > 64 giants: accumulate partial sums
+          part = alloc(2, nqp, B);
+          a = lsqp(part, 0, 2, level, level);
         }
+        const double rows = (double)nqp * B;
+        Scope sc(this, P_MAC, 8.0 * N * rows * (G.ng * (beta + 1.0) + 2.0 + 2.0 * G.has_zero));
+        if (orion_launch_lt_giant(a, dg, own, t0, z, G, d_tb, N, stream))
+          throw std::runtime_error("lt_giant launch failed");
+        if (g0 > 0) ew(EW_ADD, la, la, a);
       }
-      LimbSet la = lsqp(acc, 0, 2, level, level);
-      if (j != 0) {
-        const u64 g = galois_element(j);
-        const Poly& key = galois_key(g);
-        moddown(t, 1, 1, level, level, lsq(t1q, 0, 1, level));
-        Poly Dj = decompose(lsq(t1q, 0, 1, level), level, B);
-        mac(c, Dj, key, level, false);
-        LimbSet c0 = lsqp(c, 0, 1, level, level);
-        ew(EW_ADD, c0, c0, lsqp(t, 0, 1, level, level));
-        automorph(la, lsqp(c, 0, 2, level, level), g, acc_init);
-      } else {
-        if (acc_init)
-          ew(EW_ADD, la, la, lsqp(t, 0, 2, level, level));
-        else
-          copy(la, lsqp(t, 0, 2, level, level));
-      }
-      acc_init = true;
+    } else {
+      copy(la, z);
     }
+    // 5.
     Ciphertext out = new_ct(level, B, ct.scale * (long double)mods[T.level]);
-    if (!acc_init) throw std::runtime_error("linear transform without diagonals");
-    moddown(acc, 0, 2, level, level, lsq(out.poly, 0, 2, level));
+    moddown(la, level, lsq(out.poly, 0, 2, level));
     return out;
   }
 
@@ -1811,11 +1937,13 @@ void LoadPlaintextDiagonal(char* data, unsigned long len, int tid, unsigned long
   memcpy(host.data(), data, len);
   c.upload(p.poly, host);
   T.diags[(int)diagIdx & (c.N / 2 - 1)] = p;
+  T.plan_dirty = true;
   API_END_VOID
 }
 void RemovePlaintextDiagonals(int tid) {
   API_BEGIN
   ctx().lts.get(tid).diags.clear();
+  ctx().lts.get(tid).plan_dirty = true;
   API_END_VOID
 }
 void RemoveRotationKeys(void) {

@@ -26,6 +26,7 @@ struct ModConst {
   u64 bar_mu;   // floor(2^(2k) / q), k = bitlen(q)   (Barrett)
   int bar_k;    // bitlen(q)
   int f64;      // 1: NTT in float64 arithmetic (q < 2^ORION_F64_BITS)
+  u64 bar_mu2;  // floor(2^(2k+2) / q)                    (Barrett for x < 4 q^2)
   u64 ninv, ninv_s;  // N^-1 and its Shoup companion
   double qd, qinv_d, ninv_d;  // float64 path: q, 1/q, centered N^-1
 };
@@ -138,3 +139,79 @@ struct BasisExtTable {
   u64 S_t[ORION_MAXLIMB];
   u64 vS_t[ORION_MAXLIMB][ORION_MAXSRC + 1];  // (t - v*S mod t) mod t, v = 0..ns (Lattigo vtimesqmodp)
 };
+
+// ---------------------------------------------------------------------------
+// grouped launches (one launch for many independent key switches / rotations)
+// ---------------------------------------------------------------------------
+#define ORION_MAXGROUP 64
+struct MacGroups {  // ks_mac_kernel: group g uses key[g]
+  const u64* key[ORION_MAXGROUP];
+  long long out_gstride, d_gstride, add_gstride, own_gstride;
+  const u64* add0;  // optional comp-0 addend, layout of out comp 0 (stride add_gstride per group)
+  int K;            // digit width (own limbs of digit i: l / K == i)
+};
+
+// BSGS linear transform plan (device-resident, one per LinTrans): giants in
+// evaluation order, baby slots in the order of LinTrans::babies
+#define LT_MAXB 16   // baby rotations held in registers by one lt_bsgs launch
+#define LT_MAXG 64   // giants per plan
+#define LT_MAXSLOT 64
+struct LtPlan {
+  unsigned long long mask[LT_MAXG];      // bit s: giant g uses baby slot s
+  const u64* pt[LT_MAXG][LT_MAXSLOT];    // diagonal (QP plaintext) of (giant, slot), or null
+};
+struct LtBabies {  // the baby steps of register slots [s0, s0 + nb) of one lt_bsgs launch
+  const u64* key[LT_MAXB];  // Galois key of the slot (null: the zero baby)
+  const u32* idx[LT_MAXB];  // its NTT-domain automorphism index
+  int nb, s0, beta, K, level, nmod_key;
+  u64 pq[ORION_MAXLIMB], pqs[ORION_MAXLIMB];  // P mod q_l and Shoup companion (0 on the P limbs)
+};
+struct LtGiants {  // the nonzero giant steps of one lt_giant launch
+  const u64* key[ORION_MAXGROUP];
+  const u32* idx[ORION_MAXGROUP];
+  int ng, beta, K, level, nmod_key, has_zero;
+  long long d_gstride, own_gstride, t0_gstride;
+};
+
+// ---------------------------------------------------------------------------
+// split multiply-accumulate: up to 4 products x*y of operands < 2^61 summed in
+// three 64-bit partial sums, 4 v_mad_u64_u32 + 3 adds per product:
+//   lo (+ carries c) = sum x0*y0,  mid = sum x0*y1 + x1*y0,  hi = sum x1*y1
+// (x1, y1 < 2^29: mid < 8 * 2^61 = 2^64).  mac_reduce folds the parts into a
+// 128-bit value < 4 q^2 and Barrett-reduces it to [0, q).
+// ---------------------------------------------------------------------------
+struct MacAcc {
+  u64 lo, mid, hi;
+  u32 c;
+};
+__device__ __forceinline__ void mac_zero(MacAcc& a) {
+  a.lo = a.mid = a.hi = 0;
+  a.c = 0;
+}
+__device__ __forceinline__ void mac_add(MacAcc& a, u64 x, u64 y) {
+  const u32 x0 = (u32)x, x1 = (u32)(x >> 32), y0 = (u32)y, y1 = (u32)(y >> 32);
+  const u64 p = (u64)x0 * y0;
+  a.lo += p;
+  a.c += (a.lo < p);
+  a.mid += (u64)x0 * y1;
+  a.mid += (u64)x1 * y0;
+  a.hi += (u64)x1 * y1;
+}
+// Barrett reduction of hi:lo = x < 4 q^2 (bitlen(q) = k <= 61) with
+// mu2 = floor(2^(2k+2)/q): t1 = x >> (k-1) < 2^(k+3), q_est = (t1*mu2) >> (k+3)
+// is low by at most 2, so two conditional subtractions finish it.
+__device__ __forceinline__ u64 barrett_4q2(u64 hi, u64 lo, const ModConst& m) {
+  const int k = m.bar_k;
+  const u64 t1 = (lo >> (k - 1)) | (hi << (65 - k));
+  const u64 ph = mulhi64(t1, m.bar_mu2), pl = t1 * m.bar_mu2;
+  const u64 t2 = (k < 61 ? pl >> (k + 3) : 0) | (ph << (61 - k));
+  u64 r = lo - t2 * m.q;
+  r = r >= m.q ? r - m.q : r;
+  return r >= m.q ? r - m.q : r;
+}
+__device__ __forceinline__ u64 mac_reduce(const MacAcc& a, const ModConst& m) {
+  const u64 ml = a.mid << 32;
+  const u64 L = a.lo + ml;
+  const u64 H = a.hi + (a.mid >> 32) + a.c + (L < ml);
+  return barrett_4q2(H, L, m);
+}

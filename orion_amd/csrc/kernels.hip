@@ -160,46 +160,56 @@ __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in,
   }
 }
 
-// Gadget-product MAC: out_c[j] = sum_i D_i[j] * key[i][c][mod_j]  (c = 0, 1)
-// D: comps = digits, limbs = QP positions.  key layout [dnum][2][L+K][N].
-__global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, const u64* __restrict__ key,
-                                                     int beta, int nmod_key, const DeviceTables* __restrict__ tb,
-                                                     int N, int accumulate) {
+// Gadget-product MAC over G groups (one evaluation key per group):
+//   out_g,c[j] = add0_g[j]*(c == 0) + sum_i D_g,i[j] * key_g[i][c][mod_j]   (c = 0, 1)
+// D: comps = digits, limbs = QP positions; group g's digits start at
+// D.p + g*d_gstride (d_gstride = 0: one decomposition shared by every group,
+// the hoisted baby steps of a BSGS transform).  If own.p is set, digit i's
+// own Q limbs (l / K == i) are read from `own` (the NTT-domain input of the
+// decomposition, group stride own_gstride) instead of D, so the decomposition
+// never copies them.  out comps 0/1 of group g at out.p + g*out_gstride.
+// key layout [dnum][2][L+K][N].
+__global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, LimbSet own, MacGroups G, int beta,
+                                                     int nmod_key, const DeviceTables* __restrict__ tb, int N) {
   const int row = blockIdx.y;
   const int bi = row % out.nbatch;
-  const int l = row / out.nbatch;
+  const int r = row / out.nbatch;
+  const int l = r % out.nlimb;
+  const int g = r / out.nlimb;
   const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
   if (n >= N) return;
   const int m = out.mod[l];
   const ModConst mc = tb->mc[m];
   const u64 q = mc.q;
+  const u64* key = G.key[g];
+  const u64* dp = D.p + g * G.d_gstride;
+  const int owndigit = (own.p && l < own.nlimb) ? l / G.K : -1;
+  u64* op = out.p + g * G.out_gstride;
   ulonglong2 r0 = make_ulonglong2(0, 0), r1 = make_ulonglong2(0, 0);
-  if (accumulate) {
-    r0 = *(const ulonglong2*)(out.p + row_off(out, 0, l, bi) + n);
-    r1 = *(const ulonglong2*)(out.p + row_off(out, 1, l, bi) + n);
-  }
-  // d, key < q: each product < q^2; sum 4 of them in 128 bits, reduce once
-  Acc128 s0x = {0, 0}, s0y = {0, 0}, s1x = {0, 0}, s1y = {0, 0};
+  if (G.add0) r0 = *(const ulonglong2*)(G.add0 + g * G.add_gstride + row_off(out, 0, l, bi) + n);
+  MacAcc s0x, s0y, s1x, s1y;
+  mac_zero(s0x), mac_zero(s0y), mac_zero(s1x), mac_zero(s1y);
   for (int i = 0; i < beta; ++i) {
-    const ulonglong2 d = *(const ulonglong2*)(D.p + row_off(D, i, l, bi) + n);
+    const ulonglong2 d = i == owndigit ? *(const ulonglong2*)(own.p + g * G.own_gstride + row_off(own, 0, l, bi) + n)
+                                       : *(const ulonglong2*)(dp + row_off(D, i, l, bi) + n);
     const u64* kb = key + ((long long)(i * 2 + 0) * nmod_key + m) * N + n;
     const u64* ka = key + ((long long)(i * 2 + 1) * nmod_key + m) * N + n;
     const ulonglong2 b = *(const ulonglong2*)kb;
     const ulonglong2 a = *(const ulonglong2*)ka;
-    mac128(s0x, d.x, b.x);
-    mac128(s0y, d.y, b.y);
-    mac128(s1x, d.x, a.x);
-    mac128(s1y, d.y, a.y);
+    mac_add(s0x, d.x, b.x);
+    mac_add(s0y, d.y, b.y);
+    mac_add(s1x, d.x, a.x);
+    mac_add(s1y, d.y, a.y);
     if ((i & 3) == 3 || i == beta - 1) {
-      r0.x = add_mod(r0.x, barrett128_4(s0x.hi, s0x.lo, mc), q);
-      r0.y = add_mod(r0.y, barrett128_4(s0y.hi, s0y.lo, mc), q);
-      r1.x = add_mod(r1.x, barrett128_4(s1x.hi, s1x.lo, mc), q);
-      r1.y = add_mod(r1.y, barrett128_4(s1y.hi, s1y.lo, mc), q);
-      s0x = s0y = s1x = s1y = Acc128{0, 0};
+      r0.x = add_mod(r0.x, mac_reduce(s0x, mc), q);
+      r0.y = add_mod(r0.y, mac_reduce(s0y, mc), q);
+      r1.x = add_mod(r1.x, mac_reduce(s1x, mc), q);
+      r1.y = add_mod(r1.y, mac_reduce(s1y, mc), q);
+      mac_zero(s0x), mac_zero(s0y), mac_zero(s1x), mac_zero(s1y);
     }
   }
-  *(ulonglong2*)(out.p + row_off(out, 0, l, bi) + n) = r0;
-  *(ulonglong2*)(out.p + row_off(out, 1, l, bi) + n) = r1;
+  *(ulonglong2*)(op + row_off(out, 0, l, bi) + n) = r0;
+  *(ulonglong2*)(op + row_off(out, 1, l, bi) + n) = r1;
 }
 
 // NTT-domain automorphism: o[j] = a[idx[j]]  (optionally o += a[idx[j]])
@@ -225,45 +235,139 @@ __global__ void __launch_bounds__(256) automorph_kernel(LimbSet o, LimbSet a, co
   *(ulonglong2*)dst = z;
 }
 
-// BSGS giant-step MAC (lintrans MultiplyByDiagMatrixBSGS inner loop, fused):
-//   t[c][l][b] = sum_i pt_i[l] * rot_i[c][l][b]   for c = 0, 1
-// rot_i share t's layout; pt_i is one limb plane per QP position (pt_pos[l]).
-// Grid: x = image (fastest, so the blocks that reuse a pt chunk run together),
-// y = coefficient chunk, z = limb.  Products are summed in 128 bits and
-// reduced once per 4 terms.
-struct LtMacArgs {
-  const u64* rot[ORION_MAXBABY];
-  const u64* pt[ORION_MAXBABY];
-};
-__global__ void __launch_bounds__(256) lt_mac_kernel(LimbSet t, LtMacArgs A, int m, const unsigned char* __restrict__ pt_pos_unused,
-                                                     LimbSet ptl, const DeviceTables* __restrict__ tb, int N) {
-  const int bi = blockIdx.x;
-  const int n = (blockIdx.y * blockDim.x + threadIdx.x) * 2;
-  const int l = blockIdx.z;
-  if (n >= N) return;
-  const ModConst mc = tb->mc[t.mod[l]];
-  const long long ro0 = row_off(t, 0, l, bi) + n, ro1 = row_off(t, 1, l, bi) + n;
-  const long long po = (long long)ptl.pos[l] * ptl.limb_stride + n;
-  Acc128 a0x = {0, 0}, a0y = {0, 0}, a1x = {0, 0}, a1y = {0, 0};
-  u64 r0x = 0, r0y = 0, r1x = 0, r1y = 0;
-  for (int i = 0; i < m; ++i) {
-    const ulonglong2 p = *(const ulonglong2*)(A.pt[i] + po);
-    const ulonglong2 x0 = *(const ulonglong2*)(A.rot[i] + ro0);
-    const ulonglong2 x1 = *(const ulonglong2*)(A.rot[i] + ro1);
-    mac128(a0x, p.x, x0.x);
-    mac128(a0y, p.y, x0.y);
-    mac128(a1x, p.x, x1.x);
-    mac128(a1y, p.y, x1.y);
-    if ((i & 3) == 3 || i == m - 1) {
-      r0x = add_mod(r0x, barrett128_4(a0x.hi, a0x.lo, mc), mc.q);
-      r0y = add_mod(r0y, barrett128_4(a0y.hi, a0y.lo, mc), mc.q);
-      r1x = add_mod(r1x, barrett128_4(a1x.hi, a1x.lo, mc), mc.q);
-      r1y = add_mod(r1y, barrett128_4(a1y.hi, a1y.lo, mc), mc.q);
-      a0x = a0y = a1x = a1y = Acc128{0, 0};
+// One gadget product of a hoisted key switch, read at the automorphism index j:
+//   (sum_i D_i[j] * key[i][0][m][j],  sum_i D_i[j] * key[i][1][m][j])   mod q
+// D_i rows at dp + i*dstride; digit `owndigit` comes from ownp instead.
+__device__ __forceinline__ void gadget_at(const u64* __restrict__ dp, long long dstride, const u64* ownp,
+                                          int owndigit, const u64* __restrict__ key, int beta, int nmod_key, int m,
+                                          int N, int j, const ModConst& mc, u64& r0, u64& r1) {
+  MacAcc a0, a1;
+  mac_zero(a0), mac_zero(a1);
+  r0 = r1 = 0;
+  for (int i = 0; i < beta; ++i) {
+    const u64 d = i == owndigit ? ownp[j] : dp[i * dstride + j];
+    const u64 k0 = key[((long long)(i * 2 + 0) * nmod_key + m) * N + j];
+    const u64 k1 = key[((long long)(i * 2 + 1) * nmod_key + m) * N + j];
+    mac_add(a0, d, k0);
+    mac_add(a1, d, k1);
+    if ((i & 3) == 3 || i == beta - 1) {
+      r0 = add_mod(r0, mac_reduce(a0, mc), mc.q);
+      r1 = add_mod(r1, mac_reduce(a1, mc), mc.q);
+      mac_zero(a0), mac_zero(a1);
     }
   }
-  *(ulonglong2*)(t.p + ro0) = make_ulonglong2(r0x, r0y);
-  *(ulonglong2*)(t.p + ro1) = make_ulonglong2(r1x, r1y);
+}
+
+// Hoisted BSGS linear transform, baby steps and giant inner products fused
+// (lintrans MultiplyByDiagMatrixBSGS):
+//   rot_s  = sigma_s( gadget(D, key_s) + (P * ct0, 0) )   s != 0   (QP, hoisted key switch)
+//   rot_0  = (P * ct0, P * ct1) on Q, 0 on P
+//   t_g[c] = sum_{s in babies(g)} pt_{g,s} * rot_s[c]
+// The NTT-domain automorphism maps every aligned block of 2^k coefficients
+// onto an aligned block, so the gathers of one wave stay inside one 512-B
+// segment of each source row.  Each thread builds all baby rotations of its
+// coefficient in registers and loops over the giants: the rotations never
+// touch HBM, and every diagonal (shared by the batch; the image index is the
+// fastest grid dimension) is read from L2.
+template <int MB>
+__global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb,
+                                                      const LtPlan* __restrict__ P, int g0, int g1, int accumulate,
+                                                      LimbSet ptl, const DeviceTables* __restrict__ tb, int N) {
+  const int bi = blockIdx.x;
+  const int n = blockIdx.y * blockDim.x + threadIdx.x;
+  const int l = blockIdx.z;
+  if (n >= N) return;
+  const int m = t0.mod[l];
+  const ModConst mc = tb->mc[m];
+  const bool isq = l <= Bb.level;
+  const long long ro = row_off(t0, 0, l, bi) + n;
+  const long long po = (long long)ptl.pos[l] * ptl.limb_stride + n;
+  const u64* c0p = ct.p + row_off(ct, 0, isq ? l : 0, bi);
+  const u64* c1p = ct.p + row_off(ct, 1, isq ? l : 0, bi);
+  const u64* dp = D.p + row_off(D, 0, l, bi);
+  const int owndigit = isq ? l / Bb.K : -1;
+  const u64 pq = Bb.pq[l], pqs = Bb.pqs[l];
+  u64 x0[MB], x1[MB];
+#pragma unroll
+  for (int s = 0; s < MB; ++s) {
+    x0[s] = x1[s] = 0;
+    if (s < Bb.nb) {
+      if (Bb.key[s]) {
+        const int j = Bb.idx[s][n];
+        u64 r0, r1;
+        gadget_at(dp, D.comp_stride, c1p, owndigit, Bb.key[s], Bb.beta, Bb.nmod_key, m, N, j, mc, r0, r1);
+        if (isq) r0 = add_mod(r0, shoup_mul(c0p[j], pq, pqs, mc.q), mc.q);
+        x0[s] = r0;
+        x1[s] = r1;
+      } else if (isq) {
+        x0[s] = shoup_mul(c0p[n], pq, pqs, mc.q);
+        x1[s] = shoup_mul(c1p[n], pq, pqs, mc.q);
+      }
+    }
+  }
+  for (int g = g0; g < g1; ++g) {
+    const unsigned long long mask = P->mask[g] >> Bb.s0;
+    u64 r0 = 0, r1 = 0;
+    if (accumulate) {
+      r0 = t0.p[(long long)(g - g0) * t0.comp_stride + ro];
+      r1 = t1.p[(long long)(g - g0) * t1.comp_stride + ro];
+    }
+    // issue every diagonal load of this giant before the first product so
+    // their latencies overlap (the branches are wave-uniform)
+    u64 pv[MB];
+#pragma unroll
+    for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? P->pt[g][Bb.s0 + s][po] : 0;
+    MacAcc a0, a1;
+    mac_zero(a0), mac_zero(a1);
+#pragma unroll
+    for (int s = 0; s < MB; ++s) {
+      if ((mask >> s) & 1ull) {
+        mac_add(a0, pv[s], x0[s]);
+        mac_add(a1, pv[s], x1[s]);
+      }
+      if ((s & 3) == 3) {
+        r0 = add_mod(r0, mac_reduce(a0, mc), mc.q);
+        r1 = add_mod(r1, mac_reduce(a1, mc), mc.q);
+        mac_zero(a0), mac_zero(a1);
+      }
+    }
+    t0.p[(long long)(g - g0) * t0.comp_stride + ro] = r0;
+    t1.p[(long long)(g - g0) * t1.comp_stride + ro] = r1;
+  }
+}
+
+// Giant steps of a hoisted BSGS transform, key switches and accumulation fused:
+//   acc[c] = sum_g sigma_g( gadget(D_g, key_g)[c] + (c == 0) * t0_g ) + z[c]
+// D_g: decomposition of ModDown(t1_g) (digit i of group g at D.p + g*d_gstride
+// + i*D.comp_stride; its own Q limbs read from `own`, the ModDown output);
+// z = the zero giant's (t0, t1), added without automorphism.
+__global__ void __launch_bounds__(256) lt_giant_kernel(LimbSet acc, LimbSet D, LimbSet own, LimbSet t0, LimbSet z,
+                                                       LtGiants G, const DeviceTables* __restrict__ tb, int N) {
+  const int bi = blockIdx.x;
+  const int n = blockIdx.y * blockDim.x + threadIdx.x;
+  const int l = blockIdx.z;
+  if (n >= N) return;
+  const int m = acc.mod[l];
+  const ModConst mc = tb->mc[m];
+  const bool isq = l <= G.level;
+  const int owndigit = isq ? l / G.K : -1;
+  const long long dro = row_off(D, 0, l, bi), oro = row_off(own, 0, isq ? l : 0, bi), tro = row_off(t0, 0, l, bi);
+  u64 r0 = 0, r1 = 0;
+  for (int g = 0; g < G.ng; ++g) {
+    const int j = G.idx[g][n];
+    u64 a0, a1;
+    gadget_at(D.p + g * G.d_gstride + dro, D.comp_stride, own.p + g * G.own_gstride + oro, owndigit, G.key[g],
+              G.beta, G.nmod_key, m, N, j, mc, a0, a1);
+    a0 = add_mod(a0, t0.p[g * G.t0_gstride + tro + j], mc.q);
+    r0 = add_mod(r0, a0, mc.q);
+    r1 = add_mod(r1, a1, mc.q);
+  }
+  if (G.has_zero) {
+    r0 = add_mod(r0, z.p[row_off(z, 0, l, bi) + n], mc.q);
+    r1 = add_mod(r1, z.p[row_off(z, 1, l, bi) + n], mc.q);
+  }
+  acc.p[row_off(acc, 0, l, bi) + n] = r0;
+  acc.p[row_off(acc, 1, l, bi) + n] = r1;
 }
 
 inline dim3 ew_grid(int N, int rows) { return dim3((N / 2 + 255) / 256, rows); }
@@ -317,24 +421,34 @@ int orion_launch_basis_ext(const LimbSet& out, const LimbSet& in, const BasisExt
   return 0;
 }
 
-int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const u64* key, int beta, int nmod_key,
-                        const DeviceTables* tb, int N, int accumulate, hipStream_t st) {
-  const int rows = out.nlimb * out.nbatch;
-  hipLaunchKernelGGL(ks_mac_kernel, ew_grid(N, rows), dim3(256), 0, st, out, D, key, beta, nmod_key, tb, N,
-                     accumulate);
+int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const LimbSet& own, const MacGroups& G, int ngroup,
+                        int beta, int nmod_key, const DeviceTables* tb, int N, hipStream_t st) {
+  const int rows = ngroup * out.nlimb * out.nbatch;
+  if (rows == 0) return 0;
+  if (ngroup > ORION_MAXGROUP) return -1;
+  hipLaunchKernelGGL(ks_mac_kernel, ew_grid(N, rows), dim3(256), 0, st, out, D, own, G, beta, nmod_key, tb, N);
   return 0;
 }
 
-int orion_launch_lt_mac(const LimbSet& t, const u64* const* rot, const u64* const* pt, int m, const LimbSet& ptl,
-                        const DeviceTables* tb, int N, hipStream_t st) {
-  if (m < 1 || m > ORION_MAXBABY) return -1;
-  LtMacArgs A;
-  for (int i = 0; i < m; ++i) {
-    A.rot[i] = rot[i];
-    A.pt[i] = pt[i];
-  }
-  dim3 g(t.nbatch, (N / 2 + 255) / 256, t.nlimb);
-  hipLaunchKernelGGL(lt_mac_kernel, g, dim3(256), 0, st, t, A, m, (const unsigned char*)nullptr, ptl, tb, N);
+int orion_launch_lt_bsgs(const LimbSet& t0, const LimbSet& t1, const LimbSet& D, const LimbSet& ct,
+                         const LtBabies& Bb, const LtPlan* plan, int g0, int g1, int accumulate, const LimbSet& ptl,
+                         const DeviceTables* tb, int N, hipStream_t st) {
+  if (Bb.nb < 1 || Bb.nb > LT_MAXB || g1 <= g0) return -1;
+  dim3 g(t0.nbatch, (N + 255) / 256, t0.nlimb);
+  if (Bb.nb <= 8)
+    hipLaunchKernelGGL(lt_bsgs_kernel<8>, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate, ptl, tb,
+                       N);
+  else
+    hipLaunchKernelGGL(lt_bsgs_kernel<16>, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate, ptl, tb,
+                       N);
+  return 0;
+}
+
+int orion_launch_lt_giant(const LimbSet& acc, const LimbSet& D, const LimbSet& own, const LimbSet& t0,
+                          const LimbSet& z, const LtGiants& G, const DeviceTables* tb, int N, hipStream_t st) {
+  if (G.ng > ORION_MAXGROUP) return -1;
+  dim3 g(acc.nbatch, (N + 255) / 256, acc.nlimb);
+  hipLaunchKernelGGL(lt_giant_kernel, g, dim3(256), 0, st, acc, D, own, t0, z, G, tb, N);
   return 0;
 }
 
