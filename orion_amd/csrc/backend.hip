@@ -23,6 +23,7 @@
 #include "hostmath.h"
 
 int orion_launch_ntt(int logN, const LimbSet& s, const DeviceTables* tb, bool inverse, hipStream_t st);
+int orion_launch_ntt_io(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st);
 int orion_ntt_init();
 int orion_launch_ew(int op, const LimbSet& o, const LimbSet& a, const LimbSet& b, const u64* s, const u64* ss,
                     const DeviceTables* tb, int N, hipStream_t st);
@@ -350,6 +351,19 @@ struct Context {
   }
 
   // -- kernel wrappers ------------------------------------------------------------
+  // NTT / INTT with a fused prologue (load, basis extension, rescale prep) and
+  // epilogue (store, subtract-and-scale); bytes: 16 N per limb-transform
+  static NttIO nio(const LimbSet& dst, const LimbSet& src) {
+    NttIO io;
+    memset(&io, 0, sizeof(io));
+    io.dst = dst;
+    io.src = src;
+    return io;
+  }
+  void ntt_io(const NttIO& io, bool inv) {
+    Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, 16.0 * N * io.dst.ncomp * io.dst.nlimb * io.dst.nbatch);
+    if (orion_launch_ntt_io(logN, io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
+  }
   void ntt(const LimbSet& s, bool inv) {
     Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, 16.0 * N * s.ncomp * s.nlimb * s.nbatch);
     if (orion_launch_ntt(logN, s, d_tb, inv, stream)) throw std::runtime_error("unsupported logN for NTT");
@@ -706,8 +720,7 @@ struct Context {
     const int beta = (level + 1 + K - 1) / K;
     const int nqp = level + 1 + K;
     Poly cinv = alloc(nc, level + 1, B);
-    copy(lsq(cinv, 0, nc, level), c);
-    ntt(lsq(cinv, 0, nc, level), true);
+    ntt_io(nio(lsq(cinv, 0, nc, level), c), true);  // out-of-place INTT
     Poly D = alloc(nc * beta, nqp, B);
     const long long dstride = (long long)beta * D.comp_stride();
     for (int i = 0; i < beta; ++i) {
@@ -719,6 +732,9 @@ struct Context {
       LimbSet in = ls(cinv, 0, nc, iota(lo, hi), iota(lo, hi));
       LimbSet out = ls(D, i, nc, tpos, tmod);
       out.comp_stride = dstride;
+      // ModUp as its own kernel: y_i and the float64 quotient are shared by every
+      // target (fusing it into the NTT prologue recomputes them per target limb,
+      // and the NTT is VALU-bound, so that was measured slower)
       {
         Scope sc(this, P_BEXT, 8.0 * N * B * nc * (in.nlimb + out.nlimb));
         orion_launch_basis_ext(out, in, T, d_tb, N, stream);
@@ -769,14 +785,16 @@ struct Context {
       Scope sc(this, P_BEXT, 8.0 * N * B * nc * (K + level + 1));
       orion_launch_basis_ext(le, xp, moddown_tab(level), d_tb, N, stream);
     }
-    ntt(le, false);
-    std::vector<u64> pinv;
+    NttIO io = nio(out, le);  // NTT of the extension and (x_Q - .) * P^-1, fused
+    io.epi = NTT_EPI_SUBSCALE;
+    io.ex = limbs(x, 0, level + 1);
     for (int j = 0; j <= level; ++j) {
       u64 P = 1;
       for (int k = 0; k < K; ++k) P = hm_mulmod(P, mods[L + k] % mods[j], mods[j]);
-      pinv.push_back(hm_invmod(P, mods[j]));
+      io.s[j] = hm_invmod(P, mods[j]);
+      io.ss[j] = hm_shoup(io.s[j], mods[j]);
     }
-    ew(EW_SUBSCALE, out, limbs(x, 0, level + 1), le, &pinv);
+    ntt_io(io, false);
   }
   // full key switch of c (Q, level) -> (k0, k1) written to out comps 0/1 (Q, level)
   void keyswitch(const LimbSet& c, int level, int B, const Poly& key, const Poly& out) {
@@ -816,19 +834,21 @@ struct Context {
     const int l = ct.level;
     if (l < 1) throw std::runtime_error("cannot rescale a level-0 ciphertext");
     const int B = ct.poly.B;
-    ntt(ls(ct.poly, 0, 2, {l}, {l}), true);
-    Poly T = alloc(2, l, B);
-    LimbSet lt = lsq(T, 0, 2, l - 1);
-    {
-      Scope sc(this, P_RSPREP, 8.0 * N * B * 2 * (1 + l));
-      orion_launch_rescale_prep(lt, ct.poly.ptr() + l * ct.poly.limb_stride(), ct.poly.comp_stride(),
-                                ct.poly.batch_stride(), l, d_tb, N, stream);
-    }
-    ntt(lt, false);
-    std::vector<u64> inv;
-    for (int j = 0; j < l; ++j) inv.push_back(hm_invmod(mods[l] % mods[j], mods[j]));
+    LimbSet last = ls(ct.poly, 0, 2, {l}, {l});
+    ntt(last, true);
+    // (DivRoundByLastModulusNTT) prep of every other limb, NTT and (c - .) * q_l^-1, fused
     LimbSet cq = lsq(ct.poly, 0, 2, l - 1);
-    ew(EW_SUBSCALE, cq, cq, lt, &inv);
+    NttIO io = nio(cq, last);
+    io.pro = NTT_PRO_RESCALE;
+    io.modL = l;
+    io.epi = NTT_EPI_SUBSCALE;
+    io.ex = cq;
+    for (int j = 0; j < l; ++j) {
+      io.s[j] = hm_invmod(mods[l] % mods[j], mods[j]);
+      io.ss[j] = hm_shoup(io.s[j], mods[j]);
+    }
+    (void)B;
+    ntt_io(io, false);
     ct.level = l - 1;
     ct.scale /= (long double)mods[l];
   }

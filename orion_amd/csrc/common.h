@@ -215,3 +215,56 @@ __device__ __forceinline__ u64 mac_reduce(const MacAcc& a, const ModConst& m) {
   const u64 H = a.hi + (a.mid >> 32) + a.c + (L < ml);
   return barrett_4q2(H, L, m);
 }
+
+// ---------------------------------------------------------------------------
+// exact basis extension of one coefficient (Lattigo ModUpExact restated;
+// SURVEY App. A.5): sources x_i (i < ns, coefficient domain) -> target t.
+// The float64 quotient is accumulated in source order with explicit
+// round-to-nearest multiply and add (no FMA contraction) so that it matches
+// the CPU restatement bit for bit.  y[] and v are shared by every target.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ u64 bext_prep(const BasisExtTable* __restrict__ T, const DeviceTables* __restrict__ tb,
+                                         const u64* x, u64* y) {
+  double vf = 0.0;
+  const int ns = T->ns;
+#pragma unroll
+  for (int i = 0; i < ORION_MAXSRC; ++i) {
+    if (i >= ns) break;
+    const u64 si = tb->mc[T->src_mod[i]].q;
+    y[i] = shoup_mul(x[i], T->qhatinv[i], T->qhatinv_s[i], si);
+    vf = __dadd_rn(vf, __dmul_rn((double)y[i], T->qinv_f[i]));
+  }
+  return (u64)vf;
+}
+// out_t = sum_i y_i * (S/s_i mod t) - v*S  (mod t); y_i < s_i may exceed t, the
+// Shoup product accepts any 64-bit multiplicand and returns [0, 2t)
+__device__ __forceinline__ u64 bext_target(const BasisExtTable* __restrict__ T, int t, u64 q, const u64* y, u64 v) {
+  u64 acc = T->vS_t[t][v];
+  const int ns = T->ns;
+#pragma unroll
+  for (int i = 0; i < ORION_MAXSRC; ++i) {
+    if (i >= ns) break;
+    u64 r = shoup_lazy(y[i], T->qhat_t[t][i], T->qhat_ts[t][i], q);
+    r = r >= q ? r - q : r;
+    acc = add_mod(acc, r, q);
+  }
+  return acc;
+}
+
+// ---------------------------------------------------------------------------
+// NTT launch descriptor: transform + fused producer (prologue) / consumer
+// (epilogue).  Job j = (c, l, b) over dst's (ncomp, nlimb, nbatch); the limb's
+// modulus is dst.mod[l].
+//   prologue NTT_PRO_LOAD:    load row (c, l, b) of src (src == dst: in place)
+//            NTT_PRO_RESCALE: ((x + h) mod q_L) mod q_l - (h mod q_l), x = row (c, 0, b) of src
+//   epilogue NTT_EPI_STORE:   store to row (c, l, b) of dst
+//            NTT_EPI_SUBSCALE (forward only): dst = (ex - y) * s_l, ex row (c, l, b)
+// ---------------------------------------------------------------------------
+enum { NTT_PRO_LOAD = 0, NTT_PRO_RESCALE = 2 };
+enum { NTT_EPI_STORE = 0, NTT_EPI_SUBSCALE = 1 };
+struct NttIO {
+  LimbSet dst, src, ex;
+  int modL;
+  int pro, epi;
+  u64 s[ORION_MAXLIMB], ss[ORION_MAXLIMB];
+};

@@ -124,11 +124,9 @@ __global__ void __launch_bounds__(256) rescale_prep_kernel(LimbSet dst, const u6
   *(ulonglong2*)(dst.p + row_off(dst, c, l, bi) + n) = z;
 }
 
-// Exact basis extension (Lattigo ModUpExact restated).
+// Exact basis extension (Lattigo ModUpExact restated; the
+// per-coefficient math is bext_prep / bext_target in common.h).
 // in: ns source limbs (coefficient domain), out: nt target limbs.
-// The float64 quotient is accumulated in source order with explicit
-// round-to-nearest multiply and add (no FMA contraction) so that it matches
-// the CPU restatement bit for bit.
 __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in, const BasisExtTable* __restrict__ T,
                                                         const DeviceTables* __restrict__ tb, int N) {
   const int row = blockIdx.y;  // (comp, image)
@@ -136,27 +134,12 @@ __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in,
   const int c = row / out.nbatch;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
-  const int ns = T->ns, nt = T->nt;
-  u64 y[ORION_MAXSRC];
-  double vf = 0.0;
-  for (int i = 0; i < ns; ++i) {
-    const u64 si = tb->mc[T->src_mod[i]].q;
-    u64 x = in.p[row_off(in, c, i, bi) + n];
-    y[i] = shoup_mul(x, T->qhatinv[i], T->qhatinv_s[i], si);
-    vf = __dadd_rn(vf, __dmul_rn((double)y[i], T->qinv_f[i]));
-  }
-  const u64 v = (u64)vf;
-  // out_t = sum_i y_i * (S/s_i mod t) - v*S  (mod t); y_i < s_i may exceed t, the
-  // Shoup product accepts any 64-bit multiplicand and returns [0, 2t)
-  for (int t = 0; t < nt; ++t) {
+  u64 x[ORION_MAXSRC], y[ORION_MAXSRC];
+  for (int i = 0; i < T->ns; ++i) x[i] = in.p[row_off(in, c, i, bi) + n];
+  const u64 v = bext_prep(T, tb, x, y);
+  for (int t = 0; t < T->nt; ++t) {
     const u64 q = tb->mc[T->dst_mod[t]].q;
-    u64 acc = T->vS_t[t][v];
-    for (int i = 0; i < ns; ++i) {
-      u64 r = shoup_lazy(y[i], T->qhat_t[t][i], T->qhat_ts[t][i], q);
-      r = r >= q ? r - q : r;
-      acc = add_mod(acc, r, q);
-    }
-    out.p[row_off(out, c, t, bi) + n] = acc;
+    out.p[row_off(out, c, t, bi) + n] = bext_target(T, t, q, y, v);
   }
 }
 

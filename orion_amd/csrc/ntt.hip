@@ -27,17 +27,12 @@
 //         multiply piece (tools/ubench/valu_rates.hip), and the float path
 //         needs ~9 of them per butterfly instead of ~30 integer instructions.
 #include "common.h"
+#include <string.h>
 
 // timing-only ablation builds (tools/ntt_ablate.sh); 0 in the product:
 // bit 0 skips the butterfly rounds, bit 1 skips the LDS exchanges
 #ifndef NTT_ABLATE
 #define NTT_ABLATE 0
-#endif
-// forward store strategy: 0 = 16-byte stores straight from window 0 (lane
-// stride 256 B); 1 = one more LDS exchange back to window B0, then fully
-// coalesced 8-byte stores
-#ifndef NTT_FWD_COAL
-#define NTT_FWD_COAL 1
 #endif
 
 namespace {
@@ -321,14 +316,10 @@ __device__ __forceinline__ void reduce_all(typename A::T (&a)[32], const A& ar) 
   for (int k = 0; k < 32; ++k) a[k] = ar.reduce_round(a[k]);
 }
 
-__device__ __forceinline__ u64* job_ptr(const LimbSet& s, int job, int& mod) {
-  const int b = job % s.nbatch;
-  const int r = job / s.nbatch;
-  const int l = r % s.nlimb;
-  const int c = r / s.nlimb;
-  // the limb tables are indexed dynamically; force the results to be
-  // wave-uniform (SGPR) so every element address is SGPR base + lane offset
-  mod = __builtin_amdgcn_readfirstlane(s.mod[l]);
+// wave-uniform pointer to row (c, l, b) of a LimbSet: the limb tables are
+// indexed dynamically, so force the results into SGPRs so that every element
+// address is SGPR base + lane offset
+__device__ __forceinline__ u64* row_ptr(const LimbSet& s, int c, int l, int b) {
   const int pos = __builtin_amdgcn_readfirstlane(s.pos[l]);
   const long long off = c * s.comp_stride + pos * s.limb_stride + b * s.batch_stride;
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(off & 0xffffffffll));
@@ -338,14 +329,27 @@ __device__ __forceinline__ u64* job_ptr(const LimbSet& s, int job, int& mod) {
 
 // Round windows: LOGN=15 -> bits [10,15), [5,10), [0,5); LOGN=14 -> [9,14),[4,9),[0,5)
 // (last round only bits 3..0); LOGN=13 -> [8,13),[3,8),[0,5) (bits 2..0).
-template <class A, int LOGN>
-__device__ __forceinline__ void ntt_fwd_body(u64* p, const A& ar, __amdgpu_buffer_rsrc_t w, u32* lds) {
+// Thread t loads / stores element t + (k << B0) (k < 32): fully coalesced.
+template <class A, int LOGN, int PRO, int EPI>
+__device__ __forceinline__ void ntt_fwd_body(const NttIO& io, int c, int l, int b, const ModConst& mc, const A& ar,
+                                             __amdgpu_buffer_rsrc_t w, u32* lds, const DeviceTables* __restrict__ tb) {
   constexpr int N = 1 << LOGN, B0 = LOGN - 5, B1 = LOGN - 10;
   const int t = threadIdx.x;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p, 0, N * 8, 0x00020000);
   typename A::T a[32];
+  if constexpr (PRO == NTT_PRO_LOAD) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.src, c, l, b), 0, N * 8, 0x00020000);
 #pragma unroll
-  for (int k = 0; k < 32; ++k) a[k] = ar.from_u64(buf_ld(rs, t * 8, (k << B0) * 8));
+    for (int k = 0; k < 32; ++k) a[k] = ar.from_u64(buf_ld(rs, t * 8, (k << B0) * 8));
+  } else {  // NTT_PRO_RESCALE (DivRoundByLastModulusNTT), fused with the NTT of every other limb
+    const u64* sp = row_ptr(io.src, c, 0, b);
+    const u64 qL = tb->mc[io.modL].q, h = qL >> 1;
+    const u64 hm = barrett128(0, h, mc);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const u64 x = sp[t + (k << B0)];
+      a[k] = ar.from_u64(sub_mod(barrett128(0, add_mod(x, h, qL), mc), hm, mc.q));
+    }
+  }
   fwd_round<A, LOGN, B0, LOGN - 1, B0>(a, ar, w, t);
   reduce_all<A>(a, ar);
   exchange<typename A::T, B0, B1>(a, lds, t);
@@ -353,32 +357,35 @@ __device__ __forceinline__ void ntt_fwd_body(u64* p, const A& ar, __amdgpu_buffe
   reduce_all<A>(a, ar);
   exchange<typename A::T, B1, 0>(a, lds, t);
   fwd_round<A, LOGN, 0, B1 - 1, 0>(a, ar, w, t);
-  if constexpr (NTT_FWD_COAL) {
-    u64 r[32];
+  u64 r[32];
 #pragma unroll
-    for (int k = 0; k < 32; ++k) r[k] = ar.final_fwd(a[k]);
-    exchange<u64, 0, B0>(r, lds, t);
+  for (int k = 0; k < 32; ++k) r[k] = ar.final_fwd(a[k]);
+  exchange<u64, 0, B0>(r, lds, t);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.dst, c, l, b), 0, N * 8, 0x00020000);
+  if constexpr (EPI == NTT_EPI_STORE) {
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
-      buf_st(rs, r[k], t * 8, (k << B0) * 8);
+      buf_st(rd, r[k], t * 8, (k << B0) * 8);
       if ((k & 3) == 3) NTT_FENCE();
     }
-  } else {
-    // window 0: thread t holds elements 32t .. 32t+31 -> 16-byte stores
+  } else {  // NTT_EPI_SUBSCALE: dst = (ex - y) * s_l  (ModDown / rescale tail)
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.ex, c, l, b), 0, N * 8, 0x00020000);
+    const u64 s = io.s[l], ss = io.ss[l];
 #pragma unroll
-    for (int k = 0; k < 32; k += 2) {
-      const u64 x = ar.final_fwd(a[k]), y = ar.final_fwd(a[k + 1]);
-      buf_st2(rs, x, y, t * 256, k * 8);
-      if ((k & 7) == 6) NTT_FENCE();
+    for (int k = 0; k < 32; ++k) {
+      const u64 x = buf_ld(rx, t * 8, (k << B0) * 8);
+      buf_st(rd, shoup_mul(sub_mod(x, r[k], mc.q), s, ss, mc.q), t * 8, (k << B0) * 8);
+      if ((k & 7) == 7) NTT_FENCE();
     }
   }
 }
 
 template <class A, int LOGN>
-__device__ __forceinline__ void ntt_inv_body(u64* p, const A& ar, __amdgpu_buffer_rsrc_t w, u32* lds) {
+__device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int b, const A& ar,
+                                             __amdgpu_buffer_rsrc_t w, u32* lds) {
   constexpr int N = 1 << LOGN, B0 = LOGN - 5, B1 = LOGN - 10;
   const int t = threadIdx.x;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p, 0, N * 8, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.src, c, l, b), 0, N * 8, 0x00020000);
   typename A::T a[32];
 #pragma unroll
   for (int k = 0; k < 32; k += 2) {
@@ -394,78 +401,118 @@ __device__ __forceinline__ void ntt_inv_body(u64* p, const A& ar, __amdgpu_buffe
   reduce_all<A>(a, ar);
   exchange<typename A::T, B1, B0>(a, lds, t);
   inv_round<A, LOGN, B0, B0, LOGN - 1>(a, ar, w, t);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.dst, c, l, b), 0, N * 8, 0x00020000);
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
-    buf_st(rs, ar.final_inv(a[k]), t * 8, (k << B0) * 8);
+    buf_st(rd, ar.final_inv(a[k]), t * 8, (k << B0) * 8);
     if ((k & 3) == 3) NTT_FENCE();
   }
 }
 
-template <int LOGN>
-__global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_fwd_kernel(LimbSet s, const DeviceTables* __restrict__ tb) {
+__device__ __forceinline__ void job_of(const LimbSet& d, int job, int& c, int& l, int& b) {
+  b = job % d.nbatch;
+  const int r = job / d.nbatch;
+  l = r % d.nlimb;
+  c = r / d.nlimb;
+}
+
+template <int LOGN, int PRO, int EPI>
+__global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_fwd_kernel(NttIO io, const DeviceTables* __restrict__ tb) {
   constexpr int N = 1 << LOGN;
   extern __shared__ u32 lds[];
-  int mod;
-  u64* p = job_ptr(s, blockIdx.x, mod);
+  int c, l, b;
+  job_of(io.dst, blockIdx.x, c, l, b);
+  const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
   const ModConst mc = tb->mc[mod];
   if (mc.f64) {
     const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd_d[mod], 0, N * 8, 0x00020000);
-    ntt_fwd_body<F64Arith, LOGN>(p, F64Arith(mc), w, lds);
+    ntt_fwd_body<F64Arith, LOGN, PRO, EPI>(io, c, l, b, mc, F64Arith(mc), w, lds, tb);
   } else {
     const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd[mod], 0, N * 16, 0x00020000);
-    ntt_fwd_body<IntArith, LOGN>(p, IntArith(mc), w, lds);
+    ntt_fwd_body<IntArith, LOGN, PRO, EPI>(io, c, l, b, mc, IntArith(mc), w, lds, tb);
   }
 }
 
 template <int LOGN>
-__global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_inv_kernel(LimbSet s, const DeviceTables* __restrict__ tb) {
+__global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_inv_kernel(NttIO io, const DeviceTables* __restrict__ tb) {
   constexpr int N = 1 << LOGN;
   extern __shared__ u32 lds[];
-  int mod;
-  u64* p = job_ptr(s, blockIdx.x, mod);
+  int c, l, b;
+  job_of(io.dst, blockIdx.x, c, l, b);
+  const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
   const ModConst mc = tb->mc[mod];
   if (mc.f64) {
     const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->inv_d[mod], 0, N * 8, 0x00020000);
-    ntt_inv_body<F64Arith, LOGN>(p, F64Arith(mc), w, lds);
+    ntt_inv_body<F64Arith, LOGN>(io, c, l, b, F64Arith(mc), w, lds);
   } else {
     const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->inv[mod], 0, N * 16, 0x00020000);
-    ntt_inv_body<IntArith, LOGN>(p, IntArith(mc), w, lds);
+    ntt_inv_body<IntArith, LOGN>(io, c, l, b, IntArith(mc), w, lds);
   }
 }
 
+template <int LOGN, int PRO, int EPI>
+void set_lds_attr() {
+  hipFuncSetAttribute((const void*)ntt_fwd_kernel<LOGN, PRO, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      ((1 << LOGN) + (1 << LOGN) / 32) * 4);
+}
+
 template <int LOGN>
-void launch_ntt(const LimbSet& s, const DeviceTables* tb, bool inverse, hipStream_t st) {
+int launch_ntt(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
   constexpr int N = 1 << LOGN;
-  const int jobs = s.ncomp * s.nlimb * s.nbatch;
-  if (jobs == 0) return;
+  const int jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
+  if (jobs == 0) return 0;
   const size_t lds = (size_t)(N + N / 32) * sizeof(u32);
-  if (inverse)
-    hipLaunchKernelGGL(ntt_inv_kernel<LOGN>, dim3(jobs), dim3(NttGeom<LOGN>::T), lds, st, s, tb);
-  else
-    hipLaunchKernelGGL(ntt_fwd_kernel<LOGN>, dim3(jobs), dim3(NttGeom<LOGN>::T), lds, st, s, tb);
+  const dim3 g(jobs), blk(NttGeom<LOGN>::T);
+  if (inverse) {
+    if (io.pro != NTT_PRO_LOAD || io.epi != NTT_EPI_STORE) return -1;
+    hipLaunchKernelGGL(ntt_inv_kernel<LOGN>, g, blk, lds, st, io, tb);
+    return 0;
+  }
+#define FWD(P, E)                                                                        \
+  if (io.pro == P && io.epi == E) {                                                      \
+    hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, P, E>), g, blk, lds, st, io, tb);           \
+    return 0;                                                                            \
+  }
+  FWD(NTT_PRO_LOAD, NTT_EPI_STORE)
+  FWD(NTT_PRO_LOAD, NTT_EPI_SUBSCALE)
+  FWD(NTT_PRO_RESCALE, NTT_EPI_SUBSCALE)
+#undef FWD
+  return -1;
+}
+
+template <int LOGN>
+void init_lds() {
+  set_lds_attr<LOGN, NTT_PRO_LOAD, NTT_EPI_STORE>();
+  set_lds_attr<LOGN, NTT_PRO_LOAD, NTT_EPI_SUBSCALE>();
+  set_lds_attr<LOGN, NTT_PRO_RESCALE, NTT_EPI_SUBSCALE>();
+  hipFuncSetAttribute((const void*)ntt_inv_kernel<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      ((1 << LOGN) + (1 << LOGN) / 32) * 4);
 }
 
 }  // namespace
 
-// host entry: in-place NTT (inverse=false) or INTT of every limb in s
-int orion_launch_ntt(int logN, const LimbSet& s, const DeviceTables* tb, bool inverse, hipStream_t st) {
+// host entry: NTT (inverse=false) or INTT with the fused prologue / epilogue of io
+int orion_launch_ntt_io(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
   switch (logN) {
-    case 13: launch_ntt<13>(s, tb, inverse, st); return 0;
-    case 14: launch_ntt<14>(s, tb, inverse, st); return 0;
-    case 15: launch_ntt<15>(s, tb, inverse, st); return 0;
+    case 13: return launch_ntt<13>(io, tb, inverse, st);
+    case 14: return launch_ntt<14>(io, tb, inverse, st);
+    case 15: return launch_ntt<15>(io, tb, inverse, st);
     default: return -1;
   }
 }
 
-// allow >64 KiB dynamic LDS for the N = 2^15 kernels
+// in-place NTT / INTT of every limb in s
+int orion_launch_ntt(int logN, const LimbSet& s, const DeviceTables* tb, bool inverse, hipStream_t st) {
+  NttIO io;
+  memset(&io, 0, sizeof(io));
+  io.dst = io.src = s;
+  return orion_launch_ntt_io(logN, io, tb, inverse, st);
+}
+
+// allow >64 KiB dynamic LDS for the N = 2^14, 2^15 kernels
 int orion_ntt_init() {
-  hipError_t e1 = hipFuncSetAttribute((const void*)ntt_fwd_kernel<15>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (32768 + 1024) * 4);
-  hipError_t e2 = hipFuncSetAttribute((const void*)ntt_inv_kernel<15>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (32768 + 1024) * 4);
-  hipError_t e3 = hipFuncSetAttribute((const void*)ntt_fwd_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (16384 + 512) * 4);
-  hipError_t e4 = hipFuncSetAttribute((const void*)ntt_inv_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (16384 + 512) * 4);
-  return (e1 == hipSuccess && e2 == hipSuccess && e3 == hipSuccess && e4 == hipSuccess) ? 0 : -1;
+  init_lds<13>();
+  init_lds<14>();
+  init_lds<15>();
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
