@@ -360,14 +360,17 @@ struct Context {
     io.src = src;
     return io;
   }
-  void ntt_io(const NttIO& io, bool inv) {
-    Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, 16.0 * N * io.dst.ncomp * io.dst.nlimb * io.dst.nbatch);
+  int ntt_order = getenv("ORION_NTT_ORDER") ? atoi(getenv("ORION_NTT_ORDER")) : 0;
+  void ntt_io(NttIO io, bool inv) {
+    io.order = ntt_order;
+    io.jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
+    // algorithmic bytes per limb-transform: read + write the limb (16 N), + 8 N
+    // for the epilogue's second operand
+    const double per = 16.0 * N + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
+    Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, per * io.dst.ncomp * io.dst.nlimb * io.dst.nbatch);
     if (orion_launch_ntt_io(logN, io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
   }
-  void ntt(const LimbSet& s, bool inv) {
-    Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, 16.0 * N * s.ncomp * s.nlimb * s.nbatch);
-    if (orion_launch_ntt(logN, s, d_tb, inv, stream)) throw std::runtime_error("unsupported logN for NTT");
-  }
+  void ntt(const LimbSet& s, bool inv) { ntt_io(nio(s, s), inv); }
   void ew(int op, const LimbSet& o, const LimbSet& a, const LimbSet& b, const std::vector<u64>* sc = nullptr) {
     std::vector<u64> s, ss;
     if (sc) {
@@ -414,6 +417,7 @@ struct Context {
       mc.bar_k = 64 - __builtin_clzll(q);
       mc.bar_mu = (u64)(((u128)1 << (2 * mc.bar_k)) / q);
       mc.bar_mu2 = (u64)(((u128)1 << (2 * mc.bar_k + 2)) / q);
+      mc.bar_mu8 = mc.bar_k <= 52 ? (u64)(((u128)1 << (2 * mc.bar_k + 8)) / q) : 0;
       mc.ninv = hm_invmod((u64)N, q);
       mc.ninv_s = hm_shoup(mc.ninv, q);
       const u64 g = primitive_root(q);

@@ -27,6 +27,7 @@ struct ModConst {
   int bar_k;    // bitlen(q)
   int f64;      // 1: NTT in float64 arithmetic (q < 2^ORION_F64_BITS)
   u64 bar_mu2;  // floor(2^(2k+2) / q)                    (Barrett for x < 4 q^2)
+  u64 bar_mu8;  // floor(2^(2k+8) / q), k <= 52           (Barrett for x < 256 q^2)
   u64 ninv, ninv_s;  // N^-1 and its Shoup companion
   double qd, qinv_d, ninv_d;  // float64 path: q, 1/q, centered N^-1
 };
@@ -209,6 +210,25 @@ __device__ __forceinline__ u64 barrett_4q2(u64 hi, u64 lo, const ModConst& m) {
   r = r >= m.q ? r - m.q : r;
   return r >= m.q ? r - m.q : r;
 }
+// Barrett reduction of hi:lo = x < 256 q^2 for moduli of k <= 52 bits
+// (t1 = x >> (k-1) < 2^(k+9) fits 64 bits; q_est low by at most 2)
+__device__ __forceinline__ u64 barrett_256q2(u64 hi, u64 lo, const ModConst& m) {
+  const int k = m.bar_k;
+  const u64 t1 = (lo >> (k - 1)) | (hi << (65 - k));
+  const u64 ph = mulhi64(t1, m.bar_mu8), pl = t1 * m.bar_mu8;
+  const u64 t2 = (pl >> (k + 9)) | (ph << (55 - k));
+  u64 r = lo - t2 * m.q;
+  r = r >= m.q ? r - m.q : r;
+  return r >= m.q ? r - m.q : r;
+}
+// a MacAcc of up to 128 products of operands < 2^52, reduced once (x < 128 q^2;
+// x1, y1 < 2^20 keep mid and hi far below 2^64)
+__device__ __forceinline__ u64 mac_reduce_small(const MacAcc& a, const ModConst& m) {
+  const u64 ml = a.mid << 32;
+  const u64 L = a.lo + ml;
+  const u64 H = a.hi + (a.mid >> 32) + a.c + (L < ml);
+  return barrett_256q2(H, L, m);
+}
 __device__ __forceinline__ u64 mac_reduce(const MacAcc& a, const ModConst& m) {
   const u64 ml = a.mid << 32;
   const u64 L = a.lo + ml;
@@ -265,6 +285,8 @@ enum { NTT_EPI_STORE = 0, NTT_EPI_SUBSCALE = 1 };
 struct NttIO {
   LimbSet dst, src, ex;
   int modL;
+  int order;    // job decode: 0 = image fastest, 1 = limb fastest (mixes moduli inside a dispatch wave)
+  int jobs;     // ncomp * nlimb * nbatch of dst
   int pro, epi;
   u64 s[ORION_MAXLIMB], ss[ORION_MAXLIMB];
 };

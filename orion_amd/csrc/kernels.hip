@@ -302,16 +302,28 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
     for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? P->pt[g][Bb.s0 + s][po] : 0;
     MacAcc a0, a1;
     mac_zero(a0), mac_zero(a1);
+    if (mc.bar_k <= 52) {  // small moduli: one reduction per giant (block-uniform branch)
 #pragma unroll
-    for (int s = 0; s < MB; ++s) {
-      if ((mask >> s) & 1ull) {
-        mac_add(a0, pv[s], x0[s]);
-        mac_add(a1, pv[s], x1[s]);
+      for (int s = 0; s < MB; ++s) {
+        if ((mask >> s) & 1ull) {
+          mac_add(a0, pv[s], x0[s]);
+          mac_add(a1, pv[s], x1[s]);
+        }
       }
-      if ((s & 3) == 3) {
-        r0 = add_mod(r0, mac_reduce(a0, mc), mc.q);
-        r1 = add_mod(r1, mac_reduce(a1, mc), mc.q);
-        mac_zero(a0), mac_zero(a1);
+      r0 = add_mod(r0, mac_reduce_small(a0, mc), mc.q);
+      r1 = add_mod(r1, mac_reduce_small(a1, mc), mc.q);
+    } else {
+#pragma unroll
+      for (int s = 0; s < MB; ++s) {
+        if ((mask >> s) & 1ull) {
+          mac_add(a0, pv[s], x0[s]);
+          mac_add(a1, pv[s], x1[s]);
+        }
+        if ((s & 3) == 3) {
+          r0 = add_mod(r0, mac_reduce(a0, mc), mc.q);
+          r1 = add_mod(r1, mac_reduce(a1, mc), mc.q);
+          mac_zero(a0), mac_zero(a1);
+        }
       }
     }
     t0.p[(long long)(g - g0) * t0.comp_stride + ro] = r0;

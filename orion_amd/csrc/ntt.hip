@@ -34,6 +34,11 @@
 #ifndef NTT_ABLATE
 #define NTT_ABLATE 0
 #endif
+// timing switch (tools/ntt_exp.sh): NTT_LAZY skips the forward round
+// reductions for small float64 moduli
+#ifndef NTT_LAZY
+#define NTT_LAZY 1
+#endif
 
 namespace {
 
@@ -209,6 +214,11 @@ __device__ __forceinline__ void exchange(T (&a)[32], u32* lds, int t) {
   for (int k = 0; k < 32; ++k) a[k] = from_bits<T>(((u64)hi[k] << 32) | lo[k]);
 }
 
+template <class T, int LOGN, int BOLD, int BNEW>
+__device__ __forceinline__ void xchg(T (&a)[32], u32* lds, int t) {
+  exchange<T, BOLD, BNEW>(a, lds, t);
+}
+
 // Twiddle schedule of one round: its stages in execution order, each with
 // 2^(4-dk) distinct twiddles (dk = stage bit - window base B).  Twiddles are
 // software-prefetched TW_PF groups ahead through a compile-time ring, so the
@@ -350,17 +360,21 @@ __device__ __forceinline__ void ntt_fwd_body(const NttIO& io, int c, int l, int 
       a[k] = ar.from_u64(sub_mod(barrett128(0, add_mod(x, h, qL), mc), hm, mc.q));
     }
   }
+  // CT growth is additive (|t| < 2q per stage): from [0, q) the values stay
+  // below 31 q over all 15 stages, exact in float64 for q < 2^41, so the
+  // round-boundary reductions are only needed for larger float64 moduli
+  const bool lazy = NTT_LAZY && mc.bar_k <= 41;
   fwd_round<A, LOGN, B0, LOGN - 1, B0>(a, ar, w, t);
-  reduce_all<A>(a, ar);
-  exchange<typename A::T, B0, B1>(a, lds, t);
+  if (!lazy) reduce_all<A>(a, ar);
+  xchg<typename A::T, LOGN, B0, B1>(a, lds, t);
   fwd_round<A, LOGN, B1, B0 - 1, B1>(a, ar, w, t);
-  reduce_all<A>(a, ar);
-  exchange<typename A::T, B1, 0>(a, lds, t);
+  if (!lazy) reduce_all<A>(a, ar);
+  xchg<typename A::T, LOGN, B1, 0>(a, lds, t);
   fwd_round<A, LOGN, 0, B1 - 1, 0>(a, ar, w, t);
   u64 r[32];
 #pragma unroll
   for (int k = 0; k < 32; ++k) r[k] = ar.final_fwd(a[k]);
-  exchange<u64, 0, B0>(r, lds, t);
+  xchg<u64, LOGN, 0, B0>(r, lds, t);
   const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.dst, c, l, b), 0, N * 8, 0x00020000);
   if constexpr (EPI == NTT_EPI_STORE) {
 #pragma unroll
@@ -396,10 +410,10 @@ __device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int 
   }
   inv_round<A, LOGN, 0, 0, B1 - 1>(a, ar, w, t);
   reduce_all<A>(a, ar);
-  exchange<typename A::T, 0, B1>(a, lds, t);
+  xchg<typename A::T, LOGN, 0, B1>(a, lds, t);
   inv_round<A, LOGN, B1, B1, B0 - 1>(a, ar, w, t);
   reduce_all<A>(a, ar);
-  exchange<typename A::T, B1, B0>(a, lds, t);
+  xchg<typename A::T, LOGN, B1, B0>(a, lds, t);
   inv_round<A, LOGN, B0, B0, LOGN - 1>(a, ar, w, t);
   const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.dst, c, l, b), 0, N * 8, 0x00020000);
 #pragma unroll
@@ -409,27 +423,37 @@ __device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int 
   }
 }
 
-__device__ __forceinline__ void job_of(const LimbSet& d, int job, int& c, int& l, int& b) {
-  b = job % d.nbatch;
-  const int r = job / d.nbatch;
-  l = r % d.nlimb;
-  c = r / d.nlimb;
+__device__ __forceinline__ void job_of(const NttIO& io, int job, int& c, int& l, int& b) {
+  const LimbSet& d = io.dst;
+  if (io.order == 1) {
+    l = job % d.nlimb;
+    const int r = job / d.nlimb;
+    b = r % d.nbatch;
+    c = r / d.nbatch;
+  } else {
+    b = job % d.nbatch;
+    const int r = job / d.nbatch;
+    l = r % d.nlimb;
+    c = r / d.nlimb;
+  }
 }
 
 template <int LOGN, int PRO, int EPI>
 __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_fwd_kernel(NttIO io, const DeviceTables* __restrict__ tb) {
   constexpr int N = 1 << LOGN;
   extern __shared__ u32 lds[];
-  int c, l, b;
-  job_of(io.dst, blockIdx.x, c, l, b);
-  const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
-  const ModConst mc = tb->mc[mod];
-  if (mc.f64) {
-    const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd_d[mod], 0, N * 8, 0x00020000);
-    ntt_fwd_body<F64Arith, LOGN, PRO, EPI>(io, c, l, b, mc, F64Arith(mc), w, lds, tb);
-  } else {
-    const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd[mod], 0, N * 16, 0x00020000);
-    ntt_fwd_body<IntArith, LOGN, PRO, EPI>(io, c, l, b, mc, IntArith(mc), w, lds, tb);
+  {
+    int c, l, b;
+    job_of(io, blockIdx.x, c, l, b);
+    const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
+    const ModConst mc = tb->mc[mod];
+    if (mc.f64) {
+      const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd_d[mod], 0, N * 8, 0x00020000);
+      ntt_fwd_body<F64Arith, LOGN, PRO, EPI>(io, c, l, b, mc, F64Arith(mc), w, lds, tb);
+    } else {
+      const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd[mod], 0, N * 16, 0x00020000);
+      ntt_fwd_body<IntArith, LOGN, PRO, EPI>(io, c, l, b, mc, IntArith(mc), w, lds, tb);
+    }
   }
 }
 
@@ -437,16 +461,18 @@ template <int LOGN>
 __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_inv_kernel(NttIO io, const DeviceTables* __restrict__ tb) {
   constexpr int N = 1 << LOGN;
   extern __shared__ u32 lds[];
-  int c, l, b;
-  job_of(io.dst, blockIdx.x, c, l, b);
-  const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
-  const ModConst mc = tb->mc[mod];
-  if (mc.f64) {
-    const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->inv_d[mod], 0, N * 8, 0x00020000);
-    ntt_inv_body<F64Arith, LOGN>(io, c, l, b, F64Arith(mc), w, lds);
-  } else {
-    const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->inv[mod], 0, N * 16, 0x00020000);
-    ntt_inv_body<IntArith, LOGN>(io, c, l, b, IntArith(mc), w, lds);
+  {
+    int c, l, b;
+    job_of(io, blockIdx.x, c, l, b);
+    const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
+    const ModConst mc = tb->mc[mod];
+    if (mc.f64) {
+      const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->inv_d[mod], 0, N * 8, 0x00020000);
+      ntt_inv_body<F64Arith, LOGN>(io, c, l, b, F64Arith(mc), w, lds);
+    } else {
+      const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->inv[mod], 0, N * 16, 0x00020000);
+      ntt_inv_body<IntArith, LOGN>(io, c, l, b, IntArith(mc), w, lds);
+    }
   }
 }
 
@@ -461,6 +487,7 @@ int launch_ntt(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_
   constexpr int N = 1 << LOGN;
   const int jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
   if (jobs == 0) return 0;
+  if (io.jobs != jobs) return -1;
   const size_t lds = (size_t)(N + N / 32) * sizeof(u32);
   const dim3 g(jobs), blk(NttGeom<LOGN>::T);
   if (inverse) {
@@ -506,6 +533,7 @@ int orion_launch_ntt(int logN, const LimbSet& s, const DeviceTables* tb, bool in
   NttIO io;
   memset(&io, 0, sizeof(io));
   io.dst = io.src = s;
+  io.jobs = s.ncomp * s.nlimb * s.nbatch;
   return orion_launch_ntt_io(logN, io, tb, inverse, st);
 }
 

@@ -1,6 +1,8 @@
-"""NTT kernel microbenchmark (GPU): per-launch time and algorithmic GB/s for
-the float64 path (40-bit moduli) and the integer path (60-bit moduli) at
-several job counts.  Usage: python tools/ntt_bench.py"""
+"""NTT kernel microbenchmark (GPU): per-launch time and algorithmic GB/s
+(16 N bytes per limb-transform) for the float64 path (40-bit moduli), the
+integer path (60-bit moduli) and a LoLA-like mix, at several job counts.
+Usage: python tools/ntt_bench.py   (env: LOGN, JOBS, ORION_LIB, TAG;
+ORION_NTT_ORDER selects the job order of the library under test)"""
 import ctypes
 import os
 import sys
@@ -19,8 +21,10 @@ def main():
     lib = (HipLibrary(path) if path else HipLibrary()).new_scheme(logn, [40] * 8 + [60] * 8, [60], 40)
     mods = lib.moduli()
     res = []
-    for kind, mset in [("f64(40-bit)", list(range(0, 8))), ("int(60-bit)", list(range(8, 16)))]:
-        for jobs in [int(j) for j in os.environ.get("JOBS", "256,512,1024,2048").split(",")]:
+    kinds = [("f64(40-bit)", list(range(0, 8))), ("int(60-bit)", list(range(8, 16))),
+             ("mix(5:3)", [8, 0, 1, 2, 3, 4, 9, 10])]
+    for kind, mset in kinds:
+        for jobs in [int(j) for j in os.environ.get("JOBS", "256,1024,4096").split(",")]:
             nl = len(mset)
             B = jobs // nl
             rng = np.random.default_rng(0)
@@ -45,11 +49,13 @@ def main():
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / reps
                 gbs = 16 * N * jobs / (ms * 1e-3) / 1e9
-                line = f"{kind:12s} {'inv' if inv else 'fwd'} jobs={jobs:5d}  {ms*1e3:8.1f} us/launch  {gbs:7.1f} GB/s  {ms*1e3/ (jobs/256):6.1f} us per 256 limbs"
+                line = (f"{kind:12s} {'inv' if inv else 'fwd'} jobs={jobs:5d}  {ms*1e3:8.1f} us/launch  "
+                        f"{gbs:7.1f} GB/s  {ms*1e3/(jobs/256):6.1f} us per 256 limbs")
                 print(line, flush=True)
                 res.append(line)
             del dev
     tag = os.environ.get("TAG", "")
+    os.makedirs("gpurun_out", exist_ok=True)
     with open(os.path.join("gpurun_out", f"ntt_bench_{logn}{tag}.txt"), "w") as f:
         f.write("\n".join(res) + "\n")
 
