@@ -290,3 +290,28 @@ struct NttIO {
   int pro, epi;
   u64 s[ORION_MAXLIMB], ss[ORION_MAXLIMB];
 };
+
+// ---------------------------------------------------------------------------
+// multiply-accumulate for moduli below 2^48: operands split at bit 24 and kept
+// as (lo 24 bits | hi part << 32), so one product is 4 v_mad_u64_u32 with no
+// carry handling (every partial sum stays below 2^63 for up to 2^14 terms).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ u64 split24(u64 x) { return (x & 0xffffffull) | ((x >> 24) << 32); }
+struct MacS {
+  u64 lo, mid, hi;
+};
+__device__ __forceinline__ void macs_zero(MacS& a) { a.lo = a.mid = a.hi = 0; }
+__device__ __forceinline__ void macs_add(MacS& a, u64 xs, u64 ys) {
+  const u32 xb = (u32)xs, xa = (u32)(xs >> 32), yb = (u32)ys, ya = (u32)(ys >> 32);
+  a.lo += (u64)xb * yb;
+  a.mid += (u64)xa * yb;
+  a.mid += (u64)xb * ya;
+  a.hi += (u64)xa * ya;
+}
+// x = hi 2^48 + mid 2^24 + lo  (< 128 q^2)  ->  x mod q
+__device__ __forceinline__ u64 macs_reduce(const MacS& a, const ModConst& m) {
+  const u64 L1 = a.lo + (a.mid << 24);
+  const u64 L2 = L1 + (a.hi << 48);
+  const u64 H = (a.mid >> 40) + (a.hi >> 16) + (L1 < a.lo) + (L2 < L1);
+  return barrett_256q2(H, L2, m);
+}

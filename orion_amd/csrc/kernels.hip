@@ -126,20 +126,50 @@ __global__ void __launch_bounds__(256) rescale_prep_kernel(LimbSet dst, const u6
 
 // Exact basis extension (Lattigo ModUpExact restated; the
 // per-coefficient math is bext_prep / bext_target in common.h).
-// in: ns source limbs (coefficient domain), out: nt target limbs.
+// in: ns source limbs (coefficient domain), out: nt target limbs.  Two
+// coefficients per thread (16-B accesses); the per-target constants are
+// wave-uniform (SGPR) and v*S mod t is selected from the ns+1 precomputed
+// values with v_cndmask instead of a per-lane table lookup.
+__device__ __forceinline__ u64 bext_target_sel(const BasisExtTable* __restrict__ T, int t, int ns, u64 q,
+                                               const u64* y, u64 v) {
+  u64 acc = T->vS_t[t][0];
+#pragma unroll
+  for (int j = 1; j <= ORION_MAXSRC; ++j) {
+    if (j > ns) break;
+    acc = v == (u64)j ? T->vS_t[t][j] : acc;
+  }
+#pragma unroll
+  for (int i = 0; i < ORION_MAXSRC; ++i) {
+    if (i >= ns) break;
+    u64 r = shoup_lazy(y[i], T->qhat_t[t][i], T->qhat_ts[t][i], q);
+    r = r >= q ? r - q : r;
+    acc = add_mod(acc, r, q);
+  }
+  return acc;
+}
 __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in, const BasisExtTable* __restrict__ T,
                                                         const DeviceTables* __restrict__ tb, int N) {
   const int row = blockIdx.y;  // (comp, image)
   const int bi = row % out.nbatch;
   const int c = row / out.nbatch;
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
   if (n >= N) return;
-  u64 x[ORION_MAXSRC], y[ORION_MAXSRC];
-  for (int i = 0; i < T->ns; ++i) x[i] = in.p[row_off(in, c, i, bi) + n];
-  const u64 v = bext_prep(T, tb, x, y);
-  for (int t = 0; t < T->nt; ++t) {
+  const int ns = T->ns, nt = T->nt;
+  u64 x0[ORION_MAXSRC], x1[ORION_MAXSRC], y0[ORION_MAXSRC], y1[ORION_MAXSRC];
+#pragma unroll
+  for (int i = 0; i < ORION_MAXSRC; ++i) {
+    if (i >= ns) break;
+    const ulonglong2 v = *(const ulonglong2*)(in.p + row_off(in, c, i, bi) + n);
+    x0[i] = v.x;
+    x1[i] = v.y;
+  }
+  const u64 v0 = bext_prep(T, tb, x0, y0), v1 = bext_prep(T, tb, x1, y1);
+  for (int t = 0; t < nt; ++t) {
     const u64 q = tb->mc[T->dst_mod[t]].q;
-    out.p[row_off(out, c, t, bi) + n] = bext_target(T, t, q, y, v);
+    ulonglong2 o;
+    o.x = bext_target_sel(T, t, ns, q, y0, v0);
+    o.y = bext_target_sel(T, t, ns, q, y1, v1);
+    *(ulonglong2*)(out.p + row_off(out, c, t, bi) + n) = o;
   }
 }
 
@@ -170,26 +200,35 @@ __global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, Lim
   u64* op = out.p + g * G.out_gstride;
   ulonglong2 r0 = make_ulonglong2(0, 0), r1 = make_ulonglong2(0, 0);
   if (G.add0) r0 = *(const ulonglong2*)(G.add0 + g * G.add_gstride + row_off(out, 0, l, bi) + n);
-  MacAcc s0x, s0y, s1x, s1y;
-  mac_zero(s0x), mac_zero(s0y), mac_zero(s1x), mac_zero(s1y);
-  for (int i = 0; i < beta; ++i) {
-    const ulonglong2 d = i == owndigit ? *(const ulonglong2*)(own.p + g * G.own_gstride + row_off(own, 0, l, bi) + n)
-                                       : *(const ulonglong2*)(dp + row_off(D, i, l, bi) + n);
-    const u64* kb = key + ((long long)(i * 2 + 0) * nmod_key + m) * N + n;
-    const u64* ka = key + ((long long)(i * 2 + 1) * nmod_key + m) * N + n;
-    const ulonglong2 b = *(const ulonglong2*)kb;
-    const ulonglong2 a = *(const ulonglong2*)ka;
-    mac_add(s0x, d.x, b.x);
-    mac_add(s0y, d.y, b.y);
-    mac_add(s1x, d.x, a.x);
-    mac_add(s1y, d.y, a.y);
-    if ((i & 3) == 3 || i == beta - 1) {
-      r0.x = add_mod(r0.x, mac_reduce(s0x, mc), q);
-      r0.y = add_mod(r0.y, mac_reduce(s0y, mc), q);
-      r1.x = add_mod(r1.x, mac_reduce(s1x, mc), q);
-      r1.y = add_mod(r1.y, mac_reduce(s1y, mc), q);
-      mac_zero(s0x), mac_zero(s0y), mac_zero(s1x), mac_zero(s1y);
+  const long long kstride = (long long)nmod_key * N;
+  const u64* kp = key + (long long)m * N + n;
+  for (int i0 = 0; i0 < beta; i0 += 4) {  // chunks of 4 digits: 12 loads in flight
+    ulonglong2 d[4], kb[4], ka[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u;
+      if (i < beta) {
+        d[u] = i == owndigit ? *(const ulonglong2*)(own.p + g * G.own_gstride + row_off(own, 0, l, bi) + n)
+                             : *(const ulonglong2*)(dp + row_off(D, i, l, bi) + n);
+        kb[u] = *(const ulonglong2*)(kp + (2 * i + 0) * kstride);
+        ka[u] = *(const ulonglong2*)(kp + (2 * i + 1) * kstride);
+      }
     }
+    MacAcc s0x, s0y, s1x, s1y;
+    mac_zero(s0x), mac_zero(s0y), mac_zero(s1x), mac_zero(s1y);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i0 + u < beta) {
+        mac_add(s0x, d[u].x, kb[u].x);
+        mac_add(s0y, d[u].y, kb[u].y);
+        mac_add(s1x, d[u].x, ka[u].x);
+        mac_add(s1y, d[u].y, ka[u].y);
+      }
+    }
+    r0.x = add_mod(r0.x, mac_reduce(s0x, mc), q);
+    r0.y = add_mod(r0.y, mac_reduce(s0y, mc), q);
+    r1.x = add_mod(r1.x, mac_reduce(s1x, mc), q);
+    r1.y = add_mod(r1.y, mac_reduce(s1y, mc), q);
   }
   *(ulonglong2*)(op + row_off(out, 0, l, bi) + n) = r0;
   *(ulonglong2*)(op + row_off(out, 1, l, bi) + n) = r1;
@@ -221,23 +260,36 @@ __global__ void __launch_bounds__(256) automorph_kernel(LimbSet o, LimbSet a, co
 // One gadget product of a hoisted key switch, read at the automorphism index j:
 //   (sum_i D_i[j] * key[i][0][m][j],  sum_i D_i[j] * key[i][1][m][j])   mod q
 // D_i rows at dp + i*dstride; digit `owndigit` comes from ownp instead.
+// Digits go in chunks of 4: all 12 loads of a chunk are issued before the
+// first product, so their latencies overlap.
 __device__ __forceinline__ void gadget_at(const u64* __restrict__ dp, long long dstride, const u64* ownp,
                                           int owndigit, const u64* __restrict__ key, int beta, int nmod_key, int m,
                                           int N, int j, const ModConst& mc, u64& r0, u64& r1) {
-  MacAcc a0, a1;
-  mac_zero(a0), mac_zero(a1);
   r0 = r1 = 0;
-  for (int i = 0; i < beta; ++i) {
-    const u64 d = i == owndigit ? ownp[j] : dp[i * dstride + j];
-    const u64 k0 = key[((long long)(i * 2 + 0) * nmod_key + m) * N + j];
-    const u64 k1 = key[((long long)(i * 2 + 1) * nmod_key + m) * N + j];
-    mac_add(a0, d, k0);
-    mac_add(a1, d, k1);
-    if ((i & 3) == 3 || i == beta - 1) {
-      r0 = add_mod(r0, mac_reduce(a0, mc), mc.q);
-      r1 = add_mod(r1, mac_reduce(a1, mc), mc.q);
-      mac_zero(a0), mac_zero(a1);
+  const long long kstride = (long long)nmod_key * N;
+  const u64* kp = key + (long long)m * N + j;
+  for (int i0 = 0; i0 < beta; i0 += 4) {
+    u64 d[4], k0[4], k1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u;
+      if (i < beta) {
+        d[u] = i == owndigit ? ownp[j] : dp[i * dstride + j];
+        k0[u] = kp[(2 * i + 0) * kstride];
+        k1[u] = kp[(2 * i + 1) * kstride];
+      }
     }
+    MacAcc a0, a1;
+    mac_zero(a0), mac_zero(a1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i0 + u < beta) {
+        mac_add(a0, d[u], k0[u]);
+        mac_add(a1, d[u], k1[u]);
+      }
+    }
+    r0 = add_mod(r0, mac_reduce(a0, mc), mc.q);
+    r1 = add_mod(r1, mac_reduce(a1, mc), mc.q);
   }
 }
 
@@ -271,12 +323,15 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
   const int owndigit = isq ? l / Bb.K : -1;
   const u64 pq = Bb.pq[l], pqs = Bb.pqs[l];
   u64 x0[MB], x1[MB];
+  int jx[MB];
+#pragma unroll
+  for (int s = 0; s < MB; ++s) jx[s] = (s < Bb.nb && Bb.key[s]) ? (int)Bb.idx[s][n] : n;
 #pragma unroll
   for (int s = 0; s < MB; ++s) {
     x0[s] = x1[s] = 0;
     if (s < Bb.nb) {
       if (Bb.key[s]) {
-        const int j = Bb.idx[s][n];
+        const int j = jx[s];
         u64 r0, r1;
         gadget_at(dp, D.comp_stride, c1p, owndigit, Bb.key[s], Bb.beta, Bb.nmod_key, m, N, j, mc, r0, r1);
         if (isq) r0 = add_mod(r0, shoup_mul(c0p[j], pq, pqs, mc.q), mc.q);
@@ -287,6 +342,11 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
         x1[s] = shoup_mul(c1p[n], pq, pqs, mc.q);
       }
     }
+  }
+  const bool small = mc.bar_k <= 48;  // block-uniform
+  if (small) {
+#pragma unroll
+    for (int s = 0; s < MB; ++s) x0[s] = split24(x0[s]), x1[s] = split24(x1[s]);
   }
   for (int g = g0; g < g1; ++g) {
     const unsigned long long mask = P->mask[g] >> Bb.s0;
@@ -300,19 +360,22 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
     u64 pv[MB];
 #pragma unroll
     for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? P->pt[g][Bb.s0 + s][po] : 0;
-    MacAcc a0, a1;
-    mac_zero(a0), mac_zero(a1);
-    if (mc.bar_k <= 52) {  // small moduli: one reduction per giant (block-uniform branch)
+    if (small) {  // < 2^48 moduli: carry-free split products, one reduction per giant
+      MacS a0, a1;
+      macs_zero(a0), macs_zero(a1);
 #pragma unroll
       for (int s = 0; s < MB; ++s) {
         if ((mask >> s) & 1ull) {
-          mac_add(a0, pv[s], x0[s]);
-          mac_add(a1, pv[s], x1[s]);
+          const u64 ps = split24(pv[s]);
+          macs_add(a0, ps, x0[s]);
+          macs_add(a1, ps, x1[s]);
         }
       }
-      r0 = add_mod(r0, mac_reduce_small(a0, mc), mc.q);
-      r1 = add_mod(r1, mac_reduce_small(a1, mc), mc.q);
+      r0 = add_mod(r0, macs_reduce(a0, mc), mc.q);
+      r1 = add_mod(r1, macs_reduce(a1, mc), mc.q);
     } else {
+      MacAcc a0, a1;
+      mac_zero(a0), mac_zero(a1);
 #pragma unroll
       for (int s = 0; s < MB; ++s) {
         if ((mask >> s) & 1ull) {
@@ -348,8 +411,10 @@ __global__ void __launch_bounds__(256) lt_giant_kernel(LimbSet acc, LimbSet D, L
   const int owndigit = isq ? l / G.K : -1;
   const long long dro = row_off(D, 0, l, bi), oro = row_off(own, 0, isq ? l : 0, bi), tro = row_off(t0, 0, l, bi);
   u64 r0 = 0, r1 = 0;
+  int jn = G.ng > 0 ? (int)G.idx[0][n] : 0;
   for (int g = 0; g < G.ng; ++g) {
-    const int j = G.idx[g][n];
+    const int j = jn;
+    if (g + 1 < G.ng) jn = G.idx[g + 1][n];  // prefetch the next giant's index
     u64 a0, a1;
     gadget_at(D.p + g * G.d_gstride + dro, D.comp_stride, own.p + g * G.own_gstride + oro, owndigit, G.key[g],
               G.beta, G.nmod_key, m, N, j, mc, a0, a1);
@@ -412,7 +477,7 @@ int orion_launch_rescale_prep(const LimbSet& dst, const u64* src, long long src_
 int orion_launch_basis_ext(const LimbSet& out, const LimbSet& in, const BasisExtTable* T, const DeviceTables* tb,
                            int N, hipStream_t st) {
   const int rows = out.ncomp * out.nbatch;
-  hipLaunchKernelGGL(basis_ext_kernel, dim3((N + 255) / 256, rows), dim3(256), 0, st, out, in, T, tb, N);
+  hipLaunchKernelGGL(basis_ext_kernel, ew_grid(N, rows), dim3(256), 0, st, out, in, T, tb, N);
   return 0;
 }
 

@@ -1,0 +1,15 @@
+# rocprofv3 passes over the bench (all kernels): kernel trace + SQ counters + HBM bytes
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+TAG=${1:-r01}
+ARGS="--steps 2 --warmup 1 --no-cpu-baseline"
+mkdir -p gpurun_out
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o kt --output-format csv -- python bench.py $ARGS > gpurun_out/prof_${TAG}_kt.log 2>&1 || { echo "kt failed"; tail -20 gpurun_out/prof_${TAG}_kt.log; exit 1; }
+echo "kt ok"
+timeout -k 10 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_SALU -d gpurun_out/prof_$TAG -o pmc_sq --output-format csv -- python bench.py $ARGS > gpurun_out/prof_${TAG}_sq.log 2>&1 || { echo "sq failed"; tail -20 gpurun_out/prof_${TAG}_sq.log; exit 1; }
+echo "sq ok"
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_$TAG -o pmc_fetch --output-format csv -- python bench.py $ARGS > gpurun_out/prof_${TAG}_fetch.log 2>&1 || { echo "fetch failed"; exit 1; }
+echo "fetch ok"
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_$TAG -o pmc_write --output-format csv -- python bench.py $ARGS > gpurun_out/prof_${TAG}_write.log 2>&1 || { echo "write failed"; exit 1; }
+echo "write ok"
