@@ -1,0 +1,240 @@
+"""GPU parity tests of the coefficient-wise evaluator ops and of whole op
+streams at the BASELINE configs.
+
+* ct+ct, ct-ct, -ct, ct+pt, ct-pt, ct*pt, ct+scalar, ct*int, ct*float and
+  CloneCiphertext (/root/reference/orion/backend/lattigo/evaluator.go:48-294,
+  tensors.go / tensors.py:229), checked bit for bit against a numpy
+  restatement of the same modular arithmetic (integers, exact);
+* MLP N=2^14 (BASELINE config C2) and LoLA N=2^15 (C3): the reference
+  frontend's op stream replayed on the GPU and on the CPU oracle with the same
+  keys and input ciphertext, compared bit for bit;
+* size-independent properties at the full C3 size: batch invariance (every
+  image of a batch equals the single-image run) and the key bundle that
+  bench.py broadcasts over RCCL (export -> fresh scheme -> import).
+"""
+import numpy as np
+import pytest
+
+from tests.helpers import SMALL, rand_ct
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def small(torch_cuda, oracle_mod):
+    from orion_amd.backend import HipLibrary
+    lib = HipLibrary().new_scheme(SMALL["logn"], SMALL["logq"], SMALL["logp"], 40, h=192, seed=4321)
+    mods = lib.moduli()
+    orc = oracle_mod.Oracle(SMALL["logn"], mods, len(SMALL["logq"]), len(SMALL["logp"]))
+    return lib, orc
+
+
+def _q(orc, level):
+    return np.array(orc.moduli[:level + 1], dtype=np.uint64)[:, None]
+
+
+def _add(a, b, q):
+    s = a + b
+    return np.where(s >= q, s - q, s)
+
+
+def _sub(a, b, q):
+    return np.where(a >= b, a - b, a + q - b)
+
+
+def _mul_int(a, k, orc, level):
+    """a * k mod q_j per limb (exact, Python ints)."""
+    out = np.empty_like(a)
+    for j in range(level + 1):
+        qj = orc.moduli[j]
+        kj = k % qj
+        out[..., j, :] = np.array([(int(x) * kj) % qj for x in a[..., j, :].reshape(-1)],
+                                  dtype=np.uint64).reshape(a[..., j, :].shape)
+    return out
+
+
+def _round_half_away(x):
+    """round-half-away-from-zero of an exact rational (backend.hip add_scalar / mul_float)."""
+    from fractions import Fraction
+    x = Fraction(x)
+    return -int(-x + Fraction(1, 2)) if x < 0 else int(x + Fraction(1, 2))
+
+
+def test_ct_ct_ops(small):
+    lib, orc = small
+    rng = np.random.default_rng(21)
+    level = 4
+    q = _q(orc, level)
+    a = rand_ct(rng, orc.moduli, level, orc.N, B=2)
+    b = rand_ct(rng, orc.moduli, level, orc.N, B=2)
+    ca, cb = lib.import_ciphertext(a, 2.0 ** 40), lib.import_ciphertext(b, 2.0 ** 40)
+    assert np.array_equal(lib.export_ciphertext(lib.AddCiphertextNew(ca, cb)), _add(a, b, q))
+    assert np.array_equal(lib.export_ciphertext(lib.SubCiphertextNew(ca, cb)), _sub(a, b, q))
+    cl = lib.CloneCiphertext(ca)
+    assert np.array_equal(lib.export_ciphertext(cl), a)
+    neg = lib.Negate(cl)  # a new ciphertext: Evaluator.MulNew(ct, -1.0) (evaluator.go:48-58)
+    assert neg != cl
+    assert np.array_equal(lib.export_ciphertext(neg), _sub(np.zeros_like(a), a, q))
+    # in place, returns its input id (evaluator.go:251-257)
+    assert lib.AddCiphertext(ca, cb) == ca
+    assert np.array_equal(lib.export_ciphertext(ca), _add(a, b, q))
+
+
+def test_ct_pt_ops(small):
+    lib, orc = small
+    rng = np.random.default_rng(22)
+    level = 3
+    q = _q(orc, level)
+    a = rand_ct(rng, orc.moduli, level, orc.N, B=2)
+    p = np.stack([rng.integers(0, orc.moduli[j], orc.N, dtype=np.uint64) for j in range(level + 1)])
+    ca = lib.import_ciphertext(a, 2.0 ** 40)
+    cp = lib.import_plaintext(p, 2.0 ** 40)
+    add = lib.export_ciphertext(lib.AddPlaintextNew(ca, cp))
+    assert np.array_equal(add[:, 0], _add(a[:, 0], p[None], q)) and np.array_equal(add[:, 1], a[:, 1])
+    sub = lib.export_ciphertext(lib.SubPlaintextNew(ca, cp))
+    assert np.array_equal(sub[:, 0], _sub(a[:, 0], p[None], q)) and np.array_equal(sub[:, 1], a[:, 1])
+    mul = lib.MulPlaintextNew(ca, cp)
+    got = lib.export_ciphertext(mul)
+    mods = list(range(level + 1))
+    for bi in range(2):
+        for c in range(2):
+            assert np.array_equal(got[bi, c], orc.mul_coeffs(a[bi, c], p, mods)), (bi, c)
+    assert lib.GetCiphertextScaleF(mul) == 2.0 ** 80
+
+
+def test_scale_matching_add(small):
+    """Lower-scale operand multiplied by the integer scale ratio before the add."""
+    lib, orc = small
+    rng = np.random.default_rng(23)
+    level = 3
+    q = _q(orc, level)
+    a = rand_ct(rng, orc.moduli, level, orc.N, B=1)
+    p = np.stack([rng.integers(0, orc.moduli[j], orc.N, dtype=np.uint64) for j in range(level + 1)])
+    ca = lib.import_ciphertext(a, 2.0 ** 60)
+    cp = lib.import_plaintext(p, 2.0 ** 40)
+    got = lib.export_ciphertext(lib.AddPlaintextNew(ca, cp))
+    pr = _mul_int(p, 1 << 20, orc, level)
+    assert np.array_equal(got[0, 0], _add(a[0, 0], pr, q)) and np.array_equal(got[0, 1], a[0, 1])
+
+
+def test_scalar_ops(small):
+    lib, orc = small
+    rng = np.random.default_rng(24)
+    level = 4
+    q = _q(orc, level)
+    a = rand_ct(rng, orc.moduli, level, orc.N, B=2)
+    scale = 2.0 ** 40
+    ca = lib.import_ciphertext(a, scale)
+    # AddScalar: round(v * scale) added to every NTT slot of c0 (evaluator.go:102-119)
+    v = np.float32(-0.8125)
+    from fractions import Fraction
+    k = _round_half_away(Fraction(float(v)) * Fraction(scale))
+    got = lib.export_ciphertext(lib.AddScalarNew(ca, float(v)))
+    kv = np.array([k % m for m in orc.moduli[:level + 1]], dtype=np.uint64)[:, None]
+    assert np.array_equal(got[:, 0], _add(a[:, 0], kv[None], q)) and np.array_equal(got[:, 1], a[:, 1])
+    # MulScalarInt (evaluator.go:142-159)
+    got = lib.export_ciphertext(lib.MulScalarIntNew(ca, -7))
+    assert np.array_equal(got, _mul_int(a, -7, orc, level))
+    # MulScalarFloat: non-integer constant scaled by q_level, scale grows by q_level
+    fv = np.float32(0.37)
+    ql = orc.moduli[level]
+    kf = _round_half_away(Fraction(float(fv)) * ql)
+    m = lib.MulScalarFloatNew(ca, float(fv))
+    assert np.array_equal(lib.export_ciphertext(m), _mul_int(a, kf, orc, level))
+    assert abs(lib.GetCiphertextScaleF(m) / (scale * ql) - 1) < 1e-12
+
+
+def _replay_gpu_vs_cpu(name, seed):
+    from oracle.replay_cpu import CpuStream
+    from orion_amd.replay import OrionStream
+    st = OrionStream(name, seed=seed)
+    st.keygen()
+    st.compile()
+    lib = st.lib
+    cpu = CpuStream(name)
+    cpu.sk = lib.export_secret_key()
+    cpu.rlk = lib.export_relin_key()
+    gels = set()
+    for h in st.lt_map.values():
+        gels.update(lib.GetLinearTransformRotationKeys(h))
+    for ev in st.trace["events"]:
+        if ev["phase"] == "forward" and ev["op"] in ("RotateNew", "Rotate"):
+            gels.add(int(lib.GaloisElement(ev["args"][1])))
+    cpu.gks = {g: lib.export_galois_key(g) for g in sorted(gels)}
+    cpu.compile()
+    ct = st.encrypt_batch(st.reference_input()[None])
+    x = lib.export_ciphertext(ct)[0]
+    out = st.forward(ct)
+    got = lib.export_ciphertext(out)[0]
+    enc = [e for e in cpu.trace["events"] if e["phase"] == "input" and e["op"] == "Encode"][0]
+    ref = cpu.forward((x, x.shape[1] - 1, float(enc["args"][2])))
+    assert np.array_equal(got, ref[0])
+    res = st.decrypt_output(out)
+    exp = st.arrays["expected_output"].reshape(-1)
+    assert np.abs(res[0] - exp).mean() < 0.005  # tests/models/test_mlp.py:45-48
+    lib.DeleteScheme()
+
+
+def test_mlp_n14_matches_cpu_oracle_replay(torch_cuda):
+    """BASELINE config C2 (MLP, N=2^14, 8 Q + 2 P primes): whole forward pass."""
+    _replay_gpu_vs_cpu("mlp_n14", seed=31)
+
+
+def test_lola_n15_matches_cpu_oracle_replay(torch_cuda):
+    """BASELINE config C3 (LoLA, N=2^15): whole forward pass, bit for bit."""
+    _replay_gpu_vs_cpu("lola_n15", seed=32)
+
+
+def test_lola_n15_batch_invariance(torch_cuda):
+    """Full-size property: a batch of B copies of one ciphertext (every kernel
+    launched at batch B) gives, image by image, exactly the single-image run."""
+    from orion_amd.replay import OrionStream
+    st = OrionStream("lola_n15", seed=33)
+    st.keygen()
+    st.compile()
+    lib = st.lib
+    ct1 = st.encrypt_batch(st.reference_input()[None])
+    x = lib.export_ciphertext(ct1)
+    scale = lib.GetCiphertextScaleF(ct1)
+    ref = lib.export_ciphertext(st.forward(ct1))[0]
+    B = 6
+    ctb = lib.import_ciphertext(np.repeat(x, B, axis=0), scale)
+    got = lib.export_ciphertext(st.forward(ctb))
+    for b in range(B):
+        assert np.array_equal(got[b], ref), b
+    lib.DeleteScheme()
+
+
+def test_key_bundle_roundtrip(torch_cuda):
+    """The device key bundle bench.py broadcasts over RCCL: export on one
+    scheme, import into a fresh scheme with other seeds, keys identical."""
+    torch = torch_cuda
+    from orion_amd.replay import OrionStream
+    st = OrionStream("lola_n13", seed=34)
+    st.keygen()
+    st.compile()
+    lib = st.lib
+    g = int(lib.GaloisElement(1))
+    rlk, gk, sk = lib.export_relin_key(), lib.export_galois_key(g), lib.export_secret_key()
+    n = int(lib.KeyBundleBytes(1))
+    buf = torch.empty(n, dtype=torch.uint8, device="cuda")
+    lib.OrionHipSynchronize()
+    assert lib.lib.ExportKeyBundle(buf.data_ptr(), 1) == 0
+    lib.OrionHipSynchronize()
+    lib.DeleteScheme()
+    st2 = OrionStream("lola_n13", lib=lib, seed=99)
+    st2.compile(gen_keys=False)
+    assert lib.lib.ImportKeyBundle(buf.data_ptr(), n) == 0
+    lib.OrionHipSynchronize()
+    assert np.array_equal(lib.export_relin_key(), rlk)
+    assert np.array_equal(lib.export_galois_key(g), gk)
+    assert np.array_equal(lib.export_secret_key(), sk)
+    lib.DeleteScheme()
