@@ -29,8 +29,6 @@ int orion_launch_ew(int op, const LimbSet& o, const LimbSet& a, const LimbSet& b
                     const DeviceTables* tb, int N, hipStream_t st);
 int orion_launch_tensor(const LimbSet& d, const LimbSet& a, const LimbSet& b, const DeviceTables* tb, int N,
                         hipStream_t st);
-int orion_launch_rescale_prep(const LimbSet& dst, const u64* src, long long src_comp_stride,
-                              long long src_batch_stride, int modL, const DeviceTables* tb, int N, hipStream_t st);
 int orion_launch_basis_ext(const LimbSet& out, const LimbSet& in, const BasisExtTable* T, const DeviceTables* tb,
                            int N, hipStream_t st);
 int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const LimbSet& own, const MacGroups& G, int ngroup,

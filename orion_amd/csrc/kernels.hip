@@ -101,29 +101,6 @@ __global__ void __launch_bounds__(256) tensor_kernel(LimbSet d, LimbSet a, LimbS
   *(ulonglong2*)(d.p + row_off(d, 2, l, bi) + n) = d2;
 }
 
-// rescale step 1 (DivRoundByLastModulusNTT): from the INTT'ed last limb x_L
-// (coefficient domain, rows of src = images), t_i = ((x_L + h) mod q_L) mod q_i - (h mod q_i)
-__global__ void __launch_bounds__(256) rescale_prep_kernel(LimbSet dst, const u64* __restrict__ src,
-                                                           long long src_comp_stride, long long src_batch_stride,
-                                                           int modL, const DeviceTables* __restrict__ tb, int N) {
-  const int row = blockIdx.y;
-  const int bi = row % dst.nbatch;
-  const int r = row / dst.nbatch;
-  const int l = r % dst.nlimb;
-  const int c = r / dst.nlimb;
-  const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
-  if (n >= N) return;
-  const u64 qL = tb->mc[modL].q;
-  const u64 h = qL >> 1;
-  const ModConst mc = tb->mc[dst.mod[l]];
-  const u64 hm = barrett128(0, h, mc);
-  const ulonglong2 x = *(const ulonglong2*)(src + c * src_comp_stride + bi * src_batch_stride + n);
-  ulonglong2 z;
-  z.x = sub_mod(barrett128(0, add_mod(x.x, h, qL), mc), hm, mc.q);
-  z.y = sub_mod(barrett128(0, add_mod(x.y, h, qL), mc), hm, mc.q);
-  *(ulonglong2*)(dst.p + row_off(dst, c, l, bi) + n) = z;
-}
-
 // Exact basis extension (Lattigo ModUpExact restated; the
 // per-coefficient math is bext_prep / bext_target in common.h).
 // in: ns source limbs (coefficient domain), out: nt target limbs.  Two
@@ -465,14 +442,6 @@ int orion_launch_tensor(const LimbSet& d, const LimbSet& a, const LimbSet& b, co
   return 0;
 }
 
-int orion_launch_rescale_prep(const LimbSet& dst, const u64* src, long long src_comp_stride,
-                              long long src_batch_stride, int modL, const DeviceTables* tb, int N, hipStream_t st) {
-  const int rows = dst.ncomp * dst.nlimb * dst.nbatch;
-  if (rows == 0) return 0;
-  hipLaunchKernelGGL(rescale_prep_kernel, ew_grid(N, rows), dim3(256), 0, st, dst, src, src_comp_stride,
-                     src_batch_stride, modL, tb, N);
-  return 0;
-}
 
 int orion_launch_basis_ext(const LimbSet& out, const LimbSet& in, const BasisExtTable* T, const DeviceTables* tb,
                            int N, hipStream_t st) {
