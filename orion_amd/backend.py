@@ -20,7 +20,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liborion_hip.so")
+LIB_PATH = os.environ.get("ORION_LIB") or os.path.join(_HERE, "liborion_hip.so")
 
 c_int, c_float, c_ulong, c_double, c_char_p, c_void_p = (
     ctypes.c_int, ctypes.c_float, ctypes.c_ulong, ctypes.c_double, ctypes.c_char_p, ctypes.c_void_p)

@@ -24,6 +24,7 @@
 
 int orion_launch_ntt(int logN, const LimbSet& s, const DeviceTables* tb, bool inverse, hipStream_t st);
 int orion_launch_ntt_io(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st);
+int orion_launch_ntt2(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st);
 int orion_ntt_init();
 int orion_launch_ew(int op, const LimbSet& o, const LimbSet& a, const LimbSet& b, const u64* s, const u64* ss,
                     const DeviceTables* tb, int N, hipStream_t st);
@@ -359,9 +360,26 @@ struct Context {
     return io;
   }
   int ntt_order = getenv("ORION_NTT_ORDER") ? atoi(getenv("ORION_NTT_ORDER")) : 0;
+#ifndef ORION_NTT_DEFAULT_IMPL
+#define ORION_NTT_DEFAULT_IMPL 1
+#endif
+  // 1: one limb per workgroup (ntt.hip); 2: two-pass N = 2^15 kernels (ntt2.hip)
+  int ntt_impl = getenv("ORION_NTT_IMPL") ? atoi(getenv("ORION_NTT_IMPL")) : ORION_NTT_DEFAULT_IMPL;
   void ntt_io(NttIO io, bool inv) {
     io.order = ntt_order;
     io.jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
+    if (ntt_impl == 2 && logN == 15) {
+      Poly scratch;
+      io.mid = io.dst;
+      if (io.epi == NTT_EPI_SUBSCALE && io.ex.p == io.dst.p) {  // in-place tail: keep ex intact for pass 2
+        scratch = alloc(io.dst.ncomp, io.dst.nlimb, io.dst.nbatch);
+        io.mid = ls(scratch, 0, io.dst.ncomp, iota(0, io.dst.nlimb), std::vector<int>(io.dst.mod, io.dst.mod + io.dst.nlimb));
+      }
+      const double per = 16.0 * N + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
+      Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, per * io.jobs);
+      if (orion_launch_ntt2(io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
+      return;
+    }
     // algorithmic bytes per limb-transform: read + write the limb (16 N), + 8 N
     // for the epilogue's second operand
     const double per = 16.0 * N + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);

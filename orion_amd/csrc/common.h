@@ -284,6 +284,7 @@ enum { NTT_PRO_LOAD = 0, NTT_PRO_RESCALE = 2 };
 enum { NTT_EPI_STORE = 0, NTT_EPI_SUBSCALE = 1 };
 struct NttIO {
   LimbSet dst, src, ex;
+  LimbSet mid;  // two-pass N = 2^15 kernels: intermediate between the passes (dst's geometry)
   int modL;
   int order;    // job decode: 0 = image fastest, 1 = limb fastest (mixes moduli inside a dispatch wave)
   int jobs;     // ncomp * nlimb * nbatch of dst

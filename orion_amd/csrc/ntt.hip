@@ -29,6 +29,8 @@
 #include "common.h"
 #include <string.h>
 
+#include "ntt_arith.h"
+
 // timing-only ablation builds (tools/ntt_ablate.sh); 0 in the product:
 // bit 0 skips the butterfly rounds, bit 1 skips the LDS exchanges
 #ifndef NTT_ABLATE
@@ -59,127 +61,6 @@ __device__ __forceinline__ int lds_base(int t) {
 template <int B>
 __host__ __device__ constexpr int lds_off(int k) {
   return (k << B) + ((k << B) >> 5);
-}
-
-// The limb is addressed through a buffer descriptor built from wave-uniform
-// values: every access is a lane offset plus an immediate/SGPR offset, so no
-// per-element VGPR addresses stay live (hipcc otherwise spills them), and the
-// descriptor's range check confines the kernel to its limb.
-__device__ __forceinline__ void buf_ld2(__amdgpu_buffer_rsrc_t r, u64& x, u64& y, int voff, int soff) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
-  x = ((u64)v[1] << 32) | v[0];
-  y = ((u64)v[3] << 32) | v[2];
-}
-__device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, u64 x, u64 y, int voff, int soff) {
-  __attribute__((ext_vector_type(4))) unsigned v = {(unsigned)x, (unsigned)(x >> 32), (unsigned)y,
-                                                   (unsigned)(y >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
-}
-__device__ __forceinline__ u64 buf_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  return __builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
-}
-__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, u64 v, int voff, int soff) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), r,
-                                        voff, soff, 0);
-}
-
-#define NTT_FENCE() __builtin_amdgcn_sched_barrier(0)
-// An empty volatile asm that "redefines" a butterfly's two inputs: volatile
-// asm statements stay in program order, so no butterfly can be hoisted above
-// its predecessors by IR-level code motion (which sched_barrier cannot stop)
-// -- this is what keeps the kernel at <= 128 VGPRs (1024 threads/CU).
-#define PIN(x, y) asm volatile("" : "+v"(x), "+v"(y))
-
-// ---------------------------------------------------------------------------
-// arithmetic policies
-// ---------------------------------------------------------------------------
-struct IntArith {
-  typedef u64 T;
-  typedef ulonglong2 W;
-  u64 q, q2, ninv, ninv_s;
-  __device__ IntArith(const ModConst& m) : q(m.q), q2(m.q << 1), ninv(m.ninv), ninv_s(m.ninv_s) {}
-  __device__ __forceinline__ W tw(__amdgpu_buffer_rsrc_t r, int vidx, int sidx) const {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, vidx * 16, sidx * 16, 0);
-    return make_ulonglong2(((u64)v[1] << 32) | v[0], ((u64)v[3] << 32) | v[2]);
-  }
-  __device__ __forceinline__ T from_u64(u64 x) const { return x; }
-  // Harvey CT butterfly, values in [0, 4q)
-  __device__ __forceinline__ void ct(T& X, T& Y, const W& w) const {
-    const u64 x = X >= q2 ? X - q2 : X;
-    const u64 t = shoup_lazy(Y, w.x, w.y, q);
-    X = x + t;
-    Y = x - t + q2;
-  }
-  // Harvey GS butterfly, values in [0, 2q)
-  __device__ __forceinline__ void gs(T& X, T& Y, const W& w, bool) const {
-    const u64 x = X, y = Y;
-    const u64 s = x + y;
-    X = s >= q2 ? s - q2 : s;
-    Y = shoup_lazy(x - y + q2, w.x, w.y, q);
-  }
-  __device__ __forceinline__ T reduce_round(T x) const { return x; }  // lazy range is invariant
-  __device__ __forceinline__ u64 final_fwd(T x) const {
-    x = x >= q2 ? x - q2 : x;
-    return x >= q ? x - q : x;
-  }
-  __device__ __forceinline__ u64 final_inv(T x) const {
-    x = shoup_lazy(x, ninv, ninv_s, q);
-    return x >= q ? x - q : x;
-  }
-};
-
-struct F64Arith {
-  typedef double T;
-  typedef double W;
-  double q, qinv, ninv;
-  __device__ F64Arith(const ModConst& m) : q(m.qd), qinv(m.qinv_d), ninv(m.ninv_d) {}
-  __device__ __forceinline__ W tw(__amdgpu_buffer_rsrc_t r, int vidx, int sidx) const {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vidx * 8, sidx * 8, 0));
-  }
-  __device__ __forceinline__ T from_u64(u64 x) const { return (double)x; }
-  // a*w mod q for exact integer doubles (|a| < 16q, |w| <= q/2, q < 2^46):
-  // h + l == a*w exactly, k*q within 1.5q of h, so the result is exact and
-  // |result| < 1.5q + ulp(h)/2 < 2q
-  __device__ __forceinline__ double mulmod(double a, double w) const {
-    const double h = a * w;
-    const double l = __builtin_fma(a, w, -h);
-    const double k = __builtin_rint(h * qinv);
-    return __builtin_fma(-k, q, h) + l;
-  }
-  __device__ __forceinline__ double red(double x) const { return __builtin_fma(-__builtin_rint(x * qinv), q, x); }
-  // CT: |x|, |y| stay below ~12q inside a round (reduced at round boundaries)
-  __device__ __forceinline__ void ct(T& X, T& Y, const W& w) const {
-    const double t = mulmod(Y, w);
-    const double x = X;
-    X = x + t;
-    Y = x - t;
-  }
-  // GS: the sum is reduced every other stage
-  __device__ __forceinline__ void gs(T& X, T& Y, const W& w, bool reduce_sum) const {
-    const double x = X, y = Y;
-    const double s = x + y;
-    X = reduce_sum ? red(s) : s;
-    Y = mulmod(x - y, w);
-  }
-  __device__ __forceinline__ T reduce_round(T x) const { return red(x); }
-  __device__ __forceinline__ u64 to_u64(double x) const {
-    x = red(x);
-    x = x < 0 ? x + q : x;
-    x = x >= q ? x - q : x;
-    x = x < 0 ? x + q : x;
-    return (u64)x;
-  }
-  __device__ __forceinline__ u64 final_fwd(T x) const { return to_u64(x); }
-  __device__ __forceinline__ u64 final_inv(T x) const { return to_u64(mulmod(x, ninv)); }
-};
-
-template <class T>
-__device__ __forceinline__ u64 to_bits(T x) {
-  return __builtin_bit_cast(u64, x);
-}
-template <class T>
-__device__ __forceinline__ T from_bits(u64 x) {
-  return __builtin_bit_cast(T, x);
 }
 
 // Redistribute a[] from window BOLD to window BNEW through LDS, one 32-bit
@@ -326,17 +207,6 @@ __device__ __forceinline__ void reduce_all(typename A::T (&a)[32], const A& ar) 
   for (int k = 0; k < 32; ++k) a[k] = ar.reduce_round(a[k]);
 }
 
-// wave-uniform pointer to row (c, l, b) of a LimbSet: the limb tables are
-// indexed dynamically, so force the results into SGPRs so that every element
-// address is SGPR base + lane offset
-__device__ __forceinline__ u64* row_ptr(const LimbSet& s, int c, int l, int b) {
-  const int pos = __builtin_amdgcn_readfirstlane(s.pos[l]);
-  const long long off = c * s.comp_stride + pos * s.limb_stride + b * s.batch_stride;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(off & 0xffffffffll));
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(off >> 32));
-  return s.p + (long long)(((unsigned long long)hi << 32) | lo);
-}
-
 // Round windows: LOGN=15 -> bits [10,15), [5,10), [0,5); LOGN=14 -> [9,14),[4,9),[0,5)
 // (last round only bits 3..0); LOGN=13 -> [8,13),[3,8),[0,5) (bits 2..0).
 // Thread t loads / stores element t + (k << B0) (k < 32): fully coalesced.
@@ -423,20 +293,6 @@ __device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int 
   }
 }
 
-__device__ __forceinline__ void job_of(const NttIO& io, int job, int& c, int& l, int& b) {
-  const LimbSet& d = io.dst;
-  if (io.order == 1) {
-    l = job % d.nlimb;
-    const int r = job / d.nlimb;
-    b = r % d.nbatch;
-    c = r / d.nbatch;
-  } else {
-    b = job % d.nbatch;
-    const int r = job / d.nbatch;
-    l = r % d.nlimb;
-    c = r / d.nlimb;
-  }
-}
 
 template <int LOGN, int PRO, int EPI>
 __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_fwd_kernel(NttIO io, const DeviceTables* __restrict__ tb) {

@@ -1,0 +1,326 @@
+// ntt2.hip -- two-pass negacyclic NTT / INTT for N = 2^15 on gfx950.
+//
+// The same transform as ntt.hip (Lattigo v6 ring convention, SURVEY.md App.
+// A.3: forward Cooley-Tukey, natural order in, bit-reversed out, twiddle of the
+// butterfly group i of stage d = w[(N >> (d+1)) + i]; inverse Gentleman-Sande
+// with psi^-1 and a final N^-1), split by element bits, e = col + 256 * row:
+//   cols pass: the stages on bits 14..8 -- 256 independent 128-point transforms
+//              down the columns; 16 columns per 128-thread workgroup;
+//   rows pass: the stages on bits 7..0 -- 128 independent 256-point transforms
+//              along contiguous rows; 16 rows per 256-thread workgroup.
+// Every thread holds 16 elements (32 VGPRs) and a workgroup 18 / 34 KiB of
+// LDS, so a CU keeps several workgroups in flight and overlaps their loads,
+// butterflies and stores -- the one-limb-per-CU kernel of ntt.hip (256 KiB of
+// registers, 132 KiB of LDS per limb) cannot.  The price is a second pass over
+// the limb: the first pass writes the raw butterfly values (lazy u64 or
+// float64 bits) and the second re-reads them while they are still resident in
+// the 256 MiB Infinity Cache.
+//
+// Twiddles of the cols pass depend only on the row bits of the butterfly
+// group, identical for every column: they are wave-uniform scalar loads.
+#include "common.h"
+#include "ntt_arith.h"
+
+namespace {
+
+constexpr int LN = 15;
+constexpr int A_STRIDE = 18;   // cols pass LDS: [128 rows][18] u64, conflict-free both ways
+constexpr int B_STRIDE = 272;  // rows pass LDS: [16 rows][256 + 16 pad] u64
+__device__ __forceinline__ int b_lds(int rr, int col) { return rr * B_STRIDE + col + (col >> 4); }
+
+template <class A>
+__device__ __forceinline__ typename A::W twl(const void* t, int idx) {
+  if constexpr (sizeof(typename A::W) == 16)
+    return ((const ulonglong2*)t)[idx];
+  else
+    return ((const double*)t)[idx];
+}
+
+template <class A>
+__device__ __forceinline__ void reduce16(typename A::T (&a)[16], const A& ar) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) a[k] = ar.reduce_round(a[k]);
+}
+
+// ---------------------------------------------------------------------------
+// forward, cols pass: stages d = 14..11 (phase 1: thread (cl, rg) holds rows
+// r = rg + 8 i, i = r bits 3..6) then d = 10..8 (phase 2: rows
+// r = 8 (rg + 8 g) + j, j = r bits 0..2, slot j + 8 g)
+// ---------------------------------------------------------------------------
+template <class A, int PRO>
+__device__ __forceinline__ void fwd_cols(const NttIO& io, int c, int l, int b, int tile, const ModConst& mc,
+                                         const A& ar, const void* tw, u64* lds, bool lazy,
+                                         const DeviceTables* __restrict__ tb) {
+  const int t = threadIdx.x, cl = t & 15, rg = t >> 4;
+  const int col = tile * 16 + cl;
+  typename A::T a[16];
+  const u64* src = row_ptr(io.src, c, PRO == NTT_PRO_LOAD ? l : 0, b);
+  if constexpr (PRO == NTT_PRO_LOAD) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a[i] = ar.from_u64(src[col + ((rg + 8 * i) << 8)]);
+  } else {  // NTT_PRO_RESCALE (DivRoundByLastModulusNTT prep of every other limb)
+    const u64 qL = tb->mc[io.modL].q, h = qL >> 1;
+    const u64 hm = barrett128(0, h, mc);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const u64 x = src[col + ((rg + 8 * i) << 8)];
+      a[i] = ar.from_u64(sub_mod(barrett128(0, add_mod(x, h, qL), mc), hm, mc.q));
+    }
+  }
+#pragma unroll
+  for (int k = 3; k >= 0; --k) {  // d = 11 + k: r bit k+3 = i bit k; group = i >> (k+1)
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (!((i >> k) & 1)) ar.ct(a[i], a[i | (1 << k)], twl<A>(tw, (1 << (3 - k)) + (i >> (k + 1))));
+  }
+  if (!lazy) reduce16<A>(a, ar);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) lds[(rg + 8 * i) * A_STRIDE + cl] = to_bits(a[i]);
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j + 8 * g] = from_bits<typename A::T>(lds[(8 * (rg + 8 * g) + j) * A_STRIDE + cl]);
+#pragma unroll
+  for (int bb = 2; bb >= 0; --bb) {  // d = 8 + bb: r bit bb = j bit bb; group = r >> (bb+1)
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (!((j >> bb) & 1)) {
+          const int r = 8 * (rg + 8 * g) + j;
+          ar.ct(a[j + 8 * g], a[(j | (1 << bb)) + 8 * g], twl<A>(tw, (1 << (6 - bb)) + (r >> (bb + 1))));
+        }
+  }
+  if (!lazy) reduce16<A>(a, ar);
+  u64* mid = row_ptr(io.mid, c, l, b);
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mid[col + ((8 * (rg + 8 * g) + j) << 8)] = to_bits(a[j + 8 * g]);
+}
+
+// ---------------------------------------------------------------------------
+// forward, rows pass: stages d = 7..4 (phase 1: thread (rr, jc) holds columns
+// jc + 16 i) then d = 3..0 (phase 2: columns 16 ig + j, ig = t & 15)
+// ---------------------------------------------------------------------------
+template <class A, int EPI>
+__device__ __forceinline__ void fwd_rows(const NttIO& io, int c, int l, int b, int tile, const ModConst& mc,
+                                         const A& ar, const void* tw, u64* lds, bool lazy) {
+  const int t = threadIdx.x, rr = t >> 4, jc = t & 15;
+  const int row = tile * 16 + rr;
+  typename A::T a[16];
+  const u64* mid = row_ptr(io.mid, c, l, b) + (row << 8);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) a[i] = from_bits<typename A::T>(mid[jc + 16 * i]);
+#pragma unroll
+  for (int k = 3; k >= 0; --k) {  // d = 4 + k: col bit d = i bit k
+    const int d = 4 + k;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (!((i >> k) & 1))
+        ar.ct(a[i], a[i | (1 << k)], twl<A>(tw, (1 << (14 - d)) + ((row << (7 - d)) | (i >> (k + 1)))));
+  }
+  if (!lazy) reduce16<A>(a, ar);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) lds[b_lds(rr, jc + 16 * i)] = to_bits(a[i]);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = from_bits<typename A::T>(lds[b_lds(rr, 16 * jc + j)]);
+#pragma unroll
+  for (int d = 3; d >= 0; --d) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (!((j >> d) & 1))
+        ar.ct(a[j], a[j | (1 << d)], twl<A>(tw, (1 << (14 - d)) + ((row << (7 - d)) | ((16 * jc + j) >> (d + 1)))));
+  }
+  u64* dst = row_ptr(io.dst, c, l, b) + (row << 8) + 16 * jc;
+  if constexpr (EPI == NTT_EPI_STORE) {
+#pragma unroll
+    for (int j = 0; j < 16; j += 2)
+      *(ulonglong2*)(dst + j) = make_ulonglong2(ar.final_fwd(a[j]), ar.final_fwd(a[j + 1]));
+  } else {  // NTT_EPI_SUBSCALE: dst = (ex - y) * s_l
+    const u64* ex = row_ptr(io.ex, c, l, b) + (row << 8) + 16 * jc;
+    const u64 s = io.s[l], ss = io.ss[l];
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      const ulonglong2 x = *(const ulonglong2*)(ex + j);
+      *(ulonglong2*)(dst + j) = make_ulonglong2(shoup_mul(sub_mod(x.x, ar.final_fwd(a[j]), mc.q), s, ss, mc.q),
+                                                shoup_mul(sub_mod(x.y, ar.final_fwd(a[j + 1]), mc.q), s, ss, mc.q));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// inverse, rows pass (first): stages d = 0..3 on columns 16 ig + j, then
+// d = 4..7 on columns jc + 16 i; the sum of a float64 GS butterfly is reduced
+// every other stage and every phase ends with a full reduction
+// ---------------------------------------------------------------------------
+template <class A>
+__device__ __forceinline__ void inv_rows(const NttIO& io, int c, int l, int b, int tile, const A& ar,
+                                         const void* tw, u64* lds) {
+  const int t = threadIdx.x, rr = t >> 4, jc = t & 15;
+  const int row = tile * 16 + rr;
+  typename A::T a[16];
+  const u64* src = row_ptr(io.src, c, l, b) + (row << 8) + 16 * jc;
+#pragma unroll
+  for (int j = 0; j < 16; j += 2) {
+    const ulonglong2 x = *(const ulonglong2*)(src + j);
+    a[j] = ar.from_u64(x.x);
+    a[j + 1] = ar.from_u64(x.y);
+  }
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (!((j >> d) & 1))
+        ar.gs(a[j], a[j | (1 << d)], twl<A>(tw, (1 << (14 - d)) + ((row << (7 - d)) | ((16 * jc + j) >> (d + 1)))),
+              (d & 1) == 1);
+  }
+  reduce16<A>(a, ar);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) lds[b_lds(rr, 16 * jc + j)] = to_bits(a[j]);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) a[i] = from_bits<typename A::T>(lds[b_lds(rr, jc + 16 * i)]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // d = 4 + k
+    const int d = 4 + k;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (!((i >> k) & 1))
+        ar.gs(a[i], a[i | (1 << k)], twl<A>(tw, (1 << (14 - d)) + ((row << (7 - d)) | (i >> (k + 1)))),
+              (k & 1) == 1);
+  }
+  reduce16<A>(a, ar);
+  u64* mid = row_ptr(io.mid, c, l, b) + (row << 8);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) mid[jc + 16 * i] = to_bits(a[i]);
+}
+
+// inverse, cols pass (second): stages d = 8..10 (rows 8 (rg + 8 g) + j), then
+// d = 11..14 (rows rg + 8 i, wave-uniform twiddles), times N^-1
+template <class A>
+__device__ __forceinline__ void inv_cols(const NttIO& io, int c, int l, int b, int tile, const A& ar,
+                                         const void* tw, u64* lds) {
+  const int t = threadIdx.x, cl = t & 15, rg = t >> 4;
+  const int col = tile * 16 + cl;
+  typename A::T a[16];
+  const u64* mid = row_ptr(io.mid, c, l, b);
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j + 8 * g] = from_bits<typename A::T>(mid[col + ((8 * (rg + 8 * g) + j) << 8)]);
+#pragma unroll
+  for (int bb = 0; bb < 3; ++bb) {  // d = 8 + bb
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (!((j >> bb) & 1)) {
+          const int r = 8 * (rg + 8 * g) + j;
+          ar.gs(a[j + 8 * g], a[(j | (1 << bb)) + 8 * g], twl<A>(tw, (1 << (6 - bb)) + (r >> (bb + 1))),
+                (bb & 1) == 1);
+        }
+  }
+  reduce16<A>(a, ar);
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lds[(8 * (rg + 8 * g) + j) * A_STRIDE + cl] = to_bits(a[j + 8 * g]);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) a[i] = from_bits<typename A::T>(lds[(rg + 8 * i) * A_STRIDE + cl]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // d = 11 + k
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (!((i >> k) & 1)) ar.gs(a[i], a[i | (1 << k)], twl<A>(tw, (1 << (3 - k)) + (i >> (k + 1))), (k & 1) == 1);
+  }
+  u64* dst = row_ptr(io.dst, c, l, b);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dst[col + ((rg + 8 * i) << 8)] = ar.final_inv(a[i]);
+}
+
+// ---------------------------------------------------------------------------
+// kernels: blockIdx.x = job * tiles + tile (the tiles of one limb are adjacent)
+// ---------------------------------------------------------------------------
+template <int PRO>
+__global__ void __launch_bounds__(128) ntt2_fwd_cols(NttIO io, const DeviceTables* __restrict__ tb) {
+  __shared__ u64 lds[128 * A_STRIDE];
+  int c, l, b;
+  job_of(io, blockIdx.x >> 4, c, l, b);
+  const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
+  const ModConst mc = tb->mc[mod];
+  const bool lazy = mc.bar_k <= 41;
+  if (mc.f64)
+    fwd_cols<F64Arith, PRO>(io, c, l, b, blockIdx.x & 15, mc, F64Arith(mc), tb->fwd_d[mod], lds, lazy, tb);
+  else
+    fwd_cols<IntArith, PRO>(io, c, l, b, blockIdx.x & 15, mc, IntArith(mc), tb->fwd[mod], lds, true, tb);
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(256) ntt2_fwd_rows(NttIO io, const DeviceTables* __restrict__ tb) {
+  __shared__ u64 lds[16 * B_STRIDE];
+  int c, l, b;
+  job_of(io, blockIdx.x >> 3, c, l, b);
+  const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
+  const ModConst mc = tb->mc[mod];
+  if (mc.f64)
+    fwd_rows<F64Arith, EPI>(io, c, l, b, blockIdx.x & 7, mc, F64Arith(mc), tb->fwd_d[mod], lds, mc.bar_k <= 41);
+  else
+    fwd_rows<IntArith, EPI>(io, c, l, b, blockIdx.x & 7, mc, IntArith(mc), tb->fwd[mod], lds, true);
+}
+
+__global__ void __launch_bounds__(256) ntt2_inv_rows(NttIO io, const DeviceTables* __restrict__ tb) {
+  __shared__ u64 lds[16 * B_STRIDE];
+  int c, l, b;
+  job_of(io, blockIdx.x >> 3, c, l, b);
+  const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
+  const ModConst mc = tb->mc[mod];
+  if (mc.f64)
+    inv_rows<F64Arith>(io, c, l, b, blockIdx.x & 7, F64Arith(mc), tb->inv_d[mod], lds);
+  else
+    inv_rows<IntArith>(io, c, l, b, blockIdx.x & 7, IntArith(mc), tb->inv[mod], lds);
+}
+
+__global__ void __launch_bounds__(128) ntt2_inv_cols(NttIO io, const DeviceTables* __restrict__ tb) {
+  __shared__ u64 lds[128 * A_STRIDE];
+  int c, l, b;
+  job_of(io, blockIdx.x >> 4, c, l, b);
+  const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
+  const ModConst mc = tb->mc[mod];
+  if (mc.f64)
+    inv_cols<F64Arith>(io, c, l, b, blockIdx.x & 15, F64Arith(mc), tb->inv_d[mod], lds);
+  else
+    inv_cols<IntArith>(io, c, l, b, blockIdx.x & 15, IntArith(mc), tb->inv[mod], lds);
+}
+
+}  // namespace
+
+// host entry: two launches on stream st; io.mid must have dst's geometry and
+// must not alias io.ex (the epilogue reads ex after the first pass wrote mid)
+int orion_launch_ntt2(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
+  const int jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
+  if (jobs == 0) return 0;
+  if (io.jobs != jobs) return -1;
+  if (inverse) {
+    if (io.pro != NTT_PRO_LOAD || io.epi != NTT_EPI_STORE) return -1;
+    hipLaunchKernelGGL(ntt2_inv_rows, dim3(jobs * 8), dim3(256), 0, st, io, tb);
+    hipLaunchKernelGGL(ntt2_inv_cols, dim3(jobs * 16), dim3(128), 0, st, io, tb);
+    return 0;
+  }
+  if (io.pro == NTT_PRO_LOAD)
+    hipLaunchKernelGGL(ntt2_fwd_cols<NTT_PRO_LOAD>, dim3(jobs * 16), dim3(128), 0, st, io, tb);
+  else if (io.pro == NTT_PRO_RESCALE)
+    hipLaunchKernelGGL(ntt2_fwd_cols<NTT_PRO_RESCALE>, dim3(jobs * 16), dim3(128), 0, st, io, tb);
+  else
+    return -1;
+  if (io.epi == NTT_EPI_STORE)
+    hipLaunchKernelGGL(ntt2_fwd_rows<NTT_EPI_STORE>, dim3(jobs * 8), dim3(256), 0, st, io, tb);
+  else if (io.epi == NTT_EPI_SUBSCALE)
+    hipLaunchKernelGGL(ntt2_fwd_rows<NTT_EPI_SUBSCALE>, dim3(jobs * 8), dim3(256), 0, st, io, tb);
+  else
+    return -1;
+  return 0;
+}

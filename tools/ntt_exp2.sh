@@ -1,0 +1,15 @@
+# GPU: parity suite with the two-pass NTT, then NTT microbench + LoLA bench, one-pass vs two-pass
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export JOBS=${JOBS:-1024,4096}
+ORION_NTT_IMPL=2 timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_ntt2.txt 2>&1 || { tail -40 gpurun_out/pytest_ntt2.txt; exit 1; }
+tail -1 gpurun_out/pytest_ntt2.txt
+for impl in 1 2; do
+  ORION_NTT_IMPL=$impl TAG=_impl$impl timeout -k 10 200 python tools/ntt_bench.py > gpurun_out/nb_impl$impl.txt 2>&1 || exit 1
+  echo "== impl $impl"; cat gpurun_out/nb_impl$impl.txt
+done
+for impl in 1 2; do
+  ORION_NTT_IMPL=$impl timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_impl$impl.txt 2>&1 || exit 1
+  echo "== bench impl $impl"; tail -1 gpurun_out/bench_impl$impl.txt | cut -c1-200
+done
