@@ -28,12 +28,10 @@ constexpr int A_STRIDE = 18;   // cols pass LDS: [128 rows][18] u64, conflict-fr
 constexpr int B_STRIDE = 272;  // rows pass LDS: [16 rows][256 + 16 pad] u64
 __device__ __forceinline__ int b_lds(int rr, int col) { return rr * B_STRIDE + col + (col >> 4); }
 
-template <class A>
-__device__ __forceinline__ typename A::W twl(const void* t, int idx) {
-  if constexpr (sizeof(typename A::W) == 16)
-    return ((const ulonglong2*)t)[idx];
-  else
-    return ((const double*)t)[idx];
+// twiddle tables through a buffer descriptor: w[vidx + sidx], vidx per lane,
+// sidx wave-uniform (an SGPR / immediate offset)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t twr(const void* t, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)t, 0, bytes, 0x00020000);
 }
 
 template <class A>
@@ -49,7 +47,7 @@ __device__ __forceinline__ void reduce16(typename A::T (&a)[16], const A& ar) {
 // ---------------------------------------------------------------------------
 template <class A, int PRO>
 __device__ __forceinline__ void fwd_cols(const NttIO& io, int c, int l, int b, int tile, const ModConst& mc,
-                                         const A& ar, const void* tw, u64* lds, bool lazy,
+                                         const A& ar, __amdgpu_buffer_rsrc_t tw, u64* lds, bool lazy,
                                          const DeviceTables* __restrict__ tb) {
   const int t = threadIdx.x, cl = t & 15, rg = t >> 4;
   const int col = tile * 16 + cl;
@@ -71,7 +69,7 @@ __device__ __forceinline__ void fwd_cols(const NttIO& io, int c, int l, int b, i
   for (int k = 3; k >= 0; --k) {  // d = 11 + k: r bit k+3 = i bit k; group = i >> (k+1)
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-      if (!((i >> k) & 1)) ar.ct(a[i], a[i | (1 << k)], twl<A>(tw, (1 << (3 - k)) + (i >> (k + 1))));
+      if (!((i >> k) & 1)) ar.ct(a[i], a[i | (1 << k)], ar.tw(tw, 0, (1 << (3 - k)) + (i >> (k + 1))));
   }
   if (!lazy) reduce16<A>(a, ar);
 #pragma unroll
@@ -89,7 +87,7 @@ __device__ __forceinline__ void fwd_cols(const NttIO& io, int c, int l, int b, i
       for (int j = 0; j < 8; ++j)
         if (!((j >> bb) & 1)) {
           const int r = 8 * (rg + 8 * g) + j;
-          ar.ct(a[j + 8 * g], a[(j | (1 << bb)) + 8 * g], twl<A>(tw, (1 << (6 - bb)) + (r >> (bb + 1))));
+          ar.ct(a[j + 8 * g], a[(j | (1 << bb)) + 8 * g], ar.tw(tw, (1 << (6 - bb)) + (r >> (bb + 1)), 0));
         }
   }
   if (!lazy) reduce16<A>(a, ar);
@@ -106,7 +104,7 @@ __device__ __forceinline__ void fwd_cols(const NttIO& io, int c, int l, int b, i
 // ---------------------------------------------------------------------------
 template <class A, int EPI>
 __device__ __forceinline__ void fwd_rows(const NttIO& io, int c, int l, int b, int tile, const ModConst& mc,
-                                         const A& ar, const void* tw, u64* lds, bool lazy) {
+                                         const A& ar, __amdgpu_buffer_rsrc_t tw, u64* lds, bool lazy) {
   const int t = threadIdx.x, rr = t >> 4, jc = t & 15;
   const int row = tile * 16 + rr;
   typename A::T a[16];
@@ -119,7 +117,7 @@ __device__ __forceinline__ void fwd_rows(const NttIO& io, int c, int l, int b, i
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       if (!((i >> k) & 1))
-        ar.ct(a[i], a[i | (1 << k)], twl<A>(tw, (1 << (14 - d)) + ((row << (7 - d)) | (i >> (k + 1)))));
+        ar.ct(a[i], a[i | (1 << k)], ar.tw(tw, (1 << (14 - d)) + ((row << (7 - d)) | (i >> (k + 1))), 0));
   }
   if (!lazy) reduce16<A>(a, ar);
 #pragma unroll
@@ -132,7 +130,7 @@ __device__ __forceinline__ void fwd_rows(const NttIO& io, int c, int l, int b, i
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       if (!((j >> d) & 1))
-        ar.ct(a[j], a[j | (1 << d)], twl<A>(tw, (1 << (14 - d)) + ((row << (7 - d)) | ((16 * jc + j) >> (d + 1)))));
+        ar.ct(a[j], a[j | (1 << d)], ar.tw(tw, (1 << (14 - d)) + ((row << (7 - d)) | ((16 * jc + j) >> (d + 1))), 0));
   }
   u64* dst = row_ptr(io.dst, c, l, b) + (row << 8) + 16 * jc;
   if constexpr (EPI == NTT_EPI_STORE) {
@@ -158,7 +156,7 @@ __device__ __forceinline__ void fwd_rows(const NttIO& io, int c, int l, int b, i
 // ---------------------------------------------------------------------------
 template <class A>
 __device__ __forceinline__ void inv_rows(const NttIO& io, int c, int l, int b, int tile, const A& ar,
-                                         const void* tw, u64* lds) {
+                                         __amdgpu_buffer_rsrc_t tw, u64* lds) {
   const int t = threadIdx.x, rr = t >> 4, jc = t & 15;
   const int row = tile * 16 + rr;
   typename A::T a[16];
@@ -174,7 +172,7 @@ __device__ __forceinline__ void inv_rows(const NttIO& io, int c, int l, int b, i
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       if (!((j >> d) & 1))
-        ar.gs(a[j], a[j | (1 << d)], twl<A>(tw, (1 << (14 - d)) + ((row << (7 - d)) | ((16 * jc + j) >> (d + 1)))),
+        ar.gs(a[j], a[j | (1 << d)], ar.tw(tw, (1 << (14 - d)) + ((row << (7 - d)) | ((16 * jc + j) >> (d + 1))), 0),
               (d & 1) == 1);
   }
   reduce16<A>(a, ar);
@@ -189,7 +187,7 @@ __device__ __forceinline__ void inv_rows(const NttIO& io, int c, int l, int b, i
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       if (!((i >> k) & 1))
-        ar.gs(a[i], a[i | (1 << k)], twl<A>(tw, (1 << (14 - d)) + ((row << (7 - d)) | (i >> (k + 1)))),
+        ar.gs(a[i], a[i | (1 << k)], ar.tw(tw, (1 << (14 - d)) + ((row << (7 - d)) | (i >> (k + 1))), 0),
               (k & 1) == 1);
   }
   reduce16<A>(a, ar);
@@ -202,7 +200,7 @@ __device__ __forceinline__ void inv_rows(const NttIO& io, int c, int l, int b, i
 // d = 11..14 (rows rg + 8 i, wave-uniform twiddles), times N^-1
 template <class A>
 __device__ __forceinline__ void inv_cols(const NttIO& io, int c, int l, int b, int tile, const A& ar,
-                                         const void* tw, u64* lds) {
+                                         __amdgpu_buffer_rsrc_t tw, u64* lds) {
   const int t = threadIdx.x, cl = t & 15, rg = t >> 4;
   const int col = tile * 16 + cl;
   typename A::T a[16];
@@ -219,7 +217,7 @@ __device__ __forceinline__ void inv_cols(const NttIO& io, int c, int l, int b, i
       for (int j = 0; j < 8; ++j)
         if (!((j >> bb) & 1)) {
           const int r = 8 * (rg + 8 * g) + j;
-          ar.gs(a[j + 8 * g], a[(j | (1 << bb)) + 8 * g], twl<A>(tw, (1 << (6 - bb)) + (r >> (bb + 1))),
+          ar.gs(a[j + 8 * g], a[(j | (1 << bb)) + 8 * g], ar.tw(tw, (1 << (6 - bb)) + (r >> (bb + 1)), 0),
                 (bb & 1) == 1);
         }
   }
@@ -235,7 +233,7 @@ __device__ __forceinline__ void inv_cols(const NttIO& io, int c, int l, int b, i
   for (int k = 0; k < 4; ++k) {  // d = 11 + k
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-      if (!((i >> k) & 1)) ar.gs(a[i], a[i | (1 << k)], twl<A>(tw, (1 << (3 - k)) + (i >> (k + 1))), (k & 1) == 1);
+      if (!((i >> k) & 1)) ar.gs(a[i], a[i | (1 << k)], ar.tw(tw, 0, (1 << (3 - k)) + (i >> (k + 1))), (k & 1) == 1);
   }
   u64* dst = row_ptr(io.dst, c, l, b);
 #pragma unroll
@@ -254,9 +252,9 @@ __global__ void __launch_bounds__(128) ntt2_fwd_cols(NttIO io, const DeviceTable
   const ModConst mc = tb->mc[mod];
   const bool lazy = mc.bar_k <= 41;
   if (mc.f64)
-    fwd_cols<F64Arith, PRO>(io, c, l, b, blockIdx.x & 15, mc, F64Arith(mc), tb->fwd_d[mod], lds, lazy, tb);
+    fwd_cols<F64Arith, PRO>(io, c, l, b, blockIdx.x & 15, mc, F64Arith(mc), twr(tb->fwd_d[mod], (1 << LN) * 8), lds, lazy, tb);
   else
-    fwd_cols<IntArith, PRO>(io, c, l, b, blockIdx.x & 15, mc, IntArith(mc), tb->fwd[mod], lds, true, tb);
+    fwd_cols<IntArith, PRO>(io, c, l, b, blockIdx.x & 15, mc, IntArith(mc), twr(tb->fwd[mod], (1 << LN) * 16), lds, true, tb);
 }
 
 template <int EPI>
@@ -267,9 +265,9 @@ __global__ void __launch_bounds__(256) ntt2_fwd_rows(NttIO io, const DeviceTable
   const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
   const ModConst mc = tb->mc[mod];
   if (mc.f64)
-    fwd_rows<F64Arith, EPI>(io, c, l, b, blockIdx.x & 7, mc, F64Arith(mc), tb->fwd_d[mod], lds, mc.bar_k <= 41);
+    fwd_rows<F64Arith, EPI>(io, c, l, b, blockIdx.x & 7, mc, F64Arith(mc), twr(tb->fwd_d[mod], (1 << LN) * 8), lds, mc.bar_k <= 41);
   else
-    fwd_rows<IntArith, EPI>(io, c, l, b, blockIdx.x & 7, mc, IntArith(mc), tb->fwd[mod], lds, true);
+    fwd_rows<IntArith, EPI>(io, c, l, b, blockIdx.x & 7, mc, IntArith(mc), twr(tb->fwd[mod], (1 << LN) * 16), lds, true);
 }
 
 __global__ void __launch_bounds__(256) ntt2_inv_rows(NttIO io, const DeviceTables* __restrict__ tb) {
@@ -279,9 +277,9 @@ __global__ void __launch_bounds__(256) ntt2_inv_rows(NttIO io, const DeviceTable
   const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
   const ModConst mc = tb->mc[mod];
   if (mc.f64)
-    inv_rows<F64Arith>(io, c, l, b, blockIdx.x & 7, F64Arith(mc), tb->inv_d[mod], lds);
+    inv_rows<F64Arith>(io, c, l, b, blockIdx.x & 7, F64Arith(mc), twr(tb->inv_d[mod], (1 << LN) * 8), lds);
   else
-    inv_rows<IntArith>(io, c, l, b, blockIdx.x & 7, IntArith(mc), tb->inv[mod], lds);
+    inv_rows<IntArith>(io, c, l, b, blockIdx.x & 7, IntArith(mc), twr(tb->inv[mod], (1 << LN) * 16), lds);
 }
 
 __global__ void __launch_bounds__(128) ntt2_inv_cols(NttIO io, const DeviceTables* __restrict__ tb) {
@@ -291,9 +289,9 @@ __global__ void __launch_bounds__(128) ntt2_inv_cols(NttIO io, const DeviceTable
   const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
   const ModConst mc = tb->mc[mod];
   if (mc.f64)
-    inv_cols<F64Arith>(io, c, l, b, blockIdx.x & 15, F64Arith(mc), tb->inv_d[mod], lds);
+    inv_cols<F64Arith>(io, c, l, b, blockIdx.x & 15, F64Arith(mc), twr(tb->inv_d[mod], (1 << LN) * 8), lds);
   else
-    inv_cols<IntArith>(io, c, l, b, blockIdx.x & 15, IntArith(mc), tb->inv[mod], lds);
+    inv_cols<IntArith>(io, c, l, b, blockIdx.x & 15, IntArith(mc), twr(tb->inv[mod], (1 << LN) * 16), lds);
 }
 
 }  // namespace
