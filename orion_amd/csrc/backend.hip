@@ -24,7 +24,7 @@
 
 int orion_launch_ntt(int logN, const LimbSet& s, const DeviceTables* tb, bool inverse, hipStream_t st);
 int orion_launch_ntt_io(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st);
-int orion_launch_ntt2(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st);
+int orion_launch_ntt2(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st);
 int orion_ntt_init();
 int orion_launch_ew(int op, const LimbSet& o, const LimbSet& a, const LimbSet& b, const u64* s, const u64* ss,
                     const DeviceTables* tb, int N, hipStream_t st);
@@ -368,7 +368,7 @@ struct Context {
   void ntt_io(NttIO io, bool inv) {
     io.order = ntt_order;
     io.jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
-    if (ntt_impl == 2 && logN == 15) {
+    if (logN == 16 || (ntt_impl == 2 && logN == 15)) {  // N = 2^16: the two-pass kernels only
       Poly scratch;
       io.mid = io.dst;
       if (io.epi == NTT_EPI_SUBSCALE && io.ex.p == io.dst.p) {  // in-place tail: keep ex intact for pass 2
@@ -377,7 +377,7 @@ struct Context {
       }
       const double per = 16.0 * N + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
       Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, per * io.jobs);
-      if (orion_launch_ntt2(io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
+      if (orion_launch_ntt2(logN, io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
       return;
     }
     // algorithmic bytes per limb-transform: read + write the limb (16 N), + 8 N
@@ -411,7 +411,7 @@ struct Context {
     dnum = (L + K - 1) / K;
     logScale = logScale_;
     h = h_;
-    if (logN < 13 || logN > 15) throw std::runtime_error("logN must be 13..15 in this build");
+    if (logN < 13 || logN > 16) throw std::runtime_error("logN must be 13..16 in this build");
     if (L + K > ORION_MAXMOD) throw std::runtime_error("too many moduli");
     for (int b : logQ)
       if (b > 61) throw std::runtime_error("moduli must be <= 61 bits");

@@ -1,12 +1,14 @@
-// ntt2.hip -- two-pass negacyclic NTT / INTT for N = 2^15 on gfx950.
+// ntt2.hip -- two-pass negacyclic NTT / INTT for N = 2^15 and 2^16 on gfx950
+// (the only NTT for N = 2^16, whose 512 KiB limb cannot live in one CU).
 //
 // The same transform as ntt.hip (Lattigo v6 ring convention, SURVEY.md App.
 // A.3: forward Cooley-Tukey, natural order in, bit-reversed out, twiddle of the
 // butterfly group i of stage d = w[(N >> (d+1)) + i]; inverse Gentleman-Sande
 // with psi^-1 and a final N^-1), split by element bits, e = col + 256 * row:
-//   cols pass: the stages on bits 14..8 -- 256 independent 128-point transforms
-//              down the columns; 16 columns per 128-thread workgroup;
-//   rows pass: the stages on bits 7..0 -- 128 independent 256-point transforms
+//   cols pass: the stages on bits LOGN-1..8 -- 256 independent 2^R-point
+//              transforms down the columns (R = LOGN - 8 = 7 or 8); 16 columns
+//              per workgroup of 16 * 2^(R-4) threads;
+//   rows pass: the stages on bits 7..0 -- 2^R independent 256-point transforms
 //              along contiguous rows; 16 rows per 256-thread workgroup.
 // Every thread holds 16 elements (32 VGPRs) and a workgroup 18 / 34 KiB of
 // LDS, so a CU keeps several workgroups in flight and overlaps their loads,
@@ -23,8 +25,7 @@
 
 namespace {
 
-constexpr int LN = 15;
-constexpr int A_STRIDE = 18;   // cols pass LDS: [128 rows][18] u64, conflict-free both ways
+constexpr int A_STRIDE = 18;   // cols pass LDS: [2^R rows][18] u64, conflict-free both ways
 constexpr int B_STRIDE = 272;  // rows pass LDS: [16 rows][256 + 16 pad] u64
 __device__ __forceinline__ int b_lds(int rr, int col) { return rr * B_STRIDE + col + (col >> 4); }
 
@@ -41,68 +42,72 @@ __device__ __forceinline__ void reduce16(typename A::T (&a)[16], const A& ar) {
 }
 
 // ---------------------------------------------------------------------------
-// forward, cols pass: stages d = 14..11 (phase 1: thread (cl, rg) holds rows
-// r = rg + 8 i, i = r bits 3..6) then d = 10..8 (phase 2: rows
-// r = 8 (rg + 8 g) + j, j = r bits 0..2, slot j + 8 g)
+// forward, cols pass (R = LOGN - 8 row bits; RG = 2^(R-4) row groups;
+// J = 2^(R-4) rows per phase-2 group, G = 16 / J groups):
+//   phase 1: thread (cl = t & 15, rg = t >> 4) holds rows r = rg + RG i,
+//            i = r bits R-4..R-1: stages d = LOGN-1 .. LOGN-4 (wave-uniform twiddles)
+//   phase 2: rows r = J (rg + RG g) + j, j = r bits 0..R-5, slot j + J g:
+//            stages d = LOGN-5 .. 8
 // ---------------------------------------------------------------------------
-template <class A, int PRO>
+template <class A, int LOGN, int PRO>
 __device__ __forceinline__ void fwd_cols(const NttIO& io, int c, int l, int b, int tile, const ModConst& mc,
                                          const A& ar, __amdgpu_buffer_rsrc_t tw, u64* lds, bool lazy,
                                          const DeviceTables* __restrict__ tb) {
+  constexpr int R = LOGN - 8, RG = 1 << (R - 4), J = 1 << (R - 4), G = 16 / J;
   const int t = threadIdx.x, cl = t & 15, rg = t >> 4;
   const int col = tile * 16 + cl;
   typename A::T a[16];
   const u64* src = row_ptr(io.src, c, PRO == NTT_PRO_LOAD ? l : 0, b);
   if constexpr (PRO == NTT_PRO_LOAD) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) a[i] = ar.from_u64(src[col + ((rg + 8 * i) << 8)]);
+    for (int i = 0; i < 16; ++i) a[i] = ar.from_u64(src[col + ((rg + RG * i) << 8)]);
   } else {  // NTT_PRO_RESCALE (DivRoundByLastModulusNTT prep of every other limb)
     const u64 qL = tb->mc[io.modL].q, h = qL >> 1;
     const u64 hm = barrett128(0, h, mc);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const u64 x = src[col + ((rg + 8 * i) << 8)];
+      const u64 x = src[col + ((rg + RG * i) << 8)];
       a[i] = ar.from_u64(sub_mod(barrett128(0, add_mod(x, h, qL), mc), hm, mc.q));
     }
   }
 #pragma unroll
-  for (int k = 3; k >= 0; --k) {  // d = 11 + k: r bit k+3 = i bit k; group = i >> (k+1)
+  for (int k = 3; k >= 0; --k) {  // d = LOGN-4+k: r bit R-4+k = i bit k; group = i >> (k+1)
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       if (!((i >> k) & 1)) ar.ct(a[i], a[i | (1 << k)], ar.tw(tw, 0, (1 << (3 - k)) + (i >> (k + 1))));
   }
   if (!lazy) reduce16<A>(a, ar);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) lds[(rg + 8 * i) * A_STRIDE + cl] = to_bits(a[i]);
+  for (int i = 0; i < 16; ++i) lds[(rg + RG * i) * A_STRIDE + cl] = to_bits(a[i]);
   __syncthreads();
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
+  for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) a[j + 8 * g] = from_bits<typename A::T>(lds[(8 * (rg + 8 * g) + j) * A_STRIDE + cl]);
+    for (int j = 0; j < J; ++j) a[j + J * g] = from_bits<typename A::T>(lds[(J * (rg + RG * g) + j) * A_STRIDE + cl]);
 #pragma unroll
-  for (int bb = 2; bb >= 0; --bb) {  // d = 8 + bb: r bit bb = j bit bb; group = r >> (bb+1)
+  for (int bb = R - 5; bb >= 0; --bb) {  // d = 8 + bb: r bit bb = j bit bb; group = r >> (bb+1)
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < G; ++g)
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
+      for (int j = 0; j < J; ++j)
         if (!((j >> bb) & 1)) {
-          const int r = 8 * (rg + 8 * g) + j;
-          ar.ct(a[j + 8 * g], a[(j | (1 << bb)) + 8 * g], ar.tw(tw, (1 << (6 - bb)) + (r >> (bb + 1)), 0));
+          const int r = J * (rg + RG * g) + j;
+          ar.ct(a[j + J * g], a[(j | (1 << bb)) + J * g], ar.tw(tw, (1 << (R - 1 - bb)) + (r >> (bb + 1)), 0));
         }
   }
   if (!lazy) reduce16<A>(a, ar);
   u64* mid = row_ptr(io.mid, c, l, b);
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
+  for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) mid[col + ((8 * (rg + 8 * g) + j) << 8)] = to_bits(a[j + 8 * g]);
+    for (int j = 0; j < J; ++j) mid[col + ((J * (rg + RG * g) + j) << 8)] = to_bits(a[j + J * g]);
 }
 
 // ---------------------------------------------------------------------------
 // forward, rows pass: stages d = 7..4 (phase 1: thread (rr, jc) holds columns
 // jc + 16 i) then d = 3..0 (phase 2: columns 16 ig + j, ig = t & 15)
 // ---------------------------------------------------------------------------
-template <class A, int EPI>
+template <class A, int LOGN, int EPI>
 __device__ __forceinline__ void fwd_rows(const NttIO& io, int c, int l, int b, int tile, const ModConst& mc,
                                          const A& ar, __amdgpu_buffer_rsrc_t tw, u64* lds, bool lazy) {
   const int t = threadIdx.x, rr = t >> 4, jc = t & 15;
@@ -117,7 +122,7 @@ __device__ __forceinline__ void fwd_rows(const NttIO& io, int c, int l, int b, i
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       if (!((i >> k) & 1))
-        ar.ct(a[i], a[i | (1 << k)], ar.tw(tw, (1 << (14 - d)) + ((row << (7 - d)) | (i >> (k + 1))), 0));
+        ar.ct(a[i], a[i | (1 << k)], ar.tw(tw, (1 << (LOGN - 1 - d)) + ((row << (7 - d)) | (i >> (k + 1))), 0));
   }
   if (!lazy) reduce16<A>(a, ar);
 #pragma unroll
@@ -130,7 +135,7 @@ __device__ __forceinline__ void fwd_rows(const NttIO& io, int c, int l, int b, i
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       if (!((j >> d) & 1))
-        ar.ct(a[j], a[j | (1 << d)], ar.tw(tw, (1 << (14 - d)) + ((row << (7 - d)) | ((16 * jc + j) >> (d + 1))), 0));
+        ar.ct(a[j], a[j | (1 << d)], ar.tw(tw, (1 << (LOGN - 1 - d)) + ((row << (7 - d)) | ((16 * jc + j) >> (d + 1))), 0));
   }
   u64* dst = row_ptr(io.dst, c, l, b) + (row << 8) + 16 * jc;
   if constexpr (EPI == NTT_EPI_STORE) {
@@ -154,7 +159,7 @@ __device__ __forceinline__ void fwd_rows(const NttIO& io, int c, int l, int b, i
 // d = 4..7 on columns jc + 16 i; the sum of a float64 GS butterfly is reduced
 // every other stage and every phase ends with a full reduction
 // ---------------------------------------------------------------------------
-template <class A>
+template <class A, int LOGN>
 __device__ __forceinline__ void inv_rows(const NttIO& io, int c, int l, int b, int tile, const A& ar,
                                          __amdgpu_buffer_rsrc_t tw, u64* lds) {
   const int t = threadIdx.x, rr = t >> 4, jc = t & 15;
@@ -172,7 +177,7 @@ __device__ __forceinline__ void inv_rows(const NttIO& io, int c, int l, int b, i
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       if (!((j >> d) & 1))
-        ar.gs(a[j], a[j | (1 << d)], ar.tw(tw, (1 << (14 - d)) + ((row << (7 - d)) | ((16 * jc + j) >> (d + 1))), 0),
+        ar.gs(a[j], a[j | (1 << d)], ar.tw(tw, (1 << (LOGN - 1 - d)) + ((row << (7 - d)) | ((16 * jc + j) >> (d + 1))), 0),
               (d & 1) == 1);
   }
   reduce16<A>(a, ar);
@@ -187,7 +192,7 @@ __device__ __forceinline__ void inv_rows(const NttIO& io, int c, int l, int b, i
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       if (!((i >> k) & 1))
-        ar.gs(a[i], a[i | (1 << k)], ar.tw(tw, (1 << (14 - d)) + ((row << (7 - d)) | (i >> (k + 1))), 0),
+        ar.gs(a[i], a[i | (1 << k)], ar.tw(tw, (1 << (LOGN - 1 - d)) + ((row << (7 - d)) | (i >> (k + 1))), 0),
               (k & 1) == 1);
   }
   reduce16<A>(a, ar);
@@ -196,129 +201,155 @@ __device__ __forceinline__ void inv_rows(const NttIO& io, int c, int l, int b, i
   for (int i = 0; i < 16; ++i) mid[jc + 16 * i] = to_bits(a[i]);
 }
 
-// inverse, cols pass (second): stages d = 8..10 (rows 8 (rg + 8 g) + j), then
-// d = 11..14 (rows rg + 8 i, wave-uniform twiddles), times N^-1
-template <class A>
+// inverse, cols pass (second): stages d = 8..LOGN-5 (rows J (rg + RG g) + j),
+// then d = LOGN-4..LOGN-1 (rows rg + RG i, wave-uniform twiddles), times N^-1
+template <class A, int LOGN>
 __device__ __forceinline__ void inv_cols(const NttIO& io, int c, int l, int b, int tile, const A& ar,
                                          __amdgpu_buffer_rsrc_t tw, u64* lds) {
+  constexpr int R = LOGN - 8, RG = 1 << (R - 4), J = 1 << (R - 4), G = 16 / J;
   const int t = threadIdx.x, cl = t & 15, rg = t >> 4;
   const int col = tile * 16 + cl;
   typename A::T a[16];
   const u64* mid = row_ptr(io.mid, c, l, b);
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
+  for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) a[j + 8 * g] = from_bits<typename A::T>(mid[col + ((8 * (rg + 8 * g) + j) << 8)]);
+    for (int j = 0; j < J; ++j) a[j + J * g] = from_bits<typename A::T>(mid[col + ((J * (rg + RG * g) + j) << 8)]);
 #pragma unroll
-  for (int bb = 0; bb < 3; ++bb) {  // d = 8 + bb
+  for (int bb = 0; bb <= R - 5; ++bb) {  // d = 8 + bb
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < G; ++g)
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
+      for (int j = 0; j < J; ++j)
         if (!((j >> bb) & 1)) {
-          const int r = 8 * (rg + 8 * g) + j;
-          ar.gs(a[j + 8 * g], a[(j | (1 << bb)) + 8 * g], ar.tw(tw, (1 << (6 - bb)) + (r >> (bb + 1)), 0),
+          const int r = J * (rg + RG * g) + j;
+          ar.gs(a[j + J * g], a[(j | (1 << bb)) + J * g], ar.tw(tw, (1 << (R - 1 - bb)) + (r >> (bb + 1)), 0),
                 (bb & 1) == 1);
         }
   }
   reduce16<A>(a, ar);
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
+  for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) lds[(8 * (rg + 8 * g) + j) * A_STRIDE + cl] = to_bits(a[j + 8 * g]);
+    for (int j = 0; j < J; ++j) lds[(J * (rg + RG * g) + j) * A_STRIDE + cl] = to_bits(a[j + J * g]);
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 16; ++i) a[i] = from_bits<typename A::T>(lds[(rg + 8 * i) * A_STRIDE + cl]);
+  for (int i = 0; i < 16; ++i) a[i] = from_bits<typename A::T>(lds[(rg + RG * i) * A_STRIDE + cl]);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {  // d = 11 + k
+  for (int k = 0; k < 4; ++k) {  // d = LOGN-4+k
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       if (!((i >> k) & 1)) ar.gs(a[i], a[i | (1 << k)], ar.tw(tw, 0, (1 << (3 - k)) + (i >> (k + 1))), (k & 1) == 1);
   }
   u64* dst = row_ptr(io.dst, c, l, b);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) dst[col + ((rg + 8 * i) << 8)] = ar.final_inv(a[i]);
+  for (int i = 0; i < 16; ++i) dst[col + ((rg + RG * i) << 8)] = ar.final_inv(a[i]);
 }
 
 // ---------------------------------------------------------------------------
-// kernels: blockIdx.x = job * tiles + tile (the tiles of one limb are adjacent)
+// kernels: blockIdx.x = job * tiles + tile (the tiles of one limb are adjacent);
+// cols pass: 16 tiles of 16 columns, 16 * 2^(LOGN-12) threads; rows pass:
+// 2^(LOGN-12) tiles of 16 rows, 256 threads
 // ---------------------------------------------------------------------------
-template <int PRO>
-__global__ void __launch_bounds__(128) ntt2_fwd_cols(NttIO io, const DeviceTables* __restrict__ tb) {
-  __shared__ u64 lds[128 * A_STRIDE];
+template <int LOGN>
+struct N2 {
+  static constexpr int R = LOGN - 8, ATHREADS = 16 << (R - 4), BTILES = 1 << (R - 4);
+};
+
+template <int LOGN, int PRO>
+__global__ void __launch_bounds__(N2<LOGN>::ATHREADS) ntt2_fwd_cols(NttIO io, const DeviceTables* __restrict__ tb) {
+  __shared__ u64 lds[(1 << N2<LOGN>::R) * A_STRIDE];
   int c, l, b;
   job_of(io, blockIdx.x >> 4, c, l, b);
   const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
   const ModConst mc = tb->mc[mod];
   const bool lazy = mc.bar_k <= 41;
   if (mc.f64)
-    fwd_cols<F64Arith, PRO>(io, c, l, b, blockIdx.x & 15, mc, F64Arith(mc), twr(tb->fwd_d[mod], (1 << LN) * 8), lds, lazy, tb);
+    fwd_cols<F64Arith, LOGN, PRO>(io, c, l, b, blockIdx.x & 15, mc, F64Arith(mc), twr(tb->fwd_d[mod], (8 << LOGN)),
+                                  lds, lazy, tb);
   else
-    fwd_cols<IntArith, PRO>(io, c, l, b, blockIdx.x & 15, mc, IntArith(mc), twr(tb->fwd[mod], (1 << LN) * 16), lds, true, tb);
+    fwd_cols<IntArith, LOGN, PRO>(io, c, l, b, blockIdx.x & 15, mc, IntArith(mc), twr(tb->fwd[mod], (16 << LOGN)),
+                                  lds, true, tb);
 }
 
-template <int EPI>
+template <int LOGN, int EPI>
 __global__ void __launch_bounds__(256) ntt2_fwd_rows(NttIO io, const DeviceTables* __restrict__ tb) {
   __shared__ u64 lds[16 * B_STRIDE];
+  constexpr int T = N2<LOGN>::BTILES;
   int c, l, b;
-  job_of(io, blockIdx.x >> 3, c, l, b);
+  job_of(io, blockIdx.x / T, c, l, b);
   const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
   const ModConst mc = tb->mc[mod];
   if (mc.f64)
-    fwd_rows<F64Arith, EPI>(io, c, l, b, blockIdx.x & 7, mc, F64Arith(mc), twr(tb->fwd_d[mod], (1 << LN) * 8), lds, mc.bar_k <= 41);
+    fwd_rows<F64Arith, LOGN, EPI>(io, c, l, b, blockIdx.x % T, mc, F64Arith(mc), twr(tb->fwd_d[mod], (8 << LOGN)),
+                                  lds, mc.bar_k <= 41);
   else
-    fwd_rows<IntArith, EPI>(io, c, l, b, blockIdx.x & 7, mc, IntArith(mc), twr(tb->fwd[mod], (1 << LN) * 16), lds, true);
+    fwd_rows<IntArith, LOGN, EPI>(io, c, l, b, blockIdx.x % T, mc, IntArith(mc), twr(tb->fwd[mod], (16 << LOGN)),
+                                  lds, true);
 }
 
+template <int LOGN>
 __global__ void __launch_bounds__(256) ntt2_inv_rows(NttIO io, const DeviceTables* __restrict__ tb) {
   __shared__ u64 lds[16 * B_STRIDE];
+  constexpr int T = N2<LOGN>::BTILES;
   int c, l, b;
-  job_of(io, blockIdx.x >> 3, c, l, b);
+  job_of(io, blockIdx.x / T, c, l, b);
   const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
   const ModConst mc = tb->mc[mod];
   if (mc.f64)
-    inv_rows<F64Arith>(io, c, l, b, blockIdx.x & 7, F64Arith(mc), twr(tb->inv_d[mod], (1 << LN) * 8), lds);
+    inv_rows<F64Arith, LOGN>(io, c, l, b, blockIdx.x % T, F64Arith(mc), twr(tb->inv_d[mod], (8 << LOGN)), lds);
   else
-    inv_rows<IntArith>(io, c, l, b, blockIdx.x & 7, IntArith(mc), twr(tb->inv[mod], (1 << LN) * 16), lds);
+    inv_rows<IntArith, LOGN>(io, c, l, b, blockIdx.x % T, IntArith(mc), twr(tb->inv[mod], (16 << LOGN)), lds);
 }
 
-__global__ void __launch_bounds__(128) ntt2_inv_cols(NttIO io, const DeviceTables* __restrict__ tb) {
-  __shared__ u64 lds[128 * A_STRIDE];
+template <int LOGN>
+__global__ void __launch_bounds__(N2<LOGN>::ATHREADS) ntt2_inv_cols(NttIO io, const DeviceTables* __restrict__ tb) {
+  __shared__ u64 lds[(1 << N2<LOGN>::R) * A_STRIDE];
   int c, l, b;
   job_of(io, blockIdx.x >> 4, c, l, b);
   const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
   const ModConst mc = tb->mc[mod];
   if (mc.f64)
-    inv_cols<F64Arith>(io, c, l, b, blockIdx.x & 15, F64Arith(mc), twr(tb->inv_d[mod], (1 << LN) * 8), lds);
+    inv_cols<F64Arith, LOGN>(io, c, l, b, blockIdx.x & 15, F64Arith(mc), twr(tb->inv_d[mod], (8 << LOGN)), lds);
   else
-    inv_cols<IntArith>(io, c, l, b, blockIdx.x & 15, IntArith(mc), twr(tb->inv[mod], (1 << LN) * 16), lds);
+    inv_cols<IntArith, LOGN>(io, c, l, b, blockIdx.x & 15, IntArith(mc), twr(tb->inv[mod], (16 << LOGN)), lds);
+}
+
+template <int LOGN>
+int launch2(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
+  const int jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
+  if (jobs == 0) return 0;
+  if (io.jobs != jobs) return -1;
+  const dim3 ga(jobs * 16), ba(N2<LOGN>::ATHREADS), gb(jobs * N2<LOGN>::BTILES), bb(256);
+  if (inverse) {
+    if (io.pro != NTT_PRO_LOAD || io.epi != NTT_EPI_STORE) return -1;
+    hipLaunchKernelGGL(ntt2_inv_rows<LOGN>, gb, bb, 0, st, io, tb);
+    hipLaunchKernelGGL(ntt2_inv_cols<LOGN>, ga, ba, 0, st, io, tb);
+    return 0;
+  }
+  if (io.pro == NTT_PRO_LOAD)
+    hipLaunchKernelGGL((ntt2_fwd_cols<LOGN, NTT_PRO_LOAD>), ga, ba, 0, st, io, tb);
+  else if (io.pro == NTT_PRO_RESCALE)
+    hipLaunchKernelGGL((ntt2_fwd_cols<LOGN, NTT_PRO_RESCALE>), ga, ba, 0, st, io, tb);
+  else
+    return -1;
+  if (io.epi == NTT_EPI_STORE)
+    hipLaunchKernelGGL((ntt2_fwd_rows<LOGN, NTT_EPI_STORE>), gb, bb, 0, st, io, tb);
+  else if (io.epi == NTT_EPI_SUBSCALE)
+    hipLaunchKernelGGL((ntt2_fwd_rows<LOGN, NTT_EPI_SUBSCALE>), gb, bb, 0, st, io, tb);
+  else
+    return -1;
+  return 0;
 }
 
 }  // namespace
 
 // host entry: two launches on stream st; io.mid must have dst's geometry and
 // must not alias io.ex (the epilogue reads ex after the first pass wrote mid)
-int orion_launch_ntt2(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
-  const int jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
-  if (jobs == 0) return 0;
-  if (io.jobs != jobs) return -1;
-  if (inverse) {
-    if (io.pro != NTT_PRO_LOAD || io.epi != NTT_EPI_STORE) return -1;
-    hipLaunchKernelGGL(ntt2_inv_rows, dim3(jobs * 8), dim3(256), 0, st, io, tb);
-    hipLaunchKernelGGL(ntt2_inv_cols, dim3(jobs * 16), dim3(128), 0, st, io, tb);
-    return 0;
+int orion_launch_ntt2(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
+  switch (logN) {
+    case 15: return launch2<15>(io, tb, inverse, st);
+    case 16: return launch2<16>(io, tb, inverse, st);
+    default: return -1;
   }
-  if (io.pro == NTT_PRO_LOAD)
-    hipLaunchKernelGGL(ntt2_fwd_cols<NTT_PRO_LOAD>, dim3(jobs * 16), dim3(128), 0, st, io, tb);
-  else if (io.pro == NTT_PRO_RESCALE)
-    hipLaunchKernelGGL(ntt2_fwd_cols<NTT_PRO_RESCALE>, dim3(jobs * 16), dim3(128), 0, st, io, tb);
-  else
-    return -1;
-  if (io.epi == NTT_EPI_STORE)
-    hipLaunchKernelGGL(ntt2_fwd_rows<NTT_EPI_STORE>, dim3(jobs * 8), dim3(256), 0, st, io, tb);
-  else if (io.epi == NTT_EPI_SUBSCALE)
-    hipLaunchKernelGGL(ntt2_fwd_rows<NTT_EPI_SUBSCALE>, dim3(jobs * 8), dim3(256), 0, st, io, tb);
-  else
-    return -1;
-  return 0;
 }

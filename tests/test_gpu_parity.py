@@ -28,7 +28,7 @@ def small(torch_cuda, oracle_mod):
     return lib, orc
 
 
-@pytest.mark.parametrize("logn", [13, 14, 15])
+@pytest.mark.parametrize("logn", [13, 14, 15, 16])
 def test_ntt_roundtrip_and_parity(torch_cuda, oracle_mod, logn):
     torch = torch_cuda
     from orion_amd.backend import HipLibrary
@@ -214,3 +214,45 @@ def _galois_elements(st):
         if ev["phase"] == "forward" and ev["op"] in ("RotateNew", "Rotate"):
             gels.add(int(lib.GaloisElement(ev["args"][1])))
     return sorted(gels)
+
+
+def test_n16_ops_parity(torch_cuda, oracle_mod):
+    """N = 2^16 (BASELINE config C4's ring degree; its NTT is the two-pass
+    kernel): mul_relin, rotate and rescale bit-exact vs the oracle."""
+    from orion_amd.backend import HipLibrary
+    logq, logp = [60, 40, 40, 40], [60, 60]
+    lib = HipLibrary().new_scheme(16, logq, logp, 40, h=192, seed=77)
+    mods = lib.moduli()
+    orc = oracle_mod.Oracle(16, mods, len(logq), len(logp))
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    rng = np.random.default_rng(16)
+    level = 3
+    a = rand_ct(rng, mods, level, orc.N, B=2)
+    b = rand_ct(rng, mods, level, orc.N, B=2)
+    ca, cb = lib.import_ciphertext(a, 2.0 ** 40), lib.import_ciphertext(b, 2.0 ** 40)
+    cc = lib.MulRelinCiphertextNew(ca, cb)
+    got = lib.export_ciphertext(cc)
+    rlk = lib.export_relin_key()
+    ref = [orc.mul_relin(a[i], b[i], rlk, level) for i in range(2)]
+    for i in range(2):
+        assert np.array_equal(got[i], ref[i]), i
+    g = int(lib.GaloisElement(3))
+    cr = lib.RotateNew(cc, 3)
+    gk = lib.export_galois_key(g)
+    rot = lib.export_ciphertext(cr)
+    for i in range(2):
+        assert np.array_equal(rot[i], orc.rotate(ref[i], g, gk, level)), i
+    lib.Rescale(cr)
+    res = lib.export_ciphertext(cr)
+    for i in range(2):
+        assert np.array_equal(res[i], orc.rescale(rot[i], level)), i
+    # functional: encode -> encrypt -> square -> decrypt at N = 2^16
+    vals = rng.standard_normal(orc.N // 2).astype(np.float32)
+    ct = lib.Encrypt(lib.Encode(list(vals), level, 1 << 40))
+    sq = lib.MulRelinCiphertextNew(ct, ct)
+    lib.Rescale(sq)
+    dec = np.array(lib.Decode(lib.Decrypt(sq)))
+    assert np.abs(dec - vals.astype(np.float64) ** 2).max() < 1e-3
+    lib.DeleteScheme()
