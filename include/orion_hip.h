@@ -157,12 +157,25 @@ int GetCiphertextBatch(int ct);
 int GetPlaintextBatch(int pt);
 double GetCiphertextScaleF(int ct);                       /* exact-ish scale (long double -> double) */
 
+/* GPU encoder with device-resident slots (e.g. a torch tensor's data_ptr):
+ * dvalues [batch][lenPerImage] float32; DecodeDevice writes the real parts of
+ * all slots, [batch][N/2] float64, to device memory (asynchronous);
+ * DecodeF64 returns them to the host as float64 (Decode casts to float32) */
+int EncodeBatchDevice(const float *dvalues, int lenPerImage, int batch, int level, double scale);
+int DecodeDevice(int pt, double *dout);
+int DecodeF64(int pt, double *out, unsigned long n);
+/* encryption randomness: ChaCha20 stream keyed from the seed (OrionHipSetSeed
+ * / NewScheme), nonce = (encryption index, image, component); the index counts
+ * Encrypt calls since the last seeding */
+unsigned int OrionHipEncryptionIndex(void);
+
 /* host import/export, canonical host layout [batch][comp][limb][N] (NTT) */
 int ImportCiphertext(const unsigned long *data, int batch, int level, double scale);
 int ExportCiphertext(int ct, unsigned long *out, unsigned long n);
 int ImportPlaintext(const unsigned long *data, int batch, int level, double scale);
 int ExportPlaintext(int pt, unsigned long *out, unsigned long n);
 int ExportSecretKey(unsigned long *out, unsigned long n);                  /* [L+K][N]           */
+int ExportPublicKey(unsigned long *out, unsigned long n);                  /* [2][L+K][N]        */
 int ExportRelinKey(unsigned long *out, unsigned long n);                   /* [dnum][2][L+K][N]  */
 int ExportGaloisKey(unsigned long galEl, unsigned long *out, unsigned long n);
 int ExportLinearTransformDiagonal(int lt, int diagIdx, unsigned long *out, unsigned long n); /* [lvl+1+K][N] */

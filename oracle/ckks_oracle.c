@@ -833,6 +833,19 @@ static void to_crt(double v, double scale, const oracle_ctx *c, const int *mods,
   }
   int neg = v < 0;
   double x = neg ? v * (-scale) : v * scale;
+  if (!(x < 18446744073709551616.0)) {
+    /* |v*scale| >= 2^64: Lattigo's big.Int path.  x is an integer
+     * mant * 2^e (e > 11); reduce it exactly. */
+    int ex;
+    double fr = frexp(x, &ex);
+    u64 mant = (u64)ldexp(fr, 53);
+    for (int m = 0; m < nm; m++) {
+      u64 q = c->mod[mods[m]];
+      u64 r = mulmod(mant % q, powmod(2 % q, (u64)(ex - 53), q), q);
+      out[m * stride] = neg ? (r ? q - r : 0) : r;
+    }
+    return;
+  }
   u64 cval = (u64)(x + 0.5);
   for (int m = 0; m < nm; m++) {
     u64 q = c->mod[mods[m]];
@@ -1059,5 +1072,120 @@ void oracle_decrypt(const oracle_ctx *c, int level, const u64 *sk, const u64 *ct
       size_t x = (size_t)j * N + n;
       pt[x] = addmod(ct[x], mulmod(ct[P + x], sk[x], q), q);
     }
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* public-key encryption sampler of the MI355X backend (encoder.hip),  */
+/* restated: ChaCha20 (RFC 8439 §2.3) counter-mode stream per          */
+/* (encryption index, image, component), uniform ternary u and a       */
+/* cumulative-table discrete Gaussian (sigma 3.2, |e| <= 19).          */
+/* ------------------------------------------------------------------ */
+static inline uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+#define QR(a, b, c, d)                          \
+  do {                                          \
+    a += b; d ^= a; d = rotl32(d, 16);          \
+    c += d; b ^= c; b = rotl32(b, 12);          \
+    a += b; d ^= a; d = rotl32(d, 8);           \
+    c += d; b ^= c; b = rotl32(b, 7);           \
+  } while (0)
+
+void oracle_chacha20_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3],
+                           uint32_t out[16]) {
+  uint32_t st[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+  for (int i = 0; i < 8; i++) st[4 + i] = key[i];
+  st[12] = counter;
+  for (int i = 0; i < 3; i++) st[13 + i] = nonce[i];
+  uint32_t x[16];
+  memcpy(x, st, sizeof(x));
+  for (int r = 0; r < 10; r++) {
+    QR(x[0], x[4], x[8], x[12]);
+    QR(x[1], x[5], x[9], x[13]);
+    QR(x[2], x[6], x[10], x[14]);
+    QR(x[3], x[7], x[11], x[15]);
+    QR(x[0], x[5], x[10], x[15]);
+    QR(x[1], x[6], x[11], x[12]);
+    QR(x[2], x[7], x[8], x[13]);
+    QR(x[3], x[4], x[9], x[14]);
+  }
+  for (int i = 0; i < 16; i++) out[i] = x[i] + st[i];
+}
+#undef QR
+
+void oracle_enc_key(u64 seed, uint32_t key[8]) {
+  u64 z = seed ^ 0x6a09e667f3bcc909ull;
+  for (int i = 0; i < 4; i++) {
+    u64 t = (z += 0x9E3779B97F4A7C15ull);
+    t = (t ^ (t >> 30)) * 0xBF58476D1CE4E5B9ull;
+    t = (t ^ (t >> 27)) * 0x94D049BB133111EBull;
+    t ^= t >> 31;
+    key[2 * i] = (uint32_t)t;
+    key[2 * i + 1] = (uint32_t)(t >> 32);
+  }
+}
+
+#define GAUSS_BOUND 19
+void oracle_gauss_cdt(double sigma, int bound, u64 *t) {
+  double rho[2 * 64 + 1], sum = 0.0, acc = 0.0;
+  for (int x = -bound; x <= bound; x++) {
+    rho[x + bound] = exp(-(double)(x * x) / (2.0 * sigma * sigma));
+    sum += rho[x + bound];
+  }
+  for (int i = 0; i < 2 * bound; i++) {
+    acc += rho[i];
+    double cv = ldexp(acc / sum, 64);
+    t[i] = cv >= 18446744073709551616.0 ? ~0ull : (u64)cv;
+  }
+}
+
+/* component comp (0 = u, 1 = e0, 2 = e1) of image `image` of encryption `enc` */
+void oracle_enc_sample(int N, const uint32_t key[8], uint32_t enc, uint32_t image, int comp,
+                       int64_t *out) {
+  u64 cdt[2 * GAUSS_BOUND];
+  oracle_gauss_cdt(3.2, GAUSS_BOUND, cdt);
+  const uint32_t nonce[3] = {enc, image, 0x454e0000u | (uint32_t)comp};
+  uint32_t w[16];
+  for (int blk = 0; blk < N / 8; blk++) {
+    oracle_chacha20_block(key, (uint32_t)blk, nonce, w);
+    for (int k = 0; k < 8; k++) {
+      u64 x = (u64)w[2 * k] | ((u64)w[2 * k + 1] << 32);
+      int64_t v;
+      if (comp == 0) {
+        v = (int64_t)(((x >> 32) * 3) >> 32) - 1;
+      } else {
+        int cnt = 0;
+        for (int t = 0; t < 2 * GAUSS_BOUND; t++) cnt += x >= cdt[t];
+        v = cnt - GAUSS_BOUND;
+      }
+      out[blk * 8 + k] = v;
+    }
+  }
+}
+
+/* c0 = u pk0 + e0 + pt, c1 = u pk1 + e1 at `level` (pk: [2][L+K][N] NTT) */
+void oracle_encrypt_pk(const oracle_ctx *c, const uint32_t key[8], uint32_t enc, uint32_t image,
+                       int level, const u64 *pk, const u64 *pt, u64 *ct) {
+  const int N = c->N, LK = c->L + c->K;
+  const size_t P = (size_t)(level + 1) * N;
+  int64_t *smp[3];
+  u64 *t[3];
+  for (int k = 0; k < 3; k++) {
+    smp[k] = (int64_t *)malloc(sizeof(int64_t) * N);
+    t[k] = (u64 *)malloc(sizeof(u64) * N);
+    oracle_enc_sample(N, key, enc, image, k, smp[k]);
+  }
+  for (int j = 0; j <= level; j++) {
+    u64 q = c->mod[j];
+    for (int k = 0; k < 3; k++) small_to_ntt(c, smp[k], j, t[k]);
+    for (int n = 0; n < N; n++) {
+      size_t x = (size_t)j * N + n;
+      u64 pk0 = pk[(size_t)j * N + n], pk1 = pk[(size_t)(LK + j) * N + n];
+      ct[x] = addmod(addmod(mulmod(t[0][n], pk0, q), t[1][n], q), pt[x], q);
+      ct[P + x] = addmod(mulmod(t[0][n], pk1, q), t[2][n], q);
+    }
+  }
+  for (int k = 0; k < 3; k++) {
+    free(smp[k]);
+    free(t[k]);
   }
 }

@@ -130,6 +130,21 @@ void oracle_encrypt_sk(const oracle_ctx *ctx, uint64_t seed, int level,
 void oracle_decrypt(const oracle_ctx *ctx, int level, const uint64_t *sk,
                     const uint64_t *ct, uint64_t *pt);
 
+/* ---- public-key encryption sampler of the HIP backend (encoder.hip) ----
+ * ChaCha20 block function (RFC 8439 §2.3); key from the scheme seed;
+ * discrete Gaussian cumulative table (2 bound entries); samples of one
+ * component (0 = u ternary, 1 = e0, 2 = e1) of one image; and
+ * c0 = u pk0 + e0 + pt, c1 = u pk1 + e1 (pk: [2][L+K][N], ct: [2][level+1][N]). */
+void oracle_chacha20_block(const uint32_t key[8], uint32_t counter,
+                           const uint32_t nonce[3], uint32_t out[16]);
+void oracle_enc_key(uint64_t seed, uint32_t key[8]);
+void oracle_gauss_cdt(double sigma, int bound, uint64_t *t);
+void oracle_enc_sample(int N, const uint32_t key[8], uint32_t enc, uint32_t image,
+                       int comp, int64_t *out);
+void oracle_encrypt_pk(const oracle_ctx *ctx, const uint32_t key[8], uint32_t enc,
+                       uint32_t image, int level, const uint64_t *pk,
+                       const uint64_t *pt, uint64_t *ct);
+
 /* coefficient-wise helpers used by tests */
 void oracle_mul_coeffs(const oracle_ctx *ctx, const int *mods, int nl,
                        const uint64_t *a, const uint64_t *b, uint64_t *out);

@@ -19,6 +19,7 @@ _LIB_PATH = os.path.join(_HERE, "build", "libckks_oracle.so")
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 _intp = ctypes.POINTER(ctypes.c_int)
 _dblp = ctypes.POINTER(ctypes.c_double)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
 
 
 def build():
@@ -58,6 +59,13 @@ def _load():
         "oracle_encrypt_sk": (None, [vp, ctypes.c_uint64, ctypes.c_int, _u64p, _u64p, _u64p]),
         "oracle_decrypt": (None, [vp, ctypes.c_int, _u64p, _u64p, _u64p]),
         "oracle_mul_coeffs": (None, [vp, _intp, ctypes.c_int, _u64p, _u64p, _u64p]),
+        "oracle_chacha20_block": (None, [_u32p, ctypes.c_uint32, _u32p, _u32p]),
+        "oracle_enc_key": (None, [ctypes.c_uint64, _u32p]),
+        "oracle_gauss_cdt": (None, [ctypes.c_double, ctypes.c_int, _u64p]),
+        "oracle_enc_sample": (None, [ctypes.c_int, _u32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                     ctypes.POINTER(ctypes.c_int64)]),
+        "oracle_encrypt_pk": (None, [vp, _u32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, _u64p, _u64p,
+                                     _u64p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -247,3 +255,43 @@ class Oracle:
         out = np.zeros_like(a)
         lib().oracle_mul_coeffs(self._h, _ip(mods), len(mods), _p(a), _p(b), _p(out))
         return out
+
+    def encrypt_pk(self, seed, enc, image, pk, pt, level):
+        """The HIP backend's public-key encryption of image `image` in
+        encryption number `enc` (encoder.hip sampler, restated)."""
+        ct = np.zeros((2, level + 1, self.N), dtype=np.uint64)
+        lib().oracle_encrypt_pk(self._h, _u32(enc_key(seed)), enc, image, level,
+                                _p(np.ascontiguousarray(pk)), _p(np.ascontiguousarray(pt)), _p(ct))
+        return ct
+
+
+def _u32(a):
+    assert a.dtype == np.uint32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_u32p)
+
+
+def chacha20_block(key, counter, nonce):
+    """RFC 8439 §2.3 block function: 8 key words, counter, 3 nonce words -> 16 words."""
+    out = np.zeros(16, dtype=np.uint32)
+    lib().oracle_chacha20_block(_u32(np.asarray(key, dtype=np.uint32)), counter,
+                                _u32(np.asarray(nonce, dtype=np.uint32)), _u32(out))
+    return out
+
+
+def enc_key(seed):
+    key = np.zeros(8, dtype=np.uint32)
+    lib().oracle_enc_key(seed, _u32(key))
+    return key
+
+
+def gauss_cdt(sigma=3.2, bound=19):
+    t = np.zeros(2 * bound, dtype=np.uint64)
+    lib().oracle_gauss_cdt(sigma, bound, _p(t))
+    return t
+
+
+def enc_sample(N, seed, enc, image, comp):
+    out = np.zeros(N, dtype=np.int64)
+    lib().oracle_enc_sample(N, _u32(enc_key(seed)), enc, image, comp,
+                            out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+    return out

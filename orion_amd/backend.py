@@ -142,6 +142,10 @@ SIGNATURES = {
     "OrionHipNumP": ([], c_int),
     "OrionHipModulus": ([c_int], c_ulong),
     "EncodeBatch": ([P(c_float), c_int, c_int, c_int, c_ulong], c_int),
+    "EncodeBatchDevice": ([c_void_p, c_int, c_int, c_int, c_double], c_int),
+    "DecodeDevice": ([c_int, c_void_p], c_int),
+    "DecodeF64": ([c_int, P(c_double), c_ulong], c_int),
+    "OrionHipEncryptionIndex": ([], ctypes.c_uint),
     "GetCiphertextBatch": ([c_int], c_int),
     "GetPlaintextBatch": ([c_int], c_int),
     "GetCiphertextScaleF": ([c_int], c_double),
@@ -150,6 +154,7 @@ SIGNATURES = {
     "ImportPlaintext": ([P(c_ulong), c_int, c_int, c_double], c_int),
     "ExportPlaintext": ([c_int, P(c_ulong), c_ulong], c_int),
     "ExportSecretKey": ([P(c_ulong), c_ulong], c_int),
+    "ExportPublicKey": ([P(c_ulong), c_ulong], c_int),
     "ExportRelinKey": ([P(c_ulong), c_ulong], c_int),
     "ExportGaloisKey": ([c_ulong, P(c_ulong), c_ulong], c_int),
     "ExportLinearTransformDiagonal": ([c_int, c_int, P(c_ulong), c_ulong], c_int),
@@ -166,8 +171,9 @@ SIGNATURES = {
 
 # the symbols a binding of the reference's Lattigo backend resolves (bindings.py:141-746 + fork extras)
 LATTIGO_SYMBOLS = [n for n in SIGNATURES if not n.startswith("OrionHip") and n not in (
-    "EncodeBatch", "GetCiphertextBatch", "GetPlaintextBatch", "GetCiphertextScaleF", "ImportCiphertext",
-    "ExportCiphertext", "ImportPlaintext", "ExportPlaintext", "ExportSecretKey", "ExportRelinKey",
+    "EncodeBatch", "EncodeBatchDevice", "DecodeDevice", "DecodeF64", "GetCiphertextBatch", "GetPlaintextBatch",
+    "GetCiphertextScaleF", "ImportCiphertext", "ExportCiphertext", "ImportPlaintext", "ExportPlaintext",
+    "ExportSecretKey", "ExportPublicKey", "ExportRelinKey",
     "ExportGaloisKey", "ExportLinearTransformDiagonal", "GetLinearTransformN1", "GaloisElement",
     "KeyBundleBytes", "ExportKeyBundle", "ImportKeyBundle")]
 
@@ -315,6 +321,11 @@ class HipLibrary:
         self._chk(self.lib.ExportSecretKey(out.ctypes.data_as(P(c_ulong)), out.size), "ExportSecretKey")
         return out
 
+    def export_public_key(self):
+        out = np.zeros((2, self.L + self.K, self.N), dtype=np.uint64)
+        self._chk(self.lib.ExportPublicKey(out.ctypes.data_as(P(c_ulong)), out.size), "ExportPublicKey")
+        return out
+
     def _evk_shape(self):
         return ((self.L + self.K - 1) // self.K, 2, self.L + self.K, self.N)
 
@@ -338,6 +349,18 @@ class HipLibrary:
         v = np.ascontiguousarray(values, dtype=np.float32)
         B, n = v.shape
         return self._chk(self.lib.EncodeBatch(v.ctypes.data_as(P(c_float)), n, B, level, int(scale)), "EncodeBatch")
+
+    def encode_batch_device(self, dvalues, level, scale):
+        """dvalues: a contiguous float32 [B][n] device tensor (torch, HBM resident)."""
+        B, n = dvalues.shape
+        return self._chk(self.lib.EncodeBatchDevice(dvalues.data_ptr(), n, B, level, float(scale)),
+                         "EncodeBatchDevice")
+
+    def decode_f64(self, pt):
+        """Slots of every image of a plaintext, float64 [B][N/2] (GPU decode)."""
+        out = np.zeros((self.GetPlaintextBatch(pt), self.N // 2), dtype=np.float64)
+        self._chk(self.lib.DecodeF64(pt, out.ctypes.data_as(P(c_double)), out.size), "DecodeF64")
+        return out
 
     def profile_read(self):
         n = 16

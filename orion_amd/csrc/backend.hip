@@ -42,6 +42,12 @@ int orion_launch_lt_bsgs(const LimbSet& t0, const LimbSet& t1, const LimbSet& D,
 int orion_launch_lt_giant(const LimbSet& acc, const LimbSet& D, const LimbSet& own, const LimbSet& t0,
                           const LimbSet& z, const LtGiants& G, const DeviceTables* tb, int N, hipStream_t st);
 
+int orion_launch_encode(const float* vals, int nvals, int B, double2* v, const double2* tw_inv, int logn,
+                        const LimbSet& out, double scale, const DeviceTables* tb, hipStream_t st);
+int orion_launch_decode(const LimbSet& x, const u64* garner, double scale, int logn, double2* v,
+                        const double2* tw_fwd, double* out, const DeviceTables* tb, hipStream_t st);
+int orion_launch_enc_sample(const LimbSet& r, const EncSampler& sp, const DeviceTables* tb, int N, hipStream_t st);
+
 namespace orion {
 
 enum { EW_ADD = 0, EW_SUB, EW_MUL, EW_MULADD, EW_NEG, EW_SCALE, EW_ADDC, EW_SUBSCALE, EW_COPY, EW_ADDSCALE };
@@ -210,8 +216,10 @@ struct Context {
   DeviceTables host_tb;
   DeviceTables* d_tb = nullptr;
   std::vector<void*> static_bufs;
-  std::unique_ptr<SpecialFFT> fft;
-  Prng prng{0x0123456789abcdefull};
+  double2 *tw_inv = nullptr, *tw_fwd = nullptr;  // special FFT twiddles (encoder.hip)
+  std::map<int, u64*> garner;                     // decode CRT tables per level
+  Prng prng{0x0123456789abcdefull};               // key generation
+  EncSampler enc_sampler;                         // encryption: ChaCha20 key, index, Gaussian table
 
   Poly sk, pk, rlk;
   bool have_sk = false, have_pk = false, have_rlk = false;
@@ -238,6 +246,7 @@ struct Context {
     lts.reset();
     for (auto& kv : autidx) hipFree(kv.second);
     for (auto& kv : betab) hipFree(kv.second);
+    for (auto& kv : garner) hipFree(kv.second);
     for (void* p : static_bufs) hipFree(p);
     if (d_tb) hipFree(d_tb);
     for (auto& r : prof_recs) {
@@ -418,7 +427,6 @@ struct Context {
     for (int b : logP)
       if (b > 61) throw std::runtime_error("moduli must be <= 61 bits");
     mods = gen_moduli(logN, logQ, logP);
-    fft.reset(new SpecialFFT(logN));
     if (!stream) {
       HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
       own_stream = true;
@@ -481,6 +489,21 @@ struct Context {
     }
     HIPCHK(hipMalloc(&d_tb, sizeof(DeviceTables)));
     HIPCHK(hipMemcpy(d_tb, &host_tb, sizeof(DeviceTables), hipMemcpyHostToDevice));
+    for (int inv = 0; inv < 2; ++inv) {
+      const std::vector<Cplx> tw = special_fft_twiddles(logN, inv != 0);
+      void* d;
+      HIPCHK(hipMalloc(&d, tw.size() * sizeof(double2)));
+      HIPCHK(hipMemcpy(d, tw.data(), tw.size() * sizeof(double2), hipMemcpyHostToDevice));
+      static_bufs.push_back(d);
+      (inv ? tw_inv : tw_fwd) = (double2*)d;
+    }
+    memset(&enc_sampler, 0, sizeof(enc_sampler));
+    gauss_cdt(3.2, ORION_GAUSS_BOUND, enc_sampler.cdt);
+  }
+  // encryption randomness: ChaCha20 key from the seed, encryption index 0
+  void seed_encryption(u64 seed) {
+    enc_key_from_seed(seed, enc_sampler.key);
+    enc_sampler.enc = 0;
   }
 
   u64 prod_mod(const std::vector<int>& src, int skip, u64 t) const {
@@ -614,11 +637,6 @@ struct Context {
       std::swap(perm[i], perm[j]);
       s[perm[i]] = (prng.next() & 1) ? 1 : -1;
     }
-    return s;
-  }
-  std::vector<int64_t> sample_ternary_uniform() {
-    std::vector<int64_t> s(N);
-    for (auto& x : s) x = (int64_t)(prng.next() % 3) - 1;
     return s;
   }
   std::vector<u64> qp_mod_list() const {
@@ -1092,120 +1110,88 @@ struct Context {
   // ---------------------------------------------------------------------------
   // encoder / encryptor
   // ---------------------------------------------------------------------------
-  // values: B images x nvals; mods: QP modulus index of each limb
-  Plaintext encode(const float* values, int nvals, int B, int level, long double scale, bool qp) {
+  // values: B images x nvals float32 slots, device memory (encoder.hip);
+  // limbs Q 0..level (+ P when qp)
+  Plaintext encode_dev(const float* dvals, int nvals, int B, int level, long double scale, bool qp) {
     const int n = N / 2;
     if (nvals > n) throw std::runtime_error("too many values for the slot count");
     std::vector<int> md = iota(0, level + 1);
     if (qp)
       for (int k = 0; k < K; ++k) md.push_back(L + k);
-    std::vector<u64> mv;
-    for (int m : md) mv.push_back(mods[m]);
     const int nl = (int)md.size();
     Plaintext pt;
     pt.level = level;
     pt.scale = scale;
     pt.qp = qp;
     pt.poly = alloc(1, nl, B);
-    std::vector<u64> host((size_t)nl * B * N);
-    std::vector<Cplx> v(n);
-    for (int b = 0; b < B; ++b) {
-      for (int i = 0; i < n; ++i) v[i] = Cplx{i < nvals ? (double)values[(size_t)b * nvals + i] : 0.0, 0.0};
-      fft->inverse(v);
-      for (int i = 0; i < n; ++i) {
-        fixed_point_crt(v[i].re, (double)scale, mv.data(), nl, host.data() + (size_t)b * N + i, (size_t)B * N);
-        fixed_point_crt(v[i].im, (double)scale, mv.data(), nl, host.data() + (size_t)b * N + i + n, (size_t)B * N);
-      }
-    }
-    upload(pt.poly, host);
-    ntt(ls(pt.poly, 0, 1, iota(0, nl), md), false);
+    Buffer v(&pool, (size_t)B * n * sizeof(double2));
+    const LimbSet out = ls(pt.poly, 0, 1, iota(0, nl), md);
+    if (orion_launch_encode(dvals, nvals, B, (double2*)v.p, tw_inv, logN - 1, out, (double)scale, d_tb, stream))
+      throw std::runtime_error("encode launch failed");
+    ntt(out, false);
     return pt;
   }
+  Plaintext encode(const float* values, int nvals, int B, int level, long double scale, bool qp) {
+    if (nvals > N / 2) throw std::runtime_error("too many values for the slot count");
+    Buffer dv(&pool, (size_t)B * nvals * sizeof(float) + 16);
+    HIPCHK(hipMemcpyAsync(dv.p, values, (size_t)B * nvals * sizeof(float), hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    return encode_dev((const float*)dv.p, nvals, B, level, scale, qp);
+  }
 
-  std::vector<float> decode(const Plaintext& pt) {
-    const int level = pt.level, B = pt.poly.B, n = N / 2, nl = level + 1;
+  // Garner table of `level`: inv[j][k] = (q_k mod q_j)^-1 mod q_j, then the
+  // mixed-radix digits of floor((Q - 1) / 2)
+  const u64* garner_table(int level) {
+    auto it = garner.find(level);
+    if (it != garner.end()) return it->second;
+    const int nl = level + 1;
+    std::vector<u64> t((size_t)nl * nl + nl, 0);
+    for (int j = 0; j < nl; ++j)
+      for (int k = 0; k < j; ++k) t[(size_t)j * nl + k] = hm_invmod(mods[k] % mods[j], mods[j]);
+    u64 rem = 0;
+    for (int j = nl - 1; j >= 0; --j) {
+      const u128 cur = (u128)rem * mods[j] + (mods[j] - 1);
+      t[(size_t)nl * nl + j] = (u64)(cur / 2);
+      rem = (u64)(cur % 2);
+    }
+    u64* d;
+    HIPCHK(hipMalloc(&d, t.size() * sizeof(u64)));
+    HIPCHK(hipMemcpy(d, t.data(), t.size() * sizeof(u64), hipMemcpyHostToDevice));
+    garner[level] = d;
+    return d;
+  }
+  // slots (real parts) of every image into device memory out[B][N/2]
+  void decode_dev(const Plaintext& pt, double* out) {
+    const int level = pt.level, B = pt.poly.B, nl = level + 1;
+    if (nl > ORION_MAXLIMB) throw std::runtime_error("decode: too many limbs");
     Poly t = alloc(1, nl, B);
-    copy(lsq(t, 0, 1, level), lsq(pt.poly, 0, 1, level));
-    ntt(lsq(t, 0, 1, level), true);
-    std::vector<u64> host;
-    download(t, host);
-    // Garner constants
-    std::vector<std::vector<u64>> inv(nl, std::vector<u64>(nl));
-    for (int i = 0; i < nl; ++i)
-      for (int k = 0; k < i; ++k) inv[i][k] = hm_invmod(mods[k] % mods[i], mods[i]);
-    std::vector<u64> half(nl);
-    {
-      u64 rem = 0;
-      for (int i = nl - 1; i >= 0; --i) {
-        u128 cur = (u128)rem * mods[i] + (mods[i] - 1);
-        half[i] = (u64)(cur / 2);
-        rem = (u64)(cur % 2);
-      }
-    }
-    std::vector<float> out((size_t)B * n);
-    std::vector<Cplx> v(n);
-    std::vector<u64> d(nl), e(nl);
-    for (int b = 0; b < B; ++b) {
-      for (int i = 0; i < N; ++i) {
-        for (int j = 0; j < nl; ++j) {
-          u64 x = host[((size_t)j * B + b) * N + i];
-          for (int k = 0; k < j; ++k) {
-            const u64 qj = mods[j];
-            x = hm_mulmod((x + qj - d[k] % qj) % qj, inv[j][k], qj);
-          }
-          d[j] = x;
-        }
-        bool greater = false;
-        for (int j = nl - 1; j >= 0; --j)
-          if (d[j] != half[j]) {
-            greater = d[j] > half[j];
-            break;
-          }
-        long double val = 0, base = 1;
-        if (!greater) {
-          for (int j = 0; j < nl; ++j) val += (long double)d[j] * base, base *= (long double)mods[j];
-        } else {
-          for (int j = 0; j < nl; ++j) e[j] = mods[j] - 1 - d[j];
-          for (int j = 0; j < nl; ++j) {
-            if (e[j] + 1 < mods[j]) {
-              e[j] += 1;
-              break;
-            }
-            e[j] = 0;
-          }
-          for (int j = 0; j < nl; ++j) val += (long double)e[j] * base, base *= (long double)mods[j];
-          val = -val;
-        }
-        const double f = (double)(val / pt.scale);
-        if (i < n)
-          v[i].re = f;
-        else
-          v[i - n].im = f;
-      }
-      fft->forward(v);
-      for (int i = 0; i < n; ++i) out[(size_t)b * n + i] = (float)v[i].re;
-    }
+    const LimbSet x = lsq(t, 0, 1, level);
+    ntt_io(nio(x, lsq(pt.poly, 0, 1, level)), true);
+    Buffer v(&pool, (size_t)B * (N / 2) * sizeof(double2));
+    if (orion_launch_decode(x, garner_table(level), (double)pt.scale, logN - 1, (double2*)v.p, tw_fwd, out, d_tb,
+                            stream))
+      throw std::runtime_error("decode launch failed");
+  }
+  std::vector<double> decode(const Plaintext& pt) {
+    const size_t cnt = (size_t)pt.poly.B * (N / 2);
+    Buffer d(&pool, cnt * sizeof(double));
+    decode_dev(pt, (double*)d.p);
+    std::vector<double> out(cnt);
+    HIPCHK(hipMemcpyAsync(out.data(), d.p, cnt * sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
     return out;
   }
 
+  // public-key encryption (Lattigo rlwe Encryptor.EncryptZero + pt):
+  // c0 = u pk0 + e0 + m, c1 = u pk1 + e1; u, e0, e1 sampled on the GPU
   Ciphertext encrypt(const Plaintext& pt) {
     if (!have_pk) throw std::runtime_error("public key not generated");
-    const int level = pt.level, B = pt.poly.B, nl = level + 1;
-    // u (ternary), e0, e1 per image, coefficient domain -> NTT
-    Poly r = alloc(3, nl, B);
-    std::vector<u64> host((size_t)3 * nl * B * N);
-    std::vector<int> md = iota(0, nl);
-    std::vector<u64> blk((size_t)nl * N);
-    for (int c = 0; c < 3; ++c) {
-      for (int b = 0; b < B; ++b) {
-        auto v = c == 0 ? sample_ternary_uniform() : sample_gauss();
-        small_residues(v, md, blk.data());
-        for (int j = 0; j < nl; ++j)
-          memcpy(&host[(((size_t)c * nl + j) * B + b) * N], &blk[(size_t)j * N], N * 8);
-      }
-    }
-    upload(r, host);
-    ntt(lsq(r, 0, 3, level), false);
+    const int level = pt.level, B = pt.poly.B;
+    Poly r = alloc(3, level + 1, B);
+    const LimbSet rs = lsq(r, 0, 3, level);
+    if (orion_launch_enc_sample(rs, enc_sampler, d_tb, N, stream)) throw std::runtime_error("sampler launch failed");
+    enc_sampler.enc += 1;
+    ntt(rs, false);
     Ciphertext ct = new_ct(level, B, pt.scale);
     LimbSet c0 = lsq(ct.poly, 0, 1, level), c1 = lsq(ct.poly, 1, 1, level);
     ew(EW_MUL, c0, lsq(r, 0, 1, level), lsq(pk, 0, 1, level, B));
@@ -1302,7 +1288,10 @@ int OrionHipSetDevice(int device) {
 void OrionHipSetSeed(unsigned long seed) {
   API_BEGIN
   g_seed = seed;
-  if (g) g->prng = Prng(seed);
+  if (g) {
+    g->prng = Prng(seed);
+    g->seed_encryption(seed);
+  }
   API_END_VOID
 }
 
@@ -1349,6 +1338,7 @@ void NewScheme(int logN, int* logQ, int lenQ, int* logP, int lenP, int logScale,
   g->stream = g_user_stream;
   g->prng = Prng(g_seed);
   g->setup(logN, std::vector<int>(logQ, logQ + lenQ), std::vector<int>(logP, logP + lenP), logScale, h);
+  g->seed_encryption(g_seed);
   API_END_VOID
 }
 
@@ -1534,12 +1524,37 @@ int EncodeBatch(float* values, int n, int B, int level, unsigned long scale) {
   return c.pts.add(c.encode(values, n, B, level, (long double)scale, false));
   API_END(-1)
 }
+int EncodeBatchDevice(const float* dvalues, int n, int B, int level, double scale) {
+  API_BEGIN
+  Context& c = ctx();
+  if (level < 0 || level >= c.L || B < 1 || !dvalues) throw std::runtime_error("invalid level/batch/pointer");
+  return c.pts.add(c.encode_dev(dvalues, n, B, level, (long double)scale, false));
+  API_END(-1)
+}
+int DecodeDevice(int pt, double* dout) {
+  API_BEGIN
+  Context& c = ctx();
+  if (!dout) throw std::runtime_error("null output pointer");
+  c.decode_dev(c.pts.get(pt), dout);
+  return 0;
+  API_END(-1)
+}
+int DecodeF64(int pt, double* out, unsigned long n) {
+  API_BEGIN
+  Context& c = ctx();
+  const Plaintext& p = c.pts.get(pt);
+  if (n < (unsigned long)p.poly.B * (c.N / 2)) throw std::runtime_error("output buffer too small");
+  std::vector<double> v = c.decode(p);
+  memcpy(out, v.data(), v.size() * sizeof(double));
+  return 0;
+  API_END(-1)
+}
 ArrayResultFloat Decode(int id) {
   ArrayResultFloat r{nullptr, 0};
   API_BEGIN
   Context& c = ctx();
-  std::vector<float> v = c.decode(c.pts.get(id));
-  r.Data = to_c_array<float, float>(v, &r.Length);
+  std::vector<double> v = c.decode(c.pts.get(id));
+  r.Data = to_c_array<double, float>(v, &r.Length);
   return r;
   API_END(r)
 }
@@ -2092,6 +2107,13 @@ int ExportSecretKey(unsigned long* out, unsigned long n) {
   return export_poly(ctx().sk, out, n);
   API_END(-1)
 }
+int ExportPublicKey(unsigned long* out, unsigned long n) {
+  API_BEGIN
+  if (!ctx().have_pk) throw std::runtime_error("no public key");
+  return export_poly(ctx().pk, out, n);
+  API_END(-1)
+}
+unsigned int OrionHipEncryptionIndex(void) { return g ? g->enc_sampler.enc : 0; }
 int ExportRelinKey(unsigned long* out, unsigned long n) {
   API_BEGIN
   if (!ctx().have_rlk) throw std::runtime_error("no relinearization key");

@@ -316,3 +316,17 @@ __device__ __forceinline__ u64 macs_reduce(const MacS& a, const ModConst& m) {
   const u64 H = (a.mid >> 40) + (a.hi >> 16) + (L1 < a.lo) + (L2 < L1);
   return barrett_256q2(H, L2, m);
 }
+
+// ---------------------------------------------------------------------------
+// encryption sampler (encoder.hip): ChaCha20 key, encryption index, and the
+// cumulative table of the discrete Gaussian (sigma 3.2, |e| <= BOUND):
+// e = -BOUND + #{t : x >= cdt[t]} for a uniform 64-bit x
+// ---------------------------------------------------------------------------
+#define ORION_GAUSS_BOUND 19
+#define ORION_ENC_DOMAIN 0x454e0000u  // 'EN': nonce word 2 of encryption streams
+struct EncSampler {
+  u32 key[8];
+  u32 enc;
+  u32 pad;
+  u64 cdt[2 * ORION_GAUSS_BOUND];
+};

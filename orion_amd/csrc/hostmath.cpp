@@ -122,84 +122,58 @@ u64 primitive_root(u64 q) {
 }
 
 // ---------------------------------------------------------------------------
-// special FFT (HEAAN / Lattigo SpecialiFFT, SpecialFFT): slot j <-> X = zeta^(5^j)
+// special FFT twiddles (HEAAN / Lattigo SpecialiFFT, SpecialFFT): slot j <->
+// X = zeta^(5^j); butterfly j of a block of length len = 2h uses
+// roots[(rot[j] mod 4len) * M / 4len] (forward) or roots[(4len - rot[j] mod
+// 4len) * M / 4len] (inverse), roots[i] = exp(2 pi i / M), M = 2N
 // ---------------------------------------------------------------------------
-SpecialFFT::SpecialFFT(int logN) : n_(1 << (logN - 1)), M_(2 << logN), rot_(n_), roots_(M_ + 1) {
+std::vector<Cplx> special_fft_twiddles(int logN, bool inverse) {
+  const int n = 1 << (logN - 1), M = 2 << logN;
+  std::vector<int> rot(n);
   int r = 1;
-  for (int i = 0; i < n_; ++i) {
-    rot_[i] = r;
-    r = (int)(((long)r * 5) % M_);
+  for (int i = 0; i < n; ++i) {
+    rot[i] = r;
+    r = (int)(((long)r * 5) % M);
   }
-  for (int i = 0; i <= M_; ++i) {
-    double ang = 2.0 * M_PI * (double)i / (double)M_;
-    roots_[i].re = cos(ang);
-    roots_[i].im = sin(ang);
+  std::vector<Cplx> roots(M + 1);
+  for (int i = 0; i <= M; ++i) {
+    double ang = 2.0 * M_PI * (double)i / (double)M;
+    roots[i].re = cos(ang);
+    roots[i].im = sin(ang);
+  }
+  std::vector<Cplx> tw(n, Cplx{0.0, 0.0});
+  for (int h = 1; h < n; h <<= 1) {
+    const int lq = h << 3, gap = M / lq;
+    for (int j = 0; j < h; ++j) tw[h + j] = roots[(inverse ? lq - rot[j] % lq : rot[j] % lq) * gap];
+  }
+  return tw;
+}
+
+void gauss_cdt(double sigma, int bound, u64* t) {
+  std::vector<double> rho(2 * bound + 1);
+  double sum = 0.0;
+  for (int x = -bound; x <= bound; ++x) {
+    rho[x + bound] = exp(-(double)(x * x) / (2.0 * sigma * sigma));
+    sum += rho[x + bound];
+  }
+  double acc = 0.0;
+  for (int i = 0; i < 2 * bound; ++i) {
+    acc += rho[i];
+    const double c = ldexp(acc / sum, 64);
+    t[i] = c >= 18446744073709551616.0 ? ~0ull : (u64)c;
   }
 }
 
-void SpecialFFT::bitrev(std::vector<Cplx>& v) const {
-  int logn = 0;
-  while ((1 << logn) < n_) ++logn;
-  for (int i = 0; i < n_; ++i) {
-    int j = (int)hm_bitrev(i, logn);
-    if (i < j) std::swap(v[i], v[j]);
-  }
-}
-
-static inline Cplx cx_mul(const Cplx& a, const Cplx& b) {
-  double ac = a.re * b.re, bd = a.im * b.im, ad = a.re * b.im, bc = a.im * b.re;
-  return Cplx{ac - bd, ad + bc};
-}
-
-void SpecialFFT::inverse(std::vector<Cplx>& v) const {
-  for (int len = n_; len >= 2; len >>= 1) {
-    const int h = len >> 1, lq = len << 2, gap = M_ / lq;
-    for (int i = 0; i < n_; i += len) {
-      for (int j = 0; j < h; ++j) {
-        Cplx& x = v[i + j];
-        Cplx& y = v[i + j + h];
-        Cplx u{x.re + y.re, x.im + y.im};
-        Cplx w{x.re - y.re, x.im - y.im};
-        x = u;
-        y = cx_mul(w, roots_[(lq - (rot_[j] % lq)) * gap]);
-      }
-    }
-  }
-  bitrev(v);
-  const double inv = 1.0 / (double)n_;
-  for (auto& c : v) {
-    c.re *= inv;
-    c.im *= inv;
-  }
-}
-
-void SpecialFFT::forward(std::vector<Cplx>& v) const {
-  bitrev(v);
-  for (int len = 2; len <= n_; len <<= 1) {
-    const int h = len >> 1, lq = len << 2, gap = M_ / lq;
-    for (int i = 0; i < n_; i += len) {
-      for (int j = 0; j < h; ++j) {
-        Cplx u = v[i + j];
-        Cplx w = cx_mul(v[i + j + h], roots_[(rot_[j] % lq) * gap]);
-        v[i + j] = Cplx{u.re + w.re, u.im + w.im};
-        v[i + j + h] = Cplx{u.re - w.re, u.im - w.im};
-      }
-    }
-  }
-}
-
-void fixed_point_crt(double v, double scale, const u64* mods, int nm, u64* out, size_t stride) {
-  if (v == 0.0) {
-    for (int m = 0; m < nm; ++m) out[m * stride] = 0;
-    return;
-  }
-  const bool neg = v < 0;
-  const double x = neg ? v * (-scale) : v * scale;
-  if (!(x < 18446744073709551616.0)) throw std::runtime_error("encode: |value*scale| >= 2^64");
-  const u64 c = (u64)(x + 0.5);
-  for (int m = 0; m < nm; ++m) {
-    const u64 r = c % mods[m];
-    out[m * stride] = neg ? (r ? mods[m] - r : 0) : r;
+void enc_key_from_seed(u64 seed, uint32_t key[8]) {
+  u64 z = seed ^ 0x6a09e667f3bcc909ull;
+  for (int i = 0; i < 4; ++i) {  // splitmix64
+    z += 0x9E3779B97F4A7C15ull;
+    u64 t = z;
+    t = (t ^ (t >> 30)) * 0xBF58476D1CE4E5B9ull;
+    t = (t ^ (t >> 27)) * 0x94D049BB133111EBull;
+    t ^= t >> 31;
+    key[2 * i] = (uint32_t)t;
+    key[2 * i + 1] = (uint32_t)(t >> 32);
   }
 }
 

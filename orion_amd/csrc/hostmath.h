@@ -27,22 +27,16 @@ u64 primitive_root(u64 q);
 struct Cplx {
   double re, im;
 };
-class SpecialFFT {
- public:
-  explicit SpecialFFT(int logN);
-  void inverse(std::vector<Cplx>& v) const;  // slots -> coefficient pairs
-  void forward(std::vector<Cplx>& v) const;  // coefficient pairs -> slots
-  int n() const { return n_; }
+// special FFT twiddles, laid out per stage: tw[h + j] (h = half-length, j < h)
+// is the factor of butterfly j of every block of length 2h; inverse = the
+// conjugate-index table of SpecialiFFT, forward = SpecialFFT's (encoder.hip)
+std::vector<Cplx> special_fft_twiddles(int logN, bool inverse);
 
- private:
-  int n_, M_;
-  std::vector<int> rot_;
-  std::vector<Cplx> roots_;
-  void bitrev(std::vector<Cplx>& v) const;
-};
-
-// round(|v|*scale) as Lattigo's SingleFloat64ToFixedPointCRT, then residues
-void fixed_point_crt(double v, double scale, const u64* mods, int nm, u64* out, size_t stride);
+// discrete Gaussian cumulative table: t[i] = floor(2^64 * P(X <= -bound + i)),
+// i < 2 bound, P(x) proportional to exp(-x^2 / (2 sigma^2)) on |x| <= bound
+void gauss_cdt(double sigma, int bound, u64* t);
+// 256-bit ChaCha20 key of the encryption sampler, from the scheme seed
+void enc_key_from_seed(u64 seed, uint32_t key[8]);
 
 // seeded PRNG (xoshiro256**)
 class Prng {

