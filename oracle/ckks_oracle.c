@@ -1189,3 +1189,179 @@ void oracle_encrypt_pk(const oracle_ctx *c, const uint32_t key[8], uint32_t enc,
     free(t[k]);
   }
 }
+
+/* ------------------------------------------------------------------ */
+/* polynomial evaluation of the HIP backend (backend.hip eval_poly,    */
+/* reached from polyeval.go:63-84), restated: power basis T_{2s} by    */
+/* squaring (Chebyshev: 2 T_s^2 - 1), recursion p = q T_s + r down to  */
+/* linear leaves, every node accumulated at an exact nominal scale.    */
+/* A ciphertext here is [2][level+1][N] with its level and scale.      */
+/* ------------------------------------------------------------------ */
+typedef struct {
+  int level;
+  long double scale;
+  u64 *v;
+} pct;
+
+static pct pct_alloc(const oracle_ctx *c, int level, long double scale) {
+  pct r = {level, scale, (u64 *)calloc((size_t)2 * (level + 1) * c->N, sizeof(u64))};
+  return r;
+}
+/* first level+1 limbs of each component of a */
+static u64 *pct_at(const oracle_ctx *c, const pct *a, int level) {
+  const size_t L = (size_t)(level + 1) * c->N, A = (size_t)(a->level + 1) * c->N;
+  u64 *o = (u64 *)malloc(sizeof(u64) * 2 * L);
+  memcpy(o, a->v, sizeof(u64) * L);
+  memcpy(o + L, a->v + A, sizeof(u64) * L);
+  return o;
+}
+static void big_const_res(const oracle_ctx *c, long double v, int level, u64 *r) {
+  int neg = v < 0;
+  long double a = floorl((neg ? -v : v) + 0.5L);
+  u64 m;
+  int e = 0;
+  if (a >= 9223372036854775808.0L) {
+    int ex;
+    long double fr = frexpl(a, &ex);
+    m = (u64)ldexpl(fr, 64);
+    e = ex - 64;
+  } else {
+    m = (u64)a;
+  }
+  for (int j = 0; j <= level; j++) {
+    u64 q = c->mod[j];
+    u64 x = mulmod(m % q, powmod(2 % q, (u64)e, q), q);
+    r[j] = neg ? (x ? q - x : 0) : x;
+  }
+}
+static void pct_rescale(const oracle_ctx *c, pct *a) {
+  u64 *o = (u64 *)malloc(sizeof(u64) * 2 * (size_t)a->level * c->N);
+  oracle_rescale(c, a->level, 2, a->v, o);
+  free(a->v);
+  a->v = o;
+  a->scale /= (long double)c->mod[a->level];
+  a->level -= 1;
+}
+static pct pct_mul_relin(const oracle_ctx *c, const pct *a, const pct *b, const u64 *rlk) {
+  int lv = a->level < b->level ? a->level : b->level;
+  u64 *x = pct_at(c, a, lv), *y = pct_at(c, b, lv);
+  pct o = pct_alloc(c, lv, a->scale * b->scale);
+  oracle_mul_relin(c, lv, x, y, rlk, o.v);
+  free(x);
+  free(y);
+  return o;
+}
+
+typedef struct {
+  const oracle_ctx *c;
+  const pct *x;
+  pct pw[17]; /* pw[k] = T_{2^k}, k >= 1 */
+  const u64 *rlk;
+} poly_run;
+
+static pct poly_acc(poly_run *R, const long double *cf, int n, int cheb, int lam, long double S) {
+  const oracle_ctx *c = R->c;
+  const int N = c->N, deg = n - 1;
+  const size_t P = (size_t)(lam + 1) * N;
+  u64 k[MAXMOD];
+  if (deg <= 1) {
+    pct o = pct_alloc(c, lam, S);
+    if (deg == 1 && cf[1] != 0) {
+      big_const_res(c, cf[1] * S / R->x->scale, lam, k);
+      u64 *x = pct_at(c, R->x, lam);
+      for (int comp = 0; comp < 2; comp++)
+        for (int j = 0; j <= lam; j++)
+          for (int i = 0; i < N; i++) {
+            size_t at = comp * P + (size_t)j * N + i;
+            o.v[at] = mulmod(x[at], k[j], c->mod[j]);
+          }
+      free(x);
+    }
+    if (cf[0] != 0) {
+      big_const_res(c, cf[0] * S, lam, k);
+      for (int j = 0; j <= lam; j++)
+        for (int i = 0; i < N; i++) o.v[(size_t)j * N + i] = addmod(o.v[(size_t)j * N + i], k[j], c->mod[j]);
+    }
+    return o;
+  }
+  int s = 1, ks = 0;
+  while (2 * s <= deg) s *= 2, ks++;
+  /* split p = q T_s + r (Chebyshev: T_{s+j} = 2 T_s T_j - T_{s-j}) */
+  long double *q = (long double *)malloc(sizeof(long double) * (deg - s + 1));
+  long double *r = (long double *)malloc(sizeof(long double) * s);
+  for (int j = 0; j <= deg - s; j++) q[j] = cf[s + j];
+  for (int j = 0; j < s; j++) r[j] = cf[j];
+  if (cheb)
+    for (int j = 1; j <= deg - s; j++) {
+      q[j] = 2 * cf[s + j];
+      r[s - j] -= cf[s + j];
+    }
+  const pct *G = &R->pw[ks];
+  pct qc = poly_acc(R, q, deg - s + 1, cheb, lam + 1, S * (long double)c->mod[lam + 1] / G->scale);
+  pct_rescale(c, &qc);
+  pct o = pct_mul_relin(c, &qc, G, R->rlk);
+  o.scale = S;
+  pct rc = poly_acc(R, r, s, cheb, lam, S);
+  for (int comp = 0; comp < 2; comp++)
+    for (int j = 0; j <= lam; j++)
+      for (int i = 0; i < N; i++) {
+        size_t at = comp * P + (size_t)j * N + i;
+        o.v[at] = addmod(o.v[at], rc.v[at], c->mod[j]);
+      }
+  free(qc.v);
+  free(rc.v);
+  free(q);
+  free(r);
+  return o;
+}
+
+/* ct: [2][level+1][N] at `level`, scale xscale; coeffs lowest degree first.
+ * out: [2][out_level+1][N]; returns out_level (-1 if level < depth). */
+int oracle_eval_poly(const oracle_ctx *c, int level, const u64 *ct, long double xscale, const double *coeffs,
+                     int n, int cheb, long double target, const u64 *rlk, u64 *out, long double *out_scale) {
+  const int deg = n - 1;
+  int depth = 0;
+  while ((1 << depth) <= deg) depth++;
+  if (level < depth) return -1;
+  pct x = {level, xscale, (u64 *)ct};
+  poly_run R;
+  memset(&R, 0, sizeof(R));
+  R.c = c;
+  R.x = &x;
+  R.rlk = rlk;
+  long double *cf = (long double *)malloc(sizeof(long double) * n);
+  for (int i = 0; i < n; i++) cf[i] = (long double)coeffs[i];
+  u64 k[MAXMOD];
+  for (int ks = 0; (2 << ks) <= deg; ks++) {
+    const pct *a = ks == 0 ? &x : &R.pw[ks];
+    pct t = pct_mul_relin(c, a, a, rlk);
+    pct_rescale(c, &t);
+    if (cheb) {
+      const size_t P = (size_t)(t.level + 1) * c->N;
+      for (size_t i = 0; i < 2 * P; i++) {
+        int j = (int)((i % P) / c->N);
+        t.v[i] = addmod(t.v[i], t.v[i], c->mod[j]);
+      }
+      big_const_res(c, -t.scale, t.level, k);
+      for (int j = 0; j <= t.level; j++)
+        for (int i = 0; i < c->N; i++)
+          t.v[(size_t)j * c->N + i] = addmod(t.v[(size_t)j * c->N + i], k[j], c->mod[j]);
+    }
+    R.pw[ks + 1] = t;
+  }
+  pct o;
+  if (deg == 0) {
+    o = poly_acc(&R, cf, n, cheb, level, target);
+  } else {
+    const int lo = level - depth;
+    o = poly_acc(&R, cf, n, cheb, lo + 1, target * (long double)c->mod[lo + 1]);
+    pct_rescale(c, &o);
+    o.scale = target;
+  }
+  memcpy(out, o.v, sizeof(u64) * 2 * (size_t)(o.level + 1) * c->N);
+  *out_scale = o.scale;
+  free(o.v);
+  for (int i = 1; i < 17; i++) free(R.pw[i].v);
+  free(cf);
+  return o.level;
+}

@@ -145,6 +145,16 @@ void oracle_encrypt_pk(const oracle_ctx *ctx, const uint32_t key[8], uint32_t en
                        uint32_t image, int level, const uint64_t *pk,
                        const uint64_t *pt, uint64_t *ct);
 
+/* ---- polynomial evaluation of the HIP backend (backend.hip eval_poly) ----
+ * p(x) (monomial or Chebyshev basis, coefficients lowest degree first) of a
+ * [2][level+1][N] ciphertext at scale xscale; writes [2][out_level+1][N] at
+ * scale *out_scale (= target) and returns out_level = level - bitlen(n-1),
+ * or -1 when level < bitlen(n-1).  rlk layout as evk. */
+int oracle_eval_poly(const oracle_ctx *ctx, int level, const uint64_t *ct,
+                     long double xscale, const double *coeffs, int n, int cheb,
+                     long double target, const uint64_t *rlk, uint64_t *out,
+                     long double *out_scale);
+
 /* coefficient-wise helpers used by tests */
 void oracle_mul_coeffs(const oracle_ctx *ctx, const int *mods, int nl,
                        const uint64_t *a, const uint64_t *b, uint64_t *out);

@@ -59,6 +59,9 @@ def _load():
         "oracle_encrypt_sk": (None, [vp, ctypes.c_uint64, ctypes.c_int, _u64p, _u64p, _u64p]),
         "oracle_decrypt": (None, [vp, ctypes.c_int, _u64p, _u64p, _u64p]),
         "oracle_mul_coeffs": (None, [vp, _intp, ctypes.c_int, _u64p, _u64p, _u64p]),
+        "oracle_eval_poly": (ctypes.c_int, [vp, ctypes.c_int, _u64p, ctypes.c_longdouble, _dblp, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_longdouble, _u64p, _u64p,
+                                            ctypes.POINTER(ctypes.c_longdouble)]),
         "oracle_chacha20_block": (None, [_u32p, ctypes.c_uint32, _u32p, _u32p]),
         "oracle_enc_key": (None, [ctypes.c_uint64, _u32p]),
         "oracle_gauss_cdt": (None, [ctypes.c_double, ctypes.c_int, _u64p]),
@@ -255,6 +258,19 @@ class Oracle:
         out = np.zeros_like(a)
         lib().oracle_mul_coeffs(self._h, _ip(mods), len(mods), _p(a), _p(b), _p(out))
         return out
+
+    def eval_poly(self, ct, level, scale, coeffs, cheb, target, rlk):
+        """The HIP backend's EvaluatePolynomial restated: returns (ct_out,
+        out_level, out_scale); coeffs lowest degree first."""
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        cf = np.ascontiguousarray(coeffs, dtype=np.float64)
+        out = np.zeros(2 * (level + 1) * self.N, dtype=np.uint64)  # [2][out_level+1][N] written flat
+        osc = ctypes.c_longdouble(0)
+        lv = lib().oracle_eval_poly(self._h, level, _p(ct), scale, cf.ctypes.data_as(_dblp), len(cf), int(cheb),
+                                    target, _p(np.ascontiguousarray(rlk)), _p(out), ctypes.byref(osc))
+        if lv < 0:
+            raise ValueError("level < depth")
+        return out[:2 * (lv + 1) * self.N].reshape(2, lv + 1, self.N).copy(), lv, osc.value
 
     def encrypt_pk(self, seed, enc, image, pk, pt, level):
         """The HIP backend's public-key encryption of image `image` in

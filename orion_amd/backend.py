@@ -229,6 +229,12 @@ class HipFunction:
     def __call__(self, *args):
         c_args, keep = [], []
         for arg in args:
+            if len(c_args) >= len(self.argtypes) and keep and isinstance(arg, (int, np.integer)) \
+                    and int(arg) == keep[-1][1]:
+                # a list argument already supplied its length (LattigoFunction
+                # expands a list to (ptr, len)); orion's poly_evaluator.py:23
+                # passes len(coeffs) once more -- drop the duplicate
+                continue
             typ = self.argtypes[len(c_args)] if len(c_args) < len(self.argtypes) else None
             c = self._convert(arg, typ)
             if isinstance(c, tuple):

@@ -1229,6 +1229,128 @@ struct Context {
     }
     return r;
   }
+  // round(c) (half away from zero) of any magnitude -> residues at `level`;
+  // |c| >= 2^63 is an integer m 2^e (64-bit long double mantissa), reduced exactly
+  std::vector<u64> big_const_residues(long double c, int level) const {
+    const bool neg = c < 0;
+    long double a = floorl((neg ? -c : c) + 0.5L);
+    u64 m;
+    int e = 0;
+    if (a >= 9223372036854775808.0L) {
+      int ex;
+      const long double fr = frexpl(a, &ex);
+      m = (u64)ldexpl(fr, 64);
+      e = ex - 64;
+    } else {
+      m = (u64)a;
+    }
+    std::vector<u64> r;
+    for (int j = 0; j <= level; ++j) {
+      const u64 q = mods[j];
+      const u64 x = hm_mulmod(m % q, hm_powmod(2 % q, (u64)e, q), q);
+      r.push_back(neg ? (x ? q - x : 0) : x);
+    }
+    return r;
+  }
+
+  // ---------------------------------------------------------------------------
+  // polynomial evaluation (polyeval.go:63-84 -> Lattigo polynomial.Evaluator):
+  // p(x) in the monomial or Chebyshev basis, consuming exactly bitlen(degree)
+  // levels (orion/nn/activation.py:22-23,106-107 plans for that) and returning
+  // exactly the requested scale.
+  //   * power basis: T_{2s} = T_s^2 (monomial) or 2 T_s^2 - 1 (Chebyshev),
+  //     each a relinearised product plus rescale;
+  //   * recursion p = q T_s + r, s the largest power of two <= deg p (the
+  //     Chebyshev split uses T_{s+j} = 2 T_s T_j - T_{s-j}), down to linear
+  //     leaves c0 + c1 x.  A node at level lam is accumulated at scale S
+  //     without rescaling; its q-branch is accumulated one level up at scale
+  //     S q_{lam+1} / scale(T_s), rescaled once and multiplied by T_s.  Leaf
+  //     constants are integers round(c S / scale(x)), so every term of a node
+  //     carries the same nominal scale and the final rescale lands exactly on
+  //     the target.
+  // ---------------------------------------------------------------------------
+  struct PolyFn {
+    bool cheb = false;
+    std::vector<long double> c;  // lowest degree first
+  };
+  struct PolyRun {
+    const Ciphertext* x;
+    std::map<int, Ciphertext> pw;  // T_{2^k}, k >= 1
+  };
+  static std::pair<std::vector<long double>, std::vector<long double>> poly_split(const std::vector<long double>& c,
+                                                                                  int s, bool cheb) {
+    const int deg = (int)c.size() - 1;
+    std::vector<long double> q(c.begin() + s, c.end()), r(c.begin(), c.begin() + s);
+    if (cheb) {
+      for (int j = 1; j <= deg - s; ++j) {
+        q[j] = 2 * c[s + j];
+        r[s - j] -= c[s + j];
+      }
+    }
+    return {q, r};
+  }
+  Ciphertext poly_acc(PolyRun& R, const std::vector<long double>& c, bool cheb, int lam, long double S) {
+    const Ciphertext& x = *R.x;
+    const int deg = (int)c.size() - 1, B = x.poly.B;
+    if (deg <= 1) {
+      Ciphertext o = new_ct(lam, B, S);
+      const LimbSet lo = lsq(o.poly, 0, 2, lam);
+      if (deg == 1 && c[1] != 0) {
+        std::vector<u64> k = big_const_residues(c[1] * S / x.scale, lam);
+        ew1(EW_SCALE, lo, lsq(x.poly, 0, 2, lam), &k);
+      } else {
+        HIPCHK(hipMemsetAsync(o.poly.ptr(), 0, (size_t)2 * (lam + 1) * B * N * sizeof(u64), stream));
+      }
+      if (c[0] != 0) {
+        std::vector<u64> k = big_const_residues(c[0] * S, lam);
+        ew1(EW_ADDC, lsq(o.poly, 0, 1, lam), lsq(o.poly, 0, 1, lam), &k);
+      }
+      return o;
+    }
+    int s = 1;
+    while (2 * s <= deg) s *= 2;
+    auto qr = poly_split(c, s, cheb);
+    const Ciphertext& G = R.pw.at(s);
+    if (G.level < lam || lam + 1 > x.level) throw std::runtime_error("polynomial evaluation: level plan violated");
+    Ciphertext qc = poly_acc(R, qr.first, cheb, lam + 1, S * (long double)mods[lam + 1] / G.scale);
+    rescale_inplace(qc);
+    Ciphertext o = mul_relin(qc, G);
+    o.scale = S;
+    Ciphertext rc = poly_acc(R, qr.second, cheb, lam, S);
+    const LimbSet lo = lsq(o.poly, 0, 2, lam);
+    ew(EW_ADD, lo, lo, lsq(rc.poly, 0, 2, lam));
+    return o;
+  }
+  Ciphertext eval_poly(const Ciphertext& x, const PolyFn& p, long double target) {
+    const int deg = (int)p.c.size() - 1;
+    if (deg < 0) throw std::runtime_error("empty polynomial");
+    int depth = 0;
+    while ((1 << depth) <= deg) ++depth;  // bits.Len64(degree)
+    if (x.level < depth)
+      throw std::runtime_error(std::to_string(x.level) + " levels < " + std::to_string(depth) +
+                               " log(d) -> cannot evaluate poly");
+    PolyRun R;
+    R.x = &x;
+    for (int s = 1; 2 * s <= deg; s *= 2) {
+      const Ciphertext& a = s == 1 ? x : R.pw.at(s);
+      Ciphertext t = mul_relin(a, a);
+      rescale_inplace(t);
+      if (p.cheb) {
+        const LimbSet lt = lsq(t.poly, 0, 2, t.level);
+        ew(EW_ADD, lt, lt, lt);
+        std::vector<u64> one = big_const_residues(-t.scale, t.level);
+        ew1(EW_ADDC, lsq(t.poly, 0, 1, t.level), lsq(t.poly, 0, 1, t.level), &one);
+      }
+      R.pw.emplace(2 * s, std::move(t));
+    }
+    if (deg == 0) return poly_acc(R, p.c, p.cheb, x.level, target);
+    const int lo = x.level - depth;
+    Ciphertext out = poly_acc(R, p.c, p.cheb, lo + 1, target * (long double)mods[lo + 1]);
+    rescale_inplace(out);
+    out.scale = target;
+    return out;
+  }
+  HandlePool<PolyFn> polys;
 };
 
 static std::unique_ptr<Context> g;
@@ -2009,17 +2131,32 @@ void RemoveRotationKeys(void) {
 
 // ---- SURVEY §8f "next": polynomial evaluation, minimax, bootstrapping ----
 void NewPolynomialEvaluator(void) {}
-int GenerateMonomial(float*, int) {
-  g_last_error = "GenerateMonomial: polynomial evaluation is not implemented in the HIP backend yet";
-  return -1;
+static int add_poly(float* coeffs, int n, bool cheb) {
+  Context& c = ctx();
+  if (!coeffs || n < 1) throw std::runtime_error("polynomial needs at least one coefficient");
+  Context::PolyFn p;
+  p.cheb = cheb;
+  for (int i = 0; i < n; ++i) p.c.push_back((long double)coeffs[i]);
+  return c.polys.add(std::move(p));
 }
-int GenerateChebyshev(float*, int) {
-  g_last_error = "GenerateChebyshev: polynomial evaluation is not implemented in the HIP backend yet";
-  return -1;
+// polyeval.go:38-47: bignum.Monomial, coefficients lowest degree first
+int GenerateMonomial(float* coeffs, int n) {
+  API_BEGIN
+  return add_poly(coeffs, n, false);
+  API_END(-1)
 }
-int EvaluatePolynomial(int, int, unsigned long) {
-  g_last_error = "EvaluatePolynomial: not implemented in the HIP backend yet";
-  return -1;
+// polyeval.go:50-60: bignum.Chebyshev on [-1, 1]
+int GenerateChebyshev(float* coeffs, int n) {
+  API_BEGIN
+  return add_poly(coeffs, n, true);
+  API_END(-1)
+}
+// polyeval.go:63-84: a new ciphertext at level - bitlen(degree), scale outScale
+int EvaluatePolynomial(int ct, int poly, unsigned long outScale) {
+  API_BEGIN
+  Context& c = ctx();
+  return c.cts.add(c.eval_poly(c.cts.get(ct), c.polys.get(poly), (long double)outScale));
+  API_END(-1)
 }
 ArrayResultDouble GenerateMinimaxSignCoeffs(int*, int, int, int, int, int) {
   g_last_error = "GenerateMinimaxSignCoeffs: not implemented in the HIP backend yet";

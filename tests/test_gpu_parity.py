@@ -135,6 +135,49 @@ def test_encrypt_parity(small):
         assert np.array_equal(got[b], orc.encrypt_pk(1234, enc, b, pk, ptv[b], level)), b
 
 
+@pytest.mark.parametrize("cheb,coeffs", [
+    (True, [0.1, 0.6, 0.0, -0.25, 0.05, 0.3, -0.02, 0.11]),                    # degree 7, depth 3
+    (True, list(np.linspace(-0.4, 0.4, 16))),                                   # degree 15, depth 4
+    (False, [0.5, -1.0, 0.25, 0.125, -0.3, 0.2]),                               # monomial degree 5
+    (False, [0.75, 0.5]),                                                       # degree 1
+    (True, [0.375]),                                                            # degree 0
+])
+def test_polynomial_parity(small, cheb, coeffs):
+    """EvaluatePolynomial (polyeval.go:63-84) vs the oracle's restatement, bit
+    for bit, plus its contract: level - bitlen(degree), exactly the target
+    scale, and decrypt ~ p(x)."""
+    lib, orc = small
+    rng = np.random.default_rng(14)
+    level, B = 5, 2
+    xs = rng.uniform(-1, 1, (B, orc.N // 2)).astype(np.float32)
+    ct = lib.Encrypt(lib.encode_batch(xs, level, 1 << 40))
+    x = lib.export_ciphertext(ct)
+    cf = np.array(coeffs, dtype=np.float32)
+    poly = lib.GenerateChebyshev(list(cf), len(cf)) if cheb else lib.GenerateMonomial(list(cf))
+    out = lib.EvaluatePolynomial(ct, poly, 1 << 40)
+    depth = int(len(cf) - 1).bit_length()
+    assert lib.GetCiphertextLevel(out) == level - depth
+    assert lib.GetCiphertextScaleF(out) == 2.0 ** 40
+    got = lib.export_ciphertext(out)
+    rlk = lib.export_relin_key()
+    for b in range(B):
+        ref, lv, sc = orc.eval_poly(x[b], level, 2.0 ** 40, cf.astype(np.float64), cheb, 2.0 ** 40, rlk)
+        assert lv == level - depth and sc == 2.0 ** 40
+        assert np.array_equal(got[b], ref), b
+    dec = lib.decode_f64(lib.Decrypt(out))
+    xd = xs.astype(np.float64)
+    exp = np.polynomial.chebyshev.chebval(xd, cf) if cheb else np.polynomial.polynomial.polyval(xd, cf)
+    assert np.abs(dec - exp).max() < 1e-3
+
+
+def test_polynomial_level_error(small):
+    lib, _ = small
+    ct = lib.Encrypt(lib.encode_batch(np.zeros((1, 8), np.float32), 1, 1 << 40))
+    poly = lib.GenerateMonomial([1.0, 0.5, 0.25, 0.125])  # degree 3: depth 2 > level 1
+    with pytest.raises(RuntimeError, match="cannot evaluate poly"):
+        lib.EvaluatePolynomial(ct, poly, 1 << 40)
+
+
 def test_rescale_parity(small):
     lib, orc = small
     rng = np.random.default_rng(3)

@@ -203,6 +203,24 @@ def test_encrypt_pk_decrypts(ckks):
     assert np.abs(dec - v).max() < 1e-4
 
 
+@pytest.mark.parametrize("cheb,deg", [(True, 7), (True, 12), (False, 5), (False, 1)])
+def test_eval_poly_functional(ckks, cheb, deg):
+    """The polynomial-evaluation restatement decrypts to p(x), consumes
+    bitlen(deg) levels and lands on the target scale exactly."""
+    o, sk = ckks
+    rng = np.random.default_rng(20 + deg)
+    v = rng.uniform(-1, 1, o.N // 2)
+    lvl = 4
+    ct = o.encrypt_sk(21, sk, o.encode(v, 2.0 ** 40, list(range(lvl + 1))), lvl)
+    rlk = o.gen_evk(4, o.mul_coeffs(sk, sk, list(range(o.L + o.K))), sk)
+    cf = rng.uniform(-0.5, 0.5, deg + 1).astype(np.float32).astype(np.float64)
+    out, lv, sc = o.eval_poly(ct, lvl, 2.0 ** 40, cf, cheb, 2.0 ** 40, rlk)
+    assert lv == lvl - int(deg).bit_length() and sc == 2.0 ** 40
+    dec = o.decode(o.decrypt(out, sk, lv), lv, 2.0 ** 40)
+    exp = np.polynomial.chebyshev.chebval(v, cf) if cheb else np.polynomial.polynomial.polyval(v, cf)
+    assert np.abs(dec - exp).max() < 1e-4
+
+
 def test_encode_matches_canonical_embedding(ckks):
     """Encoding by definition: slot j = m(zeta^(5^j)), zeta = exp(i*pi/N)."""
     o, _ = ckks
