@@ -1255,32 +1255,96 @@ static pct pct_mul_relin(const oracle_ctx *c, const pct *a, const pct *b, const 
 typedef struct {
   const oracle_ctx *c;
   const pct *x;
-  pct pw[17]; /* pw[k] = T_{2^k}, k >= 1 */
+  int cheb, max_baby;
+  pct pw[17];   /* pw[k] = T_{2^k}, k >= 1 */
+  pct baby[64]; /* T_j, j not a power of two (v == NULL until computed) */
   const u64 *rlk;
 } poly_run;
 
-static pct poly_acc(poly_run *R, const long double *cf, int n, int cheb, int lam, long double S) {
+static int ceil_log2i(int j) {
+  int k = 0;
+  while ((1 << k) < j) k++;
+  return k;
+}
+/* Lattigo bignum.OptimalSplit */
+static int optimal_split(int logd) {
+  int ls = logd >> 1;
+  int a = (1 << ls) + (1 << (logd - ls)) + logd - ls - 3;
+  int b = (1 << (ls + 1)) + (1 << (logd - ls - 1)) + logd - ls - 4;
+  if (a > b) ls++;
+  return ls;
+}
+/* T_j: x, a power from pw, or a baby step 2 T_a T_b - T_c (Chebyshev) / T_a T_b
+ * with a = 2^k - 1, b = j + 1 - 2^k (Lattigo genPower), T_c scaled by
+ * round(s_a s_b / s_c) before the rescale */
+static const pct *poly_T(poly_run *R, int j) {
   const oracle_ctx *c = R->c;
-  const int N = c->N, deg = n - 1;
+  if (j == 1) return R->x;
+  if ((j & (j - 1)) == 0) return &R->pw[ceil_log2i(j)];
+  if (R->baby[j].v) return &R->baby[j];
+  int k = ceil_log2i(j) - 1, a = (1 << k) - 1, b = j + 1 - (1 << k), cc = a > b ? a - b : b - a;
+  const pct *A = poly_T(R, a), *B = poly_T(R, b);
+  pct t = pct_mul_relin(c, A, B, R->rlk);
+  if (R->cheb) {
+    const size_t P = (size_t)(t.level + 1) * c->N;
+    u64 kk[MAXMOD];
+    for (size_t i = 0; i < 2 * P; i++) {
+      int l = (int)((i % P) / c->N);
+      t.v[i] = addmod(t.v[i], t.v[i], c->mod[l]);
+    }
+    if (cc == 0) {
+      big_const_res(c, -t.scale, t.level, kk);
+      for (int l = 0; l <= t.level; l++)
+        for (int i = 0; i < c->N; i++) t.v[(size_t)l * c->N + i] = addmod(t.v[(size_t)l * c->N + i], kk[l], c->mod[l]);
+    } else {
+      const pct *C = poly_T(R, cc);
+      u64 *cv = pct_at(c, C, t.level);
+      big_const_res(c, -(t.scale / C->scale), t.level, kk);
+      for (size_t i = 0; i < 2 * P; i++) {
+        int l = (int)((i % P) / c->N);
+        t.v[i] = addmod(t.v[i], mulmod(cv[i], kk[l], c->mod[l]), c->mod[l]);
+      }
+      free(cv);
+    }
+  }
+  pct_rescale(c, &t);
+  R->baby[j] = t;
+  return &R->baby[j];
+}
+
+static int poly_leaf(const poly_run *R, const long double *cf, int n, int lam) {
+  const int deg = n - 1;
+  if (deg <= 1) return 1;
+  if (deg >= R->max_baby) return 0;
+  for (int j = 2; j <= deg; j++)
+    if (cf[j] != 0 && R->x->level - ceil_log2i(j) < lam) return 0;
+  return 1;
+}
+
+static pct poly_acc(poly_run *R, const long double *cf, int n, int lam, long double S) {
+  const oracle_ctx *c = R->c;
+  const int N = c->N, deg = n - 1, cheb = R->cheb;
   const size_t P = (size_t)(lam + 1) * N;
   u64 k[MAXMOD];
-  if (deg <= 1) {
+  if (poly_leaf(R, cf, n, lam)) {
     pct o = pct_alloc(c, lam, S);
-    if (deg == 1 && cf[1] != 0) {
-      big_const_res(c, cf[1] * S / R->x->scale, lam, k);
-      u64 *x = pct_at(c, R->x, lam);
+    for (int j = 1; j <= deg; j++) {
+      if (cf[j] == 0) continue;
+      const pct *T = poly_T(R, j);
+      big_const_res(c, cf[j] * S / T->scale, lam, k);
+      u64 *x = pct_at(c, T, lam);
       for (int comp = 0; comp < 2; comp++)
-        for (int j = 0; j <= lam; j++)
+        for (int l = 0; l <= lam; l++)
           for (int i = 0; i < N; i++) {
-            size_t at = comp * P + (size_t)j * N + i;
-            o.v[at] = mulmod(x[at], k[j], c->mod[j]);
+            size_t at = comp * P + (size_t)l * N + i;
+            o.v[at] = addmod(o.v[at], mulmod(x[at], k[l], c->mod[l]), c->mod[l]);
           }
       free(x);
     }
     if (cf[0] != 0) {
       big_const_res(c, cf[0] * S, lam, k);
-      for (int j = 0; j <= lam; j++)
-        for (int i = 0; i < N; i++) o.v[(size_t)j * N + i] = addmod(o.v[(size_t)j * N + i], k[j], c->mod[j]);
+      for (int l = 0; l <= lam; l++)
+        for (int i = 0; i < N; i++) o.v[(size_t)l * N + i] = addmod(o.v[(size_t)l * N + i], k[l], c->mod[l]);
     }
     return o;
   }
@@ -1297,16 +1361,16 @@ static pct poly_acc(poly_run *R, const long double *cf, int n, int cheb, int lam
       r[s - j] -= cf[s + j];
     }
   const pct *G = &R->pw[ks];
-  pct qc = poly_acc(R, q, deg - s + 1, cheb, lam + 1, S * (long double)c->mod[lam + 1] / G->scale);
+  pct qc = poly_acc(R, q, deg - s + 1, lam + 1, S * (long double)c->mod[lam + 1] / G->scale);
   pct_rescale(c, &qc);
   pct o = pct_mul_relin(c, &qc, G, R->rlk);
   o.scale = S;
-  pct rc = poly_acc(R, r, s, cheb, lam, S);
+  pct rc = poly_acc(R, r, s, lam, S);
   for (int comp = 0; comp < 2; comp++)
-    for (int j = 0; j <= lam; j++)
+    for (int l = 0; l <= lam; l++)
       for (int i = 0; i < N; i++) {
-        size_t at = comp * P + (size_t)j * N + i;
-        o.v[at] = addmod(o.v[at], rc.v[at], c->mod[j]);
+        size_t at = comp * P + (size_t)l * N + i;
+        o.v[at] = addmod(o.v[at], rc.v[at], c->mod[l]);
       }
   free(qc.v);
   free(rc.v);
@@ -1329,6 +1393,9 @@ int oracle_eval_poly(const oracle_ctx *c, int level, const u64 *ct, long double 
   R.c = c;
   R.x = &x;
   R.rlk = rlk;
+  R.cheb = cheb;
+  R.max_baby = depth >= 2 ? (1 << optimal_split(depth)) : 2;
+  if (R.max_baby > 64) R.max_baby = 64;
   long double *cf = (long double *)malloc(sizeof(long double) * n);
   for (int i = 0; i < n; i++) cf[i] = (long double)coeffs[i];
   u64 k[MAXMOD];
@@ -1351,10 +1418,10 @@ int oracle_eval_poly(const oracle_ctx *c, int level, const u64 *ct, long double 
   }
   pct o;
   if (deg == 0) {
-    o = poly_acc(&R, cf, n, cheb, level, target);
+    o = poly_acc(&R, cf, n, level, target);
   } else {
     const int lo = level - depth;
-    o = poly_acc(&R, cf, n, cheb, lo + 1, target * (long double)c->mod[lo + 1]);
+    o = poly_acc(&R, cf, n, lo + 1, target * (long double)c->mod[lo + 1]);
     pct_rescale(c, &o);
     o.scale = target;
   }
@@ -1362,6 +1429,7 @@ int oracle_eval_poly(const oracle_ctx *c, int level, const u64 *ct, long double 
   *out_scale = o.scale;
   free(o.v);
   for (int i = 1; i < 17; i++) free(R.pw[i].v);
+  for (int i = 0; i < 64; i++) free(R.baby[i].v);
   free(cf);
   return o.level;
 }

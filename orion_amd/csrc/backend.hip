@@ -374,11 +374,27 @@ struct Context {
 #endif
   // 1: one limb per workgroup (ntt.hip); 2: two-pass N = 2^15 kernels (ntt2.hip)
   int ntt_impl = getenv("ORION_NTT_IMPL") ? atoi(getenv("ORION_NTT_IMPL")) : ORION_NTT_DEFAULT_IMPL;
+  // two-pass kernels: limb-transforms per chunk (0 = one launch pair for all)
+  int ntt2_chunk = getenv("ORION_NTT2_CHUNK") ? atoi(getenv("ORION_NTT2_CHUNK")) : 0;
   void ntt_io(NttIO io, bool inv) {
     io.order = ntt_order;
     io.jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
     if (logN == 16 || (ntt_impl == 2 && logN == 15)) {  // N = 2^16: the two-pass kernels only
       Poly scratch;
+      if (ntt2_chunk > 0 && io.jobs > 0) {  // chunks of jobs through one reused compact scratch
+        const int chunk = std::min(ntt2_chunk, io.jobs);
+        scratch = alloc(1, 1, chunk);
+        io.mid = ls(scratch, 0, 1, {0}, {0});
+        io.mid_compact = 1;
+        const double per = 16.0 * N + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
+        Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, per * io.jobs);
+        for (int j0 = 0; j0 < io.jobs; j0 += chunk) {
+          io.job0 = j0;
+          io.njob = std::min(chunk, io.jobs - j0);
+          if (orion_launch_ntt2(logN, io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
+        }
+        return;
+      }
       io.mid = io.dst;
       if (io.epi == NTT_EPI_SUBSCALE && io.ex.p == io.dst.p) {  // in-place tail: keep ex intact for pass 2
         scratch = alloc(io.dst.ncomp, io.dst.nlimb, io.dst.nbatch);
@@ -1258,16 +1274,20 @@ struct Context {
   // p(x) in the monomial or Chebyshev basis, consuming exactly bitlen(degree)
   // levels (orion/nn/activation.py:22-23,106-107 plans for that) and returning
   // exactly the requested scale.
-  //   * power basis: T_{2s} = T_s^2 (monomial) or 2 T_s^2 - 1 (Chebyshev),
-  //     each a relinearised product plus rescale;
+  //   * power basis (Lattigo genPower): T_{2s} = T_s^2 (Chebyshev 2 T_s^2 - 1);
+  //     baby steps T_j, j < 2^OptimalSplit(bitlen(deg)), from the split
+  //     a = 2^k - 1, b = j + 1 - 2^k (Chebyshev 2 T_a T_b - T_|a-b|, the T_c
+  //     term scaled by round(s_a s_b / s_c) before the rescale), computed on
+  //     first use; T_j sits at level(x) - ceil(log2 j);
   //   * recursion p = q T_s + r, s the largest power of two <= deg p (the
-  //     Chebyshev split uses T_{s+j} = 2 T_s T_j - T_{s-j}), down to linear
-  //     leaves c0 + c1 x.  A node at level lam is accumulated at scale S
-  //     without rescaling; its q-branch is accumulated one level up at scale
-  //     S q_{lam+1} / scale(T_s), rescaled once and multiplied by T_s.  Leaf
-  //     constants are integers round(c S / scale(x)), so every term of a node
-  //     carries the same nominal scale and the final rescale lands exactly on
-  //     the target.
+  //     Chebyshev split uses T_{s+j} = 2 T_s T_j - T_{s-j}).  A node at level
+  //     lam is accumulated at scale S without rescaling; its q-branch is
+  //     accumulated one level up at scale S q_{lam+1} / scale(T_s), rescaled
+  //     once and multiplied by T_s.  A node is a leaf sum c0 + sum c_j T_j when
+  //     its degree is 1, or below the baby-step bound with every T_j it needs
+  //     at level >= lam.  Leaf constants are integers round(c_j S / scale(T_j)),
+  //     so every term of a node carries the same nominal scale and the final
+  //     rescale lands exactly on the target.
   // ---------------------------------------------------------------------------
   struct PolyFn {
     bool cheb = false;
@@ -1275,8 +1295,47 @@ struct Context {
   };
   struct PolyRun {
     const Ciphertext* x;
-    std::map<int, Ciphertext> pw;  // T_{2^k}, k >= 1
+    bool cheb;
+    int max_baby;                    // leaves may use T_j, j < max_baby
+    std::map<int, Ciphertext> pw;    // T_{2^k}, k >= 1
+    std::map<int, Ciphertext> baby;  // T_j, j not a power of two
   };
+  static int ceil_log2(int j) {
+    int k = 0;
+    while ((1 << k) < j) ++k;
+    return k;
+  }
+  static int optimal_split(int logd) {  // Lattigo bignum.OptimalSplit
+    int ls = logd >> 1;
+    const int a = (1 << ls) + (1 << (logd - ls)) + logd - ls - 3;
+    const int b = (1 << (ls + 1)) + (1 << (logd - ls - 1)) + logd - ls - 4;
+    if (a > b) ++ls;
+    return ls;
+  }
+  const Ciphertext& poly_T(PolyRun& R, int j) {
+    if (j == 1) return *R.x;
+    if ((j & (j - 1)) == 0) return R.pw.at(j);
+    auto it = R.baby.find(j);
+    if (it != R.baby.end()) return it->second;
+    const int k = ceil_log2(j) - 1, a = (1 << k) - 1, b = j + 1 - (1 << k), c = a > b ? a - b : b - a;
+    const Ciphertext& A = poly_T(R, a);
+    const Ciphertext& Bc = poly_T(R, b);
+    Ciphertext t = mul_relin(A, Bc);
+    if (R.cheb) {
+      const LimbSet lt = lsq(t.poly, 0, 2, t.level);
+      ew(EW_ADD, lt, lt, lt);
+      if (c == 0) {
+        std::vector<u64> one = big_const_residues(-t.scale, t.level);
+        ew1(EW_ADDC, lsq(t.poly, 0, 1, t.level), lsq(t.poly, 0, 1, t.level), &one);
+      } else {
+        const Ciphertext& C = poly_T(R, c);
+        std::vector<u64> k = big_const_residues(-(t.scale / C.scale), t.level);
+        ew(EW_ADDSCALE, lt, lsq(C.poly, 0, 2, t.level), lt, &k);
+      }
+    }
+    rescale_inplace(t);
+    return R.baby.emplace(j, std::move(t)).first->second;
+  }
   static std::pair<std::vector<long double>, std::vector<long double>> poly_split(const std::vector<long double>& c,
                                                                                   int s, bool cheb) {
     const int deg = (int)c.size() - 1;
@@ -1289,18 +1348,29 @@ struct Context {
     }
     return {q, r};
   }
-  Ciphertext poly_acc(PolyRun& R, const std::vector<long double>& c, bool cheb, int lam, long double S) {
+  bool poly_leaf(const PolyRun& R, const std::vector<long double>& c, int lam) const {
+    const int deg = (int)c.size() - 1;
+    if (deg <= 1) return true;
+    if (deg >= R.max_baby) return false;
+    for (int j = 2; j <= deg; ++j)
+      if (c[j] != 0 && R.x->level - ceil_log2(j) < lam) return false;
+    return true;
+  }
+  Ciphertext poly_acc(PolyRun& R, const std::vector<long double>& c, int lam, long double S) {
     const Ciphertext& x = *R.x;
     const int deg = (int)c.size() - 1, B = x.poly.B;
-    if (deg <= 1) {
+    if (poly_leaf(R, c, lam)) {
       Ciphertext o = new_ct(lam, B, S);
       const LimbSet lo = lsq(o.poly, 0, 2, lam);
-      if (deg == 1 && c[1] != 0) {
-        std::vector<u64> k = big_const_residues(c[1] * S / x.scale, lam);
-        ew1(EW_SCALE, lo, lsq(x.poly, 0, 2, lam), &k);
-      } else {
-        HIPCHK(hipMemsetAsync(o.poly.ptr(), 0, (size_t)2 * (lam + 1) * B * N * sizeof(u64), stream));
+      bool first = true;
+      for (int j = 1; j <= deg; ++j) {
+        if (c[j] == 0) continue;
+        const Ciphertext& T = poly_T(R, j);
+        std::vector<u64> k = big_const_residues(c[j] * S / T.scale, lam);
+        ew1(first ? EW_SCALE : EW_ADDSCALE, lo, lsq(T.poly, 0, 2, lam), &k);
+        first = false;
       }
+      if (first) HIPCHK(hipMemsetAsync(o.poly.ptr(), 0, (size_t)2 * (lam + 1) * B * N * sizeof(u64), stream));
       if (c[0] != 0) {
         std::vector<u64> k = big_const_residues(c[0] * S, lam);
         ew1(EW_ADDC, lsq(o.poly, 0, 1, lam), lsq(o.poly, 0, 1, lam), &k);
@@ -1309,14 +1379,14 @@ struct Context {
     }
     int s = 1;
     while (2 * s <= deg) s *= 2;
-    auto qr = poly_split(c, s, cheb);
+    auto qr = poly_split(c, s, R.cheb);
     const Ciphertext& G = R.pw.at(s);
     if (G.level < lam || lam + 1 > x.level) throw std::runtime_error("polynomial evaluation: level plan violated");
-    Ciphertext qc = poly_acc(R, qr.first, cheb, lam + 1, S * (long double)mods[lam + 1] / G.scale);
+    Ciphertext qc = poly_acc(R, qr.first, lam + 1, S * (long double)mods[lam + 1] / G.scale);
     rescale_inplace(qc);
     Ciphertext o = mul_relin(qc, G);
     o.scale = S;
-    Ciphertext rc = poly_acc(R, qr.second, cheb, lam, S);
+    Ciphertext rc = poly_acc(R, qr.second, lam, S);
     const LimbSet lo = lsq(o.poly, 0, 2, lam);
     ew(EW_ADD, lo, lo, lsq(rc.poly, 0, 2, lam));
     return o;
@@ -1331,6 +1401,8 @@ struct Context {
                                " log(d) -> cannot evaluate poly");
     PolyRun R;
     R.x = &x;
+    R.cheb = p.cheb;
+    R.max_baby = depth >= 2 ? std::min(64, 1 << optimal_split(depth)) : 2;
     for (int s = 1; 2 * s <= deg; s *= 2) {
       const Ciphertext& a = s == 1 ? x : R.pw.at(s);
       Ciphertext t = mul_relin(a, a);
@@ -1343,9 +1415,9 @@ struct Context {
       }
       R.pw.emplace(2 * s, std::move(t));
     }
-    if (deg == 0) return poly_acc(R, p.c, p.cheb, x.level, target);
+    if (deg == 0) return poly_acc(R, p.c, x.level, target);
     const int lo = x.level - depth;
-    Ciphertext out = poly_acc(R, p.c, p.cheb, lo + 1, target * (long double)mods[lo + 1]);
+    Ciphertext out = poly_acc(R, p.c, lo + 1, target * (long double)mods[lo + 1]);
     rescale_inplace(out);
     out.scale = target;
     return out;

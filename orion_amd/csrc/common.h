@@ -289,6 +289,10 @@ struct NttIO {
   int order;    // job decode: 0 = image fastest, 1 = limb fastest (mixes moduli inside a dispatch wave)
   int jobs;     // ncomp * nlimb * nbatch of dst
   int pro, epi;
+  // two-pass kernels, chunked: this launch covers jobs [job0, job0 + njob) and
+  // mid is a compact scratch of njob rows (row = job - job0), reused by every
+  // chunk so the intermediate can stay in the Infinity Cache
+  int job0, njob, mid_compact;
   u64 s[ORION_MAXLIMB], ss[ORION_MAXLIMB];
 };
 

@@ -41,6 +41,17 @@
 #ifndef NTT_LAZY
 #define NTT_LAZY 1
 #endif
+// timing switch: 1 = the forward kernel stores its last round directly (each
+// thread's 32 consecutive outputs as 16-B stores) instead of exchanging back
+// to the strided layout first
+#ifndef NTT_FWD_DIRECT
+#define NTT_FWD_DIRECT 0
+#endif
+// timing switch: 1 = the inverse kernel loads coalesced (element t + 1024 k)
+// and exchanges to the consecutive layout, instead of 16-B strided loads
+#ifndef NTT_INV_COAL
+#define NTT_INV_COAL 0
+#endif
 
 namespace {
 
@@ -244,8 +255,30 @@ __device__ __forceinline__ void ntt_fwd_body(const NttIO& io, int c, int l, int 
   u64 r[32];
 #pragma unroll
   for (int k = 0; k < 32; ++k) r[k] = ar.final_fwd(a[k]);
-  xchg<u64, LOGN, 0, B0>(r, lds, t);
   const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.dst, c, l, b), 0, N * 8, 0x00020000);
+  if constexpr (NTT_FWD_DIRECT) {  // thread t holds outputs 32 t .. 32 t + 31
+    if constexpr (EPI == NTT_EPI_STORE) {
+#pragma unroll
+      for (int k = 0; k < 32; k += 2) {
+        buf_st2(rd, r[k], r[k + 1], t * 256, k * 8);
+        if ((k & 7) == 6) NTT_FENCE();
+      }
+    } else {
+      const __amdgpu_buffer_rsrc_t rx =
+          __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.ex, c, l, b), 0, N * 8, 0x00020000);
+      const u64 s = io.s[l], ss = io.ss[l];
+#pragma unroll
+      for (int k = 0; k < 32; k += 2) {
+        u64 x, y;
+        buf_ld2(rx, x, y, t * 256, k * 8);
+        buf_st2(rd, shoup_mul(sub_mod(x, r[k], mc.q), s, ss, mc.q), shoup_mul(sub_mod(y, r[k + 1], mc.q), s, ss, mc.q),
+                t * 256, k * 8);
+        if ((k & 7) == 6) NTT_FENCE();
+      }
+    }
+    return;
+  }
+  xchg<u64, LOGN, 0, B0>(r, lds, t);
   if constexpr (EPI == NTT_EPI_STORE) {
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
@@ -271,12 +304,21 @@ __device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int 
   const int t = threadIdx.x;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.src, c, l, b), 0, N * 8, 0x00020000);
   typename A::T a[32];
+  if constexpr (NTT_INV_COAL) {
+    u64 x[32];
 #pragma unroll
-  for (int k = 0; k < 32; k += 2) {
-    u64 x, y;
-    buf_ld2(rs, x, y, t * 256, k * 8);
-    a[k] = ar.from_u64(x);
-    a[k + 1] = ar.from_u64(y);
+    for (int k = 0; k < 32; ++k) x[k] = buf_ld(rs, t * 8, (k << B0) * 8);
+    xchg<u64, LOGN, B0, 0>(x, lds, t);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) a[k] = ar.from_u64(x[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 32; k += 2) {
+      u64 x, y;
+      buf_ld2(rs, x, y, t * 256, k * 8);
+      a[k] = ar.from_u64(x);
+      a[k + 1] = ar.from_u64(y);
+    }
   }
   inv_round<A, LOGN, 0, 0, B1 - 1>(a, ar, w, t);
   reduce_all<A>(a, ar);

@@ -35,6 +35,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t twr(const void* t, int bytes) 
   return __builtin_amdgcn_make_buffer_rsrc((void*)t, 0, bytes, 0x00020000);
 }
 
+// intermediate row of job (c, l, b): dst's geometry, or a compact scratch row
+__device__ __forceinline__ u64* mid_row(const NttIO& io, int job, int c, int l, int b) {
+  if (io.mid_compact) {
+    const unsigned r = __builtin_amdgcn_readfirstlane((unsigned)(job - io.job0));
+    return io.mid.p + (long long)r * io.mid.batch_stride;
+  }
+  return row_ptr(io.mid, c, l, b);
+}
+
 template <class A>
 __device__ __forceinline__ void reduce16(typename A::T (&a)[16], const A& ar) {
 #pragma unroll
@@ -50,7 +59,7 @@ __device__ __forceinline__ void reduce16(typename A::T (&a)[16], const A& ar) {
 //            stages d = LOGN-5 .. 8
 // ---------------------------------------------------------------------------
 template <class A, int LOGN, int PRO>
-__device__ __forceinline__ void fwd_cols(const NttIO& io, int c, int l, int b, int tile, const ModConst& mc,
+__device__ __forceinline__ void fwd_cols(const NttIO& io, int job, int c, int l, int b, int tile, const ModConst& mc,
                                          const A& ar, __amdgpu_buffer_rsrc_t tw, u64* lds, bool lazy,
                                          const DeviceTables* __restrict__ tb) {
   constexpr int R = LOGN - 8, RG = 1 << (R - 4), J = 1 << (R - 4), G = 16 / J;
@@ -96,7 +105,7 @@ __device__ __forceinline__ void fwd_cols(const NttIO& io, int c, int l, int b, i
         }
   }
   if (!lazy) reduce16<A>(a, ar);
-  u64* mid = row_ptr(io.mid, c, l, b);
+  u64* mid = mid_row(io, job, c, l, b);
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -108,12 +117,12 @@ __device__ __forceinline__ void fwd_cols(const NttIO& io, int c, int l, int b, i
 // jc + 16 i) then d = 3..0 (phase 2: columns 16 ig + j, ig = t & 15)
 // ---------------------------------------------------------------------------
 template <class A, int LOGN, int EPI>
-__device__ __forceinline__ void fwd_rows(const NttIO& io, int c, int l, int b, int tile, const ModConst& mc,
+__device__ __forceinline__ void fwd_rows(const NttIO& io, int job, int c, int l, int b, int tile, const ModConst& mc,
                                          const A& ar, __amdgpu_buffer_rsrc_t tw, u64* lds, bool lazy) {
   const int t = threadIdx.x, rr = t >> 4, jc = t & 15;
   const int row = tile * 16 + rr;
   typename A::T a[16];
-  const u64* mid = row_ptr(io.mid, c, l, b) + (row << 8);
+  const u64* mid = mid_row(io, job, c, l, b) + (row << 8);
 #pragma unroll
   for (int i = 0; i < 16; ++i) a[i] = from_bits<typename A::T>(mid[jc + 16 * i]);
 #pragma unroll
@@ -160,7 +169,7 @@ __device__ __forceinline__ void fwd_rows(const NttIO& io, int c, int l, int b, i
 // every other stage and every phase ends with a full reduction
 // ---------------------------------------------------------------------------
 template <class A, int LOGN>
-__device__ __forceinline__ void inv_rows(const NttIO& io, int c, int l, int b, int tile, const A& ar,
+__device__ __forceinline__ void inv_rows(const NttIO& io, int job, int c, int l, int b, int tile, const A& ar,
                                          __amdgpu_buffer_rsrc_t tw, u64* lds) {
   const int t = threadIdx.x, rr = t >> 4, jc = t & 15;
   const int row = tile * 16 + rr;
@@ -196,7 +205,7 @@ __device__ __forceinline__ void inv_rows(const NttIO& io, int c, int l, int b, i
               (k & 1) == 1);
   }
   reduce16<A>(a, ar);
-  u64* mid = row_ptr(io.mid, c, l, b) + (row << 8);
+  u64* mid = mid_row(io, job, c, l, b) + (row << 8);
 #pragma unroll
   for (int i = 0; i < 16; ++i) mid[jc + 16 * i] = to_bits(a[i]);
 }
@@ -204,13 +213,13 @@ __device__ __forceinline__ void inv_rows(const NttIO& io, int c, int l, int b, i
 // inverse, cols pass (second): stages d = 8..LOGN-5 (rows J (rg + RG g) + j),
 // then d = LOGN-4..LOGN-1 (rows rg + RG i, wave-uniform twiddles), times N^-1
 template <class A, int LOGN>
-__device__ __forceinline__ void inv_cols(const NttIO& io, int c, int l, int b, int tile, const A& ar,
+__device__ __forceinline__ void inv_cols(const NttIO& io, int job, int c, int l, int b, int tile, const A& ar,
                                          __amdgpu_buffer_rsrc_t tw, u64* lds) {
   constexpr int R = LOGN - 8, RG = 1 << (R - 4), J = 1 << (R - 4), G = 16 / J;
   const int t = threadIdx.x, cl = t & 15, rg = t >> 4;
   const int col = tile * 16 + cl;
   typename A::T a[16];
-  const u64* mid = row_ptr(io.mid, c, l, b);
+  const u64* mid = mid_row(io, job, c, l, b);
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -260,15 +269,16 @@ template <int LOGN, int PRO>
 __global__ void __launch_bounds__(N2<LOGN>::ATHREADS) ntt2_fwd_cols(NttIO io, const DeviceTables* __restrict__ tb) {
   __shared__ u64 lds[(1 << N2<LOGN>::R) * A_STRIDE];
   int c, l, b;
-  job_of(io, blockIdx.x >> 4, c, l, b);
+  const int job = io.job0 + (blockIdx.x >> 4);
+  job_of(io, job, c, l, b);
   const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
   const ModConst mc = tb->mc[mod];
   const bool lazy = mc.bar_k <= 41;
   if (mc.f64)
-    fwd_cols<F64Arith, LOGN, PRO>(io, c, l, b, blockIdx.x & 15, mc, F64Arith(mc), twr(tb->fwd_d[mod], (8 << LOGN)),
+    fwd_cols<F64Arith, LOGN, PRO>(io, job, c, l, b, blockIdx.x & 15, mc, F64Arith(mc), twr(tb->fwd_d[mod], (8 << LOGN)),
                                   lds, lazy, tb);
   else
-    fwd_cols<IntArith, LOGN, PRO>(io, c, l, b, blockIdx.x & 15, mc, IntArith(mc), twr(tb->fwd[mod], (16 << LOGN)),
+    fwd_cols<IntArith, LOGN, PRO>(io, job, c, l, b, blockIdx.x & 15, mc, IntArith(mc), twr(tb->fwd[mod], (16 << LOGN)),
                                   lds, true, tb);
 }
 
@@ -277,14 +287,15 @@ __global__ void __launch_bounds__(256) ntt2_fwd_rows(NttIO io, const DeviceTable
   __shared__ u64 lds[16 * B_STRIDE];
   constexpr int T = N2<LOGN>::BTILES;
   int c, l, b;
-  job_of(io, blockIdx.x / T, c, l, b);
+  const int job = io.job0 + blockIdx.x / T;
+  job_of(io, job, c, l, b);
   const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
   const ModConst mc = tb->mc[mod];
   if (mc.f64)
-    fwd_rows<F64Arith, LOGN, EPI>(io, c, l, b, blockIdx.x % T, mc, F64Arith(mc), twr(tb->fwd_d[mod], (8 << LOGN)),
+    fwd_rows<F64Arith, LOGN, EPI>(io, job, c, l, b, blockIdx.x % T, mc, F64Arith(mc), twr(tb->fwd_d[mod], (8 << LOGN)),
                                   lds, mc.bar_k <= 41);
   else
-    fwd_rows<IntArith, LOGN, EPI>(io, c, l, b, blockIdx.x % T, mc, IntArith(mc), twr(tb->fwd[mod], (16 << LOGN)),
+    fwd_rows<IntArith, LOGN, EPI>(io, job, c, l, b, blockIdx.x % T, mc, IntArith(mc), twr(tb->fwd[mod], (16 << LOGN)),
                                   lds, true);
 }
 
@@ -293,33 +304,38 @@ __global__ void __launch_bounds__(256) ntt2_inv_rows(NttIO io, const DeviceTable
   __shared__ u64 lds[16 * B_STRIDE];
   constexpr int T = N2<LOGN>::BTILES;
   int c, l, b;
-  job_of(io, blockIdx.x / T, c, l, b);
+  const int job = io.job0 + blockIdx.x / T;
+  job_of(io, job, c, l, b);
   const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
   const ModConst mc = tb->mc[mod];
   if (mc.f64)
-    inv_rows<F64Arith, LOGN>(io, c, l, b, blockIdx.x % T, F64Arith(mc), twr(tb->inv_d[mod], (8 << LOGN)), lds);
+    inv_rows<F64Arith, LOGN>(io, job, c, l, b, blockIdx.x % T, F64Arith(mc), twr(tb->inv_d[mod], (8 << LOGN)), lds);
   else
-    inv_rows<IntArith, LOGN>(io, c, l, b, blockIdx.x % T, IntArith(mc), twr(tb->inv[mod], (16 << LOGN)), lds);
+    inv_rows<IntArith, LOGN>(io, job, c, l, b, blockIdx.x % T, IntArith(mc), twr(tb->inv[mod], (16 << LOGN)), lds);
 }
 
 template <int LOGN>
 __global__ void __launch_bounds__(N2<LOGN>::ATHREADS) ntt2_inv_cols(NttIO io, const DeviceTables* __restrict__ tb) {
   __shared__ u64 lds[(1 << N2<LOGN>::R) * A_STRIDE];
   int c, l, b;
-  job_of(io, blockIdx.x >> 4, c, l, b);
+  const int job = io.job0 + (blockIdx.x >> 4);
+  job_of(io, job, c, l, b);
   const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
   const ModConst mc = tb->mc[mod];
   if (mc.f64)
-    inv_cols<F64Arith, LOGN>(io, c, l, b, blockIdx.x & 15, F64Arith(mc), twr(tb->inv_d[mod], (8 << LOGN)), lds);
+    inv_cols<F64Arith, LOGN>(io, job, c, l, b, blockIdx.x & 15, F64Arith(mc), twr(tb->inv_d[mod], (8 << LOGN)), lds);
   else
-    inv_cols<IntArith, LOGN>(io, c, l, b, blockIdx.x & 15, IntArith(mc), twr(tb->inv[mod], (16 << LOGN)), lds);
+    inv_cols<IntArith, LOGN>(io, job, c, l, b, blockIdx.x & 15, IntArith(mc), twr(tb->inv[mod], (16 << LOGN)), lds);
 }
 
 template <int LOGN>
 int launch2(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
-  const int jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
-  if (jobs == 0) return 0;
-  if (io.jobs != jobs) return -1;
+  const int total = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
+  if (total == 0) return 0;
+  if (io.jobs != total) return -1;
+  const int jobs = io.njob ? io.njob : total;
+  if (io.job0 < 0 || io.job0 + jobs > total) return -1;
+  if (io.mid_compact && io.mid.batch_stride < (1 << LOGN)) return -1;
   const dim3 ga(jobs * 16), ba(N2<LOGN>::ATHREADS), gb(jobs * N2<LOGN>::BTILES), bb(256);
   if (inverse) {
     if (io.pro != NTT_PRO_LOAD || io.epi != NTT_EPI_STORE) return -1;

@@ -138,6 +138,7 @@ def test_encrypt_parity(small):
 @pytest.mark.parametrize("cheb,coeffs", [
     (True, [0.1, 0.6, 0.0, -0.25, 0.05, 0.3, -0.02, 0.11]),                    # degree 7, depth 3
     (True, list(np.linspace(-0.4, 0.4, 16))),                                   # degree 15, depth 4
+    (True, list(0.3 * np.cos(np.arange(32)) / (1 + np.arange(32)))),           # degree 31, depth 5
     (False, [0.5, -1.0, 0.25, 0.125, -0.3, 0.2]),                               # monomial degree 5
     (False, [0.75, 0.5]),                                                       # degree 1
     (True, [0.375]),                                                            # degree 0
@@ -349,9 +350,15 @@ def test_n16_ops_parity(torch_cuda, oracle_mod):
         assert np.array_equal(res[i], orc.rescale(rot[i], level)), i
     # functional: encode -> encrypt -> square -> decrypt at N = 2^16
     vals = rng.standard_normal(orc.N // 2).astype(np.float32)
-    ct = lib.Encrypt(lib.Encode(list(vals), level, 1 << 40))
+    pt = lib.Encode(list(vals), level, 1 << 40)
+    # the encoder's FFT runs its 3 widest stages in registers at N = 2^16
+    assert np.array_equal(lib.export_plaintext(pt)[0],
+                          orc.encode(vals.astype(np.float64), 2.0 ** 40, list(range(level + 1))))
+    ct = lib.Encrypt(pt)
     sq = lib.MulRelinCiphertextNew(ct, ct)
     lib.Rescale(sq)
-    dec = np.array(lib.Decode(lib.Decrypt(sq)))
+    dp = lib.Decrypt(sq)
+    dec = lib.decode_f64(dp)[0]
+    assert np.array_equal(dec, orc.decode(lib.export_plaintext(dp)[0], level - 1, lib.GetCiphertextScaleF(sq)))
     assert np.abs(dec - vals.astype(np.float64) ** 2).max() < 1e-3
     lib.DeleteScheme()

@@ -203,7 +203,7 @@ def test_encrypt_pk_decrypts(ckks):
     assert np.abs(dec - v).max() < 1e-4
 
 
-@pytest.mark.parametrize("cheb,deg", [(True, 7), (True, 12), (False, 5), (False, 1)])
+@pytest.mark.parametrize("cheb,deg", [(True, 7), (True, 12), (True, 15), (False, 5), (False, 15), (False, 1)])
 def test_eval_poly_functional(ckks, cheb, deg):
     """The polynomial-evaluation restatement decrypts to p(x), consumes
     bitlen(deg) levels and lands on the target scale exactly."""

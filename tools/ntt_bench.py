@@ -23,6 +23,9 @@ def main():
     res = []
     kinds = [("f64(40-bit)", list(range(0, 8))), ("int(60-bit)", list(range(8, 16))),
              ("mix(5:3)", [8, 0, 1, 2, 3, 4, 9, 10])]
+    only = os.environ.get("KINDS")
+    if only:
+        kinds = [k for k in kinds if k[0].split("(")[0] in only.split(",")]
     for kind, mset in kinds:
         for jobs in [int(j) for j in os.environ.get("JOBS", "256,1024,4096").split(",")]:
             nl = len(mset)
