@@ -2230,9 +2230,33 @@ int EvaluatePolynomial(int ct, int poly, unsigned long outScale) {
   return c.cts.add(c.eval_poly(c.cts.get(ct), c.polys.get(poly), (long double)outScale));
   API_END(-1)
 }
-ArrayResultDouble GenerateMinimaxSignCoeffs(int*, int, int, int, int, int) {
-  g_last_error = "GenerateMinimaxSignCoeffs: not implemented in the HIP backend yet";
-  return ArrayResultDouble{nullptr, 0};
+// polyeval.go:91-167: composite minimax sign coefficients (compile-time, host),
+// cached per (degrees, prec, logalpha, logerr) like minimaxSignMap; the last
+// polynomial is mapped from [-1, 1] to [0, 1] (halved, + 0.5).  The Remez
+// restatement works in long double, whatever `prec` asks for.
+static std::map<std::string, std::vector<double>> g_minimax_cache;
+ArrayResultDouble GenerateMinimaxSignCoeffs(int* degrees, int n, int prec, int logalpha, int logerr, int debug) {
+  ArrayResultDouble r{nullptr, 0};
+  API_BEGIN
+  (void)debug;
+  std::vector<int> deg;
+  for (int i = 0; i < n; ++i) deg.push_back(degrees[i]);
+  if (deg.empty()) throw std::runtime_error("at least one degree is required");
+  std::string key;
+  for (int d : deg) key += std::to_string(d) + ",";
+  key += "|" + std::to_string(prec) + "|" + std::to_string(logalpha) + "|" + std::to_string(logerr);
+  auto it = g_minimax_cache.find(key);
+  if (it == g_minimax_cache.end()) {
+    std::vector<std::vector<double>> polys = minimax_sign_composite(deg, logalpha);
+    for (double& c : polys.back()) c /= 2;
+    polys.back()[0] += 0.5;
+    std::vector<double> flat;
+    for (auto& p : polys) flat.insert(flat.end(), p.begin(), p.end());
+    it = g_minimax_cache.emplace(key, flat).first;
+  }
+  r.Data = to_c_array<double, double>(it->second, &r.Length);
+  return r;
+  API_END(r)
 }
 void NewBootstrapper(int*, int, int) { g_last_error = "NewBootstrapper: bootstrapping is not implemented yet"; }
 int Bootstrap(int, int) {

@@ -222,3 +222,138 @@ int64_t Prng::gaussian(double sigma, double bound) {
 }
 
 }  // namespace orion
+
+namespace orion {
+// ---------------------------------------------------------------------------
+// composite minimax approximation of sign (polyeval.go:91-167 ->
+// Lattigo minimax.GenMinimaxCompositePolynomial), restated with the classic
+// Remez exchange in long double.  sign is odd, so each stage is an odd
+// Chebyshev series p(x) = sum_k c_k T_{2k+1}(x) fitted to 1 on [a, 1]; the
+// stage maps [a, 1] into [1 - e, 1 + e], and is divided by 1 + e so the next
+// stage works on [(1 - e) / (1 + e), 1].
+// ---------------------------------------------------------------------------
+namespace {
+typedef long double ld;
+
+ld cheb_odd_eval(const std::vector<ld>& c, ld x) {  // sum_k c_k T_{2k+1}(x)
+  ld t0 = 1, t1 = x, s = 0;
+  for (size_t n = 1, k = 0; k < c.size(); ++n) {
+    if (n & 1) s += c[k++] * t1;
+    const ld t2 = 2 * x * t1 - t0;
+    t0 = t1;
+    t1 = t2;
+  }
+  return s;
+}
+ld cheb_T(int n, ld x) {
+  ld t0 = 1, t1 = x;
+  if (n == 0) return t0;
+  for (int i = 1; i < n; ++i) {
+    const ld t2 = 2 * x * t1 - t0;
+    t0 = t1;
+    t1 = t2;
+  }
+  return t1;
+}
+// Gaussian elimination with partial pivoting, A is n x (n+1) augmented
+std::vector<ld> solve(std::vector<std::vector<ld>> A) {
+  const int n = (int)A.size();
+  for (int col = 0; col < n; ++col) {
+    int piv = col;
+    for (int r = col + 1; r < n; ++r)
+      if (fabsl(A[r][col]) > fabsl(A[piv][col])) piv = r;
+    std::swap(A[col], A[piv]);
+    if (A[col][col] == 0) throw std::runtime_error("minimax: singular Remez system");
+    for (int r = 0; r < n; ++r) {
+      if (r == col) continue;
+      const ld f = A[r][col] / A[col][col];
+      for (int k = col; k <= n; ++k) A[r][k] -= f * A[col][k];
+    }
+  }
+  std::vector<ld> x(n);
+  for (int i = 0; i < n; ++i) x[i] = A[i][n] / A[i][i];
+  return x;
+}
+// best odd approximation of degree <= deg of 1 on [a, 1]; returns coefficients, sets err
+std::vector<ld> remez_sign(int deg, ld a, ld& err) {
+  const int n = (deg - 1) / 2 + 1;  // odd terms T_1, T_3, ..., T_{2n-1}
+  std::vector<ld> xs(n + 1);
+  for (int i = 0; i <= n; ++i) xs[i] = (a + 1) / 2 - (1 - a) / 2 * cosl(3.14159265358979323846264338327950288L * i / n);
+  std::vector<ld> c(n, 0);
+  const int G = 4000 * n;
+  std::vector<ld> grid(G), eg(G);
+  for (int j = 0; j < G; ++j) grid[j] = (a + 1) / 2 - (1 - a) / 2 * cosl(3.14159265358979323846264338327950288L * j / (G - 1));
+  ld E = 0;
+  for (int it = 0; it < 100; ++it) {
+    std::vector<std::vector<ld>> A(n + 1, std::vector<ld>(n + 2));
+    for (int i = 0; i <= n; ++i) {
+      for (int k = 0; k < n; ++k) A[i][k] = cheb_T(2 * k + 1, xs[i]);
+      A[i][n] = (i & 1) ? -1 : 1;
+      A[i][n + 1] = 1;
+    }
+    std::vector<ld> sol = solve(A);
+    for (int k = 0; k < n; ++k) c[k] = sol[k];
+    E = fabsl(sol[n]);
+    // local extrema of e(x) = p(x) - 1 on the grid, refined by ternary search
+    for (int j = 0; j < G; ++j) eg[j] = cheb_odd_eval(c, grid[j]) - 1;
+    std::vector<ld> ex, ev;
+    for (int j = 0; j < G; ++j) {
+      const bool l = j == 0 || fabsl(eg[j]) >= fabsl(eg[j - 1]);
+      const bool r = j == G - 1 || fabsl(eg[j]) >= fabsl(eg[j + 1]);
+      if (!(l && r)) continue;
+      ld x = grid[j];
+      if (j > 0 && j < G - 1) {
+        ld lo = grid[j - 1], hi = grid[j + 1];
+        const ld sg = eg[j] >= 0 ? 1 : -1;
+        for (int t = 0; t < 60; ++t) {
+          const ld m1 = lo + (hi - lo) / 3, m2 = hi - (hi - lo) / 3;
+          if (sg * (cheb_odd_eval(c, m1) - 1) < sg * (cheb_odd_eval(c, m2) - 1))
+            lo = m1;
+          else
+            hi = m2;
+        }
+        x = (lo + hi) / 2;
+      }
+      const ld v = cheb_odd_eval(c, x) - 1;
+      if (!ex.empty() && ((v >= 0) == (ev.back() >= 0))) {  // same sign: keep the larger
+        if (fabsl(v) > fabsl(ev.back())) ex.back() = x, ev.back() = v;
+        continue;
+      }
+      ex.push_back(x);
+      ev.push_back(v);
+    }
+    while ((int)ex.size() > n + 1) {  // drop the smaller end extremum
+      if (fabsl(ev.front()) < fabsl(ev.back()))
+        ex.erase(ex.begin()), ev.erase(ev.begin());
+      else
+        ex.pop_back(), ev.pop_back();
+    }
+    ld emax = 0;
+    for (ld v : ev) emax = std::max(emax, fabsl(v));
+    err = emax;
+    if ((int)ex.size() < n + 1) break;  // cannot alternate further: keep the current solution
+    xs = ex;
+    if (emax - E <= 1e-12L * emax) break;
+  }
+  return c;
+}
+}  // namespace
+
+std::vector<std::vector<double>> minimax_sign_composite(const std::vector<int>& degrees, int logalpha) {
+  std::vector<std::vector<double>> out;
+  ld a = ldexpl(1.0L, -logalpha);
+  for (size_t i = 0; i < degrees.size(); ++i) {
+    const int d = degrees[i];
+    if (d < 1) throw std::runtime_error("minimax: degrees must be >= 1");
+    ld err = 0;
+    std::vector<ld> c = remez_sign(d, a, err);
+    if (!(err < 1)) throw std::runtime_error("minimax: degree too small for the interval");
+    const bool last = i + 1 == degrees.size();
+    std::vector<double> p(d + 1, 0.0);
+    for (size_t k = 0; k < c.size(); ++k) p[2 * k + 1] = (double)(last ? c[k] : c[k] / (1 + err));
+    out.push_back(p);
+    a = (1 - err) / (1 + err);
+  }
+  return out;
+}
+}  // namespace orion
