@@ -259,6 +259,38 @@ def test_linear_transform_parity(small):
     assert np.abs(dec - exp).max() < 1e-3
 
 
+def test_serialization_roundtrip(small):
+    """io_mode save/load paths (keygenerator.go:38-58, lineartransform.go:131-193):
+    secret key, a Galois key and an LT diagonal survive serialise -> drop ->
+    load bit for bit, and the reloaded transform gives the same ciphertext."""
+    lib, orc = small
+    sk = lib.export_secret_key()
+    blob, _ = lib.SerializeSecretKey()
+    lib.LoadSecretKey(blob)
+    assert np.array_equal(lib.export_secret_key(), sk)
+    g = int(lib.GaloisElement(5))
+    blob, _ = lib.GenerateAndSerializeRotationKey(g)
+    gk = lib.export_galois_key(g)
+    lib.RemoveRotationKeys()
+    lib.LoadRotationKey(blob, g)
+    assert np.array_equal(lib.export_galois_key(g), gk)
+    rng = np.random.default_rng(8)
+    slots, level = orc.N // 2, 3
+    idx = [0, 5, 40]
+    diags = rng.uniform(-1, 1, (len(idx), slots)).astype(np.float32)
+    lt = lib.GenerateLinearTransform(idx, list(diags.reshape(-1)), level, 2.0, "none")
+    lib.GenerateConsolidatedRotationKeys(lib.GetLinearTransformRotationKeys(lt))
+    ct = lib.Encrypt(lib.Encode(list(rng.standard_normal(slots).astype(np.float32)), level, 1 << 40))
+    ref = lib.export_ciphertext(lib.EvaluateLinearTransform(lt, ct))
+    blobs = {d: lib.SerializeDiagonal(lt, d)[0] for d in idx}
+    pts = {d: lib.export_lt_diagonal(lt, d, level) for d in idx}
+    lib.RemovePlaintextDiagonals(lt)
+    for d in idx:
+        lib.LoadPlaintextDiagonal(blobs[d], lt, d)
+        assert np.array_equal(lib.export_lt_diagonal(lt, d, level), pts[d])
+    assert np.array_equal(lib.export_ciphertext(lib.EvaluateLinearTransform(lt, ct)), ref)
+
+
 def test_lola_n13_end_to_end(torch_cuda):
     """The reference frontend's LoLA op stream (tests/golden/lola_n13_*) replayed
     through the C-ABI: decrypted output vs the cleartext PyTorch model, the
