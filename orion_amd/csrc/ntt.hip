@@ -52,6 +52,14 @@
 #ifndef NTT_INV_COAL
 #define NTT_INV_COAL 0
 #endif
+// scheduling windows: a sched_barrier after every NTT_FENCE_FWD (forward) /
+// NTT_FENCE_INV (inverse) butterflies bounds the live registers to <= 128
+#ifndef NTT_FENCE_FWD
+#define NTT_FENCE_FWD 4
+#endif
+#ifndef NTT_FENCE_INV
+#define NTT_FENCE_INV 2
+#endif
 
 namespace {
 
@@ -170,10 +178,10 @@ __device__ __forceinline__ void run_stage(typename A::T (&a)[32], typename A::W 
     PIN(a[k0], a[k1]);
     if constexpr (FWD) {
       ar.ct(a[k0], a[k1], W);
-      if ((pr & 3) == 3) NTT_FENCE();
+      if ((pr & (NTT_FENCE_FWD - 1)) == NTT_FENCE_FWD - 1) NTT_FENCE();
     } else {
       ar.gs(a[k0], a[k1], W, (S & 1) == 1);
-      if ((pr & 1) == 1) NTT_FENCE();
+      if ((pr & (NTT_FENCE_INV - 1)) == NTT_FENCE_INV - 1) NTT_FENCE();
     }
   }
 }
