@@ -17,6 +17,7 @@
 #include <string>
 #include <unordered_map>
 #include <vector>
+#include <complex>
 
 #include "../../include/orion_hip.h"
 #include "common.h"
@@ -47,6 +48,12 @@ int orion_launch_encode(const float* vals, int nvals, int B, double2* v, const d
 int orion_launch_decode(const LimbSet& x, const u64* garner, double scale, int logn, double2* v,
                         const double2* tw_fwd, double* out, const DeviceTables* tb, hipStream_t st);
 int orion_launch_enc_sample(const LimbSet& r, const EncSampler& sp, const DeviceTables* tb, int N, hipStream_t st);
+int orion_launch_encode_c(double2* v, int B, const double2* tw_inv, int logn, const LimbSet& out, double scale,
+                          const DeviceTables* tb, hipStream_t st);
+int orion_launch_modraise(const LimbSet& out, const LimbSet& in, const DeviceTables* tb, int N, hipStream_t st);
+
+static void bsgs_split(int rot, int slots, int N1, int* giant, int* baby);
+static int find_best_n1(const std::vector<int>& idx, int slots, int logMaxRatio);
 
 namespace orion {
 
@@ -930,9 +937,11 @@ struct Context {
     return out;
   }
 
-  Ciphertext rotate(const Ciphertext& a, int k) {
+  Ciphertext rotate(const Ciphertext& a, int k) { return apply_galois(a, galois_element(k)); }
+  // sigma_g(a): key switch of c1 with the Galois key of g, + c0, NTT-domain permutation
+  // (g = 2N - 1 is the complex conjugation of the slots)
+  Ciphertext apply_galois(const Ciphertext& a, u64 g) {
     const int level = a.level, B = a.poly.B;
-    const u64 g = galois_element(k);
     const Poly& key = galois_key(g);
     Poly t = alloc(2, level + 1, B);
     keyswitch(lsq(a.poly, 1, 1, level), level, B, key, t);
@@ -1423,6 +1432,279 @@ struct Context {
     return out;
   }
   HandlePool<PolyFn> polys;
+
+  // ---------------------------------------------------------------------------
+  // bootstrapping (bootstrapper.go:19-80), full slots:
+  //   ModRaise (level 0 -> top, t = m + q0 I) -> CoeffsToSlots (the special
+  //   inverse FFT's butterfly stages, merged into 3 BSGS transforms with
+  //   complex diagonals; the final bit reversal is skipped because EvalMod is
+  //   slot-wise and SlotsToCoeffs starts with the matching one) -> real and
+  //   imaginary parts (conjugation key) -> EvalMod (Chebyshev approximation of
+  //   cos(2 pi (x - 1/4) / 2^r) on [-(K+1), K+1], then r double angles, giving
+  //   sin(2 pi x) = 2 pi m / q0 + O(m^3)) -> recombination (x i as X^(N/2)) ->
+  //   SlotsToCoeffs (forward FFT stages, 3 transforms) -> the input scale.
+  // The transforms use the scheme's own chain from the top: 3 CoeffsToSlots
+  // levels, depth(poly) + r EvalMod levels, 3 SlotsToCoeffs levels.
+  // ---------------------------------------------------------------------------
+  typedef std::complex<double> cplx;
+  typedef std::map<int, std::vector<cplx>> DiagMap;  // rotation offset -> diagonal (n slots)
+
+  Plaintext encode_complex(const std::vector<cplx>& v, int level, long double scale, bool qp) {
+    const int n = N / 2;
+    std::vector<int> md = iota(0, level + 1);
+    if (qp)
+      for (int k = 0; k < K; ++k) md.push_back(L + k);
+    const int nl = (int)md.size();
+    Plaintext pt;
+    pt.level = level;
+    pt.scale = scale;
+    pt.qp = qp;
+    pt.poly = alloc(1, nl, 1);
+    std::vector<double2> host(n);
+    for (int i = 0; i < n; ++i) host[i] = make_double2(v[i].real(), v[i].imag());
+    Buffer dv(&pool, (size_t)n * sizeof(double2));
+    HIPCHK(hipMemcpyAsync(dv.p, host.data(), host.size() * sizeof(double2), hipMemcpyHostToDevice, stream));
+    const LimbSet out = ls(pt.poly, 0, 1, iota(0, nl), md);
+    if (orion_launch_encode_c((double2*)dv.p, 1, tw_inv, logN - 1, out, (double)scale, d_tb, stream))
+      throw std::runtime_error("encode launch failed");
+    HIPCHK(hipStreamSynchronize(stream));
+    ntt(out, false);
+    return pt;
+  }
+  // BSGS transform y = sum_d diag_d * rot(x, d) with complex diagonals encoded at scale q_level
+  LinTrans make_lt_complex(const DiagMap& dm, int level) {
+    const int slots = N / 2;
+    LinTrans T;
+    T.level = level;
+    T.ratio = 2;
+    for (auto& kv : dm) T.idx.push_back(kv.first);
+    T.N1 = find_best_n1(T.idx, slots, 0);
+    std::set<int> seenb;
+    for (int d : T.idx) {
+      int gi, bi;
+      bsgs_split(d, slots, T.N1, &gi, &bi);
+      T.index[gi].push_back(bi);
+      if (!seenb.count(bi)) {
+        seenb.insert(bi);
+        T.babies.push_back(bi);
+      }
+    }
+    for (auto& kv : T.index) {
+      std::sort(kv.second.begin(), kv.second.end());
+      T.giants.push_back(kv.first);
+    }
+    std::vector<cplx> vec(slots);
+    for (auto& kv : dm) {
+      int gi, bi;
+      bsgs_split(kv.first, slots, T.N1, &gi, &bi);
+      for (int s2 = 0; s2 < slots; ++s2) vec[s2] = kv.second[((s2 - gi) % slots + slots) % slots];
+      T.diags[kv.first & (slots - 1)] = encode_complex(vec, level, (long double)mods[level], true);
+    }
+    return T;
+  }
+  // one butterfly stage of the special FFT as a diagonal map (offsets mod n)
+  DiagMap fft_stage(int len, bool inverse, const std::vector<Cplx>& tw) const {
+    const int n = N / 2, h = len / 2;
+    DiagMap m;
+    auto at = [&](int off) -> std::vector<cplx>& {
+      auto it = m.find(off);
+      if (it == m.end()) it = m.emplace(off, std::vector<cplx>(n, cplx(0, 0))).first;
+      return it->second;
+    };
+    std::vector<cplx>&d0 = at(0), &dp = at(h), &dm = at(n - h);
+    for (int p = 0; p < n; ++p) {
+      const int j = p & (len - 1);
+      if (j < h) {
+        const cplx w = inverse ? cplx(1, 0) : cplx(tw[h + j].re, tw[h + j].im);
+        d0[p] += 1.0;
+        dp[p] += w;  // x_{p+h}
+      } else {
+        const cplx w(tw[h + j - h].re, tw[h + j - h].im);
+        if (inverse) {  // (x_{p-h} - x_p) w
+          dm[p] += w;
+          d0[p] -= w;
+        } else {  // x_{p-h} - w x_p
+          dm[p] += 1.0;
+          d0[p] -= w;
+        }
+      }
+    }
+    return m;
+  }
+  // (A o B): apply B, then A
+  DiagMap diag_compose(const DiagMap& A, const DiagMap& Bm) const {
+    const int n = N / 2;
+    DiagMap C;
+    for (auto& a : A)
+      for (auto& b : Bm) {
+        const int off = (a.first + b.first) % n;
+        auto it = C.find(off);
+        if (it == C.end()) it = C.emplace(off, std::vector<cplx>(n, cplx(0, 0))).first;
+        for (int p = 0; p < n; ++p) it->second[p] += a.second[p] * b.second[(p + a.first) % n];
+      }
+    return C;
+  }
+  struct Bootstrapper {
+    int K = 0, r = 3, degree = 63;
+    PolyFn cosp;
+    std::vector<LinTrans> cts, stc;  // in application order
+    int top = 0;
+    Poly mono_i;      // NTT of X^(N/2) (x i on every slot), all Q limbs
+    long double s_y = 0;  // scale of the EvalMod output
+    u64 F = 1;        // message pre-scaling before ModRaise: F m ~ q0 / 2^12 at the default scale
+  };
+  std::unique_ptr<Bootstrapper> btp;
+
+  void new_bootstrapper() {
+    const int n = N / 2, logn = logN - 1;
+    auto B = std::unique_ptr<Bootstrapper>(new Bootstrapper());
+    // EvalMod range from the secret's Hamming weight: I ~ N(0, (h+1)/12) per coefficient
+    B->K = (int)ceil(6.0 * sqrt((h + 1) / 12.0)) + 2;
+    // Chebyshev interpolation of cos(2 pi ((K+1) u - 1/4) / 2^r) at degree+1 nodes on [-1, 1]
+    {
+      const int d = B->degree, m = d + 1;
+      const long double PI = 3.14159265358979323846264338327950288L;
+      std::vector<long double> fx(m), c(m, 0);
+      for (int k = 0; k < m; ++k) {
+        const long double u = cosl(PI * (k + 0.5L) / m);
+        fx[k] = cosl(2 * PI * ((B->K + 1) * u - 0.25L) / (long double)(1 << B->r));
+      }
+      for (int j = 0; j < m; ++j) {
+        long double acc = 0;
+        for (int k = 0; k < m; ++k) acc += fx[k] * cosl(PI * j * (k + 0.5L) / m);
+        c[j] = acc * (j == 0 ? 1.0L : 2.0L) / m;
+      }
+      B->cosp.cheb = true;
+      B->cosp.c = c;
+    }
+    int depth_poly = 0;
+    while ((1 << depth_poly) <= B->degree) ++depth_poly;
+    const int need = 3 + depth_poly + B->r + 3;
+    if (L - 1 < need) throw std::runtime_error("bootstrapping needs " + std::to_string(need) + " levels above level 0");
+    B->top = L - 1;
+    {  // EvalMod sees x = F m / q0 + I: raise the message to ~2^-12 of q0 (sin x ~ x to 2^-22)
+      const int lg = (63 - __builtin_clzll(mods[0])) - logScale - 12;
+      B->F = lg > 0 ? (1ull << lg) : 1;
+    }
+    // merged FFT stage groups: 3 groups, stages split as evenly as possible
+    const std::vector<Cplx> twi = special_fft_twiddles(logN, true), twf = special_fft_twiddles(logN, false);
+    auto groups = [&](bool inverse) {
+      std::vector<std::vector<int>> g(3);
+      std::vector<int> lens;
+      for (int len = inverse ? n : 2; inverse ? len >= 2 : len <= n; len = inverse ? len / 2 : len * 2) lens.push_back(len);
+      int at = 0;
+      for (int k = 0; k < 3; ++k) {
+        const int cnt = (int)(lens.size() - at) / (3 - k);
+        for (int i = 0; i < cnt; ++i) g[k].push_back(lens[at++]);
+      }
+      return g;
+    };
+    // CoeffsToSlots: slots of t / q0 -> bitrev((t_j + i t_{j+n}) / q0) / (2 (K+1)); the 1/n of the
+    // inverse transform and the 1 / (2 (K+1)) of EvalMod's input fold into the first group
+    {
+      auto g = groups(true);
+      int level = B->top;
+      for (int k = 0; k < 3; ++k) {
+        DiagMap M;
+        M[0] = std::vector<cplx>(n, cplx(k == 0 ? 1.0 / ((double)n * 2.0 * (B->K + 1)) : 1.0, 0));
+        for (int len : g[k]) M = diag_compose(fft_stage(len, true, twi), M);
+        B->cts.push_back(make_lt_complex(M, level--));
+      }
+      (void)logn;
+    }
+    // scale of the EvalMod output (simulated: CtS keeps scale q0, poly lands on 2^60 exactly)
+    {
+      const int lvl_poly = B->top - 3 - depth_poly;
+      long double sc = ldexpl(1.0L, 60);
+      int lv = lvl_poly;
+      for (int k = 0; k < B->r; ++k) sc = sc * sc / (long double)mods[lv--];
+      B->s_y = sc;
+      // SlotsToCoeffs: forward stages, c = q0 / (2 pi s_y) folded into the first group so
+      // the output decodes at the input scale
+      auto g = groups(false);
+      int level = lv;
+      const long double PI = 3.14159265358979323846264338327950288L;
+      const double cst = (double)((long double)mods[0] / (2 * PI * (long double)B->F * sc));
+      for (int k = 0; k < 3; ++k) {
+        DiagMap M;
+        M[0] = std::vector<cplx>(n, cplx(k == 0 ? cst : 1.0, 0));
+        for (int len : g[k]) M = diag_compose(fft_stage(len, false, twf), M);
+        B->stc.push_back(make_lt_complex(M, level--));
+      }
+    }
+    // x i on every slot = multiplication by X^(N/2)
+    {
+      B->mono_i = alloc(1, L, 1);
+      std::vector<u64> host((size_t)L * N, 0);
+      for (int l = 0; l < L; ++l) host[(size_t)l * N + N / 2] = 1;
+      upload(B->mono_i, host);
+      ntt(lsq(B->mono_i, 0, 1, L - 1), false);
+    }
+    btp = std::move(B);
+  }
+
+  Ciphertext mul_i(const Ciphertext& a) {
+    Ciphertext o = new_ct(a.level, a.poly.B, a.scale);
+    LimbSet mi = ls(btp->mono_i, 0, 1, iota(0, a.level + 1), iota(0, a.level + 1), a.poly.B);
+    mi.ncomp = 2;
+    mi.comp_stride = 0;  // one plaintext for both components
+    ew(EW_MUL, lsq(o.poly, 0, 2, a.level), lsq(a.poly, 0, 2, a.level), mi);
+    return o;
+  }
+  Ciphertext lt_rescale(LinTrans& T, const Ciphertext& x) {
+    Ciphertext y = eval_lt(T, x);
+    rescale_inplace(y);
+    y.scale = x.scale;  // diagonals at scale q_level
+    return y;
+  }
+  Ciphertext eval_mod(const Ciphertext& u) {
+    Ciphertext y = eval_poly(u, btp->cosp, ldexpl(1.0L, 60));
+    for (int k = 0; k < btp->r; ++k) {  // cos(2a) = 2 cos(a)^2 - 1
+      Ciphertext t = mul_relin(y, y);
+      rescale_inplace(t);
+      const LimbSet lt = lsq(t.poly, 0, 2, t.level);
+      ew(EW_ADD, lt, lt, lt);
+      std::vector<u64> one = big_const_residues(-t.scale, t.level);
+      ew1(EW_ADDC, lsq(t.poly, 0, 1, t.level), lsq(t.poly, 0, 1, t.level), &one);
+      y = std::move(t);
+    }
+    return y;
+  }
+  Ciphertext bootstrap(const Ciphertext& in) {
+    if (!btp) throw std::runtime_error("no bootstrapper: call NewBootstrapper first");
+    const int B = in.poly.B;
+    // ModRaise: level-0 residues (coefficient domain) lifted to every Q limb
+    Poly c0 = alloc(2, 1, B);
+    ntt_io(nio(lsq(c0, 0, 2, 0), lsq(in.poly, 0, 2, 0)), true);
+    if (btp->F > 1) {
+      std::vector<u64> f{btp->F % mods[0]};
+      ew1(EW_SCALE, lsq(c0, 0, 2, 0), lsq(c0, 0, 2, 0), &f);
+    }
+    Ciphertext t = new_ct(L - 1, B, (long double)mods[0]);
+    const LimbSet tl = lsq(t.poly, 0, 2, L - 1);
+    if (orion_launch_modraise(tl, lsq(c0, 0, 2, 0), d_tb, N, stream)) throw std::runtime_error("modraise failed");
+    ntt(tl, false);
+    // CoeffsToSlots
+    Ciphertext z = lt_rescale(btp->cts[0], t);
+    z = lt_rescale(btp->cts[1], z);
+    z = lt_rescale(btp->cts[2], z);
+    // real and imaginary parts: z + conj z, -i (z - conj z)
+    Ciphertext zc = apply_galois(z, 2 * (u64)N - 1);
+    Ciphertext re = new_ct(z.level, B, z.scale), im = new_ct(z.level, B, z.scale);
+    ew(EW_ADD, lsq(re.poly, 0, 2, z.level), lsq(z.poly, 0, 2, z.level), lsq(zc.poly, 0, 2, z.level));
+    ew(EW_SUB, lsq(im.poly, 0, 2, z.level), lsq(zc.poly, 0, 2, z.level), lsq(z.poly, 0, 2, z.level));
+    im = mul_i(im);  // (conj z - z) i = -i (z - conj z)
+    // EvalMod on both
+    Ciphertext yr = eval_mod(re), yi = eval_mod(im);
+    Ciphertext y = mul_i(yi);
+    ew(EW_ADD, lsq(y.poly, 0, 2, y.level), lsq(y.poly, 0, 2, y.level), lsq(yr.poly, 0, 2, y.level));
+    // SlotsToCoeffs
+    Ciphertext o = lt_rescale(btp->stc[0], y);
+    o = lt_rescale(btp->stc[1], o);
+    o = lt_rescale(btp->stc[2], o);
+    o.scale = in.scale;
+    return o;
+  }
 };
 
 static std::unique_ptr<Context> g;
@@ -2258,12 +2540,33 @@ ArrayResultDouble GenerateMinimaxSignCoeffs(int* degrees, int n, int prec, int l
   return r;
   API_END(r)
 }
-void NewBootstrapper(int*, int, int) { g_last_error = "NewBootstrapper: bootstrapping is not implemented yet"; }
-int Bootstrap(int, int) {
-  g_last_error = "Bootstrap: bootstrapping is not implemented in the HIP backend yet";
-  return -1;
+// bootstrapper.go:19-58.  The transforms run on the scheme's own modulus chain
+// (its top 3 + depth(EvalMod) + 3 levels), so logPs (extra key-switching
+// primes of Lattigo's extended bootstrapping chain) is not used; full slots only.
+void NewBootstrapper(int* logPs, int n, int slots) {
+  API_BEGIN
+  (void)logPs;
+  (void)n;
+  Context& c = ctx();
+  if (slots != c.N / 2)
+    throw std::runtime_error("bootstrapping supports full slots (" + std::to_string(c.N / 2) + ") only");
+  if (!c.btp) c.new_bootstrapper();
+  API_END_VOID
 }
-void DeleteBootstrappers(void) {}
+// bootstrapper.go:61-80: a new ciphertext refreshed to the level below the
+// bootstrapping circuit, at the input's scale
+int Bootstrap(int ct, int slots) {
+  API_BEGIN
+  Context& c = ctx();
+  if (slots != c.N / 2) throw std::runtime_error("bootstrapping supports full slots only");
+  return c.cts.add(c.bootstrap(c.cts.get(ct)));
+  API_END(-1)
+}
+void DeleteBootstrappers(void) {
+  API_BEGIN
+  if (g) g->btp.reset();
+  API_END_VOID
+}
 
 // ---- import / export ----
 static void to_canonical(const std::vector<u64>& dev, int ncomp, int nl, int B, int N, unsigned long* out) {

@@ -229,6 +229,24 @@ __global__ void dec_out_kernel(const double2* __restrict__ v, double* __restrict
   if (i < total) out[i] = v[i].x;
 }
 
+// bootstrapping ModRaise: coefficient-domain residues mod q0 (row (c, 0, b) of
+// in) -> centred integers in (-q0/2, q0/2] -> residues of every limb of out
+__global__ void modraise_kernel(LimbSet out, LimbSet in, const DeviceTables* __restrict__ tb, int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const int b = blockIdx.y % out.nbatch, c = blockIdx.y / out.nbatch;
+  const u64 q0 = tb->mc[in.mod[0]].q;
+  const u64 x = in.p[(size_t)c * in.comp_stride + (size_t)in.pos[0] * in.limb_stride + (size_t)b * in.batch_stride + i];
+  const bool neg = x > (q0 >> 1);
+  const u64 a = neg ? q0 - x : x;
+  u64* o = out.p + (size_t)c * out.comp_stride + (size_t)b * out.batch_stride + i;
+  for (int l = 0; l < out.nlimb; ++l) {
+    const u64 q = tb->mc[out.mod[l]].q;
+    const u64 r = a % q;
+    o[(size_t)out.pos[l] * out.limb_stride] = neg ? (r ? q - r : 0) : r;
+  }
+}
+
 // ---- ChaCha20 (RFC 8439 §2.3) ----
 __device__ __forceinline__ u32 rotl32(u32 x, int k) { return (x << k) | (x >> (32 - k)); }
 #define CHACHA_QR(a, b, c, d) \
@@ -338,7 +356,22 @@ int orion_launch_decode(const LimbSet& x, const u64* garner, double scale, int l
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// complex slots already in v ([B][n] double2, overwritten): FFT + CRT (no load step)
+int orion_launch_encode_c(double2* v, int B, const double2* tw_inv, int logn, const LimbSet& out, double scale,
+                          const DeviceTables* tb, hipStream_t st) {
+  const int n = 1 << logn;
+  if (fft_run(v, tw_inv, logn, B, true, st)) return -1;
+  enc_crt_kernel<<<dim3((unsigned)((2 * n + 255) / 256), (unsigned)B), 256, 0, st>>>(v, out, scale, 1.0 / (double)n,
+                                                                                    logn, tb);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int orion_launch_enc_sample(const LimbSet& r, const EncSampler& sp, const DeviceTables* tb, int N, hipStream_t st) {
   enc_sample_kernel<<<dim3((unsigned)((N / 8 + 255) / 256), (unsigned)r.nbatch, 3), 256, 0, st>>>(r, sp, tb, N);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int orion_launch_modraise(const LimbSet& out, const LimbSet& in, const DeviceTables* tb, int N, hipStream_t st) {
+  modraise_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)(out.ncomp * out.nbatch)), 256, 0, st>>>(out, in, tb, N);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
