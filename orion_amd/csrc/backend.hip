@@ -1551,7 +1551,7 @@ struct Context {
     int top = 0;
     Poly mono_i;      // NTT of X^(N/2) (x i on every slot), all Q limbs
     long double s_y = 0;  // scale of the EvalMod output
-    u64 F = 1;        // message pre-scaling before ModRaise: F m ~ q0 / 2^12 at the default scale
+    u64 F = 1;        // message pre-scaling before ModRaise: F m <= q0 / 2^9 at the default scale
   };
   std::unique_ptr<Bootstrapper> btp;
 
@@ -1582,8 +1582,8 @@ struct Context {
     const int need = 3 + depth_poly + B->r + 3;
     if (L - 1 < need) throw std::runtime_error("bootstrapping needs " + std::to_string(need) + " levels above level 0");
     B->top = L - 1;
-    {  // EvalMod sees x = F m / q0 + I: raise the message to ~2^-12 of q0 (sin x ~ x to 2^-22)
-      const int lg = (63 - __builtin_clzll(mods[0])) - logScale - 12;
+    {  // EvalMod sees x = F m / q0 + I: raise the message to <= 2^-9 of q0 (sin 2 pi x ~ 2 pi x to 3e-5)
+      const int lg = (63 - __builtin_clzll(mods[0])) - logScale - 9;
       B->F = lg > 0 ? (1ull << lg) : 1;
     }
     // merged FFT stage groups: 3 groups, stages split as evenly as possible
@@ -1599,14 +1599,17 @@ struct Context {
       }
       return g;
     };
-    // CoeffsToSlots: slots of t / q0 -> bitrev((t_j + i t_{j+n}) / q0) / (2 (K+1)); the 1/n of the
-    // inverse transform and the 1 / (2 (K+1)) of EvalMod's input fold into the first group
+    // CoeffsToSlots: slots of t / q0 -> bitrev((t_j + i t_{j+n}) / q0) / (2 (K+1)).  The 1/n of
+    // the inverse transform and EvalMod's 1 / (2 (K+1)) are spread over the groups (2^-r per
+    // group of r stages, the cube root of 1 / (2 (K+1)) each), so no diagonal is small against
+    // the fixed-point grid of its encoding
     {
       auto g = groups(true);
       int level = B->top;
+      const double kf = cbrt(1.0 / (2.0 * (B->K + 1)));
       for (int k = 0; k < 3; ++k) {
         DiagMap M;
-        M[0] = std::vector<cplx>(n, cplx(k == 0 ? 1.0 / ((double)n * 2.0 * (B->K + 1)) : 1.0, 0));
+        M[0] = std::vector<cplx>(n, cplx(ldexp(kf, -(int)g[k].size()), 0));
         for (int len : g[k]) M = diag_compose(fft_stage(len, true, twi), M);
         B->cts.push_back(make_lt_complex(M, level--));
       }
@@ -1619,15 +1622,16 @@ struct Context {
       int lv = lvl_poly;
       for (int k = 0; k < B->r; ++k) sc = sc * sc / (long double)mods[lv--];
       B->s_y = sc;
-      // SlotsToCoeffs: forward stages, c = q0 / (2 pi s_y) folded into the first group so
-      // the output decodes at the input scale
+      // SlotsToCoeffs: forward stages times c = q0 / (2 pi F s_y), so the output decodes at
+      // the input scale
       auto g = groups(false);
       int level = lv;
       const long double PI = 3.14159265358979323846264338327950288L;
       const double cst = (double)((long double)mods[0] / (2 * PI * (long double)B->F * sc));
+      const double cf = cbrt(cst);  // spread like CoeffsToSlots' constant
       for (int k = 0; k < 3; ++k) {
         DiagMap M;
-        M[0] = std::vector<cplx>(n, cplx(k == 0 ? cst : 1.0, 0));
+        M[0] = std::vector<cplx>(n, cplx(cf, 0));
         for (int len : g[k]) M = diag_compose(fft_stage(len, false, twf), M);
         B->stc.push_back(make_lt_complex(M, level--));
       }

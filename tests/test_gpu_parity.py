@@ -394,3 +394,51 @@ def test_n16_ops_parity(torch_cuda, oracle_mod):
     assert np.array_equal(dec, orc.decode(lib.export_plaintext(dp)[0], level - 1, lib.GetCiphertextScaleF(sq)))
     assert np.abs(dec - vals.astype(np.float64) ** 2).max() < 1e-3
     lib.DeleteScheme()
+
+
+BTP_LOGQ = [60] + [40] * 5 + [60] * 9 + [55] * 3  # residual 3 + SlotsToCoeffs 3 | EvalMod 9 | CoeffsToSlots 3
+
+
+@pytest.mark.parametrize("h", [32, 192])
+def test_bootstrap_functional(torch_cuda, h):
+    """Bootstrap (bootstrapper.go:19-80) of a level-0 batch: the refreshed
+    ciphertext sits 15 levels below the top (3 CoeffsToSlots + 6 polynomial + 3
+    double-angle + 3 SlotsToCoeffs), keeps the input scale exactly and
+    decrypts to the input.  Parity with Lattigo's bootstrapper is unpinned
+    (different circuit parameters); the bar is the functional one."""
+    from orion_amd.backend import HipLibrary
+    lib = HipLibrary().new_scheme(13, BTP_LOGQ, [60, 60], 40, h=h, seed=5)
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    n = lib.N // 2
+    with pytest.raises(RuntimeError, match="full slots"):
+        lib.NewBootstrapper([61, 61], n // 2)
+    lib.NewBootstrapper([61, 61], n)
+    rng = np.random.default_rng(h)
+    vals = rng.uniform(-1, 1, (2, n)).astype(np.float32)
+    ct = lib.Encrypt(lib.encode_batch(vals, 0, 1 << 40))
+    out = lib.Bootstrap(ct, n)
+    assert lib.GetCiphertextLevel(out) == len(BTP_LOGQ) - 1 - 15
+    assert lib.GetCiphertextScaleF(out) == 2.0 ** 40
+    dec = lib.decode_f64(lib.Decrypt(out))
+    err = np.abs(dec - vals.astype(np.float64))
+    assert err.max() < 1e-5 and err.mean() < 1e-6, (err.max(), err.mean())  # measured ~6e-8 / 1.4e-8
+    # the refreshed ciphertext computes: square and rescale
+    sq = lib.MulRelinCiphertextNew(out, out)
+    lib.Rescale(sq)
+    d2 = lib.decode_f64(lib.Decrypt(sq))
+    assert np.abs(d2 - vals.astype(np.float64) ** 2).max() < 1e-4
+    lib.DeleteBootstrappers()
+    with pytest.raises(RuntimeError, match="no bootstrapper"):
+        lib.Bootstrap(ct, n)
+    lib.DeleteScheme()
+
+
+def test_bootstrap_needs_levels(torch_cuda):
+    from orion_amd.backend import HipLibrary
+    lib = HipLibrary().new_scheme(13, [60] + [40] * 8, [60, 60], 40, h=32, seed=6)
+    lib.GenerateSecretKey()
+    with pytest.raises(RuntimeError, match="levels"):
+        lib.NewBootstrapper([61, 61], lib.N // 2)
+    lib.DeleteScheme()

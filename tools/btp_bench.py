@@ -1,0 +1,52 @@
+"""Bootstrapping latency/throughput on the GPU: full-slot
+Bootstrap of B level-0 ciphertexts at N = 2^LOGN on a chain with
+residual 3 + SlotsToCoeffs 3 (40-bit), EvalMod 9 (60-bit), CoeffsToSlots 3
+(55-bit) levels.  Prints one JSON line per batch size (keys already generated:
+the first call generates the rotation keys and is not timed)."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from orion_amd.backend import HipLibrary  # noqa: E402
+
+
+def main():
+    logn = int(os.environ.get("LOGN", 16))
+    logq = [60] + [40] * 5 + [60] * 9 + [55] * 3
+    lib = HipLibrary().new_scheme(logn, logq, [60, 60], 40, h=192, seed=9)
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    n = lib.N // 2
+    t0 = time.perf_counter()
+    lib.NewBootstrapper([61] * 8, n)
+    setup = time.perf_counter() - t0
+    rng = np.random.default_rng(0)
+    for B in [int(b) for b in os.environ.get("BATCH", "1,8").split(",")]:
+        vals = rng.uniform(-1, 1, (B, n)).astype(np.float32)
+        ct = lib.Encrypt(lib.encode_batch(vals, 0, 1 << 40))
+        lib.DeleteCiphertext(lib.Bootstrap(ct, n))  # warm: rotation keys, buffers
+        lib.OrionHipSynchronize()
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            out = lib.Bootstrap(ct, n)
+            lib.OrionHipSynchronize()
+            if _ < reps - 1:
+                lib.DeleteCiphertext(out)
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        dec = lib.decode_f64(lib.Decrypt(out))
+        err = np.abs(dec - vals.astype(np.float64))
+        print(json.dumps({"op": "Bootstrap (full slots)", "logN": logn, "h": 192, "batch": B,
+                          "ms_per_batch": round(ms, 2), "bootstraps_per_s": round(B / (ms / 1e3), 2),
+                          "levels_consumed": len(logq) - 1 - lib.GetCiphertextLevel(out),
+                          "max_abs_err": float(err.max()), "mean_abs_err": float(err.mean()),
+                          "setup_s": round(setup, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
