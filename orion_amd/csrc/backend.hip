@@ -383,10 +383,15 @@ struct Context {
   int ntt_impl = getenv("ORION_NTT_IMPL") ? atoi(getenv("ORION_NTT_IMPL")) : ORION_NTT_DEFAULT_IMPL;
   // two-pass kernels: limb-transforms per chunk (0 = one launch pair for all)
   int ntt2_chunk = getenv("ORION_NTT2_CHUNK") ? atoi(getenv("ORION_NTT2_CHUNK")) : 0;
+  // N = 2^15 launches with fewer limb-transforms than this use the two-pass
+  // kernels: one limb per CU leaves most of the 256 CUs idle there (8 jobs:
+  // 15 vs 37 us; 64 jobs: 32 vs 40 us, float64 path).  Batched launches
+  // (>= 128 jobs at 64 images) keep the one-pass kernel.
+  int ntt2_below = getenv("ORION_NTT2_BELOW") ? atoi(getenv("ORION_NTT2_BELOW")) : 128;
   void ntt_io(NttIO io, bool inv) {
     io.order = ntt_order;
     io.jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
-    if (logN == 16 || (ntt_impl == 2 && logN == 15)) {  // N = 2^16: the two-pass kernels only
+    if (logN == 16 || (logN == 15 && (ntt_impl == 2 || io.jobs < ntt2_below))) {  // N = 2^16: two-pass only
       Poly scratch;
       if (ntt2_chunk > 0 && io.jobs > 0) {  // chunks of jobs through one reused compact scratch
         const int chunk = std::min(ntt2_chunk, io.jobs);
