@@ -138,6 +138,10 @@ void NewBootstrapper(int *logPs, int n, int slots);                        /* bo
 int Bootstrap(int ct, int slots);                                          /* bootstrapper.go:61 */
 void DeleteBootstrappers(void);                                            /* bootstrapper.go:91 */
 
+/* ---- the fork's Python layer beyond the Lattigo set ---- */
+int ModDropCiphertext(int ct);     /* evaluator.py:30-41 (HEonGPU _ModDropCiphertext): drop the top modulus, in place */
+int GetPolyDepth(int poly);        /* poly_evaluator.py:58-59: levels EvaluatePolynomial consumes */
+
 /* ================= Part 2: MI355X extensions ================= */
 const char *OrionHipLastError(void);
 void OrionHipClearError(void);

@@ -126,6 +126,8 @@ SIGNATURES = {
     "LoadPlaintextDiagonal": ([P(ctypes.c_ubyte), c_ulong, c_int, c_ulong], None),
     "RemovePlaintextDiagonals": ([c_int], None),
     "RemoveRotationKeys": ([], None),
+    "ModDropCiphertext": ([c_int], c_int),
+    "GetPolyDepth": ([c_int], c_int),
     "NewBootstrapper": ([P(c_int), c_int, c_int], None),
     "Bootstrap": ([c_int, c_int], c_int),
     "DeleteBootstrappers": ([], None),
@@ -175,7 +177,7 @@ LATTIGO_SYMBOLS = [n for n in SIGNATURES if not n.startswith("OrionHip") and n n
     "GetCiphertextScaleF", "ImportCiphertext", "ExportCiphertext", "ImportPlaintext", "ExportPlaintext",
     "ExportSecretKey", "ExportPublicKey", "ExportRelinKey",
     "ExportGaloisKey", "ExportLinearTransformDiagonal", "GetLinearTransformN1", "GaloisElement",
-    "KeyBundleBytes", "ExportKeyBundle", "ImportKeyBundle")]
+    "KeyBundleBytes", "ExportKeyBundle", "ImportKeyBundle", "ModDropCiphertext", "GetPolyDepth")]
 
 
 def load_library(path=LIB_PATH):
@@ -270,6 +272,13 @@ class HipLibrary:
         self.lib = load_library(path)
         for name in SIGNATURES:
             setattr(self, name, HipFunction(self.lib, name))
+
+    # evaluator.py:30-41 calls the HEonGPU binding's private
+    # _ModDropCiphertext(arithmeticoperator_handle, ct, None)
+    arithmeticoperator_handle = None
+
+    def _ModDropCiphertext(self, handle, ct, _stream=None):
+        return self.ModDropCiphertext(ct)
 
     def setup_bindings(self, orion_params):
         """Same flow as LattigoLibrary.setup_bindings -> NewScheme (bindings.py:126-179)."""

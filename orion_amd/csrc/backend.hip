@@ -2116,6 +2116,17 @@ int RescaleNew(int id) {  // evaluator.go:92-99: rescales the input in place, re
   API_END(-1)
 }
 
+// evaluator.py:30-41 (the fork's HEonGPU-only mod_drop): drop the top modulus
+// in place, scale unchanged; returns the input id
+int ModDropCiphertext(int id) {
+  API_BEGIN
+  Ciphertext& a = ctx().cts.get(id);
+  if (a.level < 1) throw std::runtime_error("cannot drop the last modulus");
+  a.level -= 1;
+  return id;
+  API_END(-1)
+}
+
 static Ciphertext add_scalar(Context& c, const Ciphertext& a, float v, bool inplace_target, Ciphertext* dst) {
   (void)inplace_target;
   long double x = (long double)v * a.scale;
@@ -2512,6 +2523,15 @@ int GenerateMonomial(float* coeffs, int n) {
 int GenerateChebyshev(float* coeffs, int n) {
   API_BEGIN
   return add_poly(coeffs, n, true);
+  API_END(-1)
+}
+// poly_evaluator.py:58-59: levels an evaluation consumes, bits.Len64(degree)
+int GetPolyDepth(int poly) {
+  API_BEGIN
+  const int deg = (int)ctx().polys.get(poly).c.size() - 1;
+  int d = 0;
+  while ((1 << d) <= deg) ++d;
+  return d;
   API_END(-1)
 }
 // polyeval.go:63-84: a new ciphertext at level - bitlen(degree), scale outScale

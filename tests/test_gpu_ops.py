@@ -110,6 +110,20 @@ def test_ct_pt_ops(small):
     assert lib.GetCiphertextScaleF(mul) == 2.0 ** 80
 
 
+def test_mod_drop_and_poly_depth(small):
+    """evaluator.py:30-41 mod_drop through the HEonGPU-style private call, and
+    poly_evaluator.py:58-59 GetPolyDepth."""
+    lib, orc = small
+    rng = np.random.default_rng(25)
+    a = rand_ct(rng, orc.moduli, 4, orc.N, B=1)
+    ca = lib.import_ciphertext(a, 2.0 ** 40)
+    assert lib._ModDropCiphertext(lib.arithmeticoperator_handle, ca, None) == ca
+    assert lib.GetCiphertextLevel(ca) == 3 and lib.GetCiphertextScaleF(ca) == 2.0 ** 40
+    assert np.array_equal(lib.export_ciphertext(ca)[0], a[0][:, :4])
+    for deg, depth in [(0, 0), (1, 1), (7, 3), (8, 4), (31, 5)]:
+        assert lib.GetPolyDepth(lib.GenerateMonomial([0.5] * (deg + 1))) == depth
+
+
 def test_scale_matching_add(small):
     """Lower-scale operand multiplied by the integer scale ratio before the add."""
     lib, orc = small
