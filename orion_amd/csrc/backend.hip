@@ -455,14 +455,33 @@ struct Context {
     for (int b : logP)
       if (b > 61) throw std::runtime_error("moduli must be <= 61 bits");
     mods = gen_moduli(logN, logQ, logP);
+    logQ_bits = logQ;
+    logP_bits = logP;
     if (!stream) {
       HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
       own_stream = true;
     }
     orion_ntt_init();
     memset(&host_tb, 0, sizeof(host_tb));
+    for (int m = 0; m < L + K; ++m) build_mod_tables(m);
+    HIPCHK(hipMalloc(&d_tb, sizeof(DeviceTables)));
+    HIPCHK(hipMemcpy(d_tb, &host_tb, sizeof(DeviceTables), hipMemcpyHostToDevice));
+    for (int inv = 0; inv < 2; ++inv) {
+      const std::vector<Cplx> tw = special_fft_twiddles(logN, inv != 0);
+      void* d;
+      HIPCHK(hipMalloc(&d, tw.size() * sizeof(double2)));
+      HIPCHK(hipMemcpy(d, tw.data(), tw.size() * sizeof(double2), hipMemcpyHostToDevice));
+      static_bufs.push_back(d);
+      (inv ? tw_inv : tw_fwd) = (double2*)d;
+    }
+    memset(&enc_sampler, 0, sizeof(enc_sampler));
+    gauss_cdt(3.2, ORION_GAUSS_BOUND, enc_sampler.cdt);
+  }
+  std::vector<int> logQ_bits, logP_bits;
+  // per-modulus constants and NTT twiddle tables of QP index m (host_tb; device copy by the caller)
+  void build_mod_tables(int m) {
     std::vector<ulonglong2> fw(N), iv(N);
-    for (int m = 0; m < L + K; ++m) {
+    {
       const u64 q = mods[m];
       ModConst& mc = host_tb.mc[m];
       mc.q = q;
@@ -515,18 +534,68 @@ struct Context {
       host_tb.fwd[m] = (const ulonglong2*)dfw;
       host_tb.inv[m] = (const ulonglong2*)div;
     }
-    HIPCHK(hipMalloc(&d_tb, sizeof(DeviceTables)));
-    HIPCHK(hipMemcpy(d_tb, &host_tb, sizeof(DeviceTables), hipMemcpyHostToDevice));
-    for (int inv = 0; inv < 2; ++inv) {
-      const std::vector<Cplx> tw = special_fft_twiddles(logN, inv != 0);
-      void* d;
-      HIPCHK(hipMalloc(&d, tw.size() * sizeof(double2)));
-      HIPCHK(hipMemcpy(d, tw.data(), tw.size() * sizeof(double2), hipMemcpyHostToDevice));
-      static_bufs.push_back(d);
-      (inv ? tw_inv : tw_fwd) = (double2*)d;
+  }
+
+  // secret key coefficients (ternary) from its first limb
+  std::vector<int64_t> secret_coeffs() {
+    Poly t = alloc(1, 1, 1);
+    ntt_io(nio(ls(t, 0, 1, {0}, {0}), ls(sk, 0, 1, {0}, {0})), true);
+    std::vector<u64> host;
+    download(t, host);
+    std::vector<int64_t> s(N);
+    const u64 q0 = mods[0];
+    for (int i = 0; i < N; ++i) s[i] = host[i] > q0 / 2 ? -(int64_t)(q0 - host[i]) : (int64_t)host[i];
+    return s;
+  }
+  // append Q primes above the current top (Lattigo's bootstrapping chain sits
+  // above the residual chain).  P keeps its primes (the generator allocates
+  // per bit size in list order, so P is listed before the extension) and
+  // moves to the end of the index space; the secret key is re-expanded, the
+  // public/relinearisation keys are regenerated and Galois keys are dropped
+  // (regenerated on first use).  QP plaintexts stay valid: their P limbs hold
+  // the same primes and are addressed as L + k at use time.
+  void extend_chain(const std::vector<int>& ext) {
+    if (!have_sk) throw std::runtime_error("extending the modulus chain needs the secret key");
+    const int Lold = L, Lnew = L + (int)ext.size();
+    if (Lnew + K > ORION_MAXMOD || Lnew + K > ORION_MAXLIMB) throw std::runtime_error("modulus chain too long");
+    std::vector<int> bits = logQ_bits;
+    bits.insert(bits.end(), logP_bits.begin(), logP_bits.end());
+    bits.insert(bits.end(), ext.begin(), ext.end());
+    const std::vector<u64> g = gen_moduli(logN, bits, {});
+    std::vector<u64> nm(g.begin(), g.begin() + Lold);
+    nm.insert(nm.end(), g.begin() + Lold + K, g.end());
+    nm.insert(nm.end(), g.begin() + Lold, g.begin() + Lold + K);
+    for (int i = 0; i < Lold; ++i)
+      if (nm[i] != mods[i]) throw std::runtime_error("chain extension changed a Q prime");
+    for (int k = 0; k < K; ++k)
+      if (nm[Lnew + k] != mods[Lold + k]) throw std::runtime_error("chain extension changed a P prime");
+    const std::vector<int64_t> s = secret_coeffs();
+    HIPCHK(hipStreamSynchronize(stream));
+    const DeviceTables old = host_tb;
+    mods = nm;
+    L = Lnew;
+    dnum = (L + K - 1) / K;
+    logQ_bits.insert(logQ_bits.end(), ext.begin(), ext.end());
+    for (int k = 0; k < K; ++k) {
+      host_tb.mc[L + k] = old.mc[Lold + k];
+      host_tb.fwd[L + k] = old.fwd[Lold + k];
+      host_tb.inv[L + k] = old.inv[Lold + k];
+      host_tb.fwd_d[L + k] = old.fwd_d[Lold + k];
+      host_tb.inv_d[L + k] = old.inv_d[Lold + k];
     }
-    memset(&enc_sampler, 0, sizeof(enc_sampler));
-    gauss_cdt(3.2, ORION_GAUSS_BOUND, enc_sampler.cdt);
+    for (int m = Lold; m < L; ++m) build_mod_tables(m);
+    HIPCHK(hipMemcpy(d_tb, &host_tb, sizeof(DeviceTables), hipMemcpyHostToDevice));
+    for (auto& kv : betab) hipFree(kv.second);
+    betab.clear();
+    betab_pos.clear();
+    sk = alloc(1, L + K, 1);
+    std::vector<u64> host((size_t)(L + K) * N);
+    small_residues(s, iota(0, L + K), host.data());
+    upload(sk, host);
+    ntt(ls(sk, 0, 1, iota(0, L + K), iota(0, L + K)), false);
+    gks.clear();
+    if (have_pk) gen_public();
+    if (have_rlk) gen_relin();
   }
   // encryption randomness: ChaCha20 key from the seed, encryption index 0
   void seed_encryption(u64 seed) {
@@ -1448,8 +1517,9 @@ struct Context {
   //   cos(2 pi (x - 1/4) / 2^r) on [-(K+1), K+1], then r double angles, giving
   //   sin(2 pi x) = 2 pi m / q0 + O(m^3)) -> recombination (x i as X^(N/2)) ->
   //   SlotsToCoeffs (forward FFT stages, 3 transforms) -> the input scale.
-  // The transforms use the scheme's own chain from the top: 3 CoeffsToSlots
-  // levels, depth(poly) + r EvalMod levels, 3 SlotsToCoeffs levels.
+  // NewBootstrapper extends the chain above the residual one by the 15 levels
+  // the circuit consumes (3 CoeffsToSlots, depth(poly) + r EvalMod, 3
+  // SlotsToCoeffs), so the output lands on the residual chain's top level.
   // ---------------------------------------------------------------------------
   typedef std::complex<double> cplx;
   typedef std::map<int, std::vector<cplx>> DiagMap;  // rotation offset -> diagonal (n slots)
@@ -1584,8 +1654,15 @@ struct Context {
     }
     int depth_poly = 0;
     while ((1 << depth_poly) <= B->degree) ++depth_poly;
-    const int need = 3 + depth_poly + B->r + 3;
-    if (L - 1 < need) throw std::runtime_error("bootstrapping needs " + std::to_string(need) + " levels above level 0");
+    // Lattigo's bootstrapping parameters extend the residual chain (bootstrapper.go:33-41):
+    // SlotsToCoeffs 3 x 40-bit, EvalMod depth(poly) + r x 60-bit, CoeffsToSlots 3 x 55-bit,
+    // so the refreshed ciphertext comes out at the residual chain's top level
+    {
+      std::vector<int> ext(3, 40);
+      ext.insert(ext.end(), depth_poly + B->r, 60);
+      ext.insert(ext.end(), 3, 55);
+      extend_chain(ext);
+    }
     B->top = L - 1;
     {  // EvalMod sees x = F m / q0 + I: raise the message to <= 2^-9 of q0 (sin 2 pi x ~ 2 pi x to 3e-5)
       const int lg = (63 - __builtin_clzll(mods[0])) - logScale - 9;
@@ -2569,9 +2646,10 @@ ArrayResultDouble GenerateMinimaxSignCoeffs(int* degrees, int n, int prec, int l
   return r;
   API_END(r)
 }
-// bootstrapper.go:19-58.  The transforms run on the scheme's own modulus chain
-// (its top 3 + depth(EvalMod) + 3 levels), so logPs (extra key-switching
-// primes of Lattigo's extended bootstrapping chain) is not used; full slots only.
+// bootstrapper.go:19-58.  Like Lattigo's bootstrapping parameters, the modulus
+// chain is extended above the residual chain by the 15 levels the circuit uses
+// (keys regenerated for it); the key-switching P primes stay those of the
+// scheme, so logPs is not used.  Full slots only.
 void NewBootstrapper(int* logPs, int n, int slots) {
   API_BEGIN
   (void)logPs;

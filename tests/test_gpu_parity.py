@@ -396,30 +396,46 @@ def test_n16_ops_parity(torch_cuda, oracle_mod):
     lib.DeleteScheme()
 
 
-BTP_LOGQ = [60] + [40] * 5 + [60] * 9 + [55] * 3  # residual 3 + SlotsToCoeffs 3 | EvalMod 9 | CoeffsToSlots 3
+BTP_LOGQ = [60] + [40] * 5  # the residual chain; NewBootstrapper extends it by 15 levels
 
 
 @pytest.mark.parametrize("h", [32, 192])
 def test_bootstrap_functional(torch_cuda, h):
-    """Bootstrap (bootstrapper.go:19-80) of a level-0 batch: the refreshed
-    ciphertext sits 15 levels below the top (3 CoeffsToSlots + 6 polynomial + 3
-    double-angle + 3 SlotsToCoeffs), keeps the input scale exactly and
-    decrypts to the input.  Parity with Lattigo's bootstrapper is unpinned
-    (different circuit parameters); the bar is the functional one."""
+    """Bootstrap (bootstrapper.go:19-80) of a level-0 batch.  As with Lattigo's
+    bootstrapping parameters, NewBootstrapper extends the modulus chain above
+    the residual one (3 CoeffsToSlots + 6 polynomial + 3 double-angle + 3
+    SlotsToCoeffs levels), so the refreshed ciphertext sits on the residual
+    top level, at the input scale exactly, and decrypts to the input.  A
+    ciphertext and a linear transform made before the extension keep working.
+    Parity with Lattigo's bootstrapper is unpinned (different circuit
+    parameters); the bar is the functional one."""
     from orion_amd.backend import HipLibrary
     lib = HipLibrary().new_scheme(13, BTP_LOGQ, [60, 60], 40, h=h, seed=5)
     lib.GenerateSecretKey()
     lib.GeneratePublicKey()
     lib.GenerateRelinearizationKey()
     n = lib.N // 2
+    rng = np.random.default_rng(h)
+    vals = rng.uniform(-1, 1, (2, n)).astype(np.float32)
+    pre = lib.Encrypt(lib.encode_batch(vals, 3, 1 << 40))
+    idx = [0, 3]
+    diags = rng.uniform(-1, 1, (2, n)).astype(np.float32)
+    lt = lib.GenerateLinearTransform(idx, list(diags.reshape(-1)), 3, 2.0, "none")
+    q_before = list(lib.GetModuliChain())
     with pytest.raises(RuntimeError, match="full slots"):
         lib.NewBootstrapper([61, 61], n // 2)
     lib.NewBootstrapper([61, 61], n)
-    rng = np.random.default_rng(h)
-    vals = rng.uniform(-1, 1, (2, n)).astype(np.float32)
+    q_after = list(lib.GetModuliChain())
+    assert q_after[:len(q_before)] == q_before and len(q_after) == len(q_before) + 15
+    # state from before the extension: decrypt, and the transform
+    assert np.abs(lib.decode_f64(lib.Decrypt(pre)) - vals).max() < 1e-5
+    y = lib.EvaluateLinearTransform(lt, pre)
+    lib.Rescale(y)
+    exp = sum(diags[i].astype(np.float64) * np.roll(vals, -d, axis=1) for i, d in enumerate(idx))
+    assert np.abs(lib.decode_f64(lib.Decrypt(y)) - exp).max() < 1e-3
     ct = lib.Encrypt(lib.encode_batch(vals, 0, 1 << 40))
     out = lib.Bootstrap(ct, n)
-    assert lib.GetCiphertextLevel(out) == len(BTP_LOGQ) - 1 - 15
+    assert lib.GetCiphertextLevel(out) == len(BTP_LOGQ) - 1
     assert lib.GetCiphertextScaleF(out) == 2.0 ** 40
     dec = lib.decode_f64(lib.Decrypt(out))
     err = np.abs(dec - vals.astype(np.float64))
@@ -432,13 +448,4 @@ def test_bootstrap_functional(torch_cuda, h):
     lib.DeleteBootstrappers()
     with pytest.raises(RuntimeError, match="no bootstrapper"):
         lib.Bootstrap(ct, n)
-    lib.DeleteScheme()
-
-
-def test_bootstrap_needs_levels(torch_cuda):
-    from orion_amd.backend import HipLibrary
-    lib = HipLibrary().new_scheme(13, [60] + [40] * 8, [60, 60], 40, h=32, seed=6)
-    lib.GenerateSecretKey()
-    with pytest.raises(RuntimeError, match="levels"):
-        lib.NewBootstrapper([61, 61], lib.N // 2)
     lib.DeleteScheme()

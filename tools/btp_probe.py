@@ -13,7 +13,7 @@ from orion_amd.backend import HipLibrary  # noqa: E402
 
 
 def main():
-    logq = [60] + [40] * 5 + [60] * 9 + [55] * 3
+    logq = [60] + [40] * 5  # residual; NewBootstrapper extends it
     lib = HipLibrary().new_scheme(13, logq, [60, 60], 40, h=32, seed=3)
     lib.GenerateSecretKey()
     lib.GeneratePublicKey()

@@ -9,7 +9,7 @@ from orion_amd.backend import HipLibrary  # noqa: E402
 
 
 def run(logn, h, amp, lib):
-    logq = [60] + [40] * 5 + [60] * 9 + [55] * 3
+    logq = [60] + [40] * 5  # residual; NewBootstrapper extends it
     lib.new_scheme(logn, logq, [60, 60], 40, h=h, seed=9)
     lib.GenerateSecretKey()
     lib.GeneratePublicKey()
