@@ -16,7 +16,9 @@ typedef uint64_t u64;
 typedef uint32_t u32;
 
 #define ORION_MAXMOD 80   // max |Q| + |P|
+#ifndef ORION_MAXLIMB
 #define ORION_MAXLIMB 64  // max limbs touched by one kernel launch (QP at one level)
+#endif
 
 // ---------------------------------------------------------------------------
 // per-modulus constants (device-resident table, indexed by QP modulus index)
