@@ -2649,14 +2649,23 @@ ArrayResultDouble GenerateMinimaxSignCoeffs(int* degrees, int n, int prec, int l
 // bootstrapper.go:19-58.  Like Lattigo's bootstrapping parameters, the modulus
 // chain is extended above the residual chain by the 15 levels the circuit uses
 // (keys regenerated for it); the key-switching P primes stay those of the
-// scheme, so logPs is not used.  Full slots only.
+// scheme, so logPs is not used.
+// Sparse slot counts (tensors.py:294-305 passes 2^ceil(log2(elements)) <= N/2)
+// share the one full-slot circuit: Orion's inputs are full-slot encodings whose
+// unused slots are zeroed before the bootstrap (operations.py:76-84), and the
+// full circuit returns every slot as it came in, so no post-scale is needed
+// (Lattigo's sparse circuit leaves replicas there and multiplies by
+// 2^(LogMaxSlots - LogSlots), bootstrapper.go:73-74).
+static void check_slots(const Context& c, int slots) {
+  if (slots < 1 || slots > c.N / 2 || (slots & (slots - 1)))
+    throw std::runtime_error("slots must be a power of two <= " + std::to_string(c.N / 2));
+}
 void NewBootstrapper(int* logPs, int n, int slots) {
   API_BEGIN
   (void)logPs;
   (void)n;
   Context& c = ctx();
-  if (slots != c.N / 2)
-    throw std::runtime_error("bootstrapping supports full slots (" + std::to_string(c.N / 2) + ") only");
+  check_slots(c, slots);
   if (!c.btp) c.new_bootstrapper();
   API_END_VOID
 }
@@ -2665,7 +2674,7 @@ void NewBootstrapper(int* logPs, int n, int slots) {
 int Bootstrap(int ct, int slots) {
   API_BEGIN
   Context& c = ctx();
-  if (slots != c.N / 2) throw std::runtime_error("bootstrapping supports full slots only");
+  check_slots(c, slots);
   return c.cts.add(c.bootstrap(c.cts.get(ct)));
   API_END(-1)
 }

@@ -422,8 +422,8 @@ def test_bootstrap_functional(torch_cuda, h):
     diags = rng.uniform(-1, 1, (2, n)).astype(np.float32)
     lt = lib.GenerateLinearTransform(idx, list(diags.reshape(-1)), 3, 2.0, "none")
     q_before = list(lib.GetModuliChain())
-    with pytest.raises(RuntimeError, match="full slots"):
-        lib.NewBootstrapper([61, 61], n // 2)
+    with pytest.raises(RuntimeError, match="power of two"):
+        lib.NewBootstrapper([61, 61], 3 * n // 4)
     lib.NewBootstrapper([61, 61], n)
     q_after = list(lib.GetModuliChain())
     assert q_after[:len(q_before)] == q_before and len(q_after) == len(q_before) + 15
@@ -445,6 +445,11 @@ def test_bootstrap_functional(torch_cuda, h):
     lib.Rescale(sq)
     d2 = lib.decode_f64(lib.Decrypt(sq))
     assert np.abs(d2 - vals.astype(np.float64) ** 2).max() < 1e-4
+    # sparse slot count (tensors.py bootstrap): unused slots zeroed, they stay zero
+    sp = vals.copy()
+    sp[:, n // 4:] = 0
+    out_s = lib.Bootstrap(lib.Encrypt(lib.encode_batch(sp, 0, 1 << 40)), n // 4)
+    assert np.abs(lib.decode_f64(lib.Decrypt(out_s)) - sp).max() < 1e-5
     lib.DeleteBootstrappers()
     with pytest.raises(RuntimeError, match="no bootstrapper"):
         lib.Bootstrap(ct, n)
