@@ -228,9 +228,10 @@ namespace orion {
 // composite minimax approximation of sign (polyeval.go:91-167 ->
 // Lattigo minimax.GenMinimaxCompositePolynomial), restated with the classic
 // Remez exchange in long double.  sign is odd, so each stage is an odd
-// Chebyshev series p(x) = sum_k c_k T_{2k+1}(x) fitted to 1 on [a, 1]; the
-// stage maps [a, 1] into [1 - e, 1 + e], and is divided by 1 + e so the next
-// stage works on [(1 - e) / (1 + e), 1].
+// Chebyshev series p(x) = sum_k c_k T_{2k+1}(x) fitted to 1 on [a, 1]; every
+// stage but the last is divided by its maximum on [-1, 1] (times 1 + 2^-10),
+// so the next stage's inputs stay inside [-1, 1], and the next stage is
+// fitted on [min over [a, 1] of the scaled stage, 1].
 // ---------------------------------------------------------------------------
 namespace {
 typedef long double ld;
@@ -349,10 +350,26 @@ std::vector<std::vector<double>> minimax_sign_composite(const std::vector<int>& 
     std::vector<ld> c = remez_sign(d, a, err);
     if (!(err < 1)) throw std::runtime_error("minimax: degree too small for the interval");
     const bool last = i + 1 == degrees.size();
+    // a stage's image must stay inside the next stage's Chebyshev domain for
+    // every input in [-1, 1], including the gap (-a, a) it is not fitted on,
+    // with room for the float32 coefficients and the homomorphic noise: scale
+    // by the true maximum of |p| on [0, 1] (p is odd), times 1 + 2^-10
+    ld norm = 1;
+    if (!last) {
+      ld mx = 0, mn_fit = 2;
+      const int G = 200000;
+      for (int j = 0; j <= G; ++j) {
+        const ld x = (ld)j / G;
+        const ld v = fabsl(cheb_odd_eval(c, x));
+        mx = std::max(mx, v);
+        if (x >= a) mn_fit = std::min(mn_fit, v);
+      }
+      norm = mx * (1 + ldexpl(1.0L, -10));
+      a = mn_fit / norm;
+    }
     std::vector<double> p(d + 1, 0.0);
-    for (size_t k = 0; k < c.size(); ++k) p[2 * k + 1] = (double)(last ? c[k] : c[k] / (1 + err));
+    for (size_t k = 0; k < c.size(); ++k) p[2 * k + 1] = (double)(c[k] / norm);
     out.push_back(p);
-    a = (1 - err) / (1 + err);
   }
   return out;
 }

@@ -49,7 +49,11 @@ _CT_OPS = {
     "MulScalarFloat": ("ct", "float"), "MulScalarFloatNew": ("ct", "float"),
     "Negate": ("ct",),
     "EvaluateLinearTransform": ("lt", "ct"),
+    "EvaluatePolynomial": ("ct", "poly", "int"),
+    "Bootstrap": ("ct", "int"),
 }
+# ops that allocate a new ciphertext handle
+_NEW_CT = ("EvaluateLinearTransform", "EvaluatePolynomial", "Bootstrap", "Negate")
 
 
 class OrionStream:
@@ -65,7 +69,7 @@ class OrionStream:
                             device=device)
         self.slots = self.meta["slots"]
         self.synthetic = synthetic_diagonals
-        self.pt_map, self.ct_map, self.lt_map = {}, {}, {}
+        self.pt_map, self.ct_map, self.lt_map, self.poly_map = {}, {}, {}, {}
         self.input_level = self.meta["input_level"]
         self._events = self.trace["events"]
 
@@ -107,6 +111,12 @@ class OrionStream:
                     lib.GenerateConsolidatedRotationKeys(lib.GetLinearTransformRotationKeys(h))
             elif op == "DeletePlaintext" and args[0] in self.pt_map:
                 lib.DeletePlaintext(self.pt_map.pop(args[0]))
+            elif op in ("GenerateChebyshev", "GenerateMonomial"):  # poly_evaluator.py:15-23
+                coeffs = self.arrays[ev["arrays"] + "_coeffs"]
+                self.poly_map[ret] = (lib.GenerateChebyshev(list(coeffs), len(coeffs)) if op == "GenerateChebyshev"
+                                      else lib.GenerateMonomial(list(coeffs)))
+            elif op == "NewBootstrapper":  # bootstrapper.py:9-13 (extends the chain, regenerates keys)
+                lib.NewBootstrapper([61], args[1])
         # rotation amounts used by the forward pass (hybrid output rotations)
         if gen_keys:
             for ev in self._events:
@@ -134,7 +144,8 @@ class OrionStream:
         return self.arrays["input"]
 
     # -- forward: the timed net(ct) ------------------------------------------------
-    def forward(self, ct_in):
+    def forward(self, ct_in, hook=None):
+        """hook(event, handle): called after every replayed op (debugging)."""
         lib = self.lib
         in_ids = self.meta["input_ids"]
         ct_map = {in_ids[0]: ct_in}
@@ -169,10 +180,12 @@ class OrionStream:
             cargs = []
             for k, a in zip(kinds, args):
                 cargs.append(ct_map[a] if k == "ct" else self.pt_map[a] if k == "pt" else
-                             self.lt_map[a] if k == "lt" else a)
+                             self.lt_map[a] if k == "lt" else self.poly_map[a] if k == "poly" else a)
             h = getattr(lib, op)(*cargs)
+            if hook is not None:
+                hook(ev, h)
             if ret is not None:
-                if op.endswith("New") or op == "EvaluateLinearTransform":
+                if op.endswith("New") or op in _NEW_CT:
                     owned.add(h)
                 ct_map[ret] = h
         out_ids = self.meta["output_ids"]

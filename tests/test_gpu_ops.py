@@ -252,3 +252,22 @@ def test_key_bundle_roundtrip(torch_cuda):
     assert np.array_equal(lib.export_galois_key(g), gk)
     assert np.array_equal(lib.export_secret_key(), sk)
     lib.DeleteScheme()
+
+
+def test_resnet20_end_to_end(torch_cuda):
+    """ResNet-20 (CIFAR-10) with the reference's configs/resnet.yml parameters
+    (N=2^13, [60] + [30]x32, h=192): the reference frontend's op stream
+    (tests/golden/resnet20_n13_*: 147 linear transforms, 138 polynomial
+    evaluations for the composite-minimax ReLUs, 42 bootstraps) replayed on the
+    GPU; decrypted logits vs the cleartext model (exact ReLU), the
+    reference's own gate (tests/models/test_mlp.py:45-48, MAE < 0.005)."""
+    from orion_amd.replay import OrionStream
+    st = OrionStream("resnet20_n13", seed=3)
+    st.keygen()
+    st.compile()
+    ct = st.encrypt_batch(st.reference_input())
+    res = st.decrypt_output(st.forward(ct))[0]
+    exp = st.arrays["expected_output"].reshape(-1)
+    assert np.abs(res - exp).mean() < 0.005, (res, exp)
+    assert np.argmax(res) == np.argmax(exp)
+    st.lib.DeleteScheme()

@@ -30,7 +30,32 @@ CONFIGS = {
     "mlp_n13": dict(model="MLP", logn=13, logq=[29, 26, 26, 26, 26, 26], logp=[29, 29], logscale=26, h=8192),
     # small LoLA for fast CPU/GPU end-to-end tests
     "lola_n13": dict(model="LoLA", logn=13, logq=[50] + [40] * 6, logp=[60, 60], logscale=40, h=192),
+    # ResNet-20 (CIFAR-10) with the reference's configs/resnet.yml parameters (N=2^13, 30-bit chain,
+    # bootstrapping); C4's ring degree is 2^16
+    "resnet20_n13": dict(model="ResNet20", logn=13, logq=[60] + [30] * 32, logp=[60, 60], logscale=30, h=192,
+                         boot_logp=[61] * 8, shape=(3, 32, 32), fuse=False),
 }
+
+
+def _tracer_shim():
+    """The fork's StatsTracker.update_batch_size reads shape attributes off
+    every traced module, including torch.nn.Identity (ResNet), which has none
+    (orion/core/tracer.py:235-250): give such modules empty shapes."""
+    import torch
+    from orion.core import tracer
+
+    orig = tracer.StatsTracker.update_batch_size
+
+    def patched(self, batch_size):
+        for node in self.module.graph.nodes:
+            if node.op == "call_module":
+                m = self.module.get_submodule(node.target)
+                for a in ("input_shape", "output_shape", "fhe_input_shape", "fhe_output_shape"):
+                    if not hasattr(m, a):
+                        setattr(m, a, torch.Size([batch_size]))
+        return orig(self, batch_size)
+
+    tracer.StatsTracker.update_batch_size = patched
 
 
 def _stub_modules():
@@ -67,13 +92,13 @@ class Recorder:
         self.events = []
         self.arrays = {}
         self.phase = "setup"
-        self.pts, self.cts, self.lts = {}, {}, {}
-        self._free = {"pt": [], "ct": [], "lt": []}
-        self._next = {"pt": 0, "ct": 0, "lt": 0}
+        self.pts, self.cts, self.lts, self.polys = {}, {}, {}, {}
+        self._free = {"pt": [], "ct": [], "lt": [], "poly": []}
+        self._next = {"pt": 0, "ct": 0, "lt": 0, "poly": 0}
 
     # lowest-free-id handle allocation (minheap.go:46-64)
     def _alloc(self, kind, meta):
-        table = {"pt": self.pts, "ct": self.cts, "lt": self.lts}[kind]
+        table = {"pt": self.pts, "ct": self.cts, "lt": self.lts, "poly": self.polys}[kind]
         if self._free[kind]:
             self._free[kind].sort()
             h = self._free[kind].pop(0)
@@ -263,6 +288,37 @@ class Recorder:
         m = self.cts[a]
         return self._new_ct("Negate", [a], m["level"], m["scale"])
 
+    # ---- polynomials (polyeval.go) and bootstrapping (bootstrapper.go) ----------
+    def GenerateMinimaxSignCoeffs(self, degrees, prec, logalpha, logerr, debug):
+        # the coefficients come from this build's own generator (host code, CPU)
+        from orion_amd.backend import HipLibrary
+        out = HipLibrary().GenerateMinimaxSignCoeffs(list(degrees), prec, logalpha, logerr, debug)
+        self._rec("GenerateMinimaxSignCoeffs", [list(map(int, degrees)), int(prec), int(logalpha), int(logerr)])
+        return out
+
+    def _poly(self, name, coeffs):
+        c = np.asarray(coeffs, dtype=np.float32)
+        h = self._alloc("poly", dict(n=len(c)))
+        return self._rec(name, [None], h, {"coeffs": c})
+
+    def GenerateMonomial(self, coeffs, *rest):
+        return self._poly("GenerateMonomial", coeffs)
+
+    def GenerateChebyshev(self, coeffs, *rest):
+        return self._poly("GenerateChebyshev", coeffs)
+
+    def EvaluatePolynomial(self, c, p, out_scale):
+        m = self.cts[c]
+        depth = int(self.polys[p]["n"] - 1).bit_length()
+        return self._new_ct("EvaluatePolynomial", [c, p, int(out_scale)], m["level"] - depth, int(out_scale))
+
+    def NewBootstrapper(self, logp, slots):
+        return self._rec("NewBootstrapper", [None, int(slots)])
+
+    def Bootstrap(self, c, slots):
+        m = self.cts[c]
+        return self._new_ct("Bootstrap", [c, int(slots)], len(self.moduli) - 1, m["scale"])
+
     # ---- linear transforms ------------------------------------------------
     def GenerateLinearTransform(self, idxs, data, level, ratio, io_mode):
         h = self._alloc("lt", dict(level=level, idxs=list(idxs), ratio=float(ratio)))
@@ -295,6 +351,7 @@ def run(name):
     import orion
     import orion.models as models
     from orion.core import orion as core
+    _tracer_shim()
 
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
     from oracle.oracle import gen_moduli  # primes for GetModuliChain (frontend uses them)
@@ -308,16 +365,20 @@ def run(name):
     conf = {
         "ckks_params": {"LogN": cfg["logn"], "LogQ": cfg["logq"], "LogP": cfg["logp"],
                         "LogScale": cfg["logscale"], "H": cfg["h"], "RingType": "Standard"},
+        "boot_params": {"LogP": cfg.get("boot_logp", [61] * 2)},
         "orion": {"margin": 2, "embedding_method": "hybrid", "backend": "lattigo",
-                  "fuse_modules": True, "debug": False, "diags_path": "", "keys_path": "", "io_mode": "none"},
+                  "fuse_modules": cfg.get("fuse", True), "debug": False, "diags_path": "", "keys_path": "",
+                  "io_mode": "none"},
     }
     orion.init_scheme(conf)
     net = getattr(models, cfg["model"])()
     net.eval()
     from torch.utils.data import DataLoader, TensorDataset
-    fit_imgs = torch.randn(256, 1, 28, 28)
-    fit_data = DataLoader(TensorDataset(fit_imgs, torch.zeros(256)), batch_size=1)
-    inp = torch.randn(1, 1, 28, 28)
+    shape = cfg.get("shape", (1, 28, 28))
+    nfit = 256 if shape == (1, 28, 28) else 32
+    fit_imgs = torch.randn(nfit, *shape)
+    fit_data = DataLoader(TensorDataset(fit_imgs, torch.zeros(nfit)), batch_size=1)
+    inp = torch.randn(1, *shape)
     out_clear = net(inp).detach()
     orion.fit(net, fit_data)
     rec.phase = "compile"
