@@ -33,6 +33,8 @@ int orion_launch_tensor(const LimbSet& d, const LimbSet& a, const LimbSet& b, co
                         hipStream_t st);
 int orion_launch_basis_ext(const LimbSet& out, const LimbSet& in, const BasisExtTable* T, const DeviceTables* tb,
                            int N, hipStream_t st);
+int orion_launch_modup_all(const LimbSet& D, const LimbSet& in, const BasisExtTable* const* Ts, int beta, int K,
+                           int nqp, const DeviceTables* tb, int N, hipStream_t st);
 int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const LimbSet& own, const MacGroups& G, int ngroup,
                         int beta, int nmod_key, const DeviceTables* tb, int N, hipStream_t st);
 int orion_launch_automorph(const LimbSet& o, const LimbSet& a, const u32* idx, const DeviceTables* tb, int N,
@@ -234,6 +236,7 @@ struct Context {
   std::map<u64, u32*> autidx;
   std::map<std::pair<int, int>, BasisExtTable*> betab;
   std::map<std::pair<int, int>, std::vector<int>> betab_pos;  // target positions (QP order)
+  std::map<int, BasisExtTable**> modup_arr;  // level -> device array of the digits' ModUp tables
 
   HandlePool<Plaintext> pts;
   HandlePool<Ciphertext> cts;
@@ -253,6 +256,7 @@ struct Context {
     lts.reset();
     for (auto& kv : autidx) hipFree(kv.second);
     for (auto& kv : betab) hipFree(kv.second);
+    for (auto& kv : modup_arr) hipFree(kv.second);
     for (auto& kv : garner) hipFree(kv.second);
     for (void* p : static_bufs) hipFree(p);
     if (d_tb) hipFree(d_tb);
@@ -388,6 +392,9 @@ struct Context {
   // 15 vs 37 us; 64 jobs: 32 vs 40 us, float64 path).  Batched launches
   // (>= 128 jobs at 64 images) keep the one-pass kernel.
   int ntt2_below = getenv("ORION_NTT2_BELOW") ? atoi(getenv("ORION_NTT2_BELOW")) : 128;
+  // decompositions with fewer limb-transforms per digit than this run every
+  // digit's ModUp + NTT as one launch pair (0 = always per digit)
+  int modup_merge = getenv("ORION_MODUP_MERGE") ? atoi(getenv("ORION_MODUP_MERGE")) : 256;
   void ntt_io(NttIO io, bool inv) {
     io.order = ntt_order;
     io.jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
@@ -588,6 +595,8 @@ struct Context {
     for (auto& kv : betab) hipFree(kv.second);
     betab.clear();
     betab_pos.clear();
+    for (auto& kv : modup_arr) hipFree(kv.second);
+    modup_arr.clear();
     sk = alloc(1, L + K, 1);
     std::vector<u64> host((size_t)(L + K) * N);
     small_residues(s, iota(0, L + K), host.data());
@@ -660,6 +669,19 @@ struct Context {
     BasisExtTable* d = make_betab(src, dst);
     betab[key] = d;
     betab_pos[key] = tpos;
+    return d;
+  }
+  BasisExtTable* const* modup_tabs(int level) {
+    auto it = modup_arr.find(level);
+    if (it != modup_arr.end()) return it->second;
+    const int beta = (level + 1 + K - 1) / K;
+    std::vector<BasisExtTable*> h;
+    std::vector<int> tpos;
+    for (int i = 0; i < beta; ++i) h.push_back(modup_tab(level, i, tpos));
+    BasisExtTable** d;
+    HIPCHK(hipMalloc(&d, sizeof(BasisExtTable*) * beta));
+    HIPCHK(hipMemcpy(d, h.data(), sizeof(BasisExtTable*) * beta, hipMemcpyHostToDevice));
+    modup_arr[level] = d;
     return d;
   }
   BasisExtTable* moddown_tab(int level) {
@@ -857,6 +879,22 @@ struct Context {
     Poly cinv = alloc(nc, level + 1, B);
     ntt_io(nio(lsq(cinv, 0, nc, level), c), true);  // out-of-place INTT
     Poly D = alloc(nc * beta, nqp, B);
+    if (nc * B * (nqp - K) < modup_merge && nqp <= ORION_MAXLIMB) {
+      // small decomposition: every digit's ModUp in one launch, one NTT over
+      // all digits (own limbs included: K/nqp extra transform work, traded
+      // for beta-1 fewer launch pairs)
+      std::vector<int> md;
+      for (int j = 0; j < nqp; ++j) md.push_back(qp_mod(level, j));
+      LimbSet Dl = ls(D, 0, nc * beta, iota(0, nqp), md);
+      LimbSet in = ls(cinv, 0, nc, iota(0, level + 1), iota(0, level + 1));
+      {
+        Scope sc(this, P_BEXT, 8.0 * N * B * nc * (level + 1 + beta * nqp));
+        if (orion_launch_modup_all(Dl, in, modup_tabs(level), beta, K, nqp, d_tb, N, stream))
+          throw std::runtime_error("modup_all: bad launch shape");
+      }
+      ntt(Dl, false);
+      return D;
+    }
     const long long dstride = (long long)beta * D.comp_stride();
     for (int i = 0; i < beta; ++i) {
       const int lo = i * K, hi = std::min((i + 1) * K, level + 1);

@@ -125,7 +125,7 @@ __device__ __forceinline__ u64 bext_target_sel(const BasisExtTable* __restrict__
   return acc;
 }
 __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in, const BasisExtTable* __restrict__ T,
-                                                        const DeviceTables* __restrict__ tb, int N) {
+                                                        const DeviceTables* __restrict__ tb, int N, int tchunk) {
   const int row = blockIdx.y;  // (comp, image)
   const int bi = row % out.nbatch;
   const int c = row / out.nbatch;
@@ -141,12 +141,59 @@ __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in,
     x1[i] = v.y;
   }
   const u64 v0 = bext_prep(T, tb, x0, y0), v1 = bext_prep(T, tb, x1, y1);
-  for (int t = 0; t < nt; ++t) {
+  const int tend = min(nt, (int)(blockIdx.z + 1) * tchunk);
+  for (int t = blockIdx.z * tchunk; t < tend; ++t) {
     const u64 q = tb->mc[T->dst_mod[t]].q;
     ulonglong2 o;
     o.x = bext_target_sel(T, t, ns, q, y0, v0);
     o.y = bext_target_sel(T, t, ns, q, y1, v1);
     *(ulonglong2*)(out.p + row_off(out, c, t, bi) + n) = o;
+  }
+}
+
+// ModUp of every digit of a decomposition in one launch (small launches:
+// one image at N = 2^13..2^15 gives a per-digit basis_ext only 16..64
+// workgroups).  Row = (comp c, digit i, image); blockIdx.z = a chunk of the
+// nqp QP positions.  Digit i's own positions [iK, iK + ns) are copied from
+// the source limbs, so the merged NTT that follows sees defined data and D
+// holds every limb (consumers still read the own limbs from the input).
+// D: comps c*beta + i, limb pos j at D.pos[j]; Ts[i] = digit i's table.
+__global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, const BasisExtTable* const* Ts,
+                                                        int beta, int K, int nqp, const DeviceTables* __restrict__ tb,
+                                                        int N, int tchunk) {
+  const int row = blockIdx.y;
+  const int bi = row % D.nbatch;
+  const int r = row / D.nbatch;
+  const int i = r % beta;
+  const int c = r / beta;
+  const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  if (n >= N) return;
+  const BasisExtTable* __restrict__ T = Ts[i];
+  const int ns = T->ns, lo = i * K;
+  u64 x0[ORION_MAXSRC], x1[ORION_MAXSRC], y0[ORION_MAXSRC], y1[ORION_MAXSRC];
+#pragma unroll
+  for (int s = 0; s < ORION_MAXSRC; ++s) {
+    if (s >= ns) break;
+    const ulonglong2 v = *(const ulonglong2*)(in.p + row_off(in, c, lo + s, bi) + n);
+    x0[s] = v.x;
+    x1[s] = v.y;
+  }
+  const u64 v0 = bext_prep(T, tb, x0, y0), v1 = bext_prep(T, tb, x1, y1);
+  const int jend = min(nqp, (int)(blockIdx.z + 1) * tchunk);
+  for (int j = blockIdx.z * tchunk; j < jend; ++j) {
+    ulonglong2 o;
+    if (j >= lo && j < lo + ns) {
+      // own limb: the source coefficient itself (no divergence: j is uniform)
+#pragma unroll
+      for (int s = 0; s < ORION_MAXSRC; ++s)
+        if (s == j - lo) o.x = x0[s], o.y = x1[s];
+    } else {
+      const int t = j < lo ? j : j - ns;
+      const u64 q = tb->mc[T->dst_mod[t]].q;
+      o.x = bext_target_sel(T, t, ns, q, y0, v0);
+      o.y = bext_target_sel(T, t, ns, q, y1, v1);
+    }
+    *(ulonglong2*)(D.p + row_off(D, c * beta + i, j, bi) + n) = o;
   }
 }
 
@@ -408,6 +455,15 @@ __global__ void __launch_bounds__(256) lt_giant_kernel(LimbSet acc, LimbSet D, L
 }
 
 inline dim3 ew_grid(int N, int rows) { return dim3((N / 2 + 255) / 256, rows); }
+// split the targets of a small basis extension over blockIdx.z until the
+// launch has ~2048 workgroups (8 per CU); the per-coefficient prologue is
+// recomputed per chunk, which costs ns multiplies against nt/chunk targets
+inline unsigned target_chunks(dim3 g, int nt) {
+  const long long wg = (long long)g.x * g.y;
+  long long z = (2048 + wg - 1) / wg;
+  if (z > nt / 4) z = nt / 4;  // keep >= 4 targets per chunk
+  return z < 1 ? 1u : (unsigned)z;
+}
 
 }  // namespace
 
@@ -446,7 +502,20 @@ int orion_launch_tensor(const LimbSet& d, const LimbSet& a, const LimbSet& b, co
 int orion_launch_basis_ext(const LimbSet& out, const LimbSet& in, const BasisExtTable* T, const DeviceTables* tb,
                            int N, hipStream_t st) {
   const int rows = out.ncomp * out.nbatch;
-  hipLaunchKernelGGL(basis_ext_kernel, ew_grid(N, rows), dim3(256), 0, st, out, in, T, tb, N);
+  dim3 g = ew_grid(N, rows);
+  const int nt = out.nlimb;
+  g.z = target_chunks(g, nt);
+  hipLaunchKernelGGL(basis_ext_kernel, g, dim3(256), 0, st, out, in, T, tb, N, (nt + g.z - 1) / g.z);
+  return 0;
+}
+
+int orion_launch_modup_all(const LimbSet& D, const LimbSet& in, const BasisExtTable* const* Ts, int beta, int K,
+                           int nqp, const DeviceTables* tb, int N, hipStream_t st) {
+  if (beta < 1 || nqp > ORION_MAXLIMB || D.ncomp != in.ncomp * beta) return -1;
+  const int rows = D.ncomp * D.nbatch;
+  dim3 g = ew_grid(N, rows);
+  g.z = target_chunks(g, nqp);
+  hipLaunchKernelGGL(modup_all_kernel, g, dim3(256), 0, st, D, in, Ts, beta, K, nqp, tb, N, (nqp + g.z - 1) / g.z);
   return 0;
 }
 

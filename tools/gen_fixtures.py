@@ -34,6 +34,9 @@ CONFIGS = {
     # bootstrapping); C4's ring degree is 2^16
     "resnet20_n13": dict(model="ResNet20", logn=13, logq=[60] + [30] * 32, logp=[60, 60], logscale=30, h=192,
                          boot_logp=[61] * 8, shape=(3, 32, 32), fuse=False),
+    # C4 (BASELINE configs[3]): ResNet-20 at N=2^16 with the same moduli chain
+    "resnet20_n16": dict(model="ResNet20", logn=16, logq=[60] + [30] * 32, logp=[60, 60], logscale=30, h=192,
+                         boot_logp=[61] * 8, shape=(3, 32, 32), fuse=False),
 }
 
 
