@@ -83,11 +83,20 @@ def main():
     import torch
     from orion_amd import dist as odist
     world, rank, local = odist.env_ranks()
+    # ORION_BENCH_REHEARSE=1: rehearse the N-rank flow on a box with fewer GPUs
+    # (ranks share devices round-robin, gloo carries the broadcast and the
+    # max-reduce); never used for a reported number
+    rehearse = os.environ.get("ORION_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from orion_amd.replay import OrionStream
     lib_seed = 2024
@@ -156,6 +165,8 @@ def main():
     res = st.decrypt_output(outs[-1])
     exp = st.arrays["expected_output"].reshape(-1)
     mae = float(np.abs(res[0] - exp).mean())
+    if dist:  # every rank decrypts with the key bundle it received: report the worst rank
+        mae = odist.max_over_ranks(dist, mae, torch.device("cuda", local))
     for o in outs:
         lib.DeleteCiphertext(o)
     # one extra, fully profiled step (outside the timed region) for the per-kernel breakdown
@@ -248,7 +259,7 @@ def main():
                          "algorithmic_bytes_per_launch": round(n_bytes / max(n_launch, 1)),
                          "ntt_share_of_kernel_time": round(bd_ntt_ms / total_prof_ms, 3) if total_prof_ms else None},
             "cpu_baseline": cpu,
-            "check": {"mae_image0_vs_cleartext": mae, "setup_s": round(t_setup, 1)},
+            "check": {"mae_image0_vs_cleartext": mae, "mae_over_ranks": "max", "setup_s": round(t_setup, 1)},
             "client_gpu": dict(client_ms, end_to_end_images_per_s=round(
                 args.batch / ((dt / args.steps) + (client_ms["encode_encrypt_ms_per_batch"]
                                                    + client_ms["decrypt_decode_ms_per_batch"]) / 1e3) * world, 3)),
