@@ -150,7 +150,7 @@ void OrionHipSetSeed(unsigned long seed);                /* keygen / encryption 
 void OrionHipSetStream(void *hipStream);                  /* NULL = library-owned stream */
 void *OrionHipGetStream(void);
 int OrionHipSynchronize(void);
-int OrionHipLogN(void);
+int OrionHipLogN(void);                                   /* ring degree in use: logN + 1 for ConjugateInvariant */
 int OrionHipNumQ(void);
 int OrionHipNumP(void);
 unsigned long OrionHipModulus(int idx);                   /* QP index space */

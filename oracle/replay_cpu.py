@@ -32,7 +32,8 @@ class CpuStream:
         self.trace, self.arrays = _load(name)
         self.meta = self.trace["meta"]
         cfg = self.meta["config"]
-        self.logN = cfg["logn"]
+        # a ConjugateInvariant ring of degree N runs as the Standard ring of degree 2N (backend.hip NewScheme)
+        self.logN = cfg["logn"] + (1 if cfg.get("ringtype", "standard").lower() == "conjugateinvariant" else 0)
         self.L, self.K = len(cfg["logq"]), len(cfg["logp"])
         self.orc = Oracle(self.logN, gen_moduli(self.logN, cfg["logq"], cfg["logp"]), self.L, self.K)
         self.N = self.orc.N

@@ -295,7 +295,7 @@ class HipLibrary:
         if seed is not None:
             self.OrionHipSetSeed(seed)
         self.NewScheme(logn, list(logq), list(logp), logscale or logq[-1], h, ringtype, "", "none")
-        self.N = 1 << logn
+        self.N = 1 << self.OrionHipLogN()  # 2^(logn+1) for a ConjugateInvariant ring (NewScheme)
         self.L, self.K = len(logq), len(logp)
         return self
 

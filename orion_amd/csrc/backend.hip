@@ -1931,13 +1931,24 @@ void NewScheme(int logN, int* logQ, int lenQ, int* logP, int lenP, int logScale,
   (void)ioMode;
   std::string rt = ringType ? ringType : "standard";
   for (auto& ch : rt) ch = (char)tolower(ch);
-  if (rt != "standard")
-    throw std::runtime_error("ring type '" + rt + "' not supported by the HIP backend (Standard ring only)");
+  // scheme.go:50-51: any ring type other than "standard" selects Lattigo's
+  // ConjugateInvariant ring Z[X + X^-1]/(X^2N + 1) of degree N (NthRoot 4N,
+  // N real slots).  It is the subring of the Standard ring of degree 2N fixed
+  // by conjugation, with the same primes (q = 1 mod 4N), the same slot count
+  // (2N/2 = N) and the same Galois elements (5^k mod 4N), so it runs here as
+  // that Standard ring; messages are real, which is all the CI ring carries.
+  const bool ci = rt != "standard";
+  if (ci && rt != "conjugateinvariant")
+    throw std::runtime_error("unknown ring type '" + rt + "' (standard | conjugateinvariant)");
+  const int logN_ring = ci ? logN + 1 : logN;
+  if (ci && logN_ring > 16)
+    throw std::runtime_error("ConjugateInvariant ring of degree 2^" + std::to_string(logN) +
+                             " needs a degree-2^" + std::to_string(logN_ring) + " Standard ring (max 2^16)");
   g.reset();
   g.reset(new Context());
   g->stream = g_user_stream;
   g->prng = Prng(g_seed);
-  g->setup(logN, std::vector<int>(logQ, logQ + lenQ), std::vector<int>(logP, logP + lenP), logScale, h);
+  g->setup(logN_ring, std::vector<int>(logQ, logQ + lenQ), std::vector<int>(logP, logP + lenP), logScale, h);
   g->seed_encryption(g_seed);
   API_END_VOID
 }

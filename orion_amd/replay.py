@@ -66,7 +66,7 @@ class OrionStream:
         cfg = self.meta["config"]
         self.lib = lib or HipLibrary()
         self.lib.new_scheme(cfg["logn"], cfg["logq"], cfg["logp"], cfg["logscale"], h=cfg["h"], seed=seed,
-                            device=device)
+                            device=device, ringtype=cfg.get("ringtype", "standard"))
         self.slots = self.meta["slots"]
         self.synthetic = synthetic_diagonals
         self.pt_map, self.ct_map, self.lt_map, self.poly_map = {}, {}, {}, {}

@@ -202,6 +202,22 @@ def test_mlp_n14_matches_cpu_oracle_replay(torch_cuda):
     _replay_gpu_vs_cpu("mlp_n14", seed=31)
 
 
+def test_mlp_conjugate_invariant_config(torch_cuda):
+    """The reference's own tests/configs/mlp.yml (ConjugateInvariant ring,
+    N=2^13, 8192 real slots, [29]+[26]x5 / [29,29], H=8192): the frontend's op
+    stream for it runs through the C-ABI (as the conjugation-fixed subring of
+    the degree-2^14 Standard ring), bit for bit against the CPU oracle, and
+    decrypts within the reference's MAE gate (tests/models/test_mlp.py:48)."""
+    from orion_amd.backend import HipLibrary
+    lib = HipLibrary().new_scheme(13, [29] + [26] * 5, [29, 29], 26, h=8192, ringtype="ConjugateInvariant", seed=5,
+                                  device=0)
+    assert lib.N == 1 << 14 and int(lib.OrionHipLogN()) == 14
+    for q in lib.moduli():
+        assert q % (4 << 13) == 1  # NthRoot = 4N for the CI ring
+    lib.DeleteScheme()
+    _replay_gpu_vs_cpu("mlp_n13_ci", seed=34)
+
+
 def test_lola_n15_matches_cpu_oracle_replay(torch_cuda):
     """BASELINE config C3 (LoLA, N=2^15): whole forward pass, bit for bit."""
     _replay_gpu_vs_cpu("lola_n15", seed=32)

@@ -295,3 +295,18 @@ def test_cpu_replay_lola_matches_cleartext():
     v = s.decrypt(out)[:10]
     exp = s.arrays["expected_output"].reshape(-1)
     assert np.abs(v - exp).mean() < 0.005
+
+
+def test_cpu_replay_mlp_conjugate_invariant():
+    """tests/configs/mlp.yml as written (RingType ConjugateInvariant, 8192 real
+    slots): the oracle replays the frontend's op stream on the degree-2N
+    Standard ring and meets the reference MAE gate (test_mlp.py:45-48)."""
+    from oracle.replay_cpu import CpuStream
+    s = CpuStream("mlp_n13_ci")
+    assert s.N == 1 << 14 and s.slots == 1 << 13
+    s.keygen()
+    s.compile()
+    out = s.forward(s.encrypt(s.arrays["input"]))
+    v = s.decrypt(out)[:10]
+    exp = s.arrays["expected_output"].reshape(-1)
+    assert np.abs(v - exp).mean() < 0.005

@@ -28,6 +28,10 @@ CONFIGS = {
     "mlp_n14": dict(model="MLP", logn=14, logq=[60] + [40] * 7, logp=[60, 60], logscale=40, h=192),
     # C1 plumbing: configs/mlp.yml moduli sizes, Standard ring (SURVEY §7 note)
     "mlp_n13": dict(model="MLP", logn=13, logq=[29, 26, 26, 26, 26, 26], logp=[29, 29], logscale=26, h=8192),
+    # C1 exactly as the reference's own test config tests/configs/mlp.yml (ConjugateInvariant ring:
+    # N = 2^13 real slots, primes = 1 mod 4N)
+    "mlp_n13_ci": dict(model="MLP", logn=13, logq=[29, 26, 26, 26, 26, 26], logp=[29, 29], logscale=26, h=8192,
+                       ringtype="ConjugateInvariant"),
     # small LoLA for fast CPU/GPU end-to-end tests
     "lola_n13": dict(model="LoLA", logn=13, logq=[50] + [40] * 6, logp=[60, 60], logscale=40, h=192),
     # ResNet-20 (CIFAR-10) with the reference's configs/resnet.yml parameters (N=2^13, 30-bit chain,
@@ -359,15 +363,18 @@ def run(name):
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
     from oracle.oracle import gen_moduli  # primes for GetModuliChain (frontend uses them)
 
-    moduli = gen_moduli(cfg["logn"], cfg["logq"], cfg["logp"])
-    slots = 1 << (cfg["logn"] - 1)
+    ci = cfg.get("ringtype", "standard").lower() == "conjugateinvariant"
+    # parameters.py:33-36: logslots = logn (ConjugateInvariant) or logn - 1; the CI ring's NthRoot is 4N
+    moduli = gen_moduli(cfg["logn"] + ci, cfg["logq"], cfg["logp"])
+    slots = 1 << (cfg["logn"] - 1 + ci)
     rec = Recorder(moduli[: len(cfg["logq"])], slots)
     core.Scheme.setup_backend = lambda self, params: rec
 
     torch.manual_seed(42)
     conf = {
         "ckks_params": {"LogN": cfg["logn"], "LogQ": cfg["logq"], "LogP": cfg["logp"],
-                        "LogScale": cfg["logscale"], "H": cfg["h"], "RingType": "Standard"},
+                        "LogScale": cfg["logscale"], "H": cfg["h"],
+                        "RingType": cfg.get("ringtype", "Standard")},
         "boot_params": {"LogP": cfg.get("boot_logp", [61] * 2)},
         "orion": {"margin": 2, "embedding_method": "hybrid", "backend": "lattigo",
                   "fuse_modules": cfg.get("fuse", True), "debug": False, "diags_path": "", "keys_path": "",
