@@ -218,6 +218,12 @@ def test_mlp_conjugate_invariant_config(torch_cuda):
     _replay_gpu_vs_cpu("mlp_n13_ci", seed=34)
 
 
+def test_lola_conjugate_invariant_config(torch_cuda):
+    """configs/lola.yml as written (ConjugateInvariant, N=2^13, 26-bit chain,
+    H=8192): GPU replay bit for bit vs the oracle, MAE gate."""
+    _replay_gpu_vs_cpu("lola_n13_ci", seed=35)
+
+
 def test_lola_n15_matches_cpu_oracle_replay(torch_cuda):
     """BASELINE config C3 (LoLA, N=2^15): whole forward pass, bit for bit."""
     _replay_gpu_vs_cpu("lola_n15", seed=32)

@@ -32,6 +32,9 @@ CONFIGS = {
     # N = 2^13 real slots, primes = 1 mod 4N)
     "mlp_n13_ci": dict(model="MLP", logn=13, logq=[29, 26, 26, 26, 26, 26], logp=[29, 29], logscale=26, h=8192,
                        ringtype="ConjugateInvariant"),
+    # configs/lola.yml as written (ConjugateInvariant, N = 2^13, 26-bit chain)
+    "lola_n13_ci": dict(model="LoLA", logn=13, logq=[29, 26, 26, 26, 26, 26], logp=[29, 29], logscale=26, h=8192,
+                        ringtype="ConjugateInvariant"),
     # small LoLA for fast CPU/GPU end-to-end tests
     "lola_n13": dict(model="LoLA", logn=13, logq=[50] + [40] * 6, logp=[60, 60], logscale=40, h=192),
     # ResNet-20 (CIFAR-10) with the reference's configs/resnet.yml parameters (N=2^13, 30-bit chain,
