@@ -379,7 +379,10 @@ struct Context {
     io.src = src;
     return io;
   }
-  int ntt_order = getenv("ORION_NTT_ORDER") ? atoi(getenv("ORION_NTT_ORDER")) : 0;
+#ifndef ORION_NTT_DEFAULT_ORDER
+#define ORION_NTT_DEFAULT_ORDER 2
+#endif
+  int ntt_order = getenv("ORION_NTT_ORDER") ? atoi(getenv("ORION_NTT_ORDER")) : ORION_NTT_DEFAULT_ORDER;
 #ifndef ORION_NTT_DEFAULT_IMPL
 #define ORION_NTT_DEFAULT_IMPL 1
 #endif
@@ -398,6 +401,12 @@ struct Context {
   void ntt_io(NttIO io, bool inv) {
     io.order = ntt_order;
     io.jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
+    if (io.order == 2) {  // integer-path (>= 2^46) limbs are ~1.4x slower per transform: dispatch them first
+      int k = 0;
+      for (int pass = 0; pass < 2; ++pass)
+        for (int l = 0; l < io.dst.nlimb; ++l)
+          if ((host_tb.mc[io.dst.mod[l]].f64 != 0) == (pass == 1)) io.lord[k++] = (unsigned char)l;
+    }
     if (logN == 16 || (logN == 15 && (ntt_impl == 2 || io.jobs < ntt2_below))) {  // N = 2^16: two-pass only
       Poly scratch;
       if (ntt2_chunk > 0 && io.jobs > 0) {  // chunks of jobs through one reused compact scratch

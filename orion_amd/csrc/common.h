@@ -288,7 +288,8 @@ struct NttIO {
   LimbSet dst, src, ex;
   LimbSet mid;  // two-pass N = 2^15 kernels: intermediate between the passes (dst's geometry)
   int modL;
-  int order;    // job decode: 0 = image fastest, 1 = limb fastest (mixes moduli inside a dispatch wave)
+  int order;    // job decode: 0 = image fastest, 1 = limb fastest (mixes moduli inside a dispatch wave),
+                // 2 = image fastest, then component, limbs in the order lord[] (slow integer-path limbs first)
   int jobs;     // ncomp * nlimb * nbatch of dst
   int pro, epi;
   // two-pass kernels, chunked: this launch covers jobs [job0, job0 + njob) and
@@ -296,6 +297,7 @@ struct NttIO {
   // chunk so the intermediate can stay in the Infinity Cache
   int job0, njob, mid_compact;
   u64 s[ORION_MAXLIMB], ss[ORION_MAXLIMB];
+  unsigned char lord[ORION_MAXLIMB];  // order 2: dispatch order of dst's limbs
 };
 
 // ---------------------------------------------------------------------------

@@ -37,11 +37,33 @@ __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, u64 v, int voff
 // ---------------------------------------------------------------------------
 // arithmetic policies
 // ---------------------------------------------------------------------------
+#ifndef NTT_INT_DIET
+#define NTT_INT_DIET 1
+#endif
+// Shoup's a*w mod q in [0, 2q) from 32-bit pieces, the quotient product added
+// as qh * (2^64 - q): t = a*w + qh*nq (mod 2^64) needs no 64-bit subtraction
+// (and no carry-chain hazards); 4 v_mad_u64_u32 + 4 v_mul_lo_u32 + 1 v_mul_hi_u32
+__device__ __forceinline__ u64 shoup_lazy_nq(u64 a, u64 w, u64 ws, u64 nq) {
+  const u32 a0 = (u32)a, a1 = (u32)(a >> 32), s0 = (u32)ws, s1 = (u32)(ws >> 32);
+  const u64 m1 = (u64)a1 * s0 + __umulhi(a0, s0);
+  const u64 m2 = (u64)a0 * s1 + (u32)m1;
+  const u64 qh = (u64)a1 * s1 + ((m1 >> 32) + (m2 >> 32));  // floor(a * ws / 2^64)
+  const u32 h0 = (u32)qh, h1 = (u32)(qh >> 32), w0 = (u32)w, w1 = (u32)(w >> 32);
+  const u32 n0 = (u32)nq, n1 = (u32)(nq >> 32);
+  const u64 lo = (u64)h0 * n0 + (u64)a0 * w0;
+  const u32 hi = (u32)(lo >> 32) + a0 * w1 + a1 * w0 + h0 * n1 + h1 * n0;
+  return ((u64)hi << 32) | (u32)lo;
+}
+
 struct IntArith {
   typedef u64 T;
   typedef ulonglong2 W;
-  u64 q, q2, ninv, ninv_s;
-  __device__ IntArith(const ModConst& m) : q(m.q), q2(m.q << 1), ninv(m.ninv), ninv_s(m.ninv_s) {}
+  u64 q, q2, ninv, ninv_s, nq;
+  __device__ IntArith(const ModConst& m) : q(m.q), q2(m.q << 1), ninv(m.ninv), ninv_s(m.ninv_s), nq(0 - m.q) {}
+  __device__ __forceinline__ u64 smul(u64 a, u64 w, u64 ws) const {
+    if constexpr (NTT_INT_DIET) return shoup_lazy_nq(a, w, ws, nq);
+    return shoup_lazy(a, w, ws, q);
+  }
   __device__ __forceinline__ W tw(__amdgpu_buffer_rsrc_t r, int vidx, int sidx) const {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, vidx * 16, sidx * 16, 0);
     return make_ulonglong2(((u64)v[1] << 32) | v[0], ((u64)v[3] << 32) | v[2]);
@@ -50,7 +72,7 @@ struct IntArith {
   // Harvey CT butterfly, values in [0, 4q)
   __device__ __forceinline__ void ct(T& X, T& Y, const W& w) const {
     const u64 x = X >= q2 ? X - q2 : X;
-    const u64 t = shoup_lazy(Y, w.x, w.y, q);
+    const u64 t = smul(Y, w.x, w.y);
     X = x + t;
     Y = x - t + q2;
   }
@@ -59,7 +81,7 @@ struct IntArith {
     const u64 x = X, y = Y;
     const u64 s = x + y;
     X = s >= q2 ? s - q2 : s;
-    Y = shoup_lazy(x - y + q2, w.x, w.y, q);
+    Y = shoup_lazy(x - y + q2, w.x, w.y, q);  // (the diet's extra live values spill the inverse kernel)
   }
   __device__ __forceinline__ T reduce_round(T x) const { return x; }  // lazy range is invariant
   __device__ __forceinline__ u64 final_fwd(T x) const {
@@ -139,7 +161,12 @@ __device__ __forceinline__ u64* row_ptr(const LimbSet& s, int c, int l, int b) {
 
 __device__ __forceinline__ void job_of(const NttIO& io, int job, int& c, int& l, int& b) {
   const LimbSet& d = io.dst;
-  if (io.order == 1) {
+  if (io.order == 2) {  // longest jobs first: a launch's last, partial round of workgroups holds the fast limbs
+    b = job % d.nbatch;
+    const int r = job / d.nbatch;
+    c = r % d.ncomp;
+    l = io.lord[r / d.ncomp];
+  } else if (io.order == 1) {
     l = job % d.nlimb;
     const int r = job / d.nlimb;
     b = r % d.nbatch;
