@@ -889,19 +889,30 @@ struct Context {
     ntt_io(nio(lsq(cinv, 0, nc, level), c), true);  // out-of-place INTT
     Poly D = alloc(nc * beta, nqp, B);
     if (nc * B * (nqp - K) < modup_merge && nqp <= ORION_MAXLIMB) {
-      // small decomposition: every digit's ModUp in one launch, one NTT over
-      // all digits (own limbs included: K/nqp extra transform work, traded
-      // for beta-1 fewer launch pairs)
+      // small decomposition: every digit's ModUp in one launch (own limbs not
+      // written), then one NTT over every digit's target limbs: limb (digit i,
+      // QP position j) of comp c sits at comp c, position i*nqp + j of a
+      // LimbSet whose comp stride spans the beta digits
       std::vector<int> md;
       for (int j = 0; j < nqp; ++j) md.push_back(qp_mod(level, j));
       LimbSet Dl = ls(D, 0, nc * beta, iota(0, nqp), md);
       LimbSet in = ls(cinv, 0, nc, iota(0, level + 1), iota(0, level + 1));
       {
-        Scope sc(this, P_BEXT, 8.0 * N * B * nc * (level + 1 + beta * nqp));
+        Scope sc(this, P_BEXT, 8.0 * N * B * nc * (level + 1 + beta * nqp - (level + 1)));
         if (orion_launch_modup_all(Dl, in, modup_tabs(level), beta, K, nqp, d_tb, N, stream))
           throw std::runtime_error("modup_all: bad launch shape");
       }
-      ntt(Dl, false);
+      std::vector<int> tpos, tmod;
+      for (int i = 0; i < beta; ++i)
+        for (int j = 0; j < nqp; ++j)
+          if (!(j >= i * K && j < std::min((i + 1) * K, level + 1))) tpos.push_back(i * nqp + j), tmod.push_back(md[j]);
+      if (beta * nqp <= 256 && (int)tpos.size() <= ORION_MAXLIMB) {
+        LimbSet T = ls(D, 0, nc, tpos, tmod);
+        T.comp_stride = (long long)beta * D.comp_stride();
+        ntt(T, false);
+      } else {
+        ntt(Dl, false);  // (own limbs transformed too; their contents are unused)
+      }
       return D;
     }
     const long long dstride = (long long)beta * D.comp_stride();

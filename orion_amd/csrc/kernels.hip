@@ -181,18 +181,14 @@ __global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, c
   const u64 v0 = bext_prep(T, tb, x0, y0), v1 = bext_prep(T, tb, x1, y1);
   const int jend = min(nqp, (int)(blockIdx.z + 1) * tchunk);
   for (int j = blockIdx.z * tchunk; j < jend; ++j) {
+    // own limbs are not written: every consumer reads them from the NTT-domain
+    // input of the decomposition (j is uniform: no divergence)
+    if (j >= lo && j < lo + ns) continue;
+    const int t = j < lo ? j : j - ns;
+    const u64 q = tb->mc[T->dst_mod[t]].q;
     ulonglong2 o;
-    if (j >= lo && j < lo + ns) {
-      // own limb: the source coefficient itself (no divergence: j is uniform)
-#pragma unroll
-      for (int s = 0; s < ORION_MAXSRC; ++s)
-        if (s == j - lo) o.x = x0[s], o.y = x1[s];
-    } else {
-      const int t = j < lo ? j : j - ns;
-      const u64 q = tb->mc[T->dst_mod[t]].q;
-      o.x = bext_target_sel(T, t, ns, q, y0, v0);
-      o.y = bext_target_sel(T, t, ns, q, y1, v1);
-    }
+    o.x = bext_target_sel(T, t, ns, q, y0, v0);
+    o.y = bext_target_sel(T, t, ns, q, y1, v1);
     *(ulonglong2*)(D.p + row_off(D, c * beta + i, j, bi) + n) = o;
   }
 }
