@@ -115,14 +115,16 @@ __device__ __forceinline__ u64 bext_target_sel(const BasisExtTable* __restrict__
     if (j > ns) break;
     acc = v == (u64)j ? T->vS_t[t][j] : acc;
   }
+  // lazy: each Shoup product is in [0, 2q) and the running sum is kept in
+  // [0, 2q) by one conditional subtraction (4q < 2^63 for q < 2^61)
+  const u64 q2 = q << 1, nq = 0 - q;
 #pragma unroll
   for (int i = 0; i < ORION_MAXSRC; ++i) {
     if (i >= ns) break;
-    u64 r = shoup_lazy(y[i], T->qhat_t[t][i], T->qhat_ts[t][i], q);
-    r = r >= q ? r - q : r;
-    acc = add_mod(acc, r, q);
+    acc += shoup_lazy_nq(y[i], T->qhat_t[t][i], T->qhat_ts[t][i], nq);
+    acc = acc >= q2 ? acc - q2 : acc;
   }
-  return acc;
+  return acc >= q ? acc - q : acc;
 }
 __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in, const BasisExtTable* __restrict__ T,
                                                         const DeviceTables* __restrict__ tb, int N, int tchunk) {
@@ -154,9 +156,9 @@ __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in,
 // ModUp of every digit of a decomposition in one launch (small launches:
 // one image at N = 2^13..2^15 gives a per-digit basis_ext only 16..64
 // workgroups).  Row = (comp c, digit i, image); blockIdx.z = a chunk of the
-// nqp QP positions.  Digit i's own positions [iK, iK + ns) are copied from
-// the source limbs, so the merged NTT that follows sees defined data and D
-// holds every limb (consumers still read the own limbs from the input).
+// nqp QP positions.  Digit i's own positions [iK, iK + ns) are not written
+// (consumers read the own limbs from the NTT-domain input, and the NTT that
+// follows covers only the target positions).
 // D: comps c*beta + i, limb pos j at D.pos[j]; Ts[i] = digit i's table.
 __global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, const BasisExtTable* const* Ts,
                                                         int beta, int K, int nqp, const DeviceTables* __restrict__ tb,

@@ -40,21 +40,6 @@ __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, u64 v, int voff
 #ifndef NTT_INT_DIET
 #define NTT_INT_DIET 1
 #endif
-// Shoup's a*w mod q in [0, 2q) from 32-bit pieces, the quotient product added
-// as qh * (2^64 - q): t = a*w + qh*nq (mod 2^64) needs no 64-bit subtraction
-// (and no carry-chain hazards); 4 v_mad_u64_u32 + 4 v_mul_lo_u32 + 1 v_mul_hi_u32
-__device__ __forceinline__ u64 shoup_lazy_nq(u64 a, u64 w, u64 ws, u64 nq) {
-  const u32 a0 = (u32)a, a1 = (u32)(a >> 32), s0 = (u32)ws, s1 = (u32)(ws >> 32);
-  const u64 m1 = (u64)a1 * s0 + __umulhi(a0, s0);
-  const u64 m2 = (u64)a0 * s1 + (u32)m1;
-  const u64 qh = (u64)a1 * s1 + ((m1 >> 32) + (m2 >> 32));  // floor(a * ws / 2^64)
-  const u32 h0 = (u32)qh, h1 = (u32)(qh >> 32), w0 = (u32)w, w1 = (u32)(w >> 32);
-  const u32 n0 = (u32)nq, n1 = (u32)(nq >> 32);
-  const u64 lo = (u64)h0 * n0 + (u64)a0 * w0;
-  const u32 hi = (u32)(lo >> 32) + a0 * w1 + a1 * w0 + h0 * n1 + h1 * n0;
-  return ((u64)hi << 32) | (u32)lo;
-}
-
 struct IntArith {
   typedef u64 T;
   typedef ulonglong2 W;
