@@ -454,3 +454,36 @@ def test_bootstrap_functional(torch_cuda, h):
     with pytest.raises(RuntimeError, match="no bootstrapper"):
         lib.Bootstrap(ct, n)
     lib.DeleteScheme()
+
+
+def test_error_contract(torch_cuda):
+    """SURVEY §8b errors: where Lattigo panics (aborting the process), the
+    C-ABI returns an error with a last-error string; the library stays usable
+    afterwards.  Bad handles, a level-0 rescale, mismatched batches.  Deleting
+    a handle twice is a no-op, as in the reference heap (minheap.go:77-81:
+    Python frees from __del__ at GC-determined times)."""
+    from orion_amd.backend import HipLibrary
+    lib = HipLibrary().new_scheme(13, [50, 40, 40], [60], 40, h=64, seed=9, device=0)
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    vals = np.linspace(-1, 1, 4096).astype(np.float32)
+    ct = lib.Encrypt(lib.Encode(vals, 2, 1 << 40))
+    for call in (lambda: lib.RotateNew(9999, 1), lambda: lib.Rescale(9999),
+                 lambda: lib.MulRelinCiphertextNew(ct, 9999), lambda: lib.Decrypt(9999)):
+        with pytest.raises(RuntimeError):
+            call()
+    low = lib.Encrypt(lib.Encode(vals, 0, 1 << 40))
+    with pytest.raises(RuntimeError, match="level-0"):
+        lib.Rescale(low)
+    b2 = lib.Encrypt(lib.encode_batch(np.stack([vals, vals]), 2, 1 << 40))
+    b3 = lib.Encrypt(lib.encode_batch(np.stack([vals, vals, vals]), 2, 1 << 40))
+    with pytest.raises(RuntimeError, match="batch"):
+        lib.AddCiphertextNew(b2, b3)
+    tmp = lib.RotateNew(ct, 1)
+    lib.DeleteCiphertext(tmp)
+    lib.DeleteCiphertext(tmp)
+    # still usable: the error paths left no device state behind
+    out = np.array(lib.Decode(lib.Decrypt(lib.RotateNew(ct, 1))))
+    assert np.abs(out[:4096] - np.roll(vals, -1)).max() < 1e-4
+    lib.DeleteScheme()
