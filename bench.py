@@ -208,6 +208,20 @@ def main():
                  "decrypt_decode_ms_per_batch": round(client(dec_once), 3)}
     lib.DeleteCiphertext(out_ct)
 
+    # BASELINE configs[2] (LoLA N=2^15, batch=1): single-image latency of the
+    # same op stream, outside the timed region (one image per launch leaves
+    # most CUs idle; the throughput line above is the batched shard)
+    ct1 = st.encrypt_batch(imgs[:1])
+    lib.DeleteCiphertext(st.forward(ct1))
+    lib.OrionHipSynchronize()
+    reps1 = 10
+    t1 = time.perf_counter()
+    for _ in range(reps1):
+        lib.DeleteCiphertext(st.forward(ct1))
+    lib.OrionHipSynchronize()
+    b1_ms = (time.perf_counter() - t1) / reps1 * 1e3
+    lib.DeleteCiphertext(ct1)
+
     images = args.batch * world * args.steps
     value = images / dt
     ntt = [prof.get("ntt_fwd", {}), prof.get("ntt_inv", {})]
@@ -263,6 +277,7 @@ def main():
             "client_gpu": dict(client_ms, end_to_end_images_per_s=round(
                 args.batch / ((dt / args.steps) + (client_ms["encode_encrypt_ms_per_batch"]
                                                    + client_ms["decrypt_decode_ms_per_batch"]) / 1e3) * world, 3)),
+            "batch1": {"ms_per_image": round(b1_ms, 3), "images_per_s": round(1e3 / b1_ms, 1)},
             "kernel_ms_per_step": {k: round(v["ms"], 3) for k, v in breakdown.items()},
             "kernel_algorithmic_gbs": {k: round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1)
                                        for k, v in breakdown.items() if v["ms"] > 0},

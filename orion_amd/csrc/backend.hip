@@ -942,7 +942,8 @@ struct Context {
   // own Q limbs of each digit read from own (group stride own_gstride)
   void mac_groups(const LimbSet& o, long long out_gstride, const LimbSet& d, long long d_gstride,
                   const LimbSet& own, long long own_gstride, const std::vector<const u64*>& keys, int beta,
-                  const u64* add0 = nullptr, long long add_gstride = 0) {
+                  const u64* add0 = nullptr, long long add_gstride = 0, int add_nq = 0,
+                  const u64* add1 = nullptr) {
     const int G = (int)keys.size();
     for (int g0 = 0; g0 < G; g0 += ORION_MAXGROUP) {
       const int ng = std::min(ORION_MAXGROUP, G - g0);
@@ -955,13 +956,22 @@ struct Context {
       mg.own_gstride = own_gstride;
       mg.K = K;
       mg.add0 = add0 ? add0 + g0 * add_gstride : nullptr;
+      mg.add1 = add1 ? add1 + g0 * add_gstride : nullptr;
+      mg.add_nq = add0 ? add_nq : 0;
+      for (int j = 0; j < mg.add_nq; ++j) {  // P mod q_j: ModDown(u + P*a) = ModDown(u) + a exactly
+        u64 P = 1;
+        for (int k = 0; k < K; ++k) P = hm_mulmod(P, mods[L + k] % mods[o.mod[j]], mods[o.mod[j]]);
+        mg.add_s[j] = P;
+        mg.add_ss[j] = hm_shoup(P, mods[o.mod[j]]);
+      }
       LimbSet oo = o, dd = d, ow = own;
       oo.p += g0 * out_gstride;
       dd.p += g0 * d_gstride;
       ow.p += g0 * own_gstride;
       const double rows = (double)o.nlimb * o.nbatch;
       const double dreads = d_gstride ? rows * ng * beta : rows * beta;
-      Scope sc(this, P_MAC, 8.0 * N * (dreads + rows * ng * (2 + (add0 ? 1 : 0)) + 2.0 * beta * ng * o.nlimb));
+      const double adds = add0 ? (add_nq ? (add1 ? 2.0 : 1.0) * add_nq / o.nlimb : 1.0) : 0.0;
+      Scope sc(this, P_MAC, 8.0 * N * (dreads + rows * ng * (2 + adds) + 2.0 * beta * ng * o.nlimb));
       if (orion_launch_ks_mac(oo, dd, ow, mg, ng, beta, L + K, d_tb, N, stream))
         throw std::runtime_error("ks_mac launch failed");
     }
@@ -989,12 +999,16 @@ struct Context {
     }
     ntt_io(io, false);
   }
-  // full key switch of c (Q, level) -> (k0, k1) written to out comps 0/1 (Q, level)
-  void keyswitch(const LimbSet& c, int level, int B, const Poly& key, const Poly& out) {
+  // full key switch of c (Q, level) -> (k0, k1) written to out comps 0/1 (Q, level);
+  // add0/add1 (optional, Q limbs 0..level with out's batch geometry): added to
+  // comps 0/1 of the result, folded into the gadget product as P * add
+  void keyswitch(const LimbSet& c, int level, int B, const Poly& key, const Poly& out,
+                 const u64* add0 = nullptr, const u64* add1 = nullptr) {
     Poly D = decompose(c, level, B);
     Poly u = alloc(2, level + 1 + K, B);
     const int beta = (level + 1 + K - 1) / K;
-    mac_groups(lsqp(u, 0, 2, level, level), 0, lsqp(D, 0, beta, level, level), 0, c, 0, {key.ptr()}, beta);
+    mac_groups(lsqp(u, 0, 2, level, level), 0, lsqp(D, 0, beta, level, level), 0, c, 0, {key.ptr()}, beta, add0, 0,
+               add0 ? level + 1 : 0, add1);
     moddown(lsqp(u, 0, 2, level, level), level, lsq(out, 0, 2, level));
   }
   std::vector<u64> p_mod_q(int level) const {
@@ -1063,9 +1077,8 @@ struct Context {
       orion_launch_tensor(ld, lsq(a.poly, 0, 2, level, B), lsq(b.poly, 0, 2, level, B), d_tb, N, stream);
     }
     Ciphertext out = new_ct(level, B, a.scale * b.scale);
-    keyswitch(lsq(d, 2, 1, level), level, B, rlk, out.poly);
-    LimbSet o = lsq(out.poly, 0, 2, level);
-    ew(EW_ADD, o, o, lsq(d, 0, 2, level));
+    // (d0, d1) + keyswitch(d2): the addition is folded into the gadget product
+    keyswitch(lsq(d, 2, 1, level), level, B, rlk, out.poly, d.ptr(), d.ptr() + d.comp_stride());
     return out;
   }
 
@@ -1076,8 +1089,8 @@ struct Context {
     const int level = a.level, B = a.poly.B;
     const Poly& key = galois_key(g);
     Poly t = alloc(2, level + 1, B);
-    keyswitch(lsq(a.poly, 1, 1, level), level, B, key, t);
-    ew(EW_ADD, lsq(t, 0, 1, level), lsq(t, 0, 1, level), lsq(a.poly, 0, 1, level));
+    // (c0, 0) + keyswitch(c1), the c0 addition folded into the gadget product
+    keyswitch(lsq(a.poly, 1, 1, level), level, B, key, t, a.poly.ptr());
     Ciphertext out = new_ct(level, B, a.scale);
     automorph(lsq(out.poly, 0, 2, level), lsq(t, 0, 2, level), g, false);
     return out;

@@ -167,6 +167,12 @@ struct MacGroups {  // ks_mac_kernel: group g uses key[g]
   long long out_gstride, d_gstride, add_gstride, own_gstride;
   const u64* add0;  // optional comp-0 addend, layout of out comp 0 (stride add_gstride per group)
   int K;            // digit width (own limbs of digit i: l / K == i)
+  // add_nq > 0: scaled Q addends instead -- out limb l < add_nq gets
+  // add{0,1}[l] * add_s[l] (the caller passes P mod q_l, so the ModDown that
+  // follows yields keyswitch + add exactly), limbs l >= add_nq (P) get 0
+  int add_nq;
+  const u64* add1;
+  u64 add_s[ORION_MAXLIMB], add_ss[ORION_MAXLIMB];
 };
 
 // BSGS linear transform plan (device-resident, one per LinTrans): giants in

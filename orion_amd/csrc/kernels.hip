@@ -221,7 +221,20 @@ __global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, Lim
   const int owndigit = (own.p && l < own.nlimb) ? l / G.K : -1;
   u64* op = out.p + g * G.out_gstride;
   ulonglong2 r0 = make_ulonglong2(0, 0), r1 = make_ulonglong2(0, 0);
-  if (G.add0) r0 = *(const ulonglong2*)(G.add0 + g * G.add_gstride + row_off(out, 0, l, bi) + n);
+  if (G.add_nq > 0) {
+    if (l < G.add_nq) {
+      const long long ao = g * G.add_gstride + row_off(out, 0, l, bi) + n;
+      const u64 s = G.add_s[l], ss = G.add_ss[l];
+      const ulonglong2 a = *(const ulonglong2*)(G.add0 + ao);
+      r0 = make_ulonglong2(shoup_mul(a.x, s, ss, q), shoup_mul(a.y, s, ss, q));
+      if (G.add1) {
+        const ulonglong2 b = *(const ulonglong2*)(G.add1 + ao);
+        r1 = make_ulonglong2(shoup_mul(b.x, s, ss, q), shoup_mul(b.y, s, ss, q));
+      }
+    }
+  } else if (G.add0) {
+    r0 = *(const ulonglong2*)(G.add0 + g * G.add_gstride + row_off(out, 0, l, bi) + n);
+  }
   const long long kstride = (long long)nmod_key * N;
   const u64* kp = key + (long long)m * N + n;
   for (int i0 = 0; i0 < beta; i0 += 4) {  // chunks of 4 digits: 12 loads in flight
