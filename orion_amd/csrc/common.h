@@ -114,19 +114,6 @@ __host__ __device__ static inline u64 barrett128(u64 hi, u64 lo, const ModConst&
 __host__ __device__ static inline u64 mul_mod(u64 a, u64 b, const ModConst& m) {
   return barrett128(mulhi64(a, b), a * b, m);
 }
-// Barrett reduction of a 128-bit sum of up to 4 products, x < 4 q^2 (q < 2^61):
-// t1 = x >> (k-1) < 2^(k+3) still fits 64 bits; the quotient estimate is low
-// by at most 4, so r < 5q < 2^64.
-__host__ __device__ static inline u64 barrett128_4(u64 hi, u64 lo, const ModConst& m) {
-  const int k = m.bar_k;
-  u64 t1 = (lo >> (k - 1)) | (hi << (65 - k));
-  u64 ph = mulhi64(t1, m.bar_mu), pl = t1 * m.bar_mu;
-  u64 t2 = (pl >> (k + 1)) | (ph << (63 - k));
-  u64 r = lo - t2 * m.q;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) r = r >= m.q ? r - m.q : r;
-  return r;
-}
 // 128-bit accumulator helpers
 struct Acc128 {
   u64 hi, lo;
@@ -279,21 +266,6 @@ __device__ __forceinline__ u64 bext_prep(const BasisExtTable* __restrict__ T, co
   }
   return (u64)vf;
 }
-// out_t = sum_i y_i * (S/s_i mod t) - v*S  (mod t); y_i < s_i may exceed t, the
-// Shoup product accepts any 64-bit multiplicand and returns [0, 2t)
-__device__ __forceinline__ u64 bext_target(const BasisExtTable* __restrict__ T, int t, u64 q, const u64* y, u64 v) {
-  u64 acc = T->vS_t[t][v];
-  const int ns = T->ns;
-#pragma unroll
-  for (int i = 0; i < ORION_MAXSRC; ++i) {
-    if (i >= ns) break;
-    u64 r = shoup_lazy(y[i], T->qhat_t[t][i], T->qhat_ts[t][i], q);
-    r = r >= q ? r - q : r;
-    acc = add_mod(acc, r, q);
-  }
-  return acc;
-}
-
 // ---------------------------------------------------------------------------
 // NTT launch descriptor: transform + fused producer (prologue) / consumer
 // (epilogue).  Job j = (c, l, b) over dst's (ncomp, nlimb, nbatch); the limb's

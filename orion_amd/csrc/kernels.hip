@@ -102,7 +102,7 @@ __global__ void __launch_bounds__(256) tensor_kernel(LimbSet d, LimbSet a, LimbS
 }
 
 // Exact basis extension (Lattigo ModUpExact restated; the
-// per-coefficient math is bext_prep / bext_target in common.h).
+// source-side math is bext_prep in common.h, the target side bext_target_sel).
 // in: ns source limbs (coefficient domain), out: nt target limbs.  Two
 // coefficients per thread (16-B accesses); the per-target constants are
 // wave-uniform (SGPR) and v*S mod t is selected from the ns+1 precomputed
