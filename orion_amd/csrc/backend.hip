@@ -398,6 +398,28 @@ struct Context {
   // decompositions with fewer limb-transforms per digit than this run every
   // digit's ModUp + NTT as one launch pair (0 = always per digit)
   int modup_merge = getenv("ORION_MODUP_MERGE") ? atoi(getenv("ORION_MODUP_MERGE")) : 256;
+  // N = 2^15 inverse launches up to ntt2_tail_max limb-transforms whose last
+  // round of one-limb workgroups would be partial (jobs / (rounds * CUs) below
+  // ntt2_tail_eff) also take the two-pass kernels: a one-pass round costs one
+  // limb's latency on every CU whether or not the CU has a job, while the
+  // two-pass kernels scale with the job count (tools/ntt_bench.py, mixed
+  // moduli, inverse: 192 jobs 61 vs 76 us, 384 jobs 98 vs 127 us).  Forward
+  // launches keep the one-pass kernel: their fused epilogues cost the
+  // two-pass kernels a scratch round trip, and the LoLA bench measured them
+  // slower (tools/ntt2_tail_ab.sh)
+  double ntt2_tail_eff = getenv("ORION_NTT2_TAIL_EFF") ? atof(getenv("ORION_NTT2_TAIL_EFF")) : 0.9;
+  int ntt2_tail_max = getenv("ORION_NTT2_TAIL_MAX") ? atoi(getenv("ORION_NTT2_TAIL_MAX")) : 1024;
+  int n_cu = 0;
+  bool ntt2_tail(int jobs) {
+    if (jobs > ntt2_tail_max || ntt2_tail_eff <= 0) return false;
+    if (n_cu == 0) {
+      int dev = 0;
+      HIPCHK(hipGetDevice(&dev));
+      HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const int rounds = (jobs + n_cu - 1) / n_cu;
+    return (double)jobs / ((double)rounds * n_cu) < ntt2_tail_eff;
+  }
   void ntt_io(NttIO io, bool inv) {
     io.order = ntt_order;
     io.jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
@@ -407,7 +429,7 @@ struct Context {
         for (int l = 0; l < io.dst.nlimb; ++l)
           if ((host_tb.mc[io.dst.mod[l]].f64 != 0) == (pass == 1)) io.lord[k++] = (unsigned char)l;
     }
-    if (logN == 16 || (logN == 15 && (ntt_impl == 2 || io.jobs < ntt2_below))) {  // N = 2^16: two-pass only
+    if (logN == 16 || (logN == 15 && (ntt_impl == 2 || io.jobs < ntt2_below || (inv && ntt2_tail(io.jobs))))) {  // N = 2^16: two-pass only
       Poly scratch;
       if (ntt2_chunk > 0 && io.jobs > 0) {  // chunks of jobs through one reused compact scratch
         const int chunk = std::min(ntt2_chunk, io.jobs);
