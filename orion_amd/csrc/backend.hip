@@ -409,7 +409,8 @@ struct Context {
   // slower (tools/ntt2_tail_ab.sh)
   double ntt2_tail_eff = getenv("ORION_NTT2_TAIL_EFF") ? atof(getenv("ORION_NTT2_TAIL_EFF")) : 0.9;
   int ntt2_tail_max = getenv("ORION_NTT2_TAIL_MAX") ? atoi(getenv("ORION_NTT2_TAIL_MAX")) : 1024;
-  // 1: plain forward launches (load prologue, store epilogue) follow the same rule
+  // 1: plain forward launches (load prologue, store epilogue) follow the same
+  // rule; 2: every forward launch that needs no scratch (not an in-place tail)
   int ntt2_tail_fwd = getenv("ORION_NTT2_TAIL_FWD") ? atoi(getenv("ORION_NTT2_TAIL_FWD")) : 1;
   int n_cu = 0;
   bool ntt2_tail(int jobs) {
@@ -432,7 +433,8 @@ struct Context {
           if ((host_tb.mc[io.dst.mod[l]].f64 != 0) == (pass == 1)) io.lord[k++] = (unsigned char)l;
     }
     if (logN == 16 || (logN == 15 && (ntt_impl == 2 || io.jobs < ntt2_below ||
-                          ((inv || (ntt2_tail_fwd && io.pro == NTT_PRO_LOAD && io.epi == NTT_EPI_STORE)) &&
+                          ((inv || (ntt2_tail_fwd == 1 && io.pro == NTT_PRO_LOAD && io.epi == NTT_EPI_STORE) ||
+                            (ntt2_tail_fwd == 2 && !(io.epi == NTT_EPI_SUBSCALE && io.ex.p == io.dst.p))) &&
                            ntt2_tail(io.jobs))))) {  // N = 2^16: two-pass only
       Poly scratch;
       if (ntt2_chunk > 0 && io.jobs > 0) {  // chunks of jobs through one reused compact scratch
