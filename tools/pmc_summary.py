@@ -52,21 +52,40 @@ def main(tag, workload="lola_n15", batch=64, logn=15):
                 elif r["Counter_Name"] == "WRITE_SIZE":
                     ntt_write += v * 1024
     ratio = (ntt_fetch + ntt_write) / ntt_alg if ntt_alg else None
-    # the batched NTT launches of the kernel trace (setup keygen launches, < 64
-    # workgroups, excluded): what bench.py's HIP-event "achieved" measures
-    tr = rows(os.path.join(d, "kt_kernel_trace.csv"))
+    # the batched NTT launches of the kernel trace, counted the way bench.py's
+    # HIP events count them: one launch per transform call, i.e. one one-pass
+    # kernel (jobs = workgroups) or one two-pass pair (ntt2.hip: cols kernel
+    # jobs*16 workgroups + rows kernel jobs*BTILES, BTILES = 2^(logn-12)),
+    # duration = the kernels' summed time; setup launches (keygen, < 64 jobs)
+    # are excluded
+    tr = sorted(rows(os.path.join(d, "kt_kernel_trace.csv")), key=lambda r: int(r["Start_Timestamp"]))
+    btiles = 1 << (logn - 12)
     n_l = 0
     n_us = n_b = 0.0
     for r in tr:
         k = r["Kernel_Name"]
-        if "ntt_" not in k:
+        if "ntt" not in k:
             continue
         wgs = int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"])
-        if wgs < 64:
+        dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        tmpl = k.split("<")[1].split(">")[0].replace(" ", "") if "<" in k else ""
+        if "ntt2_" in k:
+            cols = "_cols" in k
+            jobs = wgs // 16 if cols else wgs // btiles
+            if jobs < 64:
+                continue
+            n_us += dur
+            if cols:
+                n_l += 1
+                n_b += jobs * 16.0 * N
+            elif "ntt2_fwd_rows" in k and tmpl.endswith(",1"):  # subtract-and-scale epilogue
+                n_b += jobs * 8.0 * N
+            continue
+        if "ntt_" not in k or wgs < 64:
             continue
         n_l += 1
-        n_us += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        sub = "ntt_fwd_kernel<" in k and k.split("<")[1].split(">")[0].replace(" ", "").endswith(",1")
+        n_us += dur
+        sub = "ntt_fwd_kernel<" in k and tmpl.endswith(",1")
         n_b += wgs * (24.0 if sub else 16.0) * N
     trace = {"launches": n_l, "avg_launch_us": n_us / n_l if n_l else None,
              "algorithmic_bytes_per_launch": n_b / n_l if n_l else None,
