@@ -266,7 +266,7 @@ def main():
                                    f"LogP=[60,60], input level {st.input_level}, Standard ring",
                        "batch_per_gpu": args.batch, "global_batch": args.batch * world,
                        "parallelism": f"replicas x{world} (image shards), keys RCCL-broadcast"},
-            "roofline": {"bound": "hbm", "kernel": "ntt (fwd+inv, 1 limb per workgroup)",
+            "roofline": {"bound": "hbm", "kernel": "ntt (fwd+inv: one-pass, 1 limb per workgroup; two-pass for partial-round launches)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "launches": n_launch, "avg_launch_us": round(n_ms / max(n_launch, 1) * 1e3, 2),
