@@ -59,7 +59,7 @@ static int find_best_n1(const std::vector<int>& idx, int slots, int logMaxRatio)
 
 namespace orion {
 
-enum { EW_ADD = 0, EW_SUB, EW_MUL, EW_MULADD, EW_NEG, EW_SCALE, EW_ADDC, EW_SUBSCALE, EW_COPY, EW_ADDSCALE };
+enum { EW_ADD = 0, EW_SUB, EW_MUL, EW_MULADD, EW_NEG, EW_SCALE, EW_ADDC, EW_SUBSCALE, EW_COPY, EW_ADDSCALE, EW_SPLIT24 };
 
 #define HIPCHK(x)                                                                                  \
   do {                                                                                             \
@@ -139,6 +139,7 @@ struct LinTrans {
   float ratio = 1;
   std::vector<int> idx;                 // diagonal indices, as given
   std::map<int, Plaintext> diags;       // keyed by idx & (slots-1)
+  std::map<int, Poly> sdiags;           // plan copies for lt_bsgs: limbs below 2^48 stored split24
   std::vector<int> giants, babies;      // sorted giants; babies in first-seen order
   std::map<int, std::vector<int>> index;  // giant -> sorted babies
   // device BSGS plan (built at first evaluation, rebuilt when diagonals change)
@@ -154,6 +155,7 @@ struct LinTrans {
   LinTrans& operator=(LinTrans&& o) noexcept {
     level = o.level, N1 = o.N1, ratio = o.ratio;
     idx = std::move(o.idx), diags = std::move(o.diags), giants = std::move(o.giants), babies = std::move(o.babies);
+    sdiags = std::move(o.sdiags);
     index = std::move(o.index), slots = std::move(o.slots), gorder = std::move(o.gorder);
     std::swap(d_plan, o.d_plan), std::swap(n_plan, o.n_plan);
     plan_dirty = o.plan_dirty;
@@ -474,7 +476,7 @@ struct Context {
       s = *sc;
       for (int l = 0; l < o.nlimb; ++l) ss.push_back(hm_shoup(s[l], mods[o.mod[l]]));
     }
-    int nin = (op == EW_NEG || op == EW_SCALE || op == EW_ADDC || op == EW_COPY) ? 1 : 2;
+    int nin = (op == EW_NEG || op == EW_SCALE || op == EW_ADDC || op == EW_COPY || op == EW_SPLIT24) ? 1 : 2;
     if (op == EW_MULADD || op == EW_ADDSCALE) nin += 1;
     Scope scp(this, P_EW, 8.0 * N * o.ncomp * o.nlimb * o.nbatch * (nin + 1));
     orion_launch_ew(op, o, a, b, sc ? s.data() : nullptr, sc ? ss.data() : nullptr, d_tb, N, stream);
@@ -1172,13 +1174,25 @@ struct Context {
     const int nplan = (ng + LT_MAXG - 1) / LT_MAXG;
     std::vector<LtPlan> plans(nplan);
     memset(plans.data(), 0, plans.size() * sizeof(LtPlan));
+    // operand copies of the diagonals in lt_bsgs's split-MAC form (the
+    // diagonals themselves stay canonical for serialisation)
+    T.sdiags.clear();
+    for (auto& kv : T.diags) {
+      const Poly& src = kv.second.poly;
+      Poly dst = alloc(src.ncomp, src.nlimb, src.B);
+      std::vector<int> md;
+      for (int j = 0; j < src.nlimb; ++j) md.push_back(qp_mod(T.level, j));
+      ew(EW_SPLIT24, ls(dst, 0, 1, iota(0, src.nlimb), md), ls(src, 0, 1, iota(0, src.nlimb), md),
+         ls(src, 0, 1, iota(0, src.nlimb), md));
+      T.sdiags.emplace(kv.first, dst);
+    }
     for (int gi = 0; gi < ng; ++gi) {
       LtPlan& P = plans[gi / LT_MAXG];
       const int j = T.gorder[gi], gg = gi % LT_MAXG;
       for (int b : T.index.at(j)) {
         const int sl = slot_of.at(b);
         P.mask[gg] |= 1ull << sl;
-        P.pt[gg][sl] = T.diags.at((j + b) & (N / 2 - 1)).poly.ptr();
+        P.pt[gg][sl] = T.sdiags.at((j + b) & (N / 2 - 1)).ptr();
       }
     }
     if (T.d_plan && T.n_plan != nplan) {
@@ -2681,6 +2695,7 @@ void LoadPlaintextDiagonal(char* data, unsigned long len, int tid, unsigned long
 void RemovePlaintextDiagonals(int tid) {
   API_BEGIN
   ctx().lts.get(tid).diags.clear();
+  ctx().lts.get(tid).sdiags.clear();
   ctx().lts.get(tid).plan_dirty = true;
   API_END_VOID
 }

@@ -25,6 +25,7 @@ enum EwOp : int {
   EW_SUBSCALE = 7, // o = (a - b) * s_l
   EW_COPY = 8,     // o = a
   EW_ADDSCALE = 9, // o = o + a * s_l
+  EW_SPLIT24 = 10, // o = split24(a) on limbs below 2^48 (lt_bsgs's split-MAC operand form), else a
 };
 
 struct Scalars {
@@ -67,6 +68,7 @@ __global__ void __launch_bounds__(256) ew_kernel(LimbSet o, LimbSet a, LimbSet b
       z.y = shoup_mul(sub_mod(x.y, y.y, q), sc.s[l], sc.ss[l], q);
       break;
     case EW_COPY: z = x; break;
+    case EW_SPLIT24: z = mc.bar_k <= 48 ? make_ulonglong2(split24(x.x), split24(x.y)) : x; break;
     case EW_ADDSCALE: {
       const ulonglong2 w = *po;
       z.x = add_mod(w.x, shoup_mul(x.x, sc.s[l], sc.ss[l], q), q);
@@ -401,7 +403,7 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
 #pragma unroll
       for (int s = 0; s < MB; ++s) {
         if ((mask >> s) & 1ull) {
-          const u64 ps = split24(pv[s]);
+          const u64 ps = pv[s];  // the plan's diagonal copies are stored split (EW_SPLIT24)
           macs_add(a0, ps, x0[s]);
           macs_add(a1, ps, x1[s]);
         }
@@ -495,7 +497,7 @@ int orion_launch_ew(int op, const LimbSet& o, const LimbSet& a, const LimbSet& b
 #define CASE(OPC) \
   case OPC: hipLaunchKernelGGL(ew_kernel<OPC>, g, blk, 0, st, o, a, b, sc, tb, N); break;
     CASE(EW_ADD) CASE(EW_SUB) CASE(EW_MUL) CASE(EW_MULADD) CASE(EW_NEG) CASE(EW_SCALE) CASE(EW_ADDC)
-    CASE(EW_SUBSCALE) CASE(EW_COPY) CASE(EW_ADDSCALE)
+    CASE(EW_SUBSCALE) CASE(EW_COPY) CASE(EW_ADDSCALE) CASE(EW_SPLIT24)
 #undef CASE
     default: return -1;
   }
