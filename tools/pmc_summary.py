@@ -10,7 +10,9 @@ and SQ counter passes) and writes
 HBM bytes follow MI355X_MICROARCH.md (HBM/rocprofv3): FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide
 coalesced reads, so it is doubled.  Algorithmic bytes of an NTT launch =
-16 N per limb-transform (one workgroup of N/32 threads per limb).
+16 N per limb-transform (24 N with the subtract-and-scale epilogue), for the
+one-pass kernels (one workgroup of N/32 threads per limb) and the two-pass
+pairs (ntt2.hip) alike.
 """
 import collections
 import csv
@@ -44,11 +46,24 @@ def main(tag, workload="lola_n15", batch=64, logn=15):
             v = float(r["Counter_Value"])
             per[k][r["Counter_Name"]] += v
             per[k]["_dispatches_" + name] += 1
-            if "ntt_" in k and int(r["Grid_Size"]) >= N // 32 * 64:  # the batched launches, not keygen
-                wgs = int(r["Grid_Size"]) // (N // 32)
+            # algorithmic bytes of this dispatch (batched launches only, >= 64
+            # jobs): one-pass kernel = jobs * 16 N (24 N with the subtract-and-
+            # scale epilogue); a two-pass call's 16 N per job is booked on its
+            # cols kernel, the epilogue's extra 8 N on its rows kernel
+            wgs = int(r["Grid_Size"]) // max(1, int(r.get("Workgroup_Size") or 1))
+            tmpl = k.split("<")[1].split(">")[0].replace(" ", "") if "<" in k else ""
+            alg = None
+            if "ntt2_" in k:
+                jobs = wgs // 16 if "_cols" in k else wgs // (1 << (logn - 12))
+                if jobs >= 64:
+                    alg = jobs * 16.0 * N if "_cols" in k else (
+                        jobs * 8.0 * N if ("ntt2_fwd_rows" in k and tmpl.endswith(",1")) else 0.0)
+            elif "ntt_" in k and wgs >= 64:
+                alg = wgs * (24.0 if ("ntt_fwd_kernel" in k and tmpl.endswith(",1")) else 16.0) * N
+            if alg is not None:
                 if r["Counter_Name"] == "FETCH_SIZE":
                     ntt_fetch += 2 * v * 1024
-                    ntt_alg += wgs * 16.0 * N
+                    ntt_alg += alg
                 elif r["Counter_Name"] == "WRITE_SIZE":
                     ntt_write += v * 1024
     ratio = (ntt_fetch + ntt_write) / ntt_alg if ntt_alg else None
