@@ -123,7 +123,9 @@ __device__ __forceinline__ void xchg(T (&a)[32], u32* lds, int t) {
 // 2^(4-dk) distinct twiddles (dk = stage bit - window base B).  Twiddles are
 // software-prefetched TW_PF groups ahead through a compile-time ring, so the
 // L2 latency of a per-thread twiddle load is hidden behind earlier butterflies.
+#ifndef TW_PF
 #define TW_PF 4
+#endif
 template <int B, int DFIRST, int DLAST>
 struct RoundPlan {
   static constexpr int DIR = DLAST >= DFIRST ? 1 : -1;
