@@ -9,10 +9,20 @@ shards (weak scaling), evaluation keys generated on rank 0 and broadcast over
 RCCL/xGMI once before timing; no collective inside the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+
+--gpus N without a torch.distributed.run environment starts N rank processes
+itself (one per GPU, fresh interpreters, before anything touches the GPU);
+under torch.distributed.run, WORLD_SIZE must equal N.
+ORION_BENCH_REHEARSE=1 rehearses the N-rank flow on fewer GPUs (ranks share
+devices, gloo carries the broadcast); ORION_BENCH_DRYRUN=1 runs only the
+launcher and the collective flow on the CPU (no GPU, no number reported as a
+measurement) -- both are for tests, never for a reported value.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -22,6 +32,50 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+METRIC = "encrypted images/sec (LoLa N=2^15) + NTT HBM GB/s vs peak"
+
+
+def host_cpu():
+    """CPUs this process may use on this host, and the host's physical layout."""
+    info = {"nproc": os.cpu_count() or 1}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity"] = info["nproc"]
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+            if q != "max":
+                quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpus"] = quota
+    cores, sockets, model = set(), set(), ""
+    try:
+        phys = core = None
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                k, _, v = ln.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and not model:
+                    model = v
+                elif k == "physical id":
+                    phys = v
+                elif k == "core id":
+                    core = v
+                elif not k and phys is not None:
+                    cores.add((phys, core))
+                    sockets.add(phys)
+                    phys = core = None
+    except OSError:
+        pass
+    info["physical_cores"] = len(cores) or info["nproc"]
+    info["sockets"] = len(sockets) or 1
+    info["model"] = model
+    usable = min(info["affinity"], int(quota) if quota else info["affinity"])
+    info["usable"] = max(1, usable)
+    return info
 
 
 def parse():
@@ -33,8 +87,43 @@ def parse():
     ap.add_argument("--workload", default="lola_n15")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-images", type=int, default=8)
-    ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1))
+    # default: one worker per physical core this process may run on (the
+    # host's physical cores, capped by the cgroup CPU quota / affinity mask)
+    ap.add_argument("--cpu-workers", type=int, default=0)
     return ap.parse_args()
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """Start n rank processes of this script (fresh interpreters, nothing in
+    this parent has touched the GPU), each with the torch.distributed.run
+    environment for one local GPU; wait for all, stop the rest if one fails,
+    exit with the worst status."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            r = p.poll()
+            if r is None:
+                continue
+            alive.remove(p)
+            if r != 0:
+                rc = rc or r
+                for q in alive:  # a dead rank would leave the others waiting in a collective
+                    q.terminate()
+        time.sleep(0.2)
+    return rc if rc > 0 else (1 if rc else 0)
 
 
 def _cpu_worker(args):
@@ -54,10 +143,12 @@ def _cpu_worker(args):
 
 def cpu_baseline(name, n_images, workers):
     """The CPU parity oracle (single-threaded C restatement of the Lattigo
-    algorithms, oracle/ckks_oracle.c) running the same op stream on this host:
-    (a) one core, n_images images timed in this process; (b) all-core
-    throughput, `workers` spawned processes with one independent image
-    stream each, 2 images per worker."""
+    algorithms, oracle/ckks_oracle.c -- the builder's Lattigo stand-in, not
+    Lattigo) running the same op stream on this host: (a) one core, n_images
+    images timed in this process; (b) all-core throughput, `workers` spawned
+    processes with one independent image stream each."""
+    cpu = host_cpu()
+    workers = workers or min(cpu["physical_cores"], cpu["usable"])
     single_dt = _cpu_worker((name, n_images))
     single = n_images / single_dt
     import multiprocessing as mp
@@ -65,24 +156,71 @@ def cpu_baseline(name, n_images, workers):
     with mp.get_context("spawn").Pool(workers) as pool:
         dts = pool.map(_cpu_worker, [(name, per)] * workers)
     allcore = workers * per / max(dts)
-    model = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
-    except OSError:
-        pass
+    # the GPU box's cgroup grants fewer CPUs than the host has cores: the
+    # measured value uses what this process may run on; the linear scaling to
+    # every physical core is reported beside it as an estimate, never as value
+    est = allcore / workers * cpu["physical_cores"] if workers < cpu["physical_cores"] else None
     return dict(value=allcore, unit="images/s", cores=workers, kind="port",
+                all_physical_cores_linear_estimate=est,
+                label="builder C oracle (Lattigo stand-in), single-threaded per op",
                 single_core_images_per_s=single,
-                sample=f"{name}: oracle/ckks_oracle.c (single-threaded per op, like Lattigo); all-core = "
-                       f"{workers} processes x {per} images (slowest {max(dts):.1f} s); single core = "
-                       f"{n_images} images in {single_dt:.1f} s; host '{model}', nproc={os.cpu_count()}")
+                host={k: cpu[k] for k in ("model", "nproc", "physical_cores", "sockets", "affinity",
+                                          "cgroup_cpus", "usable")},
+                sample=f"{name}: all-core = {workers} processes x {per} images (slowest {max(dts):.1f} s); "
+                       f"single core = {n_images} images in {single_dt:.1f} s")
+
+
+def dryrun(args, world, rank):
+    """Launcher + collective flow on the CPU (tests): gloo process group,
+    bundle broadcast, barrier-bracketed stub step, max over ranks, one line."""
+    import torch
+    import torch.distributed as dist
+    from orion_amd import dist as odist
+    dev = torch.device("cpu")
+    if world > 1:
+        dist.init_process_group("gloo")
+    payload = bytes(range(256)) * 64
+    got = {}
+    if world > 1:
+        def export(buf):
+            buf.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
+        odist.broadcast_bundle(dist, lambda: len(payload), export,
+                               lambda buf: got.setdefault("ok", bytes(buf.numpy()) == payload), dev)
+    ok = got.get("ok", True) if rank else True
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.01 * args.steps)
+    dt = time.perf_counter() - t0
+    pids = [os.getpid()]
+    if world > 1:
+        dt = odist.max_over_ranks(dist, dt, dev)
+        ok = odist.sum_over_ranks(dist, 0.0 if ok else 1.0, dev) == 0
+        allp = [None] * world
+        dist.all_gather_object(allp, os.getpid())
+        pids = allp
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "dryrun": True, "value": None, "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(dt / max(args.steps, 1) * 1e3, 3),
+                          "rank_pids": pids, "bundle_broadcast_ok": ok}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
-    import torch
     from orion_amd import dist as odist
     world, rank, local = odist.env_ranks()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks", file=sys.stderr)
+        sys.exit(2)
+    if os.environ.get("ORION_BENCH_DRYRUN") == "1":
+        return dryrun(args, world, rank)
+
+    import torch
     # ORION_BENCH_REHEARSE=1: rehearse the N-rank flow on a box with fewer GPUs
     # (ranks share devices round-robin, gloo carries the broadcast and the
     # max-reduce); never used for a reported number
@@ -90,13 +228,14 @@ def main():
     if rehearse:
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
         if rehearse:
             dist.init_process_group("gloo")
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=device)
 
     from orion_amd.replay import OrionStream
     lib_seed = 2024
@@ -111,11 +250,13 @@ def main():
         st.compile(gen_keys=True)
     else:
         st.compile(gen_keys=False)
+    bundle_bytes = 0
     if world > 1:
-        # RCCL broadcast of public + evaluation keys (+ secret for output checks)
+        # RCCL broadcast of the public + evaluation keys; the secret key stays
+        # on rank 0 (outputs are gathered there for the check)
         def export(buf):
             lib.OrionHipSynchronize()
-            if lib.lib.ExportKeyBundle(buf.data_ptr(), 1) != 0:
+            if lib.lib.ExportKeyBundle(buf.data_ptr(), 0) != 0:
                 raise RuntimeError(lib.lib.OrionHipLastError().decode())
             lib.OrionHipSynchronize()
 
@@ -124,19 +265,18 @@ def main():
                 raise RuntimeError(lib.lib.OrionHipLastError().decode())
             lib.OrionHipSynchronize()
 
-        odist.broadcast_bundle(dist, lambda: lib.KeyBundleBytes(1), export, load, torch.device("cuda", local))
+        bundle_bytes = odist.broadcast_bundle(dist, lambda: lib.KeyBundleBytes(0), export, load, device)
     t_setup = time.perf_counter() - t_setup
 
     # this rank's shard of synthetic images (MNIST-shaped, N(0,1), seed 42 + rank)
     g = torch.Generator().manual_seed(42 + rank)
     imgs = torch.randn(args.batch, 1, 28, 28, generator=g).numpy()
     imgs[0] = st.reference_input().reshape(1, 28, 28)
-    ct = st.encrypt_batch(imgs)
+    ct = st.encrypt_batch(imgs)  # public-key encryption (ranks > 0 hold the broadcast pk, no sk)
     lib.OrionHipSynchronize()
 
     def step():
-        out = st.forward(ct)
-        return out
+        return st.forward(ct)
 
     for _ in range(args.warmup):
         lib.DeleteCiphertext(step())
@@ -159,14 +299,34 @@ def main():
     prof = lib.profile_read()
     if dist:
         dist.barrier()
-        dt = odist.max_over_ranks(dist, dt, torch.device("cuda", local))
+        dt = odist.max_over_ranks(dist, dt, device)
 
-    # correctness of the timed output (image 0 is the fixture's reference input)
-    res = st.decrypt_output(outs[-1])
+    # correctness of the timed output: image 0 of every shard is the fixture's
+    # reference input; each rank's output ciphertext for it is gathered to
+    # rank 0, which holds the only secret key, and decrypted there
     exp = st.arrays["expected_output"].reshape(-1)
-    mae = float(np.abs(res[0] - exp).mean())
-    if dist:  # every rank decrypts with the key bundle it received: report the worst rank
-        mae = odist.max_over_ranks(dist, mae, torch.device("cuda", local))
+    out0 = lib.export_ciphertext(outs[-1])[0]
+    level0 = lib.GetCiphertextLevel(outs[-1])
+    scale0 = lib.GetCiphertextScaleF(outs[-1])
+    shards = [out0]
+    if dist:
+        t = torch.from_numpy(out0.view(np.int64).copy()).to(device if not rehearse else "cpu")
+        allt = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        shards = [a.cpu().numpy().view(np.uint64) for a in allt]
+    mae = None
+    if rank == 0:
+        maes = []
+        n_out = int(np.prod(st.meta["output_shape"]))
+        for sh in shards:
+            h = lib.import_ciphertext(sh[None], scale0)
+            assert lib.GetCiphertextLevel(h) == level0
+            pt = lib.Decrypt(h)
+            vals = np.array(lib.Decode(pt), dtype=np.float64)[:n_out]
+            lib.DeletePlaintext(pt)
+            lib.DeleteCiphertext(h)
+            maes.append(float(np.abs(vals - exp).mean()))
+        mae = max(maes)
     for o in outs:
         lib.DeleteCiphertext(o)
     # one extra, fully profiled step (outside the timed region) for the per-kernel breakdown
@@ -176,51 +336,53 @@ def main():
     lib.OrionHipProfile(0)
     breakdown = lib.profile_read()
 
-    # client side on the GPU (outside the timed region): encode + encrypt of
-    # the batch from HBM-resident slots, and decrypt + decode of the output
-    enc_ev = [e for e in st.input_events() if e["op"] == "Encode"][0]
-    dvals = torch.zeros(args.batch, st.slots, dtype=torch.float32, device=torch.device("cuda", local))
-    dvals[:, :imgs[0].size] = torch.from_numpy(imgs.reshape(args.batch, -1)).to(dvals.device)
-    torch.cuda.synchronize()
-    out_ct = step()
-    dout = torch.empty(args.batch, lib.N // 2, dtype=torch.float64, device=dvals.device)  # DecodeDevice: [B][N/2]
+    client_ms, b1_ms = None, None
+    if rank == 0:
+        # client side on the GPU (outside the timed region): encode + encrypt of
+        # the batch from HBM-resident slots, and decrypt + decode of the output
+        enc_ev = [e for e in st.input_events() if e["op"] == "Encode"][0]
+        dvals = torch.zeros(args.batch, st.slots, dtype=torch.float32, device=device)
+        dvals[:, :imgs[0].size] = torch.from_numpy(imgs.reshape(args.batch, -1)).to(device)
+        torch.cuda.synchronize()
+        out_ct = step()
+        dout = torch.empty(args.batch, lib.N // 2, dtype=torch.float64, device=device)  # DecodeDevice: [B][N/2]
 
-    def client(fn, reps=5):
-        fn()
-        lib.OrionHipSynchronize()
-        t = time.perf_counter()
-        for _ in range(reps):
+        def client(fn, reps=5):
             fn()
-        lib.OrionHipSynchronize()
-        return (time.perf_counter() - t) / reps * 1e3
+            lib.OrionHipSynchronize()
+            t = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            lib.OrionHipSynchronize()
+            return (time.perf_counter() - t) / reps * 1e3
 
-    def enc_once():
-        pt = lib.encode_batch_device(dvals, enc_ev["args"][1], enc_ev["args"][2])
-        lib.DeleteCiphertext(lib.Encrypt(pt))
-        lib.DeletePlaintext(pt)
+        def enc_once():
+            pt = lib.encode_batch_device(dvals, enc_ev["args"][1], enc_ev["args"][2])
+            lib.DeleteCiphertext(lib.Encrypt(pt))
+            lib.DeletePlaintext(pt)
 
-    def dec_once():
-        pt = lib.Decrypt(out_ct)
-        lib.DecodeDevice(pt, dout.data_ptr())
-        lib.DeletePlaintext(pt)
+        def dec_once():
+            pt = lib.Decrypt(out_ct)
+            lib.DecodeDevice(pt, dout.data_ptr())
+            lib.DeletePlaintext(pt)
 
-    client_ms = {"encode_encrypt_ms_per_batch": round(client(enc_once), 3),
-                 "decrypt_decode_ms_per_batch": round(client(dec_once), 3)}
-    lib.DeleteCiphertext(out_ct)
+        client_ms = {"encode_encrypt_ms_per_batch": round(client(enc_once), 3),
+                     "decrypt_decode_ms_per_batch": round(client(dec_once), 3)}
+        lib.DeleteCiphertext(out_ct)
 
-    # BASELINE configs[2] (LoLA N=2^15, batch=1): single-image latency of the
-    # same op stream, outside the timed region (one image per launch leaves
-    # most CUs idle; the throughput line above is the batched shard)
-    ct1 = st.encrypt_batch(imgs[:1])
-    lib.DeleteCiphertext(st.forward(ct1))
-    lib.OrionHipSynchronize()
-    reps1 = 10
-    t1 = time.perf_counter()
-    for _ in range(reps1):
+        # BASELINE configs[2] (LoLA N=2^15, batch=1): single-image latency of the
+        # same op stream, outside the timed region (one image per launch leaves
+        # most CUs idle; the throughput line above is the batched shard)
+        ct1 = st.encrypt_batch(imgs[:1])
         lib.DeleteCiphertext(st.forward(ct1))
-    lib.OrionHipSynchronize()
-    b1_ms = (time.perf_counter() - t1) / reps1 * 1e3
-    lib.DeleteCiphertext(ct1)
+        lib.OrionHipSynchronize()
+        reps1 = 10
+        t1 = time.perf_counter()
+        for _ in range(reps1):
+            lib.DeleteCiphertext(st.forward(ct1))
+        lib.OrionHipSynchronize()
+        b1_ms = (time.perf_counter() - t1) / reps1 * 1e3
+        lib.DeleteCiphertext(ct1)
 
     images = args.batch * world * args.steps
     value = images / dt
@@ -249,7 +411,7 @@ def main():
             except Exception as e:  # the baseline must never break the GPU line
                 cpu = dict(value=None, unit="images/s", cores=1, kind="port", sample=f"failed: {e}")
         line = {
-            "metric": "encrypted images/sec (LoLa N=2^15) + NTT HBM GB/s vs peak",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "images/s",
             "n_gpus": world,
@@ -265,7 +427,8 @@ def main():
             "config": {"workload": f"LoLA (models/lola.py) {args.workload}: N=2^15, LogQ=[60]+[40]x11, "
                                    f"LogP=[60,60], input level {st.input_level}, Standard ring",
                        "batch_per_gpu": args.batch, "global_batch": args.batch * world,
-                       "parallelism": f"replicas x{world} (image shards), keys RCCL-broadcast"},
+                       "parallelism": f"replicas x{world} (image shards), keys RCCL-broadcast"
+                                      + (" (rehearsal: gloo, shared GPUs)" if rehearse else "")},
             "roofline": {"bound": "hbm", "kernel": "ntt (fwd+inv: one-pass, 1 limb per workgroup; two-pass for partial-round launches)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -273,7 +436,8 @@ def main():
                          "algorithmic_bytes_per_launch": round(n_bytes / max(n_launch, 1)),
                          "ntt_share_of_kernel_time": round(bd_ntt_ms / total_prof_ms, 3) if total_prof_ms else None},
             "cpu_baseline": cpu,
-            "check": {"mae_image0_vs_cleartext": mae, "mae_over_ranks": "max", "setup_s": round(t_setup, 1)},
+            "check": {"mae_image0_vs_cleartext": mae, "mae_over_ranks": "max (outputs gathered to rank 0)",
+                      "setup_s": round(t_setup, 1), "key_bundle_bytes": bundle_bytes},
             "client_gpu": dict(client_ms, end_to_end_images_per_s=round(
                 args.batch / ((dt / args.steps) + (client_ms["encode_encrypt_ms_per_batch"]
                                                    + client_ms["decrypt_decode_ms_per_batch"]) / 1e3) * world, 3)),

@@ -68,6 +68,8 @@ void GenerateSecretKey(void);                                              /* ke
 void GeneratePublicKey(void);                                              /* keygenerator.go:23 */
 void GenerateRelinearizationKey(void);                                     /* keygenerator.go:28 */
 void GenerateEvaluationKeys(void);                                         /* keygenerator.go:33 */
+/* Serialize / Load calls use Lattigo v6's MarshalBinary layouts (orion_amd/csrc/wire.h):
+ * rlwe.SecretKey, rlwe.GaloisKey and ringqp.Poly, coefficients in Montgomery form */
 ArrayResultByte SerializeSecretKey(void);                                  /* keygenerator.go:38 */
 void LoadSecretKey(char *data, unsigned long len);                         /* keygenerator.go:49 */
 
@@ -126,8 +128,10 @@ void LoadPlaintextDiagonal(char *data, unsigned long len, int transformId,
 void RemovePlaintextDiagonals(int transformId);                            /* lineartransform.go:196 */
 void RemoveRotationKeys(void);                                             /* lineartransform.go:204 */
 
-/* ---------------- polynomial evaluator / bootstrapping (next) ----------------
- * Exported so the binding resolves; they fail with an error in this round.  */
+/* ---------------- polynomial evaluator / bootstrapping ----------------
+ * Implemented on the GPU: Lattigo's polynomial-evaluator
+ * contract (level - bitlen(degree), exact target scale) and a bootstrapper
+ * that extends the modulus chain above the residual one.  */
 void NewPolynomialEvaluator(void);                                         /* polyeval.go:33 */
 int GenerateMonomial(float *coeffs, int n);                                /* polyeval.go:38 */
 int GenerateChebyshev(float *coeffs, int n);                               /* polyeval.go:50 */
@@ -178,6 +182,10 @@ int ImportCiphertext(const unsigned long *data, int batch, int level, double sca
 int ExportCiphertext(int ct, unsigned long *out, unsigned long n);
 int ImportPlaintext(const unsigned long *data, int batch, int level, double scale);
 int ExportPlaintext(int pt, unsigned long *out, unsigned long n);
+/* the same canonical layout in device memory (e.g. a torch.uint64/int64 tensor
+ * on the library's GPU): no host round trip, asynchronous on the library stream */
+int ImportCiphertextDevice(const unsigned long *dptr, int batch, int level, double scale);
+int ExportCiphertextDevice(int ct, unsigned long *dptr, unsigned long n);
 int ExportSecretKey(unsigned long *out, unsigned long n);                  /* [L+K][N]           */
 int ExportPublicKey(unsigned long *out, unsigned long n);                  /* [2][L+K][N]        */
 int ExportRelinKey(unsigned long *out, unsigned long n);                   /* [dnum][2][L+K][N]  */
@@ -195,7 +203,7 @@ int ImportKeyBundle(const void *dptr, unsigned long bytes);
 /* kernel timing with HIP events on the library stream; enable: 0 = off,
  * 1 = every category, otherwise a bit mask of categories (bit 0 ntt_fwd,
  * 1 ntt_inv, 2 elementwise, 3 basis_ext, 4 ks_mac, 5 automorph, 6 tensor,
- * 7 rescale_prep) */
+ * 7 rescale_prep, 8 lt_bsgs) */
 void OrionHipProfile(int enable);
 /* fills up to max entries: name (32 chars each), launches, total ms, algorithmic bytes */
 int OrionHipProfileRead(char *names, long *launches, double *ms, double *bytes, int max);

@@ -155,6 +155,8 @@ SIGNATURES = {
     "ExportCiphertext": ([c_int, P(c_ulong), c_ulong], c_int),
     "ImportPlaintext": ([P(c_ulong), c_int, c_int, c_double], c_int),
     "ExportPlaintext": ([c_int, P(c_ulong), c_ulong], c_int),
+    "ImportCiphertextDevice": ([c_void_p, c_int, c_int, c_double], c_int),
+    "ExportCiphertextDevice": ([c_int, c_void_p, c_ulong], c_int),
     "ExportSecretKey": ([P(c_ulong), c_ulong], c_int),
     "ExportPublicKey": ([P(c_ulong), c_ulong], c_int),
     "ExportRelinKey": ([P(c_ulong), c_ulong], c_int),
@@ -175,6 +177,7 @@ SIGNATURES = {
 LATTIGO_SYMBOLS = [n for n in SIGNATURES if not n.startswith("OrionHip") and n not in (
     "EncodeBatch", "EncodeBatchDevice", "DecodeDevice", "DecodeF64", "GetCiphertextBatch", "GetPlaintextBatch",
     "GetCiphertextScaleF", "ImportCiphertext", "ExportCiphertext", "ImportPlaintext", "ExportPlaintext",
+    "ImportCiphertextDevice", "ExportCiphertextDevice",
     "ExportSecretKey", "ExportPublicKey", "ExportRelinKey",
     "ExportGaloisKey", "ExportLinearTransformDiagonal", "GetLinearTransformN1", "GaloisElement",
     "KeyBundleBytes", "ExportKeyBundle", "ImportKeyBundle", "ModDropCiphertext", "GetPolyDepth")]
@@ -315,6 +318,18 @@ class HipLibrary:
         B, _, nl, _ = arr.shape
         h = self.lib.ImportCiphertext(arr.ctypes.data_as(P(c_ulong)), B, nl - 1, float(scale))
         return self._chk(h, "ImportCiphertext")
+
+    def import_ciphertext_device(self, t, scale):
+        """t: a contiguous [B][2][level+1][N] int64/uint64 device tensor (torch), NTT domain."""
+        assert t.is_cuda and t.is_contiguous() and t.dim() == 4 and t.shape[3] == self.N and t.element_size() == 8
+        return self._chk(self.lib.ImportCiphertextDevice(t.data_ptr(), t.shape[0], t.shape[2] - 1, float(scale)),
+                         "ImportCiphertextDevice")
+
+    def export_ciphertext_device(self, ct, out):
+        """Copy ciphertext `ct` into the device tensor `out` ([B][2][level+1][N], 8-byte elements)."""
+        assert out.is_cuda and out.is_contiguous() and out.element_size() == 8
+        self._chk(self.lib.ExportCiphertextDevice(ct, out.data_ptr(), out.numel()), "ExportCiphertextDevice")
+        return out
 
     def export_plaintext(self, pt):
         B = self.GetPlaintextBatch(pt)

@@ -1,4 +1,6 @@
 """Build liborion_hip.so in-tree for gfx950 (hipcc, no JIT cache)."""
+import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -13,7 +15,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: the float64 quotient of the exact basis extension and the
 # encoder FFT must round exactly as written (bit parity with the CPU oracle).
 FLAGS = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result"]
-SOURCES = ["ntt.hip", "ntt2.hip", "kernels.hip", "encoder.hip", "backend.hip", "hostmath.cpp"]
+SOURCES = ["ntt.hip", "ntt2.hip", "kernels.hip", "encoder.hip", "backend.hip", "hostmath.cpp", "wire.cpp"]
 
 
 def _needs(obj, deps):
@@ -23,18 +25,33 @@ def _needs(obj, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _stamp(build_dir, recipe):
+    """Rebuild everything when the compiler, the arch or any flag changed since
+    the objects in build_dir were made (mtimes alone miss a new -D flag)."""
+    path = os.path.join(build_dir, "recipe.json")
+    digest = hashlib.sha256(json.dumps(recipe, sort_keys=True).encode()).hexdigest()
+    old = None
+    if os.path.exists(path):
+        with open(path) as f:
+            old = json.load(f).get("digest")
+    return path, digest, old != digest
+
+
 def build(verbose=False, extra_flags=(), lib=LIB, build_dir=BUILD):
     """Compile liborion_hip.so (extra_flags/lib/build_dir: timing-only variants)."""
     BUILD_, LIB_ = build_dir, lib
     os.makedirs(BUILD_, exist_ok=True)
+    recipe = {"hipcc": HIPCC, "arch": ARCH, "flags": FLAGS + list(extra_flags), "sources": SOURCES}
+    stamp, digest, changed = _stamp(BUILD_, recipe)
     headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     headers.append(os.path.join(HERE, "..", "include", "orion_hip.h"))
+    headers.append(os.path.abspath(__file__))
     objs, jobs = [], []
     for src in SOURCES:
         path = os.path.join(CSRC, src)
         obj = os.path.join(BUILD_, src + ".o")
         objs.append(obj)
-        if _needs(obj, [path] + headers):
+        if changed or _needs(obj, [path] + headers):
             cmd = [HIPCC] + FLAGS + list(extra_flags) + ["-c", path, "-o", obj]
             if src.endswith(".hip"):
                 cmd.insert(1, f"--offload-arch={ARCH}")
@@ -49,8 +66,10 @@ def build(verbose=False, extra_flags=(), lib=LIB, build_dir=BUILD):
 
     with ThreadPoolExecutor(max_workers=4) as ex:
         list(ex.map(run, jobs))
-    if jobs or not os.path.exists(LIB_):
+    if jobs or changed or not os.path.exists(LIB_):
         run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_] + objs)
+    with open(stamp, "w") as f:
+        json.dump({"digest": digest, "recipe": recipe}, f, indent=1)
     return LIB_
 
 

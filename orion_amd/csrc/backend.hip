@@ -22,6 +22,7 @@
 #include "../../include/orion_hip.h"
 #include "common.h"
 #include "hostmath.h"
+#include "wire.h"
 
 int orion_launch_ntt(int logN, const LimbSet& s, const DeviceTables* tb, bool inverse, hipStream_t st);
 int orion_launch_ntt_io(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st);
@@ -1219,6 +1220,10 @@ struct Context {
     const int B = ct.poly.B, nqp = level + 1 + K;
     const int beta = (level + 1 + K - 1) / K;
     if (T.giants.empty()) throw std::runtime_error("linear transform without diagonals");
+    for (int d : T.idx)
+      if (!T.diags.count(d & (N / 2 - 1)))
+        throw std::runtime_error("linear transform diagonal " + std::to_string(d) +
+                                 " is not loaded (io_mode load: call LoadPlaintextDiagonal first)");
     if (T.plan_dirty) build_plan(T);
     const std::vector<u64> pq = p_mod_q(level);
     const int nb = (int)T.slots.size();
@@ -1974,6 +1979,10 @@ void OrionHipSetStream(void* s) {
   API_BEGIN
   g_user_stream = (hipStream_t)s;
   if (g) {
+    // the buffer pool hands freed buffers out again with no stream tracking:
+    // drain the old stream so no kernel still reading or writing a pooled
+    // buffer overlaps the first launches on the new one
+    if (g->stream) HIPCHK(hipStreamSynchronize(g->stream));
     if (g->own_stream && g->stream) hipStreamDestroy(g->stream);
     g->own_stream = false;
     g->stream = (hipStream_t)s;
@@ -2162,6 +2171,46 @@ void GenerateRelinearizationKey(void) {
 }
 void GenerateEvaluationKeys(void) {}
 
+// ---- Lattigo v6 wire formats (wire.h): rlwe.SecretKey = ringqp.Poly ----
+static std::vector<u64> mods_of(const Context& c, int nq, bool with_p) {
+  std::vector<u64> m(c.mods.begin(), c.mods.begin() + nq);
+  if (with_p) m.insert(m.end(), c.mods.begin() + c.L, c.mods.begin() + c.L + c.K);
+  return m;
+}
+// ringqp.Poly of a [nq + K][N] host block: ring.Poly Q (nq limbs), ring.Poly P (K limbs)
+static void put_qp(std::vector<char>& b, const Context& c, const u64* data, int nq) {
+  wire::put_poly(b, data, mods_of(c, nq, false), c.N);
+  std::vector<u64> pm(c.mods.begin() + c.L, c.mods.begin() + c.L + c.K);
+  wire::put_poly(b, data + (size_t)nq * c.N, pm, c.N);
+}
+static void get_qp(wire::Reader& rd, const Context& c, u64* out, int nq, const char* what) {
+  rd.get_poly(out, mods_of(c, nq, false), c.N, what);
+  std::vector<u64> pm(c.mods.begin() + c.L, c.mods.begin() + c.L + c.K);
+  rd.get_poly(out + (size_t)nq * c.N, pm, c.N, what);
+}
+static ArrayResultByte to_bytes(const std::vector<char>& v) {
+  ArrayResultByte r{nullptr, 0};
+  r.Data = to_c_array<char, char>(v, &r.Length);
+  return r;
+}
+// rlwe.GaloisKey: GaloisElement, NthRoot, GadgetCiphertext{BaseTwoDecomposition 0,
+// Value: dnum x 1 VectorQP (k0, k1)} of a [dnum][2][L+K][N] host key
+static std::vector<char> galois_key_bytes(const Context& c, u64 galEl, const std::vector<u64>& key) {
+  std::vector<char> b;
+  const size_t qp = (size_t)(c.L + c.K) * c.N;
+  b.reserve(40 + (size_t)c.dnum * (16 + 2 * (wire::poly_bytes(c.L, c.N) + wire::poly_bytes(c.K, c.N))));
+  wire::put_u64(b, galEl);
+  wire::put_u64(b, 2 * (u64)c.N);  // NthRoot
+  wire::put_u64(b, 0);             // BaseTwoDecomposition
+  wire::put_u64(b, (u64)c.dnum);   // Matrix rows
+  for (int i = 0; i < c.dnum; ++i) {
+    wire::put_u64(b, 1);  // one column (no power-of-two decomposition)
+    wire::put_u64(b, 2);  // VectorQP length
+    for (int k = 0; k < 2; ++k) put_qp(b, c, key.data() + (2 * (size_t)i + k) * qp, c.L);
+  }
+  return b;
+}
+
 ArrayResultByte SerializeSecretKey(void) {
   ArrayResultByte r{nullptr, 0};
   API_BEGIN
@@ -2169,25 +2218,19 @@ ArrayResultByte SerializeSecretKey(void) {
   if (!c.have_sk) throw std::runtime_error("secret key not generated");
   std::vector<u64> host;
   c.download(c.sk, host);
-  std::vector<char> bytes(16 + host.size() * 8);
-  const u64 hdr[2] = {0x4f52494f4e534b31ull /* "ORIONSK1" */, (u64)host.size()};
-  memcpy(bytes.data(), hdr, 16);
-  memcpy(bytes.data() + 16, host.data(), host.size() * 8);
-  r.Data = to_c_array<char, char>(bytes, &r.Length);
-  return r;
+  std::vector<char> bytes;
+  put_qp(bytes, c, host.data(), c.L);
+  return to_bytes(bytes);
   API_END(r)
 }
 void LoadSecretKey(char* data, unsigned long len) {
   API_BEGIN
   Context& c = ctx();
-  u64 hdr[2];
-  if (len < 16) throw std::runtime_error("secret key blob too short");
-  memcpy(hdr, data, 16);
-  const size_t n = (size_t)(c.L + c.K) * c.N;
-  if (hdr[0] != 0x4f52494f4e534b31ull || hdr[1] != n || len != 16 + n * 8)
-    throw std::runtime_error("secret key blob does not match the scheme");
-  std::vector<u64> host(n);
-  memcpy(host.data(), data + 16, n * 8);
+  if (!data) throw std::runtime_error("null secret key data");
+  wire::Reader rd(data, len);
+  std::vector<u64> host((size_t)(c.L + c.K) * c.N);
+  get_qp(rd, c, host.data(), c.L, "secret key");
+  if (rd.left()) throw std::runtime_error("secret key blob has trailing bytes");
   c.sk = c.alloc(1, c.L + c.K, 1);
   c.upload(c.sk, host);
   c.have_sk = true;
@@ -2560,9 +2603,11 @@ int GenerateLinearTransform(int* diagIdx, int nIdx, float* data, int nData, int 
                             char* ioMode) {
   API_BEGIN
   Context& c = ctx();
-  (void)ioMode;
+  // lineartransform.go:79-88: in "load" mode the diagonals were serialised
+  // earlier and arrive through LoadPlaintextDiagonal, so none is encoded here
+  const bool load = ioMode && std::string(ioMode) == "load";
   const int slots = c.N / 2;
-  if ((long)nIdx * slots != (long)nData) throw std::runtime_error("diagonal data length != nIdx * slots");
+  if (!load && (long)nIdx * slots != (long)nData) throw std::runtime_error("diagonal data length != nIdx * slots");
   if (level < 0 || level >= c.L) throw std::runtime_error("invalid level");
   LinTrans T;
   T.level = level;
@@ -2586,7 +2631,7 @@ int GenerateLinearTransform(int* diagIdx, int nIdx, float* data, int nData, int 
     T.giants.push_back(kv.first);
   }
   std::vector<float> vec(slots);
-  for (int i = 0; i < nIdx; ++i) {
+  for (int i = 0; i < nIdx && !load; ++i) {
     int gi, bi;
     bsgs_split(diagIdx[i], slots, T.N1, &gi, &bi);
     const float* v = data + (size_t)i * slots;
@@ -2638,55 +2683,85 @@ void GenerateConsolidatedRotationKeys(int* galEls, int n) {
   for (int i = 0; i < n; ++i) ctx().gen_galois((u64)(unsigned)galEls[i]);
   API_END_VOID
 }
+// lineartransform.go:131-142: a fresh key, serialised and NOT kept (the
+// save path stores it to HDF5 and LoadRotationKey brings it back per layer)
 ArrayResultByte GenerateAndSerializeRotationKey(int galEl) {
   ArrayResultByte r{nullptr, 0};
   API_BEGIN
   Context& c = ctx();
-  c.gen_galois((u64)(unsigned)galEl);
+  const u64 g = (u64)(unsigned)galEl;
+  auto kept = c.gks.find(g);
+  Poly saved;
+  if (kept != c.gks.end()) {
+    saved = kept->second;
+    c.gks.erase(kept);
+  }
+  c.gen_galois(g);
   std::vector<u64> host;
-  c.download(c.gks.at((u64)(unsigned)galEl), host);
-  std::vector<char> bytes(host.size() * 8);
-  memcpy(bytes.data(), host.data(), bytes.size());
-  r.Data = to_c_array<char, char>(bytes, &r.Length);
-  return r;
+  c.download(c.gks.at(g), host);
+  c.gks.erase(g);
+  if (saved.buf) c.gks[g] = saved;
+  return to_bytes(galois_key_bytes(c, g, host));
   API_END(r)
 }
+// lineartransform.go:145-164: unmarshal an rlwe.GaloisKey into the key set under galEl
 void LoadRotationKey(char* data, unsigned long len, unsigned long galEl) {
   API_BEGIN
   Context& c = ctx();
+  if (!data) throw std::runtime_error("null rotation key data");
+  wire::Reader rd(data, len);
+  const u64 ge = rd.get_u64(), nth = rd.get_u64(), b2 = rd.get_u64(), rows = rd.get_u64();
+  if (nth != 2 * (u64)c.N) throw std::runtime_error("rotation key: NthRoot does not match the ring");
+  if (b2 != 0) throw std::runtime_error("rotation key: power-of-two decomposition is not supported");
+  if (rows != (u64)c.dnum) throw std::runtime_error("rotation key: gadget rows != dnum of this chain");
+  if (ge != galEl) throw std::runtime_error("rotation key: blob is for Galois element " + std::to_string(ge));
+  const size_t qp = (size_t)(c.L + c.K) * c.N;
+  std::vector<u64> host(2 * (size_t)c.dnum * qp);
+  for (int i = 0; i < c.dnum; ++i) {
+    if (rd.get_u64() != 1 || rd.get_u64() != 2) throw std::runtime_error("rotation key: unexpected gadget shape");
+    for (int k = 0; k < 2; ++k) get_qp(rd, c, host.data() + (2 * (size_t)i + k) * qp, c.L, "rotation key");
+  }
+  if (rd.left()) throw std::runtime_error("rotation key blob has trailing bytes");
   Poly k = c.alloc(2 * c.dnum, c.L + c.K, 1);
-  if (len != (unsigned long)k.ncomp * k.nlimb * c.N * 8) throw std::runtime_error("rotation key blob size mismatch");
-  std::vector<u64> host(len / 8);
-  memcpy(host.data(), data, len);
   c.upload(k, host);
   c.gks[galEl] = k;
   API_END_VOID
 }
+// lineartransform.go:167-183: the diagonal's ringqp.Poly (Q at the transform's
+// level, P), after which the transform forgets it until LoadPlaintextDiagonal
 ArrayResultByte SerializeDiagonal(int tid, int diagIdx) {
   ArrayResultByte r{nullptr, 0};
   API_BEGIN
   Context& c = ctx();
-  const Plaintext& p = c.lts.get(tid).diags.at(diagIdx & (c.N / 2 - 1));
+  LinTrans& T = c.lts.get(tid);
+  const int key = diagIdx & (c.N / 2 - 1);
+  auto it = T.diags.find(key);
+  if (it == T.diags.end()) throw std::runtime_error("diagonal " + std::to_string(diagIdx) + " is not loaded");
   std::vector<u64> host;
-  c.download(p.poly, host);
-  std::vector<char> bytes(host.size() * 8);
-  memcpy(bytes.data(), host.data(), bytes.size());
-  r.Data = to_c_array<char, char>(bytes, &r.Length);
-  return r;
+  c.download(it->second.poly, host);
+  std::vector<char> bytes;
+  put_qp(bytes, c, host.data(), T.level + 1);
+  T.diags.erase(it);
+  T.sdiags.erase(key);
+  T.plan_dirty = true;
+  return to_bytes(bytes);
   API_END(r)
 }
+// lineartransform.go:186-200
 void LoadPlaintextDiagonal(char* data, unsigned long len, int tid, unsigned long diagIdx) {
   API_BEGIN
   Context& c = ctx();
+  if (!data) throw std::runtime_error("null diagonal data");
   LinTrans& T = c.lts.get(tid);
   Plaintext p;
   p.level = T.level;
   p.qp = true;
   p.scale = (long double)c.mods[T.level];
   p.poly = c.alloc(1, T.level + 1 + c.K, 1);
-  if (len != (unsigned long)p.poly.nlimb * c.N * 8) throw std::runtime_error("diagonal blob size mismatch");
-  std::vector<u64> host(len / 8);
-  memcpy(host.data(), data, len);
+  wire::Reader rd(data, len);
+  std::vector<u64> host((size_t)p.poly.nlimb * c.N);
+  get_qp(rd, c, host.data(), T.level + 1, "diagonal");
+  if (rd.left()) throw std::runtime_error("diagonal blob has trailing bytes");
   c.upload(p.poly, host);
   T.diags[(int)diagIdx & (c.N / 2 - 1)] = p;
   T.plan_dirty = true;
@@ -2825,9 +2900,14 @@ static std::vector<u64> from_canonical(const unsigned long* in, int ncomp, int n
         memcpy(dev.data() + (((size_t)c * nl + l) * B + b) * N, in + (((size_t)b * ncomp + c) * nl + l) * N, N * 8);
   return dev;
 }
+static void check_import(const Context& c, const void* data, int B, int level) {
+  if (!data) throw std::runtime_error("null data pointer");
+  if (level < 0 || level >= c.L || B < 1) throw std::runtime_error("invalid level/batch");
+}
 int ImportCiphertext(const unsigned long* data, int B, int level, double scale) {
   API_BEGIN
   Context& c = ctx();
+  check_import(c, data, B, level);
   Ciphertext ct = c.new_ct(level, B, (long double)scale);
   c.upload(ct.poly, from_canonical(data, 2, level + 1, B, c.N));
   return c.cts.add(std::move(ct));
@@ -2847,9 +2927,46 @@ int ExportCiphertext(int id, unsigned long* out, unsigned long n) {
   return 0;
   API_END(-1)
 }
+// canonical [B][2][nl][N] device layout <-> the library's [2][nl][B][N]: one
+// strided 2-D copy per (comp, limb) plane, no host round trip
+static void copy_planes(Context& c, u64* dst, long long dpitch, const u64* src, long long spitch, int nplane, int B,
+                        long long dplane, long long splane) {
+  for (int p = 0; p < nplane; ++p)
+    HIPCHK(hipMemcpy2DAsync(dst + p * dplane, dpitch * 8, src + p * splane, spitch * 8, (size_t)c.N * 8, B,
+                            hipMemcpyDeviceToDevice, c.stream));
+}
+int ImportCiphertextDevice(const unsigned long* dptr, int B, int level, double scale) {
+  API_BEGIN
+  Context& c = ctx();
+  check_import(c, dptr, B, level);
+  const int nl = level + 1;
+  Ciphertext ct = c.new_ct(level, B, (long double)scale);
+  // plane (comp, limb) = p: library offset p*B*N, canonical offset p*N with row pitch 2*nl*N
+  copy_planes(c, ct.poly.ptr(), c.N, (const u64*)dptr, (long long)2 * nl * c.N, 2 * nl, B, (long long)B * c.N, c.N);
+  return c.cts.add(std::move(ct));
+  API_END(-1)
+}
+int ExportCiphertextDevice(int id, unsigned long* dptr, unsigned long n) {
+  API_BEGIN
+  Context& c = ctx();
+  if (!dptr) throw std::runtime_error("null output pointer");
+  const Ciphertext& ct = c.cts.get(id);
+  const int nl = ct.level + 1, B = ct.poly.B;
+  if (n != (unsigned long)B * 2 * nl * c.N) throw std::runtime_error("export buffer size mismatch");
+  // a ciphertext's limb planes may be allocated for a higher level: address them by its strides
+  const Poly& P = ct.poly;
+  for (int comp = 0; comp < 2; ++comp)
+    for (int l = 0; l < nl; ++l)
+      HIPCHK(hipMemcpy2DAsync((u64*)dptr + ((size_t)comp * nl + l) * c.N, (size_t)2 * nl * c.N * 8,
+                              P.ptr() + comp * P.comp_stride() + l * P.limb_stride(), (size_t)c.N * 8,
+                              (size_t)c.N * 8, B, hipMemcpyDeviceToDevice, c.stream));
+  return 0;
+  API_END(-1)
+}
 int ImportPlaintext(const unsigned long* data, int B, int level, double scale) {
   API_BEGIN
   Context& c = ctx();
+  check_import(c, data, B, level);
   Plaintext p;
   p.level = level;
   p.scale = (long double)scale;
@@ -2913,14 +3030,23 @@ int ExportLinearTransformDiagonal(int tid, int diagIdx, unsigned long* out, unsi
 }
 
 // ---- key bundle for RCCL broadcast ----
-// layout: header u64[4] {magic, ngk, withSecret, haveRlk}, galEls[ngk], then
-// pk, rlk, gk_0..gk_{ngk-1}, [sk] as raw device polys
+// layout: header u64[KB_HDR] {magic, ngk, withSecret, haveRlk, logN, L, K,
+// dnum, moduli digest}, galEls[ngk], then pk, rlk, gk_0..gk_{ngk-1}, [sk] as
+// raw device polys.  The importer rejects a bundle made for another chain.
+enum { KB_HDR = 9 };
+static const u64 KB_MAGIC = 0x4f52494f4e4b4232ull;  // "ORIONKB2"
+static u64 moduli_digest(const Context& c) {
+  u64 h = 0xcbf29ce484222325ull;  // FNV-1a over the QP moduli
+  for (u64 q : c.mods)
+    for (int b = 0; b < 8; ++b) h = (h ^ ((q >> (8 * b)) & 0xff)) * 0x100000001b3ull;
+  return h;
+}
 unsigned long KeyBundleBytes(int withSecret) {
   API_BEGIN
   Context& c = ctx();
   const size_t key = (size_t)2 * c.dnum * (c.L + c.K) * c.N * 8, pk = (size_t)2 * (c.L + c.K) * c.N * 8,
                sk = (size_t)(c.L + c.K) * c.N * 8;
-  size_t hdr = (4 + c.gks.size()) * 8;
+  size_t hdr = (KB_HDR + c.gks.size()) * 8;
   hdr = (hdr + 255) & ~(size_t)255;
   return hdr + pk + (c.have_rlk ? key : 0) + c.gks.size() * key + (withSecret ? sk : 0);
   API_END(0)
@@ -2928,9 +3054,11 @@ unsigned long KeyBundleBytes(int withSecret) {
 int ExportKeyBundle(void* dptr, int withSecret) {
   API_BEGIN
   Context& c = ctx();
+  if (!dptr) throw std::runtime_error("null bundle pointer");
   if (!c.have_pk) throw std::runtime_error("no public key");
   if (withSecret && !c.have_sk) throw std::runtime_error("no secret key");
-  std::vector<u64> hdr = {0x4f52494f4e4b4231ull, (u64)c.gks.size(), (u64)(withSecret ? 1 : 0), (u64)c.have_rlk};
+  std::vector<u64> hdr = {KB_MAGIC, (u64)c.gks.size(), (u64)(withSecret ? 1 : 0), (u64)c.have_rlk,
+                          (u64)c.logN, (u64)c.L, (u64)c.K, (u64)c.dnum, moduli_digest(c)};
   for (auto& kv : c.gks) hdr.push_back(kv.first);
   size_t off = ((hdr.size() * 8) + 255) & ~(size_t)255;
   char* d = (char*)dptr;
@@ -2951,12 +3079,18 @@ int ExportKeyBundle(void* dptr, int withSecret) {
 int ImportKeyBundle(const void* dptr, unsigned long bytes) {
   API_BEGIN
   Context& c = ctx();
-  u64 h4[4];
-  HIPCHK(hipMemcpy(h4, dptr, 32, hipMemcpyDeviceToHost));
-  if (h4[0] != 0x4f52494f4e4b4231ull) throw std::runtime_error("not a key bundle");
+  if (!dptr) throw std::runtime_error("null bundle pointer");
+  if (bytes < KB_HDR * 8) throw std::runtime_error("key bundle shorter than its header");
+  u64 h4[KB_HDR];
+  HIPCHK(hipMemcpy(h4, dptr, sizeof(h4), hipMemcpyDeviceToHost));
+  if (h4[0] != KB_MAGIC) throw std::runtime_error("not a key bundle");
+  if (h4[4] != (u64)c.logN || h4[5] != (u64)c.L || h4[6] != (u64)c.K || h4[7] != (u64)c.dnum ||
+      h4[8] != moduli_digest(c))
+    throw std::runtime_error("key bundle was made for another modulus chain (logN/L/K/dnum/moduli differ)");
+  if (h4[1] > (bytes / 8 - KB_HDR)) throw std::runtime_error("key bundle truncated (galois element list)");
   std::vector<u64> gels(h4[1]);
-  if (h4[1]) HIPCHK(hipMemcpy(gels.data(), (const char*)dptr + 32, h4[1] * 8, hipMemcpyDeviceToHost));
-  size_t off = ((4 + h4[1]) * 8 + 255) & ~(size_t)255;
+  if (h4[1]) HIPCHK(hipMemcpy(gels.data(), (const char*)dptr + KB_HDR * 8, h4[1] * 8, hipMemcpyDeviceToHost));
+  size_t off = ((KB_HDR + h4[1]) * 8 + 255) & ~(size_t)255;
   const char* d = (const char*)dptr;
   auto get = [&](int ncomp, int nlimb) {
     Poly p = c.alloc(ncomp, nlimb, 1);

@@ -72,3 +72,38 @@ def test_shard_covers_every_image():
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             sizes = [hi - lo for lo, hi in spans]
             assert max(sizes) - min(sizes) <= 1
+
+
+def _run_bench(args, extra_env=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(ORION_BENCH_DRYRUN="1", **(extra_env or {}))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=timeout, cwd=root)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, [json.loads(ln) for ln in lines]
+
+
+def test_bench_launches_n_ranks_itself():
+    """`bench.py --gpus 2` with no torch.distributed.run environment starts two
+    rank processes itself (--gpus was ignored); rank 0 prints one
+    line with n_gpus 2, gathered from two distinct processes, after the key
+    bundle broadcast over gloo reached the other rank."""
+    r, lines = _run_bench(["--gpus", "2", "--steps", "3", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1, r.stdout
+    ln = lines[0]
+    assert ln["n_gpus"] == 2 and ln["dryrun"] is True and ln["value"] is None
+    assert len(set(ln["rank_pids"])) == 2
+    assert ln["bundle_broadcast_ok"] is True
+
+
+def test_bench_refuses_world_mismatch():
+    """Under an external launcher, WORLD_SIZE must equal --gpus."""
+    r, lines = _run_bench(["--gpus", "2"], extra_env=dict(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode == 2 and not lines
+    assert "--gpus 2" in r.stderr

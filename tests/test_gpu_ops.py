@@ -197,6 +197,12 @@ def _replay_gpu_vs_cpu(name, seed):
     lib.DeleteScheme()
 
 
+def test_mlp_n13_c1_matches_cpu_oracle_replay(torch_cuda):
+    """BASELINE config C1 (configs/mlp.yml, N=2^13, 6 Q + 2 P primes of 26-29
+    bits): whole forward pass on the GPU bit for bit vs the oracle, MAE gate."""
+    _replay_gpu_vs_cpu("mlp_n13", seed=36)
+
+
 def test_mlp_n14_matches_cpu_oracle_replay(torch_cuda):
     """BASELINE config C2 (MLP, N=2^14, 8 Q + 2 P primes): whole forward pass."""
     _replay_gpu_vs_cpu("mlp_n14", seed=31)

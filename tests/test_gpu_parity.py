@@ -259,38 +259,6 @@ def test_linear_transform_parity(small):
     assert np.abs(dec - exp).max() < 1e-3
 
 
-def test_serialization_roundtrip(small):
-    """io_mode save/load paths (keygenerator.go:38-58, lineartransform.go:131-193):
-    secret key, a Galois key and an LT diagonal survive serialise -> drop ->
-    load bit for bit, and the reloaded transform gives the same ciphertext."""
-    lib, orc = small
-    sk = lib.export_secret_key()
-    blob, _ = lib.SerializeSecretKey()
-    lib.LoadSecretKey(blob)
-    assert np.array_equal(lib.export_secret_key(), sk)
-    g = int(lib.GaloisElement(5))
-    blob, _ = lib.GenerateAndSerializeRotationKey(g)
-    gk = lib.export_galois_key(g)
-    lib.RemoveRotationKeys()
-    lib.LoadRotationKey(blob, g)
-    assert np.array_equal(lib.export_galois_key(g), gk)
-    rng = np.random.default_rng(8)
-    slots, level = orc.N // 2, 3
-    idx = [0, 5, 40]
-    diags = rng.uniform(-1, 1, (len(idx), slots)).astype(np.float32)
-    lt = lib.GenerateLinearTransform(idx, list(diags.reshape(-1)), level, 2.0, "none")
-    lib.GenerateConsolidatedRotationKeys(lib.GetLinearTransformRotationKeys(lt))
-    ct = lib.Encrypt(lib.Encode(list(rng.standard_normal(slots).astype(np.float32)), level, 1 << 40))
-    ref = lib.export_ciphertext(lib.EvaluateLinearTransform(lt, ct))
-    blobs = {d: lib.SerializeDiagonal(lt, d)[0] for d in idx}
-    pts = {d: lib.export_lt_diagonal(lt, d, level) for d in idx}
-    lib.RemovePlaintextDiagonals(lt)
-    for d in idx:
-        lib.LoadPlaintextDiagonal(blobs[d], lt, d)
-        assert np.array_equal(lib.export_lt_diagonal(lt, d, level), pts[d])
-    assert np.array_equal(lib.export_ciphertext(lib.EvaluateLinearTransform(lt, ct)), ref)
-
-
 def test_lola_n13_end_to_end(torch_cuda):
     """The reference frontend's LoLA op stream (tests/golden/lola_n13_*) replayed
     through the C-ABI: decrypted output vs the cleartext PyTorch model, the
@@ -486,4 +454,93 @@ def test_error_contract(torch_cuda):
     # still usable: the error paths left no device state behind
     out = np.array(lib.Decode(lib.Decrypt(lib.RotateNew(ct, 1))))
     assert np.abs(out[:4096] - np.roll(vals, -1)).max() < 1e-4
+    lib.DeleteScheme()
+
+
+@pytest.mark.parametrize("logn", [13, 15])
+def test_prime_sizes_across_f64_boundaries(torch_cuda, oracle_mod, logn):
+    """Q primes of 41, 42, 45, 46 and 47 bits: the float64 NTT is
+    lazy up to 41-bit moduli and reduces every round above (ntt.hip), and the
+    float64 path ends at 46-bit moduli (ORION_F64_BITS, common.h).  NTT/INTT,
+    mul_relin, rotate and rescale bit-exact vs the oracle on both sides of
+    each boundary."""
+    torch = torch_cuda
+    from orion_amd.backend import HipLibrary
+    logq, logp = [60, 40, 41, 42, 45, 46, 47], [60, 60]
+    lib = HipLibrary().new_scheme(logn, logq, logp, 40, h=192, seed=41)
+    mods = lib.moduli()
+    bits = [q.bit_length() for q in mods]
+    # lazy float64 (<= 41 bits), reduced float64 (42..46), the 46-bit edge, integer (>= 47)
+    assert min(bits) <= 41 and any(42 <= b <= 46 for b in bits) and 46 in bits and 47 in bits, bits
+    orc = oracle_mod.Oracle(logn, mods, len(logq), len(logp))
+    N, nl, B = 1 << logn, len(mods), 2
+    rng = np.random.default_rng(logn + 100)
+    import ctypes
+    host = np.stack([rng.integers(0, mods[m], (B, N), dtype=np.uint64) for m in range(nl)])
+    host[:, 1, :8] = np.array([mods[m] - 1 for m in range(nl)], dtype=np.uint64)[:, None]  # top residues
+    dev = torch.from_numpy(host.view(np.int64).copy()).cuda()
+    mods_c = (ctypes.c_int * nl)(*range(nl))
+    ptr = ctypes.cast(dev.data_ptr(), ctypes.POINTER(ctypes.c_ulong))
+    assert lib.lib.OrionHipNTT(ptr, nl, B, mods_c, 0) == 0
+    lib.OrionHipSynchronize()
+    fwd = dev.cpu().numpy().view(np.uint64)
+    for m in range(nl):
+        for b in range(B):
+            assert np.array_equal(fwd[m, b], orc.ntt(m, host[m, b])), (bits[m], b)
+    assert lib.lib.OrionHipNTT(ptr, nl, B, mods_c, 1) == 0
+    lib.OrionHipSynchronize()
+    assert np.array_equal(dev.cpu().numpy().view(np.uint64), host)
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    level = len(logq) - 1
+    a = rand_ct(rng, mods, level, N, B=1)
+    b = rand_ct(rng, mods, level, N, B=1)
+    cc = lib.MulRelinCiphertextNew(lib.import_ciphertext(a, 2.0 ** 40), lib.import_ciphertext(b, 2.0 ** 40))
+    ref = orc.mul_relin(a[0], b[0], lib.export_relin_key(), level)
+    assert np.array_equal(lib.export_ciphertext(cc)[0], ref)
+    g = int(lib.GaloisElement(7))
+    cr = lib.RotateNew(cc, 7)
+    ref = orc.rotate(ref, g, lib.export_galois_key(g), level)
+    assert np.array_equal(lib.export_ciphertext(cr)[0], ref)
+    for lv in range(level, 0, -1):  # every prime is the rescale divisor once
+        lib.Rescale(cr)
+        ref = orc.rescale(ref, lv)
+        assert np.array_equal(lib.export_ciphertext(cr)[0], ref), bits[lv]
+    lib.DeleteScheme()
+
+
+@pytest.mark.parametrize("logn", [15, 16])
+def test_ntt_edge_residues(torch_cuda, oracle_mod, logn):
+    """Constant limbs 0, 1 and q-1 (and alternating 0 / q-1) through the
+    forward and inverse NTT at the bench and ResNet ring degrees, every limb
+    of a 60/40-bit chain, vs the oracle."""
+    torch = torch_cuda
+    from orion_amd.backend import HipLibrary
+    import ctypes
+    logq = [60, 40, 40]
+    lib = HipLibrary().new_scheme(logn, logq, [60, 60], 40)
+    mods = lib.moduli()
+    orc = oracle_mod.Oracle(logn, mods, len(logq), 2)
+    N, nl = 1 << logn, len(mods)
+    pats = []
+    for m in range(nl):
+        q = mods[m]
+        alt = np.zeros(N, np.uint64)
+        alt[1::2] = q - 1
+        pats.append(np.stack([np.zeros(N, np.uint64), np.ones(N, np.uint64), np.full(N, q - 1, np.uint64), alt]))
+    host = np.stack(pats)  # [limb][4][N]
+    dev = torch.from_numpy(host.view(np.int64).copy()).cuda()
+    mods_c = (ctypes.c_int * nl)(*range(nl))
+    ptr = ctypes.cast(dev.data_ptr(), ctypes.POINTER(ctypes.c_ulong))
+    assert lib.lib.OrionHipNTT(ptr, nl, 4, mods_c, 0) == 0
+    lib.OrionHipSynchronize()
+    fwd = dev.cpu().numpy().view(np.uint64)
+    for m in range(nl):
+        for k in range(4):
+            assert np.array_equal(fwd[m, k], orc.ntt(m, host[m, k])), (m, k)
+    assert not fwd[:, 0].any()  # NTT(0) = 0
+    assert lib.lib.OrionHipNTT(ptr, nl, 4, mods_c, 1) == 0
+    lib.OrionHipSynchronize()
+    assert np.array_equal(dev.cpu().numpy().view(np.uint64), host)
     lib.DeleteScheme()
