@@ -403,6 +403,17 @@ def main():
         if tj.get("workload") == args.workload and tj.get("batch") == args.batch and n_launch:
             traffic = round(tj["hbm_bytes_per_algorithmic_byte"] * n_bytes / n_launch)
 
+    valu = None
+    vfile = os.path.join(ROOT, "profiles", "valu_roofline.json")
+    if os.path.exists(vfile):
+        with open(vfile) as f:
+            vj = json.load(f)
+        # VALU roofline of the VALU-bound kernels, from the committed rocprofv3
+        # SQ/GRBM pass over this same workload (tools/pmc_summary.py)
+        if vj.get("workload") == args.workload and vj.get("batch") == args.batch:
+            valu = {"profile": vj["tag"], "definition": vj["definition"],
+                    "valu_busy": {k: round(v["valu_busy"], 3) for k, v in vj["kernels"].items()}}
+
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -435,6 +446,7 @@ def main():
                          "launches": n_launch, "avg_launch_us": round(n_ms / max(n_launch, 1) * 1e3, 2),
                          "algorithmic_bytes_per_launch": round(n_bytes / max(n_launch, 1)),
                          "ntt_share_of_kernel_time": round(bd_ntt_ms / total_prof_ms, 3) if total_prof_ms else None},
+            "valu_roofline": valu,
             "cpu_baseline": cpu,
             "check": {"mae_image0_vs_cleartext": mae, "mae_over_ranks": "max (outputs gathered to rank 0)",
                       "setup_s": round(t_setup, 1), "key_bundle_bytes": bundle_bytes},

@@ -189,7 +189,11 @@ int ExportCiphertextDevice(int ct, unsigned long *dptr, unsigned long n);
 int ExportSecretKey(unsigned long *out, unsigned long n);                  /* [L+K][N]           */
 int ExportPublicKey(unsigned long *out, unsigned long n);                  /* [2][L+K][N]        */
 int ExportRelinKey(unsigned long *out, unsigned long n);                   /* [dnum][2][L+K][N]  */
-int ExportGaloisKey(unsigned long galEl, unsigned long *out, unsigned long n);
+int ExportGaloisKey(unsigned long galEl, unsigned long *out, unsigned long n);  /* full layout, zero past its level */
+/* Galois keys are made for the highest level they are needed at (a linear
+ * transform's level for its rotations, L-1 otherwise); a key made for level l
+ * holds ceil((l+1)/K) digits over l+1+K limbs */
+int GetGaloisKeyLevel(unsigned long galEl);
 int ExportLinearTransformDiagonal(int lt, int diagIdx, unsigned long *out, unsigned long n); /* [lvl+1+K][N] */
 int GetLinearTransformN1(int lt);
 unsigned long GaloisElement(int rotation);
@@ -203,7 +207,7 @@ int ImportKeyBundle(const void *dptr, unsigned long bytes);
 /* kernel timing with HIP events on the library stream; enable: 0 = off,
  * 1 = every category, otherwise a bit mask of categories (bit 0 ntt_fwd,
  * 1 ntt_inv, 2 elementwise, 3 basis_ext, 4 ks_mac, 5 automorph, 6 tensor,
- * 7 rescale_prep, 8 lt_bsgs) */
+ * 7 rescale_prep, 8 lt_bsgs, 9 lt_giant) */
 void OrionHipProfile(int enable);
 /* fills up to max entries: name (32 chars each), launches, total ms, algorithmic bytes */
 int OrionHipProfileRead(char *names, long *launches, double *ms, double *bytes, int max);

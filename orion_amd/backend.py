@@ -161,6 +161,7 @@ SIGNATURES = {
     "ExportPublicKey": ([P(c_ulong), c_ulong], c_int),
     "ExportRelinKey": ([P(c_ulong), c_ulong], c_int),
     "ExportGaloisKey": ([c_ulong, P(c_ulong), c_ulong], c_int),
+    "GetGaloisKeyLevel": ([c_ulong], c_int),
     "ExportLinearTransformDiagonal": ([c_int, c_int, P(c_ulong), c_ulong], c_int),
     "GetLinearTransformN1": ([c_int], c_int),
     "GaloisElement": ([c_int], c_ulong),
@@ -179,7 +180,7 @@ LATTIGO_SYMBOLS = [n for n in SIGNATURES if not n.startswith("OrionHip") and n n
     "GetCiphertextScaleF", "ImportCiphertext", "ExportCiphertext", "ImportPlaintext", "ExportPlaintext",
     "ImportCiphertextDevice", "ExportCiphertextDevice",
     "ExportSecretKey", "ExportPublicKey", "ExportRelinKey",
-    "ExportGaloisKey", "ExportLinearTransformDiagonal", "GetLinearTransformN1", "GaloisElement",
+    "ExportGaloisKey", "GetGaloisKeyLevel", "ExportLinearTransformDiagonal", "GetLinearTransformN1", "GaloisElement",
     "KeyBundleBytes", "ExportKeyBundle", "ImportKeyBundle", "ModDropCiphertext", "GetPolyDepth")]
 
 

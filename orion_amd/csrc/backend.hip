@@ -37,7 +37,7 @@ int orion_launch_basis_ext(const LimbSet& out, const LimbSet& in, const BasisExt
 int orion_launch_modup_all(const LimbSet& D, const LimbSet& in, const BasisExtTable* const* Ts, int beta, int K,
                            int nqp, const DeviceTables* tb, int N, hipStream_t st);
 int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const LimbSet& own, const MacGroups& G, int ngroup,
-                        int beta, int nmod_key, const DeviceTables* tb, int N, hipStream_t st);
+                        int beta, const DeviceTables* tb, int N, hipStream_t st);
 int orion_launch_automorph(const LimbSet& o, const LimbSet& a, const u32* idx, const DeviceTables* tb, int N,
                            int accumulate, hipStream_t st);
 int orion_launch_lt_bsgs(const LimbSet& t0, const LimbSet& t1, const LimbSet& D, const LimbSet& ct,
@@ -120,6 +120,12 @@ struct Poly {
   long long batch_stride() const { return N; }
   long long limb_stride() const { return (long long)B * N; }
   long long comp_stride() const { return (long long)nlimb * B * N; }
+};
+
+// an evaluation key made for `level` (common.h key_pos): [digit][2][level+1+K][N]
+struct EvKey {
+  Poly k;
+  int level = 0;
 };
 
 struct Ciphertext {
@@ -213,8 +219,8 @@ struct ProfRec {
   double bytes;
 };
 static const char* kProfNames[] = {"ntt_fwd", "ntt_inv", "elementwise", "basis_ext", "ks_mac", "automorph",
-                                   "tensor", "rescale_prep", "lt_bsgs"};
-enum { P_NTT_FWD = 0, P_NTT_INV, P_EW, P_BEXT, P_MAC, P_AUT, P_TENSOR, P_RSPREP, P_LTMAC, P_NCAT };
+                                   "tensor", "rescale_prep", "lt_bsgs", "lt_giant"};
+enum { P_NTT_FWD = 0, P_NTT_INV, P_EW, P_BEXT, P_MAC, P_AUT, P_TENSOR, P_RSPREP, P_LTMAC, P_LTGIANT, P_NCAT };
 
 // ---------------------------------------------------------------------------
 // context
@@ -233,9 +239,15 @@ struct Context {
   Prng prng{0x0123456789abcdefull};               // key generation
   EncSampler enc_sampler;                         // encryption: ChaCha20 key, index, Gaussian table
 
-  Poly sk, pk, rlk;
+  Poly sk, pk, rlk;  // rlk: full chain (level L - 1)
   bool have_sk = false, have_pk = false, have_rlk = false;
-  std::map<u64, Poly> gks;
+  // Galois keys, each made for the highest level it has been asked for.  A
+  // key covers only the limbs and digits of its level, so a model whose
+  // linear transforms run low in the chain (ResNet-20 at N = 2^16: LTs at
+  // levels 1-4 under a 48-prime bootstrapping chain) keeps its ~120 keys in
+  // a few GB instead of ~150 GB of full-chain keys.
+  std::map<u64, EvKey> gks;
+  std::map<u64, int> key_hint;  // galEl -> highest level of a linear transform that uses it
   std::map<u64, u32*> autidx;
   std::map<std::pair<int, int>, BasisExtTable*> betab;
   std::map<std::pair<int, int>, std::vector<int>> betab_pos;  // target positions (QP order)
@@ -835,25 +847,36 @@ struct Context {
     have_pk = true;
   }
 
-  // evaluation key switching s_in -> s_out, layout [dnum][2][L+K][N]
-  Poly gen_evk(const Poly& s_in, const Poly& s_out) {
-    Poly k = alloc(2 * dnum, L + K, 1);
-    Poly tmp = alloc(1, L + K, 1);
-    std::vector<u64> a((size_t)(L + K) * N), e((size_t)(L + K) * N);
-    for (int i = 0; i < dnum; ++i) {
-      for (int m = 0; m < L + K; ++m)
-        for (int n = 0; n < N; ++n) a[(size_t)m * N + n] = prng.uniform(mods[m]);
-      small_residues(sample_gauss(), iota(0, L + K), e.data());
+  // QP moduli of a key made for `level`: q_0..q_level, then p_0..p_{K-1}
+  std::vector<int> key_mods(int level) const {
+    std::vector<int> v = iota(0, level + 1);
+    for (int k = 0; k < K; ++k) v.push_back(L + k);
+    return v;
+  }
+  // evaluation key switching s_in -> s_out for ciphertexts up to `level`,
+  // layout [beta][2][level+1+K][N] (beta = ceil((level+1)/K) digits); a
+  // full-chain key (level L - 1) is [dnum][2][L+K][N]
+  Poly gen_evk(const Poly& s_in, const Poly& s_out, int level) {
+    const int beta = (level + 1 + K - 1) / K, nl = level + 1 + K;
+    const std::vector<int> md = key_mods(level), kp = iota(0, nl);
+    Poly k = alloc(2 * beta, nl, 1);
+    Poly tmp = alloc(1, nl, 1);
+    std::vector<u64> a((size_t)nl * N), e((size_t)nl * N);
+    for (int i = 0; i < beta; ++i) {
+      for (int x = 0; x < nl; ++x)
+        for (int n = 0; n < N; ++n) a[(size_t)x * N + n] = prng.uniform(mods[md[x]]);
+      small_residues(sample_gauss(), md, e.data());
       HIPCHK(hipMemcpyAsync(k.ptr() + (2 * i + 1) * k.comp_stride(), a.data(), a.size() * 8,
                             hipMemcpyHostToDevice, stream));
       HIPCHK(hipMemcpyAsync(k.ptr() + (2 * i) * k.comp_stride(), e.data(), e.size() * 8, hipMemcpyHostToDevice,
                             stream));
       HIPCHK(hipStreamSynchronize(stream));
-      ntt(full(k, 2 * i, 1), false);
-      ew(EW_MUL, full(tmp, 0, 1), full(k, 2 * i + 1, 1), full(s_out, 0, 1));
-      ew(EW_SUB, full(k, 2 * i, 1), full(k, 2 * i, 1), full(tmp, 0, 1));
+      const LimbSet kb = ls(k, 2 * i, 1, kp, md), ka = ls(k, 2 * i + 1, 1, kp, md), lt = ls(tmp, 0, 1, kp, md);
+      ntt(kb, false);
+      ew(EW_MUL, lt, ka, ls(s_out, 0, 1, md, md));
+      ew(EW_SUB, kb, kb, lt);
       // + P * s_in on the Q limbs of digit i
-      const int lo = i * K, hi = std::min((i + 1) * K, L);
+      const int lo = i * K, hi = std::min((i + 1) * K, level + 1);
       std::vector<int> dl = iota(lo, hi);
       std::vector<u64> pm;
       for (int j : dl) {
@@ -869,12 +892,23 @@ struct Context {
     if (!have_sk) throw std::runtime_error("secret key not generated");
     Poly s2 = alloc(1, L + K, 1);
     ew(EW_MUL, full(s2, 0, 1), full(sk, 0, 1), full(sk, 0, 1));
-    rlk = gen_evk(s2, sk);
+    rlk = gen_evk(s2, sk, L - 1);
     have_rlk = true;
   }
-  void gen_galois(u64 g) {
-    if (gks.count(g)) return;
-    if (!have_sk) throw std::runtime_error("secret key not generated");
+  int hinted_level(u64 g) const {
+    auto it = key_hint.find(g);
+    return it == key_hint.end() ? L - 1 : it->second;
+  }
+  // the Galois key of g, made for at least `level` (a key made for a lower
+  // level is replaced by one for this level)
+  void gen_galois(u64 g, int level) {
+    auto have = gks.find(g);
+    if (have != gks.end() && have->second.level >= level) return;
+    if (!have_sk)
+      throw std::runtime_error(have == gks.end() ? "secret key not generated"
+                                                 : "galois key " + std::to_string(g) + " covers level " +
+                                                       std::to_string(have->second.level) + " < " +
+                                                       std::to_string(level) + " and there is no secret key");
     const u64 M = 2 * (u64)N;
     u64 ginv = hm_powmod(g, M / 2 - 1, M);  // g^-1 mod 2N (group order N/2 divides M/2)
     if ((g * ginv) % M != 1) {
@@ -883,15 +917,11 @@ struct Context {
     }
     Poly s_out = alloc(1, L + K, 1);
     automorph(full(s_out, 0, 1), full(sk, 0, 1), ginv, false);
-    gks[g] = gen_evk(sk, s_out);
+    gks[g] = EvKey{gen_evk(sk, s_out, level), level};
   }
-  const Poly& galois_key(u64 g) {
-    auto it = gks.find(g);
-    if (it == gks.end()) {
-      gen_galois(g);  // Lattigo AddRotationKey semantics: generate on first use
-      it = gks.find(g);
-    }
-    return it->second;
+  const EvKey& galois_key(u64 g, int level) {
+    gen_galois(g, level);  // Lattigo AddRotationKey semantics: generate on first use
+    return gks.at(g);
   }
 
   // ---------------------------------------------------------------------------
@@ -972,15 +1002,16 @@ struct Context {
   //   [add0_g on comp 0] + sum_i D_g,i * keys[g]_i,   D_g at d.p + g*d_gstride,
   // own Q limbs of each digit read from own (group stride own_gstride)
   void mac_groups(const LimbSet& o, long long out_gstride, const LimbSet& d, long long d_gstride,
-                  const LimbSet& own, long long own_gstride, const std::vector<const u64*>& keys, int beta,
-                  const u64* add0 = nullptr, long long add_gstride = 0, int add_nq = 0,
-                  const u64* add1 = nullptr) {
+                  const LimbSet& own, long long own_gstride, const std::vector<const u64*>& keys,
+                  const std::vector<int>& klvl, int beta, const u64* add0 = nullptr, long long add_gstride = 0,
+                  int add_nq = 0, const u64* add1 = nullptr) {
     const int G = (int)keys.size();
     for (int g0 = 0; g0 < G; g0 += ORION_MAXGROUP) {
       const int ng = std::min(ORION_MAXGROUP, G - g0);
       MacGroups mg;
       memset(&mg, 0, sizeof(mg));
-      for (int g = 0; g < ng; ++g) mg.key[g] = keys[g0 + g];
+      for (int g = 0; g < ng; ++g) mg.key[g] = keys[g0 + g], mg.klvl[g] = klvl[g0 + g];
+      mg.L = L;
       mg.out_gstride = out_gstride;
       mg.d_gstride = d_gstride;
       mg.add_gstride = add_gstride;
@@ -1003,7 +1034,7 @@ struct Context {
       const double dreads = d_gstride ? rows * ng * beta : rows * beta;
       const double adds = add0 ? (add_nq ? (add1 ? 2.0 : 1.0) * add_nq / o.nlimb : 1.0) : 0.0;
       Scope sc(this, P_MAC, 8.0 * N * (dreads + rows * ng * (2 + adds) + 2.0 * beta * ng * o.nlimb));
-      if (orion_launch_ks_mac(oo, dd, ow, mg, ng, beta, L + K, d_tb, N, stream))
+      if (orion_launch_ks_mac(oo, dd, ow, mg, ng, beta, d_tb, N, stream))
         throw std::runtime_error("ks_mac launch failed");
     }
   }
@@ -1033,13 +1064,14 @@ struct Context {
   // full key switch of c (Q, level) -> (k0, k1) written to out comps 0/1 (Q, level);
   // add0/add1 (optional, Q limbs 0..level with out's batch geometry): added to
   // comps 0/1 of the result, folded into the gadget product as P * add
-  void keyswitch(const LimbSet& c, int level, int B, const Poly& key, const Poly& out,
+  void keyswitch(const LimbSet& c, int level, int B, const Poly& key, int klvl, const Poly& out,
                  const u64* add0 = nullptr, const u64* add1 = nullptr) {
+    if (klvl < level) throw std::runtime_error("evaluation key made for a lower level");
     Poly D = decompose(c, level, B);
     Poly u = alloc(2, level + 1 + K, B);
     const int beta = (level + 1 + K - 1) / K;
-    mac_groups(lsqp(u, 0, 2, level, level), 0, lsqp(D, 0, beta, level, level), 0, c, 0, {key.ptr()}, beta, add0, 0,
-               add0 ? level + 1 : 0, add1);
+    mac_groups(lsqp(u, 0, 2, level, level), 0, lsqp(D, 0, beta, level, level), 0, c, 0, {key.ptr()}, {klvl}, beta,
+               add0, 0, add0 ? level + 1 : 0, add1);
     moddown(lsqp(u, 0, 2, level, level), level, lsq(out, 0, 2, level));
   }
   std::vector<u64> p_mod_q(int level) const {
@@ -1109,7 +1141,7 @@ struct Context {
     }
     Ciphertext out = new_ct(level, B, a.scale * b.scale);
     // (d0, d1) + keyswitch(d2): the addition is folded into the gadget product
-    keyswitch(lsq(d, 2, 1, level), level, B, rlk, out.poly, d.ptr(), d.ptr() + d.comp_stride());
+    keyswitch(lsq(d, 2, 1, level), level, B, rlk, L - 1, out.poly, d.ptr(), d.ptr() + d.comp_stride());
     return out;
   }
 
@@ -1118,10 +1150,10 @@ struct Context {
   // (g = 2N - 1 is the complex conjugation of the slots)
   Ciphertext apply_galois(const Ciphertext& a, u64 g) {
     const int level = a.level, B = a.poly.B;
-    const Poly& key = galois_key(g);
+    const EvKey& key = galois_key(g, level);
     Poly t = alloc(2, level + 1, B);
     // (c0, 0) + keyswitch(c1), the c0 addition folded into the gadget product
-    keyswitch(lsq(a.poly, 1, 1, level), level, B, key, t, a.poly.ptr());
+    keyswitch(lsq(a.poly, 1, 1, level), level, B, key.k, key.level, t, a.poly.ptr());
     Ciphertext out = new_ct(level, B, a.scale);
     automorph(lsq(out.poly, 0, 2, level), lsq(t, 0, 2, level), g, false);
     return out;
@@ -1252,22 +1284,35 @@ struct Context {
         Bb.beta = beta;
         Bb.K = K;
         Bb.level = level;
-        Bb.nmod_key = L + K;
+        Bb.L = L;
         for (int j = 0; j <= level; ++j) Bb.pq[j] = pq[j], Bb.pqs[j] = hm_shoup(pq[j], mods[j]);
         int nrot = 0;
         for (int s = 0; s < Bb.nb; ++s) {
           const int b = T.slots[s0 + s];
           if (b == 0) continue;
           const u64 g = galois_element(b);
-          Bb.key[s] = galois_key(g).ptr();
+          const EvKey& kk = galois_key(g, level);
+          Bb.key[s] = kk.k.ptr();
+          Bb.klvl[s] = kk.level;
           Bb.idx[s] = aut_index(g);
           ++nrot;
         }
         for (int p = 0; p < T.n_plan; ++p) {
           const int gcount = std::min(LT_MAXG, ng - p * LT_MAXG);
           LimbSet t0 = lsqp(Tt, p * LT_MAXG, 1, level, level), t1 = lsqp(Tt, ng + p * LT_MAXG, 1, level, level);
+          // distinct bytes: the shared decomposition (beta digits) and ct0/ct1
+          // once per row, the giant outputs (read back when accumulating), and
+          // per QP limb the baby keys (2 beta each) and the diagonals of the
+          // plan's (giant, baby) terms, both shared by the batch
           const double rows = (double)nqp * B;
-          Scope sc(this, P_LTMAC, 8.0 * N * rows * (nrot * beta + 2.0 + 2.0 * gcount * (s0 ? 2 : 1)));
+          int npair = 0;
+          for (int gi = p * LT_MAXG; gi < p * LT_MAXG + gcount; ++gi)
+            for (int b : T.index.at(T.gorder[gi]))
+              for (int s = 0; s < Bb.nb; ++s)
+                if (T.slots[s0 + s] == b) ++npair;
+          Scope sc(this, P_LTMAC,
+                   8.0 * N * (rows * ((nzb ? beta : 0) + 2.0 + 2.0 * gcount * (s0 ? 2 : 1)) +
+                              (double)nqp * (2.0 * beta * nrot + npair)));
           if (orion_launch_lt_bsgs(t0, t1, dl, ctl, Bb, T.d_plan + p, 0, gcount, s0 > 0, ptl, d_tb, N, stream))
             throw std::runtime_error("lt_bsgs launch failed");
         }
@@ -1290,14 +1335,16 @@ struct Context {
         G.beta = beta;
         G.K = K;
         G.level = level;
-        G.nmod_key = L + K;
+        G.L = L;
         G.has_zero = (has_g0 && g0 == 0) ? 1 : 0;
         G.d_gstride = (long long)beta * Dg.comp_stride();
         G.own_gstride = T1q.comp_stride();
         G.t0_gstride = Tt.comp_stride();
         for (int k = 0; k < G.ng; ++k) {
           const u64 g = galois_element(T.gorder[g0 + k]);
-          G.key[k] = galois_key(g).ptr();
+          const EvKey& kk = galois_key(g, level);
+          G.key[k] = kk.k.ptr();
+          G.klvl[k] = kk.level;
           G.idx[k] = aut_index(g);
         }
         LimbSet dg = lsqp(Dg, g0 * beta, 1, level, level);
@@ -1309,8 +1356,11 @@ struct Context {
           part = alloc(2, nqp, B);
           a = lsqp(part, 0, 2, level, level);
         }
+        // per row: each giant's decomposition (beta) and t0 term, the output
+        // pair and the zero giant; per QP limb: each giant's key (2 beta)
         const double rows = (double)nqp * B;
-        Scope sc(this, P_MAC, 8.0 * N * rows * (G.ng * (beta + 1.0) + 2.0 + 2.0 * G.has_zero));
+        Scope sc(this, P_LTGIANT, 8.0 * N * (rows * (G.ng * (beta + 1.0) + 2.0 + 2.0 * G.has_zero) +
+                                          (double)nqp * 2.0 * beta * G.ng));
         if (orion_launch_lt_giant(a, dg, own, t0, z, G, d_tb, N, stream))
           throw std::runtime_error("lt_giant launch failed");
         if (g0 > 0) ew(EW_ADD, la, la, a);
@@ -2194,19 +2244,21 @@ static ArrayResultByte to_bytes(const std::vector<char>& v) {
   return r;
 }
 // rlwe.GaloisKey: GaloisElement, NthRoot, GadgetCiphertext{BaseTwoDecomposition 0,
-// Value: dnum x 1 VectorQP (k0, k1)} of a [dnum][2][L+K][N] host key
-static std::vector<char> galois_key_bytes(const Context& c, u64 galEl, const std::vector<u64>& key) {
+// Value: beta x 1 VectorQP (k0, k1)} of a [beta][2][level+1+K][N] host key made
+// for `level` (Lattigo's key at LevelQ = level: beta rows, level+1 Q limbs)
+static std::vector<char> galois_key_bytes(const Context& c, u64 galEl, const std::vector<u64>& key, int level) {
   std::vector<char> b;
-  const size_t qp = (size_t)(c.L + c.K) * c.N;
-  b.reserve(40 + (size_t)c.dnum * (16 + 2 * (wire::poly_bytes(c.L, c.N) + wire::poly_bytes(c.K, c.N))));
+  const int beta = (level + 1 + c.K - 1) / c.K;
+  const size_t qp = (size_t)(level + 1 + c.K) * c.N;
+  b.reserve(40 + (size_t)beta * (16 + 2 * (wire::poly_bytes(level + 1, c.N) + wire::poly_bytes(c.K, c.N))));
   wire::put_u64(b, galEl);
   wire::put_u64(b, 2 * (u64)c.N);  // NthRoot
   wire::put_u64(b, 0);             // BaseTwoDecomposition
-  wire::put_u64(b, (u64)c.dnum);   // Matrix rows
-  for (int i = 0; i < c.dnum; ++i) {
+  wire::put_u64(b, (u64)beta);     // Matrix rows
+  for (int i = 0; i < beta; ++i) {
     wire::put_u64(b, 1);  // one column (no power-of-two decomposition)
     wire::put_u64(b, 2);  // VectorQP length
-    for (int k = 0; k < 2; ++k) put_qp(b, c, key.data() + (2 * (size_t)i + k) * qp, c.L);
+    for (int k = 0; k < 2; ++k) put_qp(b, c, key.data() + (2 * (size_t)i + k) * qp, level + 1);
   }
   return b;
 }
@@ -2306,13 +2358,13 @@ int Decrypt(int ct) {
 void NewEvaluator(void) {
   API_BEGIN
   Context& c = ctx();
-  for (int i = 1; i < c.N / 2; i *= 2) c.gen_galois(c.galois_element(i));  // evaluator.go:25-31
+  for (int i = 1; i < c.N / 2; i *= 2) c.gen_galois(c.galois_element(i), c.L - 1);  // evaluator.go:25-31
   API_END_VOID
 }
 void AddRotationKey(int k) {
   API_BEGIN
   Context& c = ctx();
-  c.gen_galois(c.galois_element(k));
+  c.gen_galois(c.galois_element(k), c.L - 1);
   API_END_VOID
 }
 unsigned long GaloisElement(int k) {
@@ -2630,6 +2682,10 @@ int GenerateLinearTransform(int* diagIdx, int nIdx, float* data, int nData, int 
     std::sort(kv.second.begin(), kv.second.end());
     T.giants.push_back(kv.first);
   }
+  for (int r : T.giants)
+    if (r) c.key_hint[c.galois_element(r)] = std::max(c.key_hint[c.galois_element(r)], level);
+  for (int r : T.babies)
+    if (r) c.key_hint[c.galois_element(r)] = std::max(c.key_hint[c.galois_element(r)], level);
   std::vector<float> vec(slots);
   for (int i = 0; i < nIdx && !load; ++i) {
     int gi, bi;
@@ -2673,14 +2729,22 @@ ArrayResultInt GetLinearTransformRotationKeys(int id) {
   return r;
   API_END(r)
 }
+// keys asked for by a linear transform are made for the highest level of the
+// transforms that use them (key_hint); any other element gets a full-chain key
 void GenerateLinearTransformRotationKey(int galEl) {
   API_BEGIN
-  ctx().gen_galois((u64)(unsigned)galEl);
+  Context& c = ctx();
+  const u64 g = (u64)(unsigned)galEl;
+  if (g != 1) c.gen_galois(g, c.hinted_level(g));  // 1 = the identity (zero rotation): no key needed
   API_END_VOID
 }
 void GenerateConsolidatedRotationKeys(int* galEls, int n) {
   API_BEGIN
-  for (int i = 0; i < n; ++i) ctx().gen_galois((u64)(unsigned)galEls[i]);
+  Context& c = ctx();
+  for (int i = 0; i < n; ++i) {
+    const u64 g = (u64)(unsigned)galEls[i];
+    if (g != 1) c.gen_galois(g, c.hinted_level(g));
+  }
   API_END_VOID
 }
 // lineartransform.go:131-142: a fresh key, serialised and NOT kept (the
@@ -2691,17 +2755,18 @@ ArrayResultByte GenerateAndSerializeRotationKey(int galEl) {
   Context& c = ctx();
   const u64 g = (u64)(unsigned)galEl;
   auto kept = c.gks.find(g);
-  Poly saved;
+  EvKey saved;
   if (kept != c.gks.end()) {
     saved = kept->second;
     c.gks.erase(kept);
   }
-  c.gen_galois(g);
+  const int level = c.hinted_level(g);
+  c.gen_galois(g, level);
   std::vector<u64> host;
-  c.download(c.gks.at(g), host);
+  c.download(c.gks.at(g).k, host);
   c.gks.erase(g);
-  if (saved.buf) c.gks[g] = saved;
-  return to_bytes(galois_key_bytes(c, g, host));
+  if (saved.k.buf) c.gks[g] = saved;
+  return to_bytes(galois_key_bytes(c, g, host, level));
   API_END(r)
 }
 // lineartransform.go:145-164: unmarshal an rlwe.GaloisKey into the key set under galEl
@@ -2713,18 +2778,26 @@ void LoadRotationKey(char* data, unsigned long len, unsigned long galEl) {
   const u64 ge = rd.get_u64(), nth = rd.get_u64(), b2 = rd.get_u64(), rows = rd.get_u64();
   if (nth != 2 * (u64)c.N) throw std::runtime_error("rotation key: NthRoot does not match the ring");
   if (b2 != 0) throw std::runtime_error("rotation key: power-of-two decomposition is not supported");
-  if (rows != (u64)c.dnum) throw std::runtime_error("rotation key: gadget rows != dnum of this chain");
   if (ge != galEl) throw std::runtime_error("rotation key: blob is for Galois element " + std::to_string(ge));
-  const size_t qp = (size_t)(c.L + c.K) * c.N;
-  std::vector<u64> host(2 * (size_t)c.dnum * qp);
-  for (int i = 0; i < c.dnum; ++i) {
-    if (rd.get_u64() != 1 || rd.get_u64() != 2) throw std::runtime_error("rotation key: unexpected gadget shape");
-    for (int k = 0; k < 2; ++k) get_qp(rd, c, host.data() + (2 * (size_t)i + k) * qp, c.L, "rotation key");
+  if (rows < 1 || rows > (u64)c.dnum) throw std::runtime_error("rotation key: gadget rows outside 1..dnum");
+  if (rd.get_u64() != 1 || rd.get_u64() != 2) throw std::runtime_error("rotation key: unexpected gadget shape");
+  // the level the key was made for: its Q limb count (peeked from the first ring.Poly)
+  const u64 nq = rd.get_u64();
+  if (nq < 1 || nq > (u64)c.L) throw std::runtime_error("rotation key: Q limb count outside the chain");
+  const int level = (int)nq - 1, beta = (level + 1 + c.K - 1) / c.K;
+  if (rows != (u64)beta) throw std::runtime_error("rotation key: gadget rows do not match its level");
+  wire::Reader body(data + 48, len - 48);  // past the 4-word header and row 0's column/vector lengths
+  const size_t qp = (size_t)(level + 1 + c.K) * c.N;
+  std::vector<u64> host(2 * (size_t)beta * qp);
+  for (int i = 0; i < beta; ++i) {
+    if (i && (body.get_u64() != 1 || body.get_u64() != 2))
+      throw std::runtime_error("rotation key: unexpected gadget shape");
+    for (int k = 0; k < 2; ++k) get_qp(body, c, host.data() + (2 * (size_t)i + k) * qp, level + 1, "rotation key");
   }
-  if (rd.left()) throw std::runtime_error("rotation key blob has trailing bytes");
-  Poly k = c.alloc(2 * c.dnum, c.L + c.K, 1);
+  if (body.left()) throw std::runtime_error("rotation key blob has trailing bytes");
+  Poly k = c.alloc(2 * beta, level + 1 + c.K, 1);
   c.upload(k, host);
-  c.gks[galEl] = k;
+  c.gks[galEl] = EvKey{k, level};
   API_END_VOID
 }
 // lineartransform.go:167-183: the diagonal's ringqp.Poly (Q at the transform's
@@ -3019,7 +3092,28 @@ int ExportGaloisKey(unsigned long galEl, unsigned long* out, unsigned long n) {
   Context& c = ctx();
   auto it = c.gks.find(galEl);
   if (it == c.gks.end()) throw std::runtime_error("no galois key for element " + std::to_string(galEl));
-  return export_poly(it->second, out, n);
+  // always the full-chain layout [dnum][2][L+K][N]: a key made for a lower
+  // level fills its digits and limbs, the rest is zero
+  if (n != (unsigned long)2 * c.dnum * (c.L + c.K) * c.N) throw std::runtime_error("export buffer size mismatch");
+  const EvKey& k = it->second;
+  std::vector<u64> host;
+  c.download(k.k, host);
+  memset(out, 0, n * 8);
+  const int beta = k.k.ncomp / 2, nl = k.k.nlimb;
+  for (int i = 0; i < 2 * beta; ++i)
+    for (int x = 0; x < nl; ++x) {
+      const int m = x <= k.level ? x : c.L + (x - k.level - 1);
+      memcpy(out + ((size_t)i * (c.L + c.K) + m) * c.N, host.data() + ((size_t)i * nl + x) * c.N, (size_t)c.N * 8);
+    }
+  return 0;
+  API_END(-1)
+}
+int GetGaloisKeyLevel(unsigned long galEl) {
+  API_BEGIN
+  Context& c = ctx();
+  auto it = c.gks.find(galEl);
+  if (it == c.gks.end()) throw std::runtime_error("no galois key for element " + std::to_string(galEl));
+  return it->second.level;
   API_END(-1)
 }
 int ExportLinearTransformDiagonal(int tid, int diagIdx, unsigned long* out, unsigned long n) {
@@ -3046,9 +3140,11 @@ unsigned long KeyBundleBytes(int withSecret) {
   Context& c = ctx();
   const size_t key = (size_t)2 * c.dnum * (c.L + c.K) * c.N * 8, pk = (size_t)2 * (c.L + c.K) * c.N * 8,
                sk = (size_t)(c.L + c.K) * c.N * 8;
-  size_t hdr = (KB_HDR + c.gks.size()) * 8;
+  size_t hdr = (KB_HDR + 2 * c.gks.size()) * 8;
   hdr = (hdr + 255) & ~(size_t)255;
-  return hdr + pk + (c.have_rlk ? key : 0) + c.gks.size() * key + (withSecret ? sk : 0);
+  size_t gk = 0;
+  for (auto& kv : c.gks) gk += (size_t)kv.second.k.ncomp * kv.second.k.nlimb * c.N * 8;
+  return hdr + pk + (c.have_rlk ? key : 0) + gk + (withSecret ? sk : 0);
   API_END(0)
 }
 int ExportKeyBundle(void* dptr, int withSecret) {
@@ -3059,7 +3155,7 @@ int ExportKeyBundle(void* dptr, int withSecret) {
   if (withSecret && !c.have_sk) throw std::runtime_error("no secret key");
   std::vector<u64> hdr = {KB_MAGIC, (u64)c.gks.size(), (u64)(withSecret ? 1 : 0), (u64)c.have_rlk,
                           (u64)c.logN, (u64)c.L, (u64)c.K, (u64)c.dnum, moduli_digest(c)};
-  for (auto& kv : c.gks) hdr.push_back(kv.first);
+  for (auto& kv : c.gks) hdr.push_back(kv.first), hdr.push_back((u64)kv.second.level);
   size_t off = ((hdr.size() * 8) + 255) & ~(size_t)255;
   char* d = (char*)dptr;
   HIPCHK(hipMemcpyAsync(d, hdr.data(), hdr.size() * 8, hipMemcpyHostToDevice, c.stream));
@@ -3070,7 +3166,7 @@ int ExportKeyBundle(void* dptr, int withSecret) {
   };
   put(c.pk);
   if (c.have_rlk) put(c.rlk);
-  for (auto& kv : c.gks) put(kv.second);
+  for (auto& kv : c.gks) put(kv.second.k);
   if (withSecret) put(c.sk);
   HIPCHK(hipStreamSynchronize(c.stream));
   return 0;
@@ -3087,10 +3183,12 @@ int ImportKeyBundle(const void* dptr, unsigned long bytes) {
   if (h4[4] != (u64)c.logN || h4[5] != (u64)c.L || h4[6] != (u64)c.K || h4[7] != (u64)c.dnum ||
       h4[8] != moduli_digest(c))
     throw std::runtime_error("key bundle was made for another modulus chain (logN/L/K/dnum/moduli differ)");
-  if (h4[1] > (bytes / 8 - KB_HDR)) throw std::runtime_error("key bundle truncated (galois element list)");
-  std::vector<u64> gels(h4[1]);
-  if (h4[1]) HIPCHK(hipMemcpy(gels.data(), (const char*)dptr + KB_HDR * 8, h4[1] * 8, hipMemcpyDeviceToHost));
-  size_t off = ((KB_HDR + h4[1]) * 8 + 255) & ~(size_t)255;
+  if (h4[1] > (bytes / 8 - KB_HDR) / 2) throw std::runtime_error("key bundle truncated (galois element list)");
+  std::vector<u64> gels(2 * h4[1]);  // (element, level) pairs
+  if (h4[1]) HIPCHK(hipMemcpy(gels.data(), (const char*)dptr + KB_HDR * 8, h4[1] * 16, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < h4[1]; ++i)
+    if (gels[2 * i + 1] >= (u64)c.L) throw std::runtime_error("key bundle: galois key level outside the chain");
+  size_t off = ((KB_HDR + 2 * h4[1]) * 8 + 255) & ~(size_t)255;
   const char* d = (const char*)dptr;
   auto get = [&](int ncomp, int nlimb) {
     Poly p = c.alloc(ncomp, nlimb, 1);
@@ -3106,7 +3204,10 @@ int ImportKeyBundle(const void* dptr, unsigned long bytes) {
     c.rlk = get(2 * c.dnum, c.L + c.K);
     c.have_rlk = true;
   }
-  for (u64 ge : gels) c.gks[ge] = get(2 * c.dnum, c.L + c.K);
+  for (size_t i = 0; i < h4[1]; ++i) {
+    const int lv = (int)gels[2 * i + 1];
+    c.gks[gels[2 * i]] = EvKey{get(2 * ((lv + 1 + c.K - 1) / c.K), lv + 1 + c.K), lv};
+  }
   if (h4[2]) {
     c.sk = get(1, c.L + c.K);
     c.have_sk = true;

@@ -149,8 +149,15 @@ struct BasisExtTable {
 // grouped launches (one launch for many independent key switches / rotations)
 // ---------------------------------------------------------------------------
 #define ORION_MAXGROUP 64
-struct MacGroups {  // ks_mac_kernel: group g uses key[g]
+// An evaluation key made for level klvl holds the digits 0..ceil((klvl+1)/K)-1
+// over the limbs [q_0 .. q_klvl, p_0 .. p_{K-1}] ([digit][2][klvl+1+K][N]); a
+// full-chain key has klvl = L - 1.  QP modulus m sits at limb key_pos(m).
+__host__ __device__ static inline int key_pos(int m, int L, int klvl) { return m < L ? m : klvl + 1 + (m - L); }
+
+struct MacGroups {  // ks_mac_kernel: group g uses key[g], made for level klvl[g]
   const u64* key[ORION_MAXGROUP];
+  int klvl[ORION_MAXGROUP];
+  int L;            // Q moduli of the chain (P modulus index L + k)
   long long out_gstride, d_gstride, add_gstride, own_gstride;
   const u64* add0;  // optional comp-0 addend, layout of out comp 0 (stride add_gstride per group)
   int K;            // digit width (own limbs of digit i: l / K == i)
@@ -174,13 +181,15 @@ struct LtPlan {
 struct LtBabies {  // the baby steps of register slots [s0, s0 + nb) of one lt_bsgs launch
   const u64* key[LT_MAXB];  // Galois key of the slot (null: the zero baby)
   const u32* idx[LT_MAXB];  // its NTT-domain automorphism index
-  int nb, s0, beta, K, level, nmod_key;
+  int klvl[LT_MAXB];        // level the key was made for
+  int nb, s0, beta, K, level, L;
   u64 pq[ORION_MAXLIMB], pqs[ORION_MAXLIMB];  // P mod q_l and Shoup companion (0 on the P limbs)
 };
 struct LtGiants {  // the nonzero giant steps of one lt_giant launch
   const u64* key[ORION_MAXGROUP];
   const u32* idx[ORION_MAXGROUP];
-  int ng, beta, K, level, nmod_key, has_zero;
+  int klvl[ORION_MAXGROUP];
+  int ng, beta, K, level, L, has_zero;
   long long d_gstride, own_gstride, t0_gstride;
 };
 

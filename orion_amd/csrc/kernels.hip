@@ -205,9 +205,9 @@ __global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, c
 // own Q limbs (l / K == i) are read from `own` (the NTT-domain input of the
 // decomposition, group stride own_gstride) instead of D, so the decomposition
 // never copies them.  out comps 0/1 of group g at out.p + g*out_gstride.
-// key layout [dnum][2][L+K][N].
+// key layout [digit][2][klvl+1+K][N] (common.h key_pos).
 __global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, LimbSet own, MacGroups G, int beta,
-                                                     int nmod_key, const DeviceTables* __restrict__ tb, int N) {
+                                                     const DeviceTables* __restrict__ tb, int N) {
   const int row = blockIdx.y;
   const int bi = row % out.nbatch;
   const int r = row / out.nbatch;
@@ -237,8 +237,9 @@ __global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, Lim
   } else if (G.add0) {
     r0 = *(const ulonglong2*)(G.add0 + g * G.add_gstride + row_off(out, 0, l, bi) + n);
   }
-  const long long kstride = (long long)nmod_key * N;
-  const u64* kp = key + (long long)m * N + n;
+  const int kl = G.klvl[g];
+  const long long kstride = (long long)(kl + 1 + G.K) * N;
+  const u64* kp = key + (long long)key_pos(m, G.L, kl) * N + n;
   for (int i0 = 0; i0 < beta; i0 += 4) {  // chunks of 4 digits: 12 loads in flight
     ulonglong2 d[4], kb[4], ka[4];
 #pragma unroll
@@ -299,12 +300,13 @@ __global__ void __launch_bounds__(256) automorph_kernel(LimbSet o, LimbSet a, co
 // D_i rows at dp + i*dstride; digit `owndigit` comes from ownp instead.
 // Digits go in chunks of 4: all 12 loads of a chunk are issued before the
 // first product, so their latencies overlap.
+// key: made for level klvl (limb of modulus m at key_pos(m, L, klvl), K P limbs)
 __device__ __forceinline__ void gadget_at(const u64* __restrict__ dp, long long dstride, const u64* ownp,
-                                          int owndigit, const u64* __restrict__ key, int beta, int nmod_key, int m,
-                                          int N, int j, const ModConst& mc, u64& r0, u64& r1) {
+                                          int owndigit, const u64* __restrict__ key, int beta, int L, int K, int klvl,
+                                          int m, int N, int j, const ModConst& mc, u64& r0, u64& r1) {
   r0 = r1 = 0;
-  const long long kstride = (long long)nmod_key * N;
-  const u64* kp = key + (long long)m * N + j;
+  const long long kstride = (long long)(klvl + 1 + K) * N;
+  const u64* kp = key + (long long)key_pos(m, L, klvl) * N + j;
   for (int i0 = 0; i0 < beta; i0 += 4) {
     u64 d[4], k0[4], k1[4];
 #pragma unroll
@@ -370,7 +372,7 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
       if (Bb.key[s]) {
         const int j = jx[s];
         u64 r0, r1;
-        gadget_at(dp, D.comp_stride, c1p, owndigit, Bb.key[s], Bb.beta, Bb.nmod_key, m, N, j, mc, r0, r1);
+        gadget_at(dp, D.comp_stride, c1p, owndigit, Bb.key[s], Bb.beta, Bb.L, Bb.K, Bb.klvl[s], m, N, j, mc, r0, r1);
         if (isq) r0 = add_mod(r0, shoup_mul(c0p[j], pq, pqs, mc.q), mc.q);
         x0[s] = r0;
         x1[s] = r1;
@@ -454,7 +456,7 @@ __global__ void __launch_bounds__(256) lt_giant_kernel(LimbSet acc, LimbSet D, L
     if (g + 1 < G.ng) jn = G.idx[g + 1][n];  // prefetch the next giant's index
     u64 a0, a1;
     gadget_at(D.p + g * G.d_gstride + dro, D.comp_stride, own.p + g * G.own_gstride + oro, owndigit, G.key[g],
-              G.beta, G.nmod_key, m, N, j, mc, a0, a1);
+              G.beta, G.L, G.K, G.klvl[g], m, N, j, mc, a0, a1);
     a0 = add_mod(a0, t0.p[g * G.t0_gstride + tro + j], mc.q);
     r0 = add_mod(r0, a0, mc.q);
     r1 = add_mod(r1, a1, mc.q);
@@ -533,11 +535,11 @@ int orion_launch_modup_all(const LimbSet& D, const LimbSet& in, const BasisExtTa
 }
 
 int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const LimbSet& own, const MacGroups& G, int ngroup,
-                        int beta, int nmod_key, const DeviceTables* tb, int N, hipStream_t st) {
+                        int beta, const DeviceTables* tb, int N, hipStream_t st) {
   const int rows = ngroup * out.nlimb * out.nbatch;
   if (rows == 0) return 0;
   if (ngroup > ORION_MAXGROUP) return -1;
-  hipLaunchKernelGGL(ks_mac_kernel, ew_grid(N, rows), dim3(256), 0, st, out, D, own, G, beta, nmod_key, tb, N);
+  hipLaunchKernelGGL(ks_mac_kernel, ew_grid(N, rows), dim3(256), 0, st, out, D, own, G, beta, tb, N);
   return 0;
 }
 

@@ -228,3 +228,58 @@ def test_key_bundle_header_checks(torch_cuda):
     assert lib.lib.ImportKeyBundle(buf.data_ptr(), n) != 0
     assert "another modulus chain" in lib.lib.OrionHipLastError().decode()
     lib.DeleteScheme()
+
+
+def test_level_scoped_galois_keys(torch_cuda, oracle_mod):
+    """A rotation key asked for by a linear transform is made for that
+    transform's level (ceil((l+1)/K) digits over l+1+K limbs), so keys of
+    low-level transforms stay small under a long chain; a later use at a
+    higher level replaces it with a key for that level.  Results stay
+    bit-exact vs the oracle either way, and the key bundle carries each
+    key's level."""
+    torch = torch_cuda
+    from orion_amd.backend import HipLibrary
+    logq, logp = [55] + [40] * 7, [60, 60]
+    lib = HipLibrary().new_scheme(13, logq, logp, 40, h=192, seed=77)
+    mods = lib.moduli()
+    orc = oracle_mod.Oracle(13, mods, len(logq), len(logp))
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    slots, lt_level = orc.N // 2, 2
+    rng = np.random.default_rng(30)
+    idx = [0, 3, 9, 40]
+    diags = rng.uniform(-1, 1, (len(idx), slots)).astype(np.float32)
+    lt = lib.GenerateLinearTransform(idx, list(diags.reshape(-1)), lt_level, 2.0, "none")
+    gels = lib.GetLinearTransformRotationKeys(lt)
+    lib.GenerateConsolidatedRotationKeys(gels)
+    for g in gels:
+        if g != 1:  # the zero rotation has no key
+            assert lib.GetGaloisKeyLevel(g) == lt_level
+    x = rand_ct(rng, mods, lt_level, orc.N, B=1)
+    out = lib.export_ciphertext(lib.EvaluateLinearTransform(lt, lib.import_ciphertext(x, 2.0 ** 40)))[0]
+    pts = [lib.export_lt_diagonal(lt, d, lt_level) for d in idx]
+    gkeys = {g: lib.export_galois_key(g) for g in gels if g != 1}
+    N1 = lib.GetLinearTransformN1(lt)
+    assert np.array_equal(out, orc.lt_bsgs(x[0], lt_level, idx, pts, N1, gkeys))
+    # a rotation by one of the transform's steps, at the top level: the key is remade for it
+    k = next(r for r in (3, 9, 40, 8, 1, 2) if int(lib.GaloisElement(r)) in gkeys)
+    g = int(lib.GaloisElement(k))
+    top = len(logq) - 1
+    y = rand_ct(rng, mods, top, orc.N, B=1)
+    r = lib.export_ciphertext(lib.RotateNew(lib.import_ciphertext(y, 2.0 ** 40), k))[0]
+    assert lib.GetGaloisKeyLevel(g) == top
+    assert np.array_equal(r, orc.rotate(y[0], g, lib.export_galois_key(g), top))
+    # the bundle keeps every key at its level
+    levels = {e: lib.GetGaloisKeyLevel(e) for e in gkeys}
+    keys = {e: lib.export_galois_key(e) for e in gkeys}
+    n = lib.KeyBundleBytes(0)
+    buf = torch.empty(n, dtype=torch.uint8, device="cuda")
+    assert lib.lib.ExportKeyBundle(buf.data_ptr(), 0) == 0
+    lib.DeleteScheme()
+    lib.new_scheme(13, logq, logp, 40, h=192, seed=78)
+    assert lib.lib.ImportKeyBundle(buf.data_ptr(), n) == 0, lib.lib.OrionHipLastError()
+    for e in gkeys:
+        assert lib.GetGaloisKeyLevel(e) == levels[e]
+        assert np.array_equal(lib.export_galois_key(e), keys[e])
+    lib.DeleteScheme()

@@ -249,7 +249,7 @@ def test_linear_transform_parity(small):
     N1 = lib.GetLinearTransformN1(lt)
     assert N1 == orc.find_best_bsgs_n1(idx, 0)
     pts = [lib.export_lt_diagonal(lt, d, level) for d in idx]
-    gkeys = {g: lib.export_galois_key(g) for g in gels}
+    gkeys = {g: lib.export_galois_key(g) for g in gels if g != 1}
     ref = orc.lt_bsgs(x, level, idx, pts, N1, gkeys)
     assert np.array_equal(got, ref)
     # functional: y[k] = sum_d diag_d[k] * x[k+d]
@@ -313,7 +313,7 @@ def _galois_elements(st):
     for ev in st.trace["events"]:
         if ev["phase"] == "forward" and ev["op"] in ("RotateNew", "Rotate"):
             gels.add(int(lib.GaloisElement(ev["args"][1])))
-    return sorted(gels)
+    return sorted(g for g in gels if g != 1)  # 1: the zero rotation needs no key
 
 
 def test_n16_ops_parity(torch_cuda, oracle_mod):
@@ -543,4 +543,58 @@ def test_ntt_edge_residues(torch_cuda, oracle_mod, logn):
     assert lib.lib.OrionHipNTT(ptr, nl, 4, mods_c, 1) == 0
     lib.OrionHipSynchronize()
     assert np.array_equal(dev.cpu().numpy().view(np.uint64), host)
+    lib.DeleteScheme()
+
+
+def test_deep_chain_n16(torch_cuda, oracle_mod):
+    """BASELINE config C4's arithmetic at full depth: N = 2^16 with
+    configs/resnet.yml's chain ([60] + [30] x 32 Q primes, P = [60, 60], so 17
+    gadget digits).  Ten consecutive mul_relin -> rescale steps from the top
+    level, then a rotation and a hoisted-BSGS linear transform, each bit-exact
+    vs the oracle (two images per launch)."""
+    from orion_amd.backend import HipLibrary
+    logq, logp = [60] + [30] * 32, [60, 60]
+    lib = HipLibrary().new_scheme(16, logq, logp, 30, h=192, seed=161)
+    mods = lib.moduli()
+    orc = oracle_mod.Oracle(16, mods, len(logq), len(logp))
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    rlk = lib.export_relin_key()
+    assert rlk.shape[0] == 17
+    rng = np.random.default_rng(1616)
+    level, B = len(logq) - 1, 2
+    x = rand_ct(rng, mods, level, orc.N, B=B)
+    ct = lib.import_ciphertext(x, 2.0 ** 30)
+    ref = [x[b] for b in range(B)]
+    for step in range(10):
+        nxt = lib.MulRelinCiphertextNew(ct, ct)
+        lib.Rescale(nxt)
+        lib.DeleteCiphertext(ct)
+        ct = nxt
+        got = lib.export_ciphertext(ct)
+        for b in range(B):
+            ref[b] = orc.rescale(orc.mul_relin(ref[b], ref[b], rlk, level), level)
+            assert np.array_equal(got[b], ref[b]), (step, b)
+        level -= 1
+    del rlk
+    g = int(lib.GaloisElement(5))
+    cr = lib.RotateNew(ct, 5)
+    gk = lib.export_galois_key(g)
+    got = lib.export_ciphertext(cr)
+    for b in range(B):
+        assert np.array_equal(got[b], orc.rotate(ref[b], g, gk, level)), b
+    del gk
+    slots = orc.N // 2
+    idx = [0, 1, 2, 3, 64, 65, 1000, slots - 1]
+    diags = rng.uniform(-1, 1, (len(idx), slots)).astype(np.float32)
+    lt = lib.GenerateLinearTransform(idx, list(diags.reshape(-1)), level, 2.0, "none")
+    gels = lib.GetLinearTransformRotationKeys(lt)
+    lib.GenerateConsolidatedRotationKeys(gels)
+    out = lib.export_ciphertext(lib.EvaluateLinearTransform(lt, ct))
+    pts = [lib.export_lt_diagonal(lt, d, level) for d in idx]
+    gkeys = {e: lib.export_galois_key(e) for e in gels if e != 1}
+    N1 = lib.GetLinearTransformN1(lt)
+    for b in range(B):
+        assert np.array_equal(out[b], orc.lt_bsgs(ref[b], level, idx, pts, N1, gkeys)), b
     lib.DeleteScheme()

@@ -10,6 +10,6 @@ timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "ntt" -d gpu
 echo "fetch ok"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "ntt" -d gpurun_out/prof_$TAG -o pmc_write --output-format csv -- python bench.py $ARGS > gpurun_out/prof_${TAG}_write.log 2>&1 || { echo "write failed"; tail -20 gpurun_out/prof_${TAG}_write.log; exit 1; }
 echo "write ok"
-timeout -k 10 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_SALU --kernel-include-regex "ntt" -d gpurun_out/prof_$TAG -o pmc_sq --output-format csv -- python bench.py $ARGS > gpurun_out/prof_${TAG}_sq.log 2>&1 || { echo "sq failed"; tail -20 gpurun_out/prof_${TAG}_sq.log; exit 1; }
+timeout -k 10 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_SALU GRBM_GUI_ACTIVE --kernel-include-regex "ntt|lt_bsgs|lt_giant|basis_ext|ks_mac|modup_all" -d gpurun_out/prof_$TAG -o pmc_sq --output-format csv -- python bench.py $ARGS > gpurun_out/prof_${TAG}_sq.log 2>&1 || { echo "sq failed"; tail -20 gpurun_out/prof_${TAG}_sq.log; exit 1; }
 echo "sq ok"
 find gpurun_out/prof_$TAG -name "*.csv" | head -20

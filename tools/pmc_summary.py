@@ -105,7 +105,31 @@ def main(tag, workload="lola_n15", batch=64, logn=15):
     trace = {"launches": n_l, "avg_launch_us": n_us / n_l if n_l else None,
              "algorithmic_bytes_per_launch": n_b / n_l if n_l else None,
              "achieved_GBps": n_b / (n_us * 1e-6) / 1e9 if n_us else None}
-    summary = {"tag": tag, "ntt_hbm_bytes_per_algorithmic_byte": ratio, "ntt_trace_batched": trace,
+    # VALU roofline of the VALU-bound kernels: the fraction of SIMD cycles in
+    # which a VALU instruction was executing, sum over waves of
+    # SQ_ACTIVE_INST_VALU (quad-cycles, so x4) / (elapsed cycles x 1024 SIMDs);
+    # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md), so the
+    # elapsed cycles of the dispatches are GRBM_GUI_ACTIVE / 8.  Also the
+    # achieved VALU wave-instruction rate against 1 per 2 cycles per SIMD (a
+    # single-pass 32-bit op on SIMD32; 64-bit ops and u64 multiplies issue at
+    # 1 per 4.5-5.3 cycles, tools/ubench/valu_rates.hip)
+    valu = {}
+    for k, v in per.items():
+        g = v.get("GRBM_GUI_ACTIVE")
+        if not g or "SQ_ACTIVE_INST_VALU" not in v:
+            continue
+        cyc = g / 8.0
+        valu[k] = {"valu_busy": v["SQ_ACTIVE_INST_VALU"] * 4.0 / (cyc * 1024),
+                   "valu_insts_per_simd_cycle": v["SQ_INSTS_VALU"] / (cyc * 1024),
+                   "frac_of_single_pass_peak": v["SQ_INSTS_VALU"] / (cyc * 1024) * 2.0,
+                   "wait_inst_any_per_wave_cycle": v["SQ_WAIT_INST_ANY"] / v["SQ_WAVE_CYCLES"]
+                   if v.get("SQ_WAVE_CYCLES") else None}
+    if valu:
+        with open(os.path.join(out, "valu_roofline.json"), "w") as f:
+            json.dump({"tag": tag, "workload": workload, "batch": batch,
+                       "definition": "valu_busy = sum SQ_ACTIVE_INST_VALU*4 / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs)",
+                       "kernels": valu}, f, indent=1)
+    summary = {"tag": tag, "ntt_hbm_bytes_per_algorithmic_byte": ratio, "ntt_trace_batched": trace, "valu": valu,
                "ntt_fetch_bytes_per_algorithmic_byte": ntt_fetch / ntt_alg if ntt_alg else None,
                "kernels": {k: dict(v) for k, v in per.items()}}
     with open(os.path.join(out, f"{tag}_pmc_summary.json"), "w") as f:

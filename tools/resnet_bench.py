@@ -12,13 +12,29 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from orion_amd.replay import OrionStream  # noqa: E402
 
 
+def _heartbeat():
+    import threading
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(50)
+            print(f"[resnet_bench] alive {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
-    st = OrionStream("resnet20_n13", seed=3)
+    _heartbeat()
+    name = os.environ.get("WORKLOAD", "resnet20_n13")
+    st = OrionStream(name, seed=3)
     t0 = time.perf_counter()
     st.keygen()
+    print(f"[resnet_bench] keygen {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
     st.compile()
     st.lib.OrionHipSynchronize()
     setup = time.perf_counter() - t0
+    print(f"[resnet_bench] compile done {setup:.1f} s", file=sys.stderr, flush=True)
     img = st.reference_input()
     exp = st.arrays["expected_output"].reshape(-1)
     for B in [int(b) for b in os.environ.get("BATCH", "1,8,32").split(",")]:
@@ -31,9 +47,11 @@ def main():
         dt = time.perf_counter() - t0
         res = st.decrypt_output(out)
         mae = float(np.abs(res - exp[None]).mean())
-        print(json.dumps({"workload": "ResNet-20 CIFAR-10 (reference op stream, N=2^13, 42 bootstraps)",
+        print(json.dumps({"workload": f"ResNet-20 CIFAR-10 (reference op stream {name}, "
+                                      f"{st.forward_op_counts().get('Bootstrap', 0)} bootstraps)",
                           "batch": B, "s_per_batch": round(dt, 3), "images_per_s": round(B / dt, 3),
-                          "mae_vs_cleartext": mae, "setup_s": round(setup, 1)}), flush=True)
+                          "mae_vs_cleartext": mae, "argmax_ok": bool(np.argmax(res[0]) == np.argmax(exp)),
+                          "setup_s": round(setup, 1)}), flush=True)
         st.lib.DeleteCiphertext(out)
         st.lib.DeleteCiphertext(ct)
 
