@@ -27,6 +27,7 @@
 //         multiply piece (tools/ubench/valu_rates.hip), and the float path
 //         needs ~9 of them per butterfly instead of ~30 integer instructions.
 #include "common.h"
+#include <stdlib.h>
 #include <string.h>
 
 #include "ntt_arith.h"
@@ -59,6 +60,10 @@
 #endif
 #ifndef NTT_FENCE_INV
 #define NTT_FENCE_INV 2
+#endif
+// 1: butterflies scheduled in pairs (see run_stage)
+#ifndef NTT_PAIR
+#define NTT_PAIR 0
 #endif
 
 namespace {
@@ -158,7 +163,7 @@ template <class A, int LOGN, int B, class Plan, int S, bool FWD>
 __device__ __forceinline__ void run_stage(typename A::T (&a)[32], typename A::W (&ring)[TW_PF], const A& ar,
                                           __amdgpu_buffer_rsrc_t w, int thigh) {
   constexpr int d = Plan::d_of(S), dk = d - B;
-  typename A::W W;
+  typename A::W W, Wp;
 #pragma unroll
   for (int pr = 0; pr < 16; ++pr) {
     const int khi = pr >> dk, klo = pr & ((1 << dk) - 1);
@@ -177,6 +182,28 @@ __device__ __forceinline__ void run_stage(typename A::T (&a)[32], typename A::W 
     }
     const int k0 = (khi << (dk + 1)) | klo;
     const int k1 = k0 | (1 << dk);
+    if constexpr (NTT_PAIR) {
+      // two butterflies per scheduling region: the pins sit in front of the
+      // pair, so the scheduler can interleave the two independent chains
+      // (one butterfly is a dependent chain of 8 FP64 or ~30 integer ops)
+      if ((pr & 1) == 0) {
+        Wp = W;
+        continue;
+      }
+      const int pe = pr - 1, ke = ((pe >> dk) << (dk + 1)) | (pe & ((1 << dk) - 1)), ke1 = ke | (1 << dk);
+      PIN(a[ke], a[ke1]);
+      PIN(a[k0], a[k1]);
+      if constexpr (FWD) {
+        ar.ct(a[ke], a[ke1], Wp);
+        ar.ct(a[k0], a[k1], W);
+        if ((pr & (NTT_FENCE_FWD - 1)) == NTT_FENCE_FWD - 1) NTT_FENCE();
+      } else {
+        ar.gs(a[ke], a[ke1], Wp, (S & 1) == 1);
+        ar.gs(a[k0], a[k1], W, (S & 1) == 1);
+        if ((pr & (NTT_FENCE_INV - 1)) == NTT_FENCE_INV - 1 || NTT_FENCE_INV < 2) NTT_FENCE();
+      }
+      continue;
+    }
     PIN(a[k0], a[k1]);
     if constexpr (FWD) {
       ar.ct(a[k0], a[k1], W);
@@ -235,7 +262,11 @@ template <class A, int LOGN, int PRO, int EPI>
 __device__ __forceinline__ void ntt_fwd_body(const NttIO& io, int c, int l, int b, const ModConst& mc, const A& ar,
                                              __amdgpu_buffer_rsrc_t w, u32* lds, const DeviceTables* __restrict__ tb) {
   constexpr int N = 1 << LOGN, B0 = LOGN - 5, B1 = LOGN - 10;
-  const int t = threadIdx.x;
+  // an opaque copy of the thread index per job: keeps the persistent job loop
+  // from hoisting every thread-derived address out of the loop (LICM), whose
+  // live ranges would then span the whole body and spill
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
   typename A::T a[32];
   if constexpr (PRO == NTT_PRO_LOAD) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.src, c, l, b), 0, N * 8, 0x00020000);
@@ -311,7 +342,11 @@ template <class A, int LOGN>
 __device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int b, const A& ar,
                                              __amdgpu_buffer_rsrc_t w, u32* lds) {
   constexpr int N = 1 << LOGN, B0 = LOGN - 5, B1 = LOGN - 10;
-  const int t = threadIdx.x;
+  // an opaque copy of the thread index per job: keeps the persistent job loop
+  // from hoisting every thread-derived address out of the loop (LICM), whose
+  // live ranges would then span the whole body and spill
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.src, c, l, b), 0, N * 8, 0x00020000);
   typename A::T a[32];
   if constexpr (NTT_INV_COAL) {
@@ -346,22 +381,43 @@ __device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int 
 }
 
 
+// Persistent: a grid of at most one workgroup per CU walks the launch's jobs
+// (job = blockIdx.x + k gridDim.x, in io.order), so a CU goes from one limb's
+// stores straight to the next limb's loads: no workgroup retire/dispatch
+// bubble between limbs, and the stores drain while the next limb loads and
+// computes.  LDS needs no extra barrier between jobs: every exchange ends
+// with one.
+// The subtract-and-scale epilogue variants keep one job per workgroup: as a
+// loop their extra live values spill (36-41 VGPRs at N = 2^15).
+template <int EPI>
+struct FwdPersist {
+  static constexpr bool value = EPI == NTT_EPI_STORE;
+};
+
+template <int LOGN, int PRO, int EPI>
+__device__ __forceinline__ void ntt_fwd_job(const NttIO& io, int job, const DeviceTables* __restrict__ tb, u32* lds) {
+  constexpr int N = 1 << LOGN;
+  int c, l, b;
+  job_of(io, job, c, l, b);
+  const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
+  const ModConst mc = tb->mc[mod];
+  if (mc.f64) {
+    const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd_d[mod], 0, N * 8, 0x00020000);
+    ntt_fwd_body<F64Arith, LOGN, PRO, EPI>(io, c, l, b, mc, F64Arith(mc), w, lds, tb);
+  } else {
+    const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd[mod], 0, N * 16, 0x00020000);
+    ntt_fwd_body<IntArith, LOGN, PRO, EPI>(io, c, l, b, mc, IntArith(mc), w, lds, tb);
+  }
+}
+
 template <int LOGN, int PRO, int EPI>
 __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_fwd_kernel(NttIO io, const DeviceTables* __restrict__ tb) {
-  constexpr int N = 1 << LOGN;
   extern __shared__ u32 lds[];
-  {
-    int c, l, b;
-    job_of(io, blockIdx.x, c, l, b);
-    const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
-    const ModConst mc = tb->mc[mod];
-    if (mc.f64) {
-      const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd_d[mod], 0, N * 8, 0x00020000);
-      ntt_fwd_body<F64Arith, LOGN, PRO, EPI>(io, c, l, b, mc, F64Arith(mc), w, lds, tb);
-    } else {
-      const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd[mod], 0, N * 16, 0x00020000);
-      ntt_fwd_body<IntArith, LOGN, PRO, EPI>(io, c, l, b, mc, IntArith(mc), w, lds, tb);
-    }
+  if constexpr (FwdPersist<EPI>::value) {
+#pragma nounroll
+    for (int job = blockIdx.x; job < io.jobs; job += gridDim.x) ntt_fwd_job<LOGN, PRO, EPI>(io, job, tb, lds);
+  } else {
+    ntt_fwd_job<LOGN, PRO, EPI>(io, blockIdx.x, tb, lds);
   }
 }
 
@@ -369,9 +425,10 @@ template <int LOGN>
 __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_inv_kernel(NttIO io, const DeviceTables* __restrict__ tb) {
   constexpr int N = 1 << LOGN;
   extern __shared__ u32 lds[];
-  {
+#pragma nounroll
+  for (int job = blockIdx.x; job < io.jobs; job += gridDim.x) {
     int c, l, b;
-    job_of(io, blockIdx.x, c, l, b);
+    job_of(io, job, c, l, b);
     const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
     const ModConst mc = tb->mc[mod];
     if (mc.f64) {
@@ -390,6 +447,9 @@ void set_lds_attr() {
                       ((1 << LOGN) + (1 << LOGN) / 32) * 4);
 }
 
+// workgroups of a persistent launch (0: one workgroup per job); set by orion_ntt_init
+int g_ntt_grid = 0;
+
 template <int LOGN>
 int launch_ntt(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
   constexpr int N = 1 << LOGN;
@@ -397,16 +457,16 @@ int launch_ntt(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_
   if (jobs == 0) return 0;
   if (io.jobs != jobs) return -1;
   const size_t lds = (size_t)(N + N / 32) * sizeof(u32);
-  const dim3 g(jobs), blk(NttGeom<LOGN>::T);
+  const dim3 g(g_ntt_grid > 0 && jobs > g_ntt_grid ? g_ntt_grid : jobs), blk(NttGeom<LOGN>::T);
   if (inverse) {
     if (io.pro != NTT_PRO_LOAD || io.epi != NTT_EPI_STORE) return -1;
     hipLaunchKernelGGL(ntt_inv_kernel<LOGN>, g, blk, lds, st, io, tb);
     return 0;
   }
-#define FWD(P, E)                                                                        \
-  if (io.pro == P && io.epi == E) {                                                      \
-    hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, P, E>), g, blk, lds, st, io, tb);           \
-    return 0;                                                                            \
+#define FWD(P, E)                                                                                     \
+  if (io.pro == P && io.epi == E) {                                                                   \
+    hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, P, E>), FwdPersist<E>::value ? g : dim3(jobs), blk, lds, st, io, tb); \
+    return 0;                                                                                         \
   }
   FWD(NTT_PRO_LOAD, NTT_EPI_STORE)
   FWD(NTT_PRO_LOAD, NTT_EPI_SUBSCALE)
@@ -445,10 +505,19 @@ int orion_launch_ntt(int logN, const LimbSet& s, const DeviceTables* tb, bool in
   return orion_launch_ntt_io(logN, io, tb, inverse, st);
 }
 
-// allow >64 KiB dynamic LDS for the N = 2^14, 2^15 kernels
+// allow >64 KiB dynamic LDS for the N = 2^14, 2^15 kernels; size the
+// persistent grid: ORION_NTT_PERSIST workgroups per CU (0 = one per job)
 int orion_ntt_init() {
   init_lds<13>();
   init_lds<14>();
   init_lds<15>();
+  const char* e = getenv("ORION_NTT_PERSIST");
+  const int per_cu = e ? atoi(e) : 1;
+  int dev = 0, ncu = 0;
+  if (per_cu > 0 && hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+    g_ntt_grid = per_cu * ncu;
+  else
+    g_ntt_grid = 0;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
