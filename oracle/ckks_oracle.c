@@ -20,6 +20,15 @@ typedef uint64_t u64;
 
 struct oracle_ctx {
   int logN, N, L, K;
+  /* ConjugateInvariant ring (scheme.go:49-52): degree N, NthRoot 4N.  Its
+   * NTT is the first half of the degree-2N negacyclic NTT of the element's
+   * expansion p (p_j = a_j, p_N = 0, p_{2N-j} = -a_j): a fold
+   * b_e = a_e - W a_{N-e} (W = psi^N, the 2N NTT's first-stage twiddle),
+   * then the 2N NTT's remaining stages on the first half (twiddles
+   * fw[m + i] = fw_2N[2m + i]).  The inverse unfolds with
+   * a_e = (b_e + W b_{N-e}) / 2. */
+  int ci;
+  u64 ciw[MAXMOD], ciws[MAXMOD], inv2[MAXMOD];
   u64 mod[MAXMOD];
   u64 psi[MAXMOD];
   u64 *fw[MAXMOD];  /* fw[bitrev(j)] = psi^j            */
@@ -204,19 +213,21 @@ u64 oracle_primitive_root(u64 q) {
 /* ------------------------------------------------------------------ */
 /* context                                                             */
 /* ------------------------------------------------------------------ */
-oracle_ctx *oracle_new(int logN, const u64 *moduli, int L, int K) {
+oracle_ctx *oracle_new_ring(int logN, const u64 *moduli, int L, int K, int ci) {
   if (L + K > MAXMOD) return NULL;
   oracle_ctx *c = (oracle_ctx *)calloc(1, sizeof(oracle_ctx));
   c->logN = logN;
   c->N = 1 << logN;
   c->L = L;
   c->K = K;
-  int N = c->N;
+  c->ci = ci ? 1 : 0;
+  const int N = c->N, logM = logN + c->ci, M = 1 << logM; /* M: degree of the negacyclic NTT */
+  u64 *tf = (u64 *)malloc(sizeof(u64) * M), *ti = (u64 *)malloc(sizeof(u64) * M);
   for (int m = 0; m < L + K; m++) {
     u64 q = moduli[m];
     c->mod[m] = q;
     u64 g = oracle_primitive_root(q);
-    u64 psi = powmod(g, (q - 1) / (2 * (u64)N), q);
+    u64 psi = powmod(g, (q - 1) / (2 * (u64)M), q); /* primitive 2M-th root (2N, or 4N for CI) */
     u64 psii = invmod(psi, q);
     c->psi[m] = psi;
     c->fw[m] = (u64 *)malloc(sizeof(u64) * N);
@@ -224,20 +235,37 @@ oracle_ctx *oracle_new(int logN, const u64 *moduli, int L, int K) {
     c->iw[m] = (u64 *)malloc(sizeof(u64) * N);
     c->iws[m] = (u64 *)malloc(sizeof(u64) * N);
     u64 a = 1, b = 1;
-    for (int j = 0; j < N; j++) {
-      u64 r = bitrev(j, logN);
-      c->fw[m][r] = a;
-      c->fws[m][r] = shoup(a, q);
-      c->iw[m][r] = b;
-      c->iws[m][r] = shoup(b, q);
+    for (int j = 0; j < M; j++) {
+      u64 r = bitrev(j, logM);
+      tf[r] = a;
+      ti[r] = b;
       a = mulmod(a, psi, q);
       b = mulmod(b, psii, q);
     }
+    for (int k = 0; k < N; k++) {
+      /* CI: the N-point stage with m groups uses the 2N table's entry 2m + i */
+      int mm = 1;
+      while (2 * mm <= k) mm <<= 1;
+      const int src = c->ci ? (k ? k + mm : 0) : k;
+      c->fw[m][k] = tf[src];
+      c->fws[m][k] = shoup(tf[src], q);
+      c->iw[m][k] = ti[src];
+      c->iws[m][k] = shoup(ti[src], q);
+    }
     c->ninv[m] = invmod((u64)N, q);
     c->ninvs[m] = shoup(c->ninv[m], q);
+    if (c->ci) {
+      c->ciw[m] = tf[1]; /* psi^N */
+      c->ciws[m] = shoup(tf[1], q);
+      c->inv2[m] = (q + 1) / 2;
+    }
   }
+  free(tf);
+  free(ti);
   return c;
 }
+oracle_ctx *oracle_new(int logN, const u64 *moduli, int L, int K) { return oracle_new_ring(logN, moduli, L, K, 0); }
+int oracle_is_ci(const oracle_ctx *c) { return c->ci; }
 
 void oracle_free(oracle_ctx *c) {
   if (!c) return;
@@ -260,6 +288,13 @@ void oracle_ntt(const oracle_ctx *c, int mi, u64 *a) {
   const int N = c->N;
   const u64 q = c->mod[mi], q2 = 2 * q;
   const u64 *w = c->fw[mi], *ws = c->fws[mi];
+  if (c->ci) { /* fold: b_e = a_e - W a_{N-e}, b_0 = a_0 */
+    u64 *b = (u64 *)malloc(sizeof(u64) * N);
+    b[0] = a[0];
+    for (int e = 1; e < N; e++) b[e] = submod(a[e], mulmod(a[N - e], c->ciw[mi], q), q);
+    memcpy(a, b, sizeof(u64) * N);
+    free(b);
+  }
   int t = N;
   for (int m = 1; m < N; m <<= 1) {
     t >>= 1;
@@ -306,6 +341,13 @@ void oracle_intt(const oracle_ctx *c, int mi, u64 *a) {
     u64 X = mul_shoup_lazy(a[j], c->ninv[mi], c->ninvs[mi], q);
     if (X >= q) X -= q;
     a[j] = X;
+  }
+  if (c->ci) { /* unfold: a_e = (b_e + W b_{N-e}) / 2, a_0 = b_0 */
+    u64 *b = (u64 *)malloc(sizeof(u64) * N);
+    memcpy(b, a, sizeof(u64) * N);
+    for (int e = 1; e < N; e++)
+      a[e] = mulmod(addmod(b[e], mulmod(b[N - e], c->ciw[mi], q), q), c->inv2[mi], q);
+    free(b);
   }
 }
 
@@ -489,18 +531,20 @@ void oracle_keyswitch(const oracle_ctx *c, int level, const u64 *cx, const u64 *
 /* automorphisms                                                         */
 /* ------------------------------------------------------------------ */
 uint64_t oracle_galois_element(const oracle_ctx *c, int k) {
-  u64 M = 2 * (u64)c->N;
+  u64 M = (2 * (u64)c->N) << c->ci; /* NthRoot: 2N, or 4N for the CI ring */
   u64 e = (u64)((int64_t)k) & (M - 1);
   return powmod(5, e, M);
 }
 
+/* index over the degree-M NTT (M = 2N for CI); the CI ring keeps its first
+ * half, which every 5^k (= 1 mod 4) maps onto itself */
 static void automorphism_index(const oracle_ctx *c, u64 g, uint32_t *idx) {
-  const int N = c->N, logN = c->logN;
-  const u64 mask = 2 * (u64)N - 1;
+  const int N = c->N, logM = c->logN + c->ci;
+  const u64 mask = (2 * (u64)N << c->ci) - 1;
   for (int j = 0; j < N; j++) {
-    u64 t1 = 2 * bitrev(j, logN) + 1;
+    u64 t1 = 2 * bitrev(j, logM) + 1;
     u64 t2 = (((g * t1) & mask) - 1) >> 1;
-    idx[j] = (uint32_t)bitrev(t2, logN);
+    idx[j] = (uint32_t)bitrev(t2, logM);
   }
 }
 
@@ -618,7 +662,7 @@ static int cmp_int(const void *a, const void *b) { return (*(const int *)a > *(c
 void oracle_lt_bsgs(const oracle_ctx *c, int level, const u64 *ct, int nd, const int *diag_idx,
                     const u64 *const *pts, int N1, int ngk, const u64 *gels,
                     const u64 *const *gks, u64 *out) {
-  const int N = c->N, L = c->L, K = c->K, slots = N / 2;
+  const int N = c->N, L = c->L, K = c->K, slots = c->ci ? N : N / 2;
   const int nq = level + 1, nqp = nq + K;
   const size_t PQ = (size_t)nq * N, PQP = (size_t)nqp * N;
   int mods[MAXMOD];
@@ -854,9 +898,12 @@ static void to_crt(double v, double scale, const oracle_ctx *c, const int *mods,
   }
 }
 
+/* CI ring: n = N real slots, cyclotomic order 4N; the coefficients are the
+ * real parts of the special iFFT (the imaginary parts are the expansion's
+ * upper half, -a_{N-j}, which the CI ring does not store) */
 void oracle_encode(const oracle_ctx *c, const double *values, int nvals, double scale,
                    const int *mods, int nm, u64 *out) {
-  const int N = c->N, n = N / 2, M = 2 * N;
+  const int N = c->N, n = c->ci ? N : N / 2, M = 4 * n;
   int *rot;
   cplx *roots;
   special_tables(n, M, &rot, &roots);
@@ -865,7 +912,7 @@ void oracle_encode(const oracle_ctx *c, const double *values, int nvals, double 
   special_ifft(v, n, M, rot, roots);
   for (int i = 0; i < n; i++) {
     to_crt(v[i].re, scale, c, mods, nm, out + i, (size_t)N);
-    to_crt(v[i].im, scale, c, mods, nm, out + i + n, (size_t)N);
+    if (!c->ci) to_crt(v[i].im, scale, c, mods, nm, out + i + n, (size_t)N);
   }
   for (int m = 0; m < nm; m++) oracle_ntt(c, mods[m], out + (size_t)m * N);
   free(v);
@@ -937,7 +984,7 @@ static double crt_centered_double(const oracle_ctx *c, int level, const u64 *res
 
 void oracle_decode(const oracle_ctx *c, int level, const u64 *pt, double scale,
                    double *values) {
-  const int N = c->N, n = N / 2, M = 2 * N, nl = level + 1;
+  const int N = c->N, n = c->ci ? N : N / 2, M = 4 * n, nl = level + 1;
   u64 *x = (u64 *)malloc(sizeof(u64) * N * nl);
   memcpy(x, pt, sizeof(u64) * N * nl);
   for (int j = 0; j < nl; j++) oracle_intt(c, j, x + (size_t)j * N);
@@ -949,10 +996,14 @@ void oracle_decode(const oracle_ctx *c, int level, const u64 *pt, double scale,
   for (int i = 0; i < N; i++) {
     for (int j = 0; j < nl; j++) res[j] = x[(size_t)j * N + i];
     double f = crt_centered_double(c, level, res) / scale;
-    if (i < n)
+    if (c->ci) { /* slot input c_j = a_j - i a_{N-j} (c_0 = a_0) */
       v[i].re = f;
-    else
+      if (i) v[N - i].im = -f;
+    } else if (i < n) {
+      v[i].re = f;
+    } else {
       v[i - n].im = f;
+    }
   }
   special_fft(v, n, M, rot, roots);
   for (int i = 0; i < n; i++) values[i] = v[i].re;

@@ -44,6 +44,10 @@ int oracle_gen_moduli(int logN, const int *logQ, int lenQ, const int *logP,
                       int lenP, uint64_t *out);
 
 oracle_ctx *oracle_new(int logN, const uint64_t *moduli, int L, int K);
+/* ci = 1: Lattigo's ConjugateInvariant ring of degree 2^logN (NthRoot 4N,
+ * N real slots; scheme.go:49-52); moduli must be 1 mod 4N */
+oracle_ctx *oracle_new_ring(int logN, const uint64_t *moduli, int L, int K, int ci);
+int oracle_is_ci(const oracle_ctx *ctx);
 void oracle_free(oracle_ctx *ctx);
 int oracle_N(const oracle_ctx *ctx);
 

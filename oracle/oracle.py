@@ -34,6 +34,7 @@ def _load():
     sig = {
         "oracle_gen_moduli": (ctypes.c_int, [ctypes.c_int, _intp, ctypes.c_int, _intp, ctypes.c_int, _u64p]),
         "oracle_new": (vp, [ctypes.c_int, _u64p, ctypes.c_int, ctypes.c_int]),
+        "oracle_new_ring": (vp, [ctypes.c_int, _u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
         "oracle_free": (None, [vp]),
         "oracle_psi": (ctypes.c_uint64, [vp, ctypes.c_int]),
         "oracle_primitive_root": (ctypes.c_uint64, [ctypes.c_uint64]),
@@ -108,11 +109,15 @@ def gen_moduli(logN, logQ, logP):
 class Oracle:
     """One parameter set.  Arrays are numpy uint64, limb-major [limbs][N]."""
 
-    def __init__(self, logN, moduli, L, K):
+    def __init__(self, logN, moduli, L, K, ci=False):
+        """ci: Lattigo's ConjugateInvariant ring of degree 2^logN (NthRoot 4N,
+        N real slots; moduli = 1 mod 4N, i.e. gen_moduli(logN + 1, ...))."""
         self.logN, self.N, self.L, self.K = logN, 1 << logN, L, K
+        self.ci = bool(ci)
+        self.slots = self.N if self.ci else self.N // 2
         self.moduli = [int(m) for m in moduli]
         arr = np.array(self.moduli, dtype=np.uint64)
-        self._h = lib().oracle_new(logN, _p(arr), L, K)
+        self._h = lib().oracle_new_ring(logN, _p(arr), L, K, int(self.ci))
         self.dnum = (L + K - 1) // K if K else 0
 
     @classmethod
@@ -214,7 +219,7 @@ class Oracle:
         return out
 
     def find_best_bsgs_n1(self, diag_idx, log_ratio=0):
-        return int(lib().oracle_find_best_bsgs_n1(_ip(diag_idx), len(diag_idx), self.N // 2, log_ratio))
+        return int(lib().oracle_find_best_bsgs_n1(_ip(diag_idx), len(diag_idx), self.slots, log_ratio))
 
     def encode(self, values, scale, mods):
         v = np.ascontiguousarray(values, dtype=np.float64)
@@ -225,7 +230,7 @@ class Oracle:
 
     def decode(self, pt, level, scale):
         pt = np.ascontiguousarray(pt, dtype=np.uint64)
-        out = np.zeros(self.N // 2, dtype=np.float64)
+        out = np.zeros(self.slots, dtype=np.float64)
         lib().oracle_decode(self._h, level, _p(pt), float(scale), out.ctypes.data_as(_dblp))
         return out
 

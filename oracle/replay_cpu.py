@@ -32,12 +32,14 @@ class CpuStream:
         self.trace, self.arrays = _load(name)
         self.meta = self.trace["meta"]
         cfg = self.meta["config"]
-        # a ConjugateInvariant ring of degree N runs as the Standard ring of degree 2N (backend.hip NewScheme)
-        self.logN = cfg["logn"] + (1 if cfg.get("ringtype", "standard").lower() == "conjugateinvariant" else 0)
+        # ConjugateInvariant ring (scheme.go:49-52): degree N, NthRoot 4N (primes = 1 mod 4N), N real slots
+        self.ci = cfg.get("ringtype", "standard").lower() == "conjugateinvariant"
+        self.logN = cfg["logn"]
         self.L, self.K = len(cfg["logq"]), len(cfg["logp"])
-        self.orc = Oracle(self.logN, gen_moduli(self.logN, cfg["logq"], cfg["logp"]), self.L, self.K)
+        self.orc = Oracle(self.logN, gen_moduli(self.logN + self.ci, cfg["logq"], cfg["logp"]), self.L, self.K,
+                          ci=self.ci)
         self.N = self.orc.N
-        self.slots = self.N // 2
+        self.slots = self.orc.slots
         self.mods = self.orc.moduli
         self.seed = seed
         self.h = cfg["h"]
@@ -54,7 +56,7 @@ class CpuStream:
 
     def galois_key(self, g):
         if g not in self.gks:
-            M = 2 * self.N
+            M = (4 if self.ci else 2) * self.N  # NthRoot
             ginv = pow(g, -1, M)
             s_out = self.orc.automorphism_ntt(self.sk, ginv)
             self.gks[g] = self.orc.gen_evk(self.seed + 7 + len(self.gks), self.sk, s_out)

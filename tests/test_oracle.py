@@ -297,11 +297,61 @@ def test_cpu_replay_lola_matches_cleartext():
 
 def test_cpu_replay_mlp_conjugate_invariant():
     """tests/configs/mlp.yml as written (RingType ConjugateInvariant, 8192 real
-    slots): the oracle replays the frontend's op stream on the degree-2N
-    Standard ring and meets the reference MAE gate (test_mlp.py:45-48)."""
+    slots): the oracle replays the frontend's op stream on the native degree-N
+    CI ring (N coefficients per limb, NthRoot 4N) and meets the reference MAE
+    gate (test_mlp.py:45-48)."""
     from oracle.replay_cpu import CpuStream
     s = CpuStream("mlp_n13_ci")
-    assert s.N == 1 << 14 and s.slots == 1 << 13
+    assert s.N == 1 << 13 and s.slots == 1 << 13 and s.orc.ci
+    s.keygen()
+    s.compile()
+    out = s.forward(s.encrypt(s.arrays["input"]))
+    v = s.decrypt(out)[:10]
+    exp = s.arrays["expected_output"].reshape(-1)
+    assert np.abs(v - exp).mean() < 0.005
+
+
+def test_ci_ring_is_the_fixed_subring(oracle_mod):
+    """Pins the native ConjugateInvariant ring (scheme.go:49-52) to the
+    Standard ring of degree 2N (itself pinned by the big-integer KATs): for a
+    CI element a (N coefficients) with expansion p (p_j = a_j, p_N = 0,
+    p_{2N-j} = -a_j), the CI NTT is the first half of the 2N NTT of p, the
+    CI automorphism by 5^k is the first half of the 2N one, and the CI
+    encoding is the first half of the 2N encoding of the same real slots."""
+    logn = 11
+    mods = oracle_mod.gen_moduli(logn + 1, [40, 50, 60], [61])
+    ci = oracle_mod.Oracle(logn, mods, 3, 1, ci=True)
+    st = oracle_mod.Oracle(logn + 1, mods, 3, 1)
+    for q in mods:
+        assert q % (4 << logn) == 1  # NthRoot 4N
+    N = 1 << logn
+    rng = np.random.default_rng(5)
+    for m in range(4):
+        q = mods[m]
+        a = rng.integers(0, q, N, dtype=np.uint64)
+        p = np.zeros(2 * N, dtype=np.uint64)
+        p[:N] = a
+        p[N + 1:] = [(q - int(x)) % q for x in a[1:][::-1]]
+        ref = st.ntt(m, p)
+        got = ci.ntt(m, a)
+        assert np.array_equal(got, ref[:N]), m
+        assert np.array_equal(ci.intt(m, got), a)
+        for k in (1, 7, -3):
+            g = ci.galois_element(k)
+            assert g == st.galois_element(k) and g % 4 == 1
+            assert np.array_equal(ci.automorphism_ntt(got[None], g)[0], st.automorphism_ntt(ref[None], g)[0][:N])
+    v = rng.uniform(-1, 1, N)
+    pe = ci.encode(v, 2.0 ** 40, [0, 1])
+    assert np.array_equal(pe, st.encode(v, 2.0 ** 40, [0, 1])[:, :N])
+    assert np.abs(ci.decode(pe, 1, 2.0 ** 40) - v).max() < 1e-8
+
+
+def test_cpu_replay_lola_conjugate_invariant():
+    """configs/lola.yml as written (ConjugateInvariant, N=2^13): the oracle's
+    native CI ring replays the frontend's op stream within the MAE gate."""
+    from oracle.replay_cpu import CpuStream
+    s = CpuStream("lola_n13_ci")
+    assert s.orc.ci and s.slots == s.N
     s.keygen()
     s.compile()
     out = s.forward(s.encrypt(s.arrays["input"]))
