@@ -345,7 +345,7 @@ def main():
         dvals[:, :imgs[0].size] = torch.from_numpy(imgs.reshape(args.batch, -1)).to(device)
         torch.cuda.synchronize()
         out_ct = step()
-        dout = torch.empty(args.batch, lib.N // 2, dtype=torch.float64, device=device)  # DecodeDevice: [B][N/2]
+        dout = torch.empty(args.batch, lib.slots, dtype=torch.float64, device=device)  # DecodeDevice: [B][slots]
 
         def client(fn, reps=5):
             fn()

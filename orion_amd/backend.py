@@ -299,7 +299,9 @@ class HipLibrary:
         if seed is not None:
             self.OrionHipSetSeed(seed)
         self.NewScheme(logn, list(logq), list(logp), logscale or logq[-1], h, ringtype, "", "none")
-        self.N = 1 << self.OrionHipLogN()  # 2^(logn+1) for a ConjugateInvariant ring (NewScheme)
+        self.N = 1 << self.OrionHipLogN()  # coefficients per limb (both rings)
+        ci = str(ringtype).lower() != "standard"
+        self.slots = self.N if ci else self.N // 2  # ConjugateInvariant: N real slots (scheme.go:49-52)
         self.L, self.K = len(logq), len(logp)
         return self
 
@@ -388,8 +390,8 @@ class HipLibrary:
                          "EncodeBatchDevice")
 
     def decode_f64(self, pt):
-        """Slots of every image of a plaintext, float64 [B][N/2] (GPU decode)."""
-        out = np.zeros((self.GetPlaintextBatch(pt), self.N // 2), dtype=np.float64)
+        """Slots of every image of a plaintext, float64 [B][slots] (GPU decode)."""
+        out = np.zeros((self.GetPlaintextBatch(pt), self.GetPlaintextSlots(pt)), dtype=np.float64)
         self._chk(self.lib.DecodeF64(pt, out.ctypes.data_as(P(c_double)), out.size), "DecodeF64")
         return out
 

@@ -46,12 +46,12 @@ int orion_launch_lt_bsgs(const LimbSet& t0, const LimbSet& t1, const LimbSet& D,
 int orion_launch_lt_giant(const LimbSet& acc, const LimbSet& D, const LimbSet& own, const LimbSet& t0,
                           const LimbSet& z, const LtGiants& G, const DeviceTables* tb, int N, hipStream_t st);
 
-int orion_launch_encode(const float* vals, int nvals, int B, double2* v, const double2* tw_inv, int logn,
+int orion_launch_encode(const float* vals, int nvals, int B, double2* v, const double2* tw_inv, int logn, bool ci,
                         const LimbSet& out, double scale, const DeviceTables* tb, hipStream_t st);
-int orion_launch_decode(const LimbSet& x, const u64* garner, double scale, int logn, double2* v,
+int orion_launch_decode(const LimbSet& x, const u64* garner, double scale, int logn, bool ci, double2* v,
                         const double2* tw_fwd, double* out, const DeviceTables* tb, hipStream_t st);
 int orion_launch_enc_sample(const LimbSet& r, const EncSampler& sp, const DeviceTables* tb, int N, hipStream_t st);
-int orion_launch_encode_c(double2* v, int B, const double2* tw_inv, int logn, const LimbSet& out, double scale,
+int orion_launch_encode_c(double2* v, int B, const double2* tw_inv, int logn, bool ci, const LimbSet& out, double scale,
                           const DeviceTables* tb, hipStream_t st);
 int orion_launch_modraise(const LimbSet& out, const LimbSet& in, const DeviceTables* tb, int N, hipStream_t st);
 
@@ -227,6 +227,12 @@ enum { P_NTT_FWD = 0, P_NTT_INV, P_EW, P_BEXT, P_MAC, P_AUT, P_TENSOR, P_RSPREP,
 // ---------------------------------------------------------------------------
 struct Context {
   int logN = 0, N = 0, L = 0, K = 0, dnum = 0, logScale = 0, h = 0;
+  // ring (scheme.go:49-52): Standard Z[X]/(X^N + 1), N/2 complex slots, NthRoot
+  // 2N; or ConjugateInvariant Z[X + X^-1]/(X^2N + 1) of degree N, N real
+  // slots, NthRoot 4N (primes = 1 mod 4N; the NTT folds/unfolds, ntt.hip)
+  bool ci = false;
+  int slots = 0;
+  u64 nthroot = 0;
   std::vector<u64> mods;  // QP
   hipStream_t stream = nullptr;
   bool own_stream = false;
@@ -440,6 +446,7 @@ struct Context {
   }
   void ntt_io(NttIO io, bool inv) {
     io.order = ntt_order;
+    io.ci = ci ? 1 : 0;
     io.jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
     if (io.order == 2) {  // integer-path (>= 2^46) limbs are ~1.4x slower per transform: dispatch them first
       int k = 0;
@@ -447,7 +454,7 @@ struct Context {
         for (int l = 0; l < io.dst.nlimb; ++l)
           if ((host_tb.mc[io.dst.mod[l]].f64 != 0) == (pass == 1)) io.lord[k++] = (unsigned char)l;
     }
-    if (logN == 16 || (logN == 15 && (ntt_impl == 2 || io.jobs < ntt2_below ||
+    if (logN == 16 || (logN == 15 && !ci && (ntt_impl == 2 || io.jobs < ntt2_below ||
                           ((inv || (ntt2_tail_fwd == 1 && io.pro == NTT_PRO_LOAD && io.epi == NTT_EPI_STORE) ||
                             (ntt2_tail_fwd == 2 && !(io.epi == NTT_EPI_SUBSCALE && io.ex.p == io.dst.p))) &&
                            ntt2_tail(io.jobs))))) {  // N = 2^16: two-pass only
@@ -498,9 +505,13 @@ struct Context {
   void copy(const LimbSet& o, const LimbSet& a) { ew(EW_COPY, o, a, a); }
 
   // -- tables ---------------------------------------------------------------------
-  void setup(int logN_, const std::vector<int>& logQ, const std::vector<int>& logP, int logScale_, int h_) {
+  void setup(int logN_, const std::vector<int>& logQ, const std::vector<int>& logP, int logScale_, int h_,
+             bool ci_ = false) {
     logN = logN_;
     N = 1 << logN;
+    ci = ci_;
+    slots = ci ? N : N / 2;
+    nthroot = (2 * (u64)N) << (ci ? 1 : 0);
     L = (int)logQ.size();
     K = (int)logP.size();
     if (K < 1) throw std::runtime_error("at least one P prime is required (hybrid key switching)");
@@ -513,7 +524,7 @@ struct Context {
       if (b > 61) throw std::runtime_error("moduli must be <= 61 bits");
     for (int b : logP)
       if (b > 61) throw std::runtime_error("moduli must be <= 61 bits");
-    mods = gen_moduli(logN, logQ, logP);
+    mods = gen_moduli(logN + (ci ? 1 : 0), logQ, logP);  // q = 1 mod NthRoot
     logQ_bits = logQ;
     logP_bits = logP;
     if (!stream) {
@@ -526,7 +537,7 @@ struct Context {
     HIPCHK(hipMalloc(&d_tb, sizeof(DeviceTables)));
     HIPCHK(hipMemcpy(d_tb, &host_tb, sizeof(DeviceTables), hipMemcpyHostToDevice));
     for (int inv = 0; inv < 2; ++inv) {
-      const std::vector<Cplx> tw = special_fft_twiddles(logN, inv != 0);
+      const std::vector<Cplx> tw = special_fft_twiddles(logN + (ci ? 1 : 0), inv != 0);  // slots = 2^(that - 1)
       void* d;
       HIPCHK(hipMalloc(&d, tw.size() * sizeof(double2)));
       HIPCHK(hipMemcpy(d, tw.data(), tw.size() * sizeof(double2), hipMemcpyHostToDevice));
@@ -548,19 +559,35 @@ struct Context {
       mc.bar_mu = (u64)(((u128)1 << (2 * mc.bar_k)) / q);
       mc.bar_mu2 = (u64)(((u128)1 << (2 * mc.bar_k + 2)) / q);
       mc.bar_mu8 = mc.bar_k <= 52 ? (u64)(((u128)1 << (2 * mc.bar_k + 8)) / q) : 0;
-      mc.ninv = hm_invmod((u64)N, q);
+      // CI: the unfold's 1/2 rides on the inverse's final scaling, (2N)^-1
+      mc.ninv = hm_invmod((u64)N << (ci ? 1 : 0), q);
       mc.ninv_s = hm_shoup(mc.ninv, q);
       const u64 g = primitive_root(q);
-      const u64 psi = hm_powmod(g, (q - 1) / (2 * (u64)N), q);
+      const u64 psi = hm_powmod(g, (q - 1) / nthroot, q);  // primitive NthRoot-th root
       const u64 psii = hm_invmod(psi, q);
+      // twiddles of the degree-M negacyclic NTT, M = NthRoot / 2, bit-reversed
+      const int logM = logN + (ci ? 1 : 0), M = 1 << logM;
+      std::vector<u64> tf(M), ti(M);
       u64 a = 1, b = 1;
-      for (int j = 0; j < N; ++j) {
-        const u64 r = hm_bitrev(j, logN);
-        fw[r] = make_ulonglong2(a, hm_shoup(a, q));
-        iv[r] = make_ulonglong2(b, hm_shoup(b, q));
+      for (int j = 0; j < M; ++j) {
+        const u64 r = hm_bitrev(j, logM);
+        tf[r] = a;
+        ti[r] = b;
         a = hm_mulmod(a, psi, q);
         b = hm_mulmod(b, psii, q);
       }
+      // CI: after the fold, the N-point stage with m groups is the degree-2N
+      // NTT's stage with 2m groups on its first half: twiddle m + i -> 2m + i
+      // (oracle_new_ring)
+      for (int k = 0; k < N; ++k) {
+        int mm = 1;
+        while (2 * mm <= k) mm <<= 1;
+        const int src = ci ? (k ? k + mm : 0) : k;
+        fw[k] = make_ulonglong2(tf[src], hm_shoup(tf[src], q));
+        iv[k] = make_ulonglong2(ti[src], hm_shoup(ti[src], q));
+      }
+      mc.ciw = ci ? tf[1] : 0;  // psi^N
+      mc.ciw_s = ci ? hm_shoup(tf[1], q) : 0;
       // float64-path constants and centered twiddles for small moduli
       mc.f64 = mc.bar_k <= ORION_F64_BITS ? 1 : 0;
       mc.qd = (double)q;
@@ -748,18 +775,21 @@ struct Context {
   }
 
   u64 galois_element(int k) const {
-    const u64 M = 2 * (u64)N;
-    return hm_powmod(5, (u64)(long long)k & (M - 1), M);
+    return hm_powmod(5, (u64)(long long)k & (nthroot - 1), nthroot);
   }
   const u32* aut_index(u64 g) {
     auto it = autidx.find(g);
     if (it != autidx.end()) return it->second;
+    // CI: the index over the degree-2N NTT; the ring keeps its first half,
+    // which every g = 5^k (= 1 mod 4) maps onto itself
     std::vector<u32> idx(N);
-    const u64 mask = 2 * (u64)N - 1;
+    const int logM = logN + (ci ? 1 : 0);
+    const u64 mask = nthroot - 1;
     for (int j = 0; j < N; ++j) {
-      const u64 t1 = 2 * hm_bitrev(j, logN) + 1;
+      const u64 t1 = 2 * hm_bitrev(j, logM) + 1;
       const u64 t2 = (((g * t1) & mask) - 1) >> 1;
-      idx[j] = (u32)hm_bitrev(t2, logN);
+      idx[j] = (u32)hm_bitrev(t2, logM);
+      if (idx[j] >= (u32)N) throw std::runtime_error("Galois element does not act on the ring");
     }
     u32* d;
     HIPCHK(hipMalloc(&d, N * sizeof(u32)));
@@ -909,8 +939,8 @@ struct Context {
                                                  : "galois key " + std::to_string(g) + " covers level " +
                                                        std::to_string(have->second.level) + " < " +
                                                        std::to_string(level) + " and there is no secret key");
-    const u64 M = 2 * (u64)N;
-    u64 ginv = hm_powmod(g, M / 2 - 1, M);  // g^-1 mod 2N (group order N/2 divides M/2)
+    const u64 M = nthroot;
+    u64 ginv = hm_powmod(g, M / 2 - 1, M);  // g^-1 mod NthRoot (the group order divides M/2)
     if ((g * ginv) % M != 1) {
       for (ginv = 1; ginv < M; ginv += 2)
         if ((g * ginv) % M == 1) break;
@@ -1225,7 +1255,7 @@ struct Context {
       for (int b : T.index.at(j)) {
         const int sl = slot_of.at(b);
         P.mask[gg] |= 1ull << sl;
-        P.pt[gg][sl] = T.sdiags.at((j + b) & (N / 2 - 1)).ptr();
+        P.pt[gg][sl] = T.sdiags.at((j + b) & (slots - 1)).ptr();
       }
     }
     if (T.d_plan && T.n_plan != nplan) {
@@ -1253,7 +1283,7 @@ struct Context {
     const int beta = (level + 1 + K - 1) / K;
     if (T.giants.empty()) throw std::runtime_error("linear transform without diagonals");
     for (int d : T.idx)
-      if (!T.diags.count(d & (N / 2 - 1)))
+      if (!T.diags.count(d & (slots - 1)))
         throw std::runtime_error("linear transform diagonal " + std::to_string(d) +
                                  " is not loaded (io_mode load: call LoadPlaintextDiagonal first)");
     if (T.plan_dirty) build_plan(T);
@@ -1380,7 +1410,7 @@ struct Context {
   // values: B images x nvals float32 slots, device memory (encoder.hip);
   // limbs Q 0..level (+ P when qp)
   Plaintext encode_dev(const float* dvals, int nvals, int B, int level, long double scale, bool qp) {
-    const int n = N / 2;
+    const int n = slots;
     if (nvals > n) throw std::runtime_error("too many values for the slot count");
     std::vector<int> md = iota(0, level + 1);
     if (qp)
@@ -1393,13 +1423,14 @@ struct Context {
     pt.poly = alloc(1, nl, B);
     Buffer v(&pool, (size_t)B * n * sizeof(double2));
     const LimbSet out = ls(pt.poly, 0, 1, iota(0, nl), md);
-    if (orion_launch_encode(dvals, nvals, B, (double2*)v.p, tw_inv, logN - 1, out, (double)scale, d_tb, stream))
+    if (orion_launch_encode(dvals, nvals, B, (double2*)v.p, tw_inv, ci ? logN : logN - 1, ci, out, (double)scale,
+                            d_tb, stream))
       throw std::runtime_error("encode launch failed");
     ntt(out, false);
     return pt;
   }
   Plaintext encode(const float* values, int nvals, int B, int level, long double scale, bool qp) {
-    if (nvals > N / 2) throw std::runtime_error("too many values for the slot count");
+    if (nvals > slots) throw std::runtime_error("too many values for the slot count");
     Buffer dv(&pool, (size_t)B * nvals * sizeof(float) + 16);
     HIPCHK(hipMemcpyAsync(dv.p, values, (size_t)B * nvals * sizeof(float), hipMemcpyHostToDevice, stream));
     HIPCHK(hipStreamSynchronize(stream));
@@ -1427,20 +1458,20 @@ struct Context {
     garner[level] = d;
     return d;
   }
-  // slots (real parts) of every image into device memory out[B][N/2]
+  // slots (real parts) of every image into device memory out[B][slots]
   void decode_dev(const Plaintext& pt, double* out) {
     const int level = pt.level, B = pt.poly.B, nl = level + 1;
     if (nl > ORION_MAXLIMB) throw std::runtime_error("decode: too many limbs");
     Poly t = alloc(1, nl, B);
     const LimbSet x = lsq(t, 0, 1, level);
     ntt_io(nio(x, lsq(pt.poly, 0, 1, level)), true);
-    Buffer v(&pool, (size_t)B * (N / 2) * sizeof(double2));
-    if (orion_launch_decode(x, garner_table(level), (double)pt.scale, logN - 1, (double2*)v.p, tw_fwd, out, d_tb,
-                            stream))
+    Buffer v(&pool, (size_t)B * slots * sizeof(double2));
+    if (orion_launch_decode(x, garner_table(level), (double)pt.scale, ci ? logN : logN - 1, ci, (double2*)v.p, tw_fwd,
+                            out, d_tb, stream))
       throw std::runtime_error("decode launch failed");
   }
   std::vector<double> decode(const Plaintext& pt) {
-    const size_t cnt = (size_t)pt.poly.B * (N / 2);
+    const size_t cnt = (size_t)pt.poly.B * slots;
     Buffer d(&pool, cnt * sizeof(double));
     decode_dev(pt, (double*)d.p);
     std::vector<double> out(cnt);
@@ -1708,7 +1739,7 @@ struct Context {
     Buffer dv(&pool, (size_t)n * sizeof(double2));
     HIPCHK(hipMemcpyAsync(dv.p, host.data(), host.size() * sizeof(double2), hipMemcpyHostToDevice, stream));
     const LimbSet out = ls(pt.poly, 0, 1, iota(0, nl), md);
-    if (orion_launch_encode_c((double2*)dv.p, 1, tw_inv, logN - 1, out, (double)scale, d_tb, stream))
+    if (orion_launch_encode_c((double2*)dv.p, 1, tw_inv, logN - 1, false, out, (double)scale, d_tb, stream))
       throw std::runtime_error("encode launch failed");
     HIPCHK(hipStreamSynchronize(stream));
     ntt(out, false);
@@ -1799,6 +1830,7 @@ struct Context {
   std::unique_ptr<Bootstrapper> btp;
 
   void new_bootstrapper() {
+    if (ci) throw std::runtime_error("bootstrapping needs the Standard ring (Lattigo has no ConjugateInvariant bootstrapper)");
     const int n = N / 2, logn = logN - 1;
     auto B = std::unique_ptr<Bootstrapper>(new Bootstrapper());
     // EvalMod range from the secret's Hamming weight: I ~ N(0, (h+1)/12) per coefficient
@@ -2067,22 +2099,19 @@ void NewScheme(int logN, int* logQ, int lenQ, int* logP, int lenP, int logScale,
   for (auto& ch : rt) ch = (char)tolower(ch);
   // scheme.go:50-51: any ring type other than "standard" selects Lattigo's
   // ConjugateInvariant ring Z[X + X^-1]/(X^2N + 1) of degree N (NthRoot 4N,
-  // N real slots).  It is the subring of the Standard ring of degree 2N fixed
-  // by conjugation, with the same primes (q = 1 mod 4N), the same slot count
-  // (2N/2 = N) and the same Galois elements (5^k mod 4N), so it runs here as
-  // that Standard ring; messages are real, which is all the CI ring carries.
+  // N real slots), held natively: N coefficients per limb, the NTT folds and
+  // unfolds around the degree-N transform (ntt.hip, Context::setup).
   const bool ci = rt != "standard";
   if (ci && rt != "conjugateinvariant")
     throw std::runtime_error("unknown ring type '" + rt + "' (standard | conjugateinvariant)");
-  const int logN_ring = ci ? logN + 1 : logN;
-  if (ci && logN_ring > 16)
-    throw std::runtime_error("ConjugateInvariant ring of degree 2^" + std::to_string(logN) +
-                             " needs a degree-2^" + std::to_string(logN_ring) + " Standard ring (max 2^16)");
+  // the CI NTT folds/unfolds inside the one-pass kernels (N <= 2^15 per CU)
+  if (ci && (logN < 13 || logN > 15))
+    throw std::runtime_error("ConjugateInvariant ring: logN must be 13..15 in this build");
   g.reset();
   g.reset(new Context());
   g->stream = g_user_stream;
   g->prng = Prng(g_seed);
-  g->setup(logN_ring, std::vector<int>(logQ, logQ + lenQ), std::vector<int>(logP, logP + lenP), logScale, h);
+  g->setup(logN, std::vector<int>(logQ, logQ + lenQ), std::vector<int>(logP, logP + lenP), logScale, h, ci);
   g->seed_encryption(g_seed);
   API_END_VOID
 }
@@ -2148,13 +2177,13 @@ int GetCiphertextLevel(int id) {
 int GetPlaintextSlots(int id) {
   API_BEGIN
   ctx().pts.get(id);
-  return ctx().N / 2;
+  return ctx().slots;
   API_END(-1)
 }
 int GetCiphertextSlots(int id) {
   API_BEGIN
   ctx().cts.get(id);
-  return ctx().N / 2;
+  return ctx().slots;
   API_END(-1)
 }
 int GetCiphertextDegree(int id) {
@@ -2252,7 +2281,7 @@ static std::vector<char> galois_key_bytes(const Context& c, u64 galEl, const std
   const size_t qp = (size_t)(level + 1 + c.K) * c.N;
   b.reserve(40 + (size_t)beta * (16 + 2 * (wire::poly_bytes(level + 1, c.N) + wire::poly_bytes(c.K, c.N))));
   wire::put_u64(b, galEl);
-  wire::put_u64(b, 2 * (u64)c.N);  // NthRoot
+  wire::put_u64(b, c.nthroot);  // NthRoot
   wire::put_u64(b, 0);             // BaseTwoDecomposition
   wire::put_u64(b, (u64)beta);     // Matrix rows
   for (int i = 0; i < beta; ++i) {
@@ -2324,7 +2353,7 @@ int DecodeF64(int pt, double* out, unsigned long n) {
   API_BEGIN
   Context& c = ctx();
   const Plaintext& p = c.pts.get(pt);
-  if (n < (unsigned long)p.poly.B * (c.N / 2)) throw std::runtime_error("output buffer too small");
+  if (n < (unsigned long)p.poly.B * (c.slots)) throw std::runtime_error("output buffer too small");
   std::vector<double> v = c.decode(p);
   memcpy(out, v.data(), v.size() * sizeof(double));
   return 0;
@@ -2358,7 +2387,7 @@ int Decrypt(int ct) {
 void NewEvaluator(void) {
   API_BEGIN
   Context& c = ctx();
-  for (int i = 1; i < c.N / 2; i *= 2) c.gen_galois(c.galois_element(i), c.L - 1);  // evaluator.go:25-31
+  for (int i = 1; i < c.slots; i *= 2) c.gen_galois(c.galois_element(i), c.L - 1);  // evaluator.go:25-31
   API_END_VOID
 }
 void AddRotationKey(int k) {
@@ -2658,7 +2687,7 @@ int GenerateLinearTransform(int* diagIdx, int nIdx, float* data, int nData, int 
   // lineartransform.go:79-88: in "load" mode the diagonals were serialised
   // earlier and arrive through LoadPlaintextDiagonal, so none is encoded here
   const bool load = ioMode && std::string(ioMode) == "load";
-  const int slots = c.N / 2;
+  const int slots = c.slots;
   if (!load && (long)nIdx * slots != (long)nData) throw std::runtime_error("diagonal data length != nIdx * slots");
   if (level < 0 || level >= c.L) throw std::runtime_error("invalid level");
   LinTrans T;
@@ -2776,7 +2805,7 @@ void LoadRotationKey(char* data, unsigned long len, unsigned long galEl) {
   if (!data) throw std::runtime_error("null rotation key data");
   wire::Reader rd(data, len);
   const u64 ge = rd.get_u64(), nth = rd.get_u64(), b2 = rd.get_u64(), rows = rd.get_u64();
-  if (nth != 2 * (u64)c.N) throw std::runtime_error("rotation key: NthRoot does not match the ring");
+  if (nth != c.nthroot) throw std::runtime_error("rotation key: NthRoot does not match the ring");
   if (b2 != 0) throw std::runtime_error("rotation key: power-of-two decomposition is not supported");
   if (ge != galEl) throw std::runtime_error("rotation key: blob is for Galois element " + std::to_string(ge));
   if (rows < 1 || rows > (u64)c.dnum) throw std::runtime_error("rotation key: gadget rows outside 1..dnum");
@@ -2807,7 +2836,7 @@ ArrayResultByte SerializeDiagonal(int tid, int diagIdx) {
   API_BEGIN
   Context& c = ctx();
   LinTrans& T = c.lts.get(tid);
-  const int key = diagIdx & (c.N / 2 - 1);
+  const int key = diagIdx & (c.slots - 1);
   auto it = T.diags.find(key);
   if (it == T.diags.end()) throw std::runtime_error("diagonal " + std::to_string(diagIdx) + " is not loaded");
   std::vector<u64> host;
@@ -2836,7 +2865,7 @@ void LoadPlaintextDiagonal(char* data, unsigned long len, int tid, unsigned long
   get_qp(rd, c, host.data(), T.level + 1, "diagonal");
   if (rd.left()) throw std::runtime_error("diagonal blob has trailing bytes");
   c.upload(p.poly, host);
-  T.diags[(int)diagIdx & (c.N / 2 - 1)] = p;
+  T.diags[(int)diagIdx & (c.slots - 1)] = p;
   T.plan_dirty = true;
   API_END_VOID
 }
@@ -2930,8 +2959,8 @@ ArrayResultDouble GenerateMinimaxSignCoeffs(int* degrees, int n, int prec, int l
 // (Lattigo's sparse circuit leaves replicas there and multiplies by
 // 2^(LogMaxSlots - LogSlots), bootstrapper.go:73-74).
 static void check_slots(const Context& c, int slots) {
-  if (slots < 1 || slots > c.N / 2 || (slots & (slots - 1)))
-    throw std::runtime_error("slots must be a power of two <= " + std::to_string(c.N / 2));
+  if (slots < 1 || slots > c.slots || (slots & (slots - 1)))
+    throw std::runtime_error("slots must be a power of two <= " + std::to_string(c.slots));
 }
 void NewBootstrapper(int* logPs, int n, int slots) {
   API_BEGIN
@@ -3119,7 +3148,7 @@ int GetGaloisKeyLevel(unsigned long galEl) {
 int ExportLinearTransformDiagonal(int tid, int diagIdx, unsigned long* out, unsigned long n) {
   API_BEGIN
   Context& c = ctx();
-  return export_poly(c.lts.get(tid).diags.at(diagIdx & (c.N / 2 - 1)).poly, out, n);
+  return export_poly(c.lts.get(tid).diags.at(diagIdx & (c.slots - 1)).poly, out, n);
   API_END(-1)
 }
 

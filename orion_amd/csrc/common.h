@@ -32,6 +32,12 @@ struct ModConst {
   u64 bar_mu8;  // floor(2^(2k+8) / q), k <= 52           (Barrett for x < 256 q^2)
   u64 ninv, ninv_s;  // N^-1 and its Shoup companion
   double qd, qinv_d, ninv_d;  // float64 path: q, 1/q, centered N^-1
+  // ConjugateInvariant ring (scheme.go:49-52, NthRoot 4N): W = psi^N (a square
+  // root of -1 mod q) and its Shoup companion.  The forward NTT folds its input
+  // b_e = a_e - W a_{N-e} (the expansion reduced mod X^N - W), the inverse
+  // unfolds a_e = (b_e + W b_{N-e}) / 2, with the 1/2 folded into ninv = (2N)^-1.
+  // Zero in a Standard ring.
+  u64 ciw, ciw_s;
 };
 #define ORION_F64_BITS 46
 
@@ -294,6 +300,7 @@ struct NttIO {
                 // 2 = image fastest, then component, limbs in the order lord[] (slow integer-path limbs first)
   int jobs;     // ncomp * nlimb * nbatch of dst
   int pro, epi;
+  int ci;       // ConjugateInvariant ring: the forward folds its input, the inverse unfolds its output (ModConst::ciw)
   // two-pass kernels, chunked: this launch covers jobs [job0, job0 + njob) and
   // mid is a compact scratch of njob rows (row = job - job0), reused by every
   // chunk so the intermediate can stay in the Infinity Cache

@@ -119,9 +119,12 @@ __global__ void enc_load_kernel(const float* __restrict__ vals, int nvals, doubl
 // coefficient i of image b: bit-reversed FFT output times 1/n, then
 // round(|x| * scale) -> residues (negated for x < 0).  |x| * scale >= 2^64 is
 // an exact integer mant * 2^e and is reduced exactly (Lattigo's big.Int path).
+// Standard ring: N = 2n coefficients, real parts then imaginary parts; CI ring:
+// N = n coefficients, the real parts (the imaginary parts are the degree-2N
+// expansion's upper half, which the CI ring does not store).
 __global__ void enc_crt_kernel(const double2* __restrict__ v, LimbSet out, double scale, double inv_n, int logn,
-                               const DeviceTables* __restrict__ tb) {
-  const int n = 1 << logn, N = 2 * n;
+                               int ci, const DeviceTables* __restrict__ tb) {
+  const int n = 1 << logn, N = ci ? n : 2 * n;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
   const int b = blockIdx.y;
@@ -160,9 +163,11 @@ __global__ void enc_crt_kernel(const double2* __restrict__ v, LimbSet out, doubl
 // bit-reversed slot position of the forward FFT.
 //   garner[j * nl + k] = (q_k mod q_j)^-1 mod q_j (k < j); garner[nl * nl + j]
 //   = mixed-radix digit j of floor((Q - 1) / 2).
-__global__ void dec_crt_kernel(LimbSet x, const u64* __restrict__ garner, double scale, int logn,
+//   CI ring (N = n): slot input j is a_j - i a_{N-j} (a_0 real), so coefficient
+//   i is the real part at slot i and, negated, the imaginary part at slot N - i
+__global__ void dec_crt_kernel(LimbSet x, const u64* __restrict__ garner, double scale, int logn, int ci,
                                double2* __restrict__ v, const DeviceTables* __restrict__ tb) {
-  const int n = 1 << logn, N = 2 * n;
+  const int n = 1 << logn, N = ci ? n : 2 * n;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
   const int b = blockIdx.y, nl = x.nlimb;
@@ -220,7 +225,13 @@ __global__ void dec_crt_kernel(LimbSet x, const u64* __restrict__ garner, double
   }
   if (greater) f = -f;
   f = f / scale;
-  double* dst = reinterpret_cast<double*>(v + (size_t)b * n + brev(i & (n - 1), logn));
+  double2* const vb = v + (size_t)b * n;
+  if (ci) {
+    reinterpret_cast<double*>(vb + brev(i, logn))[0] = f;
+    reinterpret_cast<double*>(vb + brev((n - i) & (n - 1), logn))[1] = i ? -f : 0.0;
+    return;
+  }
+  double* dst = reinterpret_cast<double*>(vb + brev(i & (n - 1), logn));
   dst[i < n ? 0 : 1] = f;
 }
 
@@ -336,20 +347,22 @@ static int fft_run(double2* v, const double2* tw, int logn, int B, bool inverse,
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int orion_launch_encode(const float* vals, int nvals, int B, double2* v, const double2* tw_inv, int logn,
+// logn: log2 of the slot count (N/2 Standard, N ConjugateInvariant)
+int orion_launch_encode(const float* vals, int nvals, int B, double2* v, const double2* tw_inv, int logn, bool ci,
                         const LimbSet& out, double scale, const DeviceTables* tb, hipStream_t st) {
-  const int n = 1 << logn;
+  const int n = 1 << logn, N = ci ? n : 2 * n;
   enc_load_kernel<<<dim3((unsigned)((n + 255) / 256), (unsigned)B), 256, 0, st>>>(vals, nvals, v, n);
   if (fft_run(v, tw_inv, logn, B, true, st)) return -1;
-  enc_crt_kernel<<<dim3((unsigned)((2 * n + 255) / 256), (unsigned)B), 256, 0, st>>>(v, out, scale, 1.0 / (double)n,
-                                                                                    logn, tb);
+  enc_crt_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)B), 256, 0, st>>>(v, out, scale, 1.0 / (double)n,
+                                                                                logn, ci ? 1 : 0, tb);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int orion_launch_decode(const LimbSet& x, const u64* garner, double scale, int logn, double2* v,
+int orion_launch_decode(const LimbSet& x, const u64* garner, double scale, int logn, bool ci, double2* v,
                         const double2* tw_fwd, double* out, const DeviceTables* tb, hipStream_t st) {
-  const int n = 1 << logn, B = x.nbatch;
-  dec_crt_kernel<<<dim3((unsigned)((2 * n + 255) / 256), (unsigned)B), 256, 0, st>>>(x, garner, scale, logn, v, tb);
+  const int n = 1 << logn, B = x.nbatch, N = ci ? n : 2 * n;
+  dec_crt_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)B), 256, 0, st>>>(x, garner, scale, logn, ci ? 1 : 0,
+                                                                                v, tb);
   if (fft_run(v, tw_fwd, logn, B, false, st)) return -1;
   const size_t total = (size_t)B * n;
   dec_out_kernel<<<(unsigned)((total + 255) / 256), 256, 0, st>>>(v, out, total);
@@ -357,12 +370,12 @@ int orion_launch_decode(const LimbSet& x, const u64* garner, double scale, int l
 }
 
 // complex slots already in v ([B][n] double2, overwritten): FFT + CRT (no load step)
-int orion_launch_encode_c(double2* v, int B, const double2* tw_inv, int logn, const LimbSet& out, double scale,
-                          const DeviceTables* tb, hipStream_t st) {
-  const int n = 1 << logn;
+int orion_launch_encode_c(double2* v, int B, const double2* tw_inv, int logn, bool ci, const LimbSet& out,
+                          double scale, const DeviceTables* tb, hipStream_t st) {
+  const int n = 1 << logn, N = ci ? n : 2 * n;
   if (fft_run(v, tw_inv, logn, B, true, st)) return -1;
-  enc_crt_kernel<<<dim3((unsigned)((2 * n + 255) / 256), (unsigned)B), 256, 0, st>>>(v, out, scale, 1.0 / (double)n,
-                                                                                    logn, tb);
+  enc_crt_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)B), 256, 0, st>>>(v, out, scale, 1.0 / (double)n,
+                                                                                logn, ci ? 1 : 0, tb);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -258,10 +258,19 @@ __device__ __forceinline__ void reduce_all(typename A::T (&a)[32], const A& ar) 
 // Round windows: LOGN=15 -> bits [10,15), [5,10), [0,5); LOGN=14 -> [9,14),[4,9),[0,5)
 // (last round only bits 3..0); LOGN=13 -> [8,13),[3,8),[0,5) (bits 2..0).
 // Thread t loads / stores element t + (k << B0) (k < 32): fully coalesced.
-template <class A, int LOGN, int PRO, int EPI>
+// ConjugateInvariant fold (CI): b_e = a_e - W a_{N-e}, b_0 = a_0 (the ring
+// element's degree-2N expansion reduced mod X^N - W, W = psi^N; oracle_ntt).
+// Thread t's element e = t + k S (S = N/32) pairs with N - e = (S - t) + (31 - k) S,
+// held at the same offsets of the mirrored thread, so the partner is one more
+// coalesced (descending) load of the same limb, served by L2.
+__device__ __forceinline__ u64 ci_fold(u64 x, u64 y, const ModConst& mc) {
+  return sub_mod(x, shoup_mul(y, mc.ciw, mc.ciw_s, mc.q), mc.q);
+}
+
+template <class A, int LOGN, int PRO, int EPI, bool CI>
 __device__ __forceinline__ void ntt_fwd_body(const NttIO& io, int c, int l, int b, const ModConst& mc, const A& ar,
                                              __amdgpu_buffer_rsrc_t w, u32* lds, const DeviceTables* __restrict__ tb) {
-  constexpr int N = 1 << LOGN, B0 = LOGN - 5, B1 = LOGN - 10;
+  constexpr int N = 1 << LOGN, B0 = LOGN - 5, B1 = LOGN - 10, S = NttGeom<LOGN>::T;
   // an opaque copy of the thread index per job: keeps the persistent job loop
   // from hoisting every thread-derived address out of the loop (LICM), whose
   // live ranges would then span the whole body and spill
@@ -270,16 +279,32 @@ __device__ __forceinline__ void ntt_fwd_body(const NttIO& io, int c, int l, int 
   typename A::T a[32];
   if constexpr (PRO == NTT_PRO_LOAD) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.src, c, l, b), 0, N * 8, 0x00020000);
+    if constexpr (CI) {
 #pragma unroll
-    for (int k = 0; k < 32; ++k) a[k] = ar.from_u64(buf_ld(rs, t * 8, (k << B0) * 8));
+      for (int k = 0; k < 32; ++k) {
+        const u64 x = buf_ld(rs, t * 8, (k << B0) * 8);
+        u64 y = buf_ld(rs, (S - t) * 8, ((31 - k) << B0) * 8);  // e = 0: offset N, outside the descriptor
+        if (k == 0) y = t == 0 ? 0 : y;
+        a[k] = ar.from_u64(ci_fold(x, y, mc));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 32; ++k) a[k] = ar.from_u64(buf_ld(rs, t * 8, (k << B0) * 8));
+    }
   } else {  // NTT_PRO_RESCALE (DivRoundByLastModulusNTT), fused with the NTT of every other limb
     const u64* sp = row_ptr(io.src, c, 0, b);
     const u64 qL = tb->mc[io.modL].q, h = qL >> 1;
     const u64 hm = barrett128(0, h, mc);
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
-      const u64 x = sp[t + (k << B0)];
-      a[k] = ar.from_u64(sub_mod(barrett128(0, add_mod(x, h, qL), mc), hm, mc.q));
+      const u64 x = sub_mod(barrett128(0, add_mod(sp[t + (k << B0)], h, qL), mc), hm, mc.q);
+      if constexpr (CI) {
+        u64 y = sub_mod(barrett128(0, add_mod(sp[(N - t - (k << B0)) & (N - 1)], h, qL), mc), hm, mc.q);
+        if (k == 0) y = t == 0 ? 0 : y;
+        a[k] = ar.from_u64(ci_fold(x, y, mc));
+      } else {
+        a[k] = ar.from_u64(x);
+      }
     }
   }
   // CT growth is additive (|t| < 2q per stage): from [0, q) the values stay
@@ -338,8 +363,8 @@ __device__ __forceinline__ void ntt_fwd_body(const NttIO& io, int c, int l, int 
   }
 }
 
-template <class A, int LOGN>
-__device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int b, const A& ar,
+template <class A, int LOGN, bool CI>
+__device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int b, const ModConst& mc, const A& ar,
                                              __amdgpu_buffer_rsrc_t w, u32* lds) {
   constexpr int N = 1 << LOGN, B0 = LOGN - 5, B1 = LOGN - 10;
   // an opaque copy of the thread index per job: keeps the persistent job loop
@@ -373,6 +398,43 @@ __device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int 
   xchg<typename A::T, LOGN, B1, B0>(a, lds, t);
   inv_round<A, LOGN, B0, B0, LOGN - 1>(a, ar, w, t);
   const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.dst, c, l, b), 0, N * 8, 0x00020000);
+  if constexpr (CI) {
+    // ConjugateInvariant unfold: a_e = b_e + W b_{N-e} with b already scaled by
+    // (2N)^-1 (ninv), a_0 = 2 b_0.  The partner of row k of thread t is row
+    // 31 - k of thread S - t (t = 0: row 32 - k of thread 0), so each half of
+    // the rows is finished against the other half staged in LDS as u64
+    // (16 S words = 4N bytes, inside the exchange buffer): rows 16..31 against
+    // rows 0..15, then rows 0..15 against rows 16..31.
+    constexpr int S = NttGeom<LOGN>::T;
+    u64* const l64 = reinterpret_cast<u64*>(lds);
+    u64 r[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) r[k] = ar.final_inv(a[k]);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) l64[k * S + t] = r[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 16; k < 32; ++k) {
+      u64 y = l64[(32 - k) * S - t];  // k = 16, t = 0: e = N/2 pairs with itself
+      if (k == 16) y = t == 0 ? r[16] : y;
+      buf_st(rd, add_mod(r[k], shoup_mul(y, mc.ciw, mc.ciw_s, mc.q), mc.q), t * 8, (k << B0) * 8);
+      if ((k & 3) == 3) NTT_FENCE();
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 16; k < 32; ++k) l64[(k - 16) * S + t] = r[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const u64 y = l64[(16 - k) * S - t];  // k = 0, t = 0: e = 0, no partner
+      u64 v = add_mod(r[k], shoup_mul(y, mc.ciw, mc.ciw_s, mc.q), mc.q);
+      if (k == 0) v = t == 0 ? add_mod(r[0], r[0], mc.q) : v;
+      buf_st(rd, v, t * 8, (k << B0) * 8);
+      if ((k & 3) == 3) NTT_FENCE();
+    }
+    __syncthreads();  // the next job of a persistent workgroup writes LDS in its first exchange
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
     buf_st(rd, ar.final_inv(a[k]), t * 8, (k << B0) * 8);
@@ -394,7 +456,7 @@ struct FwdPersist {
   static constexpr bool value = EPI == NTT_EPI_STORE;
 };
 
-template <int LOGN, int PRO, int EPI>
+template <int LOGN, int PRO, int EPI, bool CI>
 __device__ __forceinline__ void ntt_fwd_job(const NttIO& io, int job, const DeviceTables* __restrict__ tb, u32* lds) {
   constexpr int N = 1 << LOGN;
   int c, l, b;
@@ -403,25 +465,25 @@ __device__ __forceinline__ void ntt_fwd_job(const NttIO& io, int job, const Devi
   const ModConst mc = tb->mc[mod];
   if (mc.f64) {
     const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd_d[mod], 0, N * 8, 0x00020000);
-    ntt_fwd_body<F64Arith, LOGN, PRO, EPI>(io, c, l, b, mc, F64Arith(mc), w, lds, tb);
+    ntt_fwd_body<F64Arith, LOGN, PRO, EPI, CI>(io, c, l, b, mc, F64Arith(mc), w, lds, tb);
   } else {
     const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd[mod], 0, N * 16, 0x00020000);
-    ntt_fwd_body<IntArith, LOGN, PRO, EPI>(io, c, l, b, mc, IntArith(mc), w, lds, tb);
+    ntt_fwd_body<IntArith, LOGN, PRO, EPI, CI>(io, c, l, b, mc, IntArith(mc), w, lds, tb);
   }
 }
 
-template <int LOGN, int PRO, int EPI>
+template <int LOGN, int PRO, int EPI, bool CI>
 __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_fwd_kernel(NttIO io, const DeviceTables* __restrict__ tb) {
   extern __shared__ u32 lds[];
   if constexpr (FwdPersist<EPI>::value) {
 #pragma nounroll
-    for (int job = blockIdx.x; job < io.jobs; job += gridDim.x) ntt_fwd_job<LOGN, PRO, EPI>(io, job, tb, lds);
+    for (int job = blockIdx.x; job < io.jobs; job += gridDim.x) ntt_fwd_job<LOGN, PRO, EPI, CI>(io, job, tb, lds);
   } else {
-    ntt_fwd_job<LOGN, PRO, EPI>(io, blockIdx.x, tb, lds);
+    ntt_fwd_job<LOGN, PRO, EPI, CI>(io, blockIdx.x, tb, lds);
   }
 }
 
-template <int LOGN>
+template <int LOGN, bool CI>
 __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_inv_kernel(NttIO io, const DeviceTables* __restrict__ tb) {
   constexpr int N = 1 << LOGN;
   extern __shared__ u32 lds[];
@@ -433,25 +495,25 @@ __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_inv_kernel(NttIO io, con
     const ModConst mc = tb->mc[mod];
     if (mc.f64) {
       const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->inv_d[mod], 0, N * 8, 0x00020000);
-      ntt_inv_body<F64Arith, LOGN>(io, c, l, b, F64Arith(mc), w, lds);
+      ntt_inv_body<F64Arith, LOGN, CI>(io, c, l, b, mc, F64Arith(mc), w, lds);
     } else {
       const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->inv[mod], 0, N * 16, 0x00020000);
-      ntt_inv_body<IntArith, LOGN>(io, c, l, b, IntArith(mc), w, lds);
+      ntt_inv_body<IntArith, LOGN, CI>(io, c, l, b, mc, IntArith(mc), w, lds);
     }
   }
 }
 
-template <int LOGN, int PRO, int EPI>
+template <int LOGN, int PRO, int EPI, bool CI>
 void set_lds_attr() {
-  hipFuncSetAttribute((const void*)ntt_fwd_kernel<LOGN, PRO, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  hipFuncSetAttribute((const void*)ntt_fwd_kernel<LOGN, PRO, EPI, CI>, hipFuncAttributeMaxDynamicSharedMemorySize,
                       ((1 << LOGN) + (1 << LOGN) / 32) * 4);
 }
 
 // workgroups of a persistent launch (0: one workgroup per job); set by orion_ntt_init
 int g_ntt_grid = 0;
 
-template <int LOGN>
-int launch_ntt(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
+template <int LOGN, bool CI>
+int launch_ntt_ring(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
   constexpr int N = 1 << LOGN;
   const int jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
   if (jobs == 0) return 0;
@@ -460,12 +522,12 @@ int launch_ntt(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_
   const dim3 g(g_ntt_grid > 0 && jobs > g_ntt_grid ? g_ntt_grid : jobs), blk(NttGeom<LOGN>::T);
   if (inverse) {
     if (io.pro != NTT_PRO_LOAD || io.epi != NTT_EPI_STORE) return -1;
-    hipLaunchKernelGGL(ntt_inv_kernel<LOGN>, g, blk, lds, st, io, tb);
+    hipLaunchKernelGGL((ntt_inv_kernel<LOGN, CI>), g, blk, lds, st, io, tb);
     return 0;
   }
 #define FWD(P, E)                                                                                     \
   if (io.pro == P && io.epi == E) {                                                                   \
-    hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, P, E>), FwdPersist<E>::value ? g : dim3(jobs), blk, lds, st, io, tb); \
+    hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, P, E, CI>), FwdPersist<E>::value ? g : dim3(jobs), blk, lds, st, io, tb); \
     return 0;                                                                                         \
   }
   FWD(NTT_PRO_LOAD, NTT_EPI_STORE)
@@ -476,12 +538,22 @@ int launch_ntt(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_
 }
 
 template <int LOGN>
-void init_lds() {
-  set_lds_attr<LOGN, NTT_PRO_LOAD, NTT_EPI_STORE>();
-  set_lds_attr<LOGN, NTT_PRO_LOAD, NTT_EPI_SUBSCALE>();
-  set_lds_attr<LOGN, NTT_PRO_RESCALE, NTT_EPI_SUBSCALE>();
-  hipFuncSetAttribute((const void*)ntt_inv_kernel<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+int launch_ntt(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
+  return io.ci ? launch_ntt_ring<LOGN, true>(io, tb, inverse, st) : launch_ntt_ring<LOGN, false>(io, tb, inverse, st);
+}
+
+template <int LOGN, bool CI>
+void init_lds_ring() {
+  set_lds_attr<LOGN, NTT_PRO_LOAD, NTT_EPI_STORE, CI>();
+  set_lds_attr<LOGN, NTT_PRO_LOAD, NTT_EPI_SUBSCALE, CI>();
+  set_lds_attr<LOGN, NTT_PRO_RESCALE, NTT_EPI_SUBSCALE, CI>();
+  hipFuncSetAttribute((const void*)ntt_inv_kernel<LOGN, CI>, hipFuncAttributeMaxDynamicSharedMemorySize,
                       ((1 << LOGN) + (1 << LOGN) / 32) * 4);
+}
+template <int LOGN>
+void init_lds() {
+  init_lds_ring<LOGN, false>();
+  init_lds_ring<LOGN, true>();
 }
 
 }  // namespace

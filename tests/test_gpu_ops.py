@@ -211,13 +211,14 @@ def test_mlp_n14_matches_cpu_oracle_replay(torch_cuda):
 def test_mlp_conjugate_invariant_config(torch_cuda):
     """The reference's own tests/configs/mlp.yml (ConjugateInvariant ring,
     N=2^13, 8192 real slots, [29]+[26]x5 / [29,29], H=8192): the frontend's op
-    stream for it runs through the C-ABI (as the conjugation-fixed subring of
-    the degree-2^14 Standard ring), bit for bit against the CPU oracle, and
-    decrypts within the reference's MAE gate (tests/models/test_mlp.py:48)."""
+    stream for it runs through the C-ABI on the native CI ring (8192
+    coefficients per limb, NthRoot 2^15), bit for bit against the CPU oracle's
+    CI ring, and decrypts within the reference's MAE gate
+    (tests/models/test_mlp.py:48)."""
     from orion_amd.backend import HipLibrary
     lib = HipLibrary().new_scheme(13, [29] + [26] * 5, [29, 29], 26, h=8192, ringtype="ConjugateInvariant", seed=5,
                                   device=0)
-    assert lib.N == 1 << 14 and int(lib.OrionHipLogN()) == 14
+    assert lib.N == 1 << 13 and lib.slots == 1 << 13 and int(lib.OrionHipLogN()) == 13
     for q in lib.moduli():
         assert q % (4 << 13) == 1  # NthRoot = 4N for the CI ring
     lib.DeleteScheme()

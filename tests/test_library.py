@@ -107,12 +107,12 @@ def test_lattigo_style_conversions(libpath):
 def test_ring_type_contract(libpath):
     """scheme.go:50-51 accepts "standard" and (any other string as)
     ConjugateInvariant; this backend names the two it supports and rejects
-    the rest, and a CI ring of degree 2^16 (run as a 2^17 Standard ring)
-    with an error string instead of an abort.  Both checks run before any
+    the rest, and a CI ring of degree 2^16 (its fold/unfold runs in the
+    one-limb-per-CU NTT, N <= 2^15) with an error string instead of an abort.  Both checks run before any
     device call, so they hold on a CPU-only host."""
     from orion_amd.backend import HipLibrary
     lib = HipLibrary()
     with pytest.raises(RuntimeError, match="unknown ring type"):
         lib.NewScheme(13, [29, 26], [29], 26, 192, "Bogus", "", "none")
-    with pytest.raises(RuntimeError, match="max 2\\^16"):
+    with pytest.raises(RuntimeError, match="logN must be 13..15"):
         lib.NewScheme(16, [60, 40], [60], 40, 192, "ConjugateInvariant", "", "none")
