@@ -154,7 +154,16 @@ void OrionHipSetSeed(unsigned long seed);                /* keygen / encryption 
 void OrionHipSetStream(void *hipStream);                  /* NULL = library-owned stream */
 void *OrionHipGetStream(void);
 int OrionHipSynchronize(void);
-int OrionHipLogN(void);                                   /* ring degree in use: logN + 1 for ConjugateInvariant */
+/* hipGraph capture of an op stream issued through this ABI: every call between
+ * Begin and End is recorded into one graph (returned id), which Launch replays
+ * on the library stream with one launch, into the same buffers (the pool pins
+ * them until Destroy).  The captured calls must not need a synchronisation:
+ * run the stream once before capturing it (keys, tables, LT plans). */
+int OrionHipGraphBegin(void);
+int OrionHipGraphEnd(void);                               /* graph id, or -1 */
+int OrionHipGraphLaunch(int graph);
+void OrionHipGraphDestroy(int graph);
+int OrionHipLogN(void);                                   /* log2 of the ring degree N (coefficients per limb) */
 int OrionHipNumQ(void);
 int OrionHipNumP(void);
 unsigned long OrionHipModulus(int idx);                   /* QP index space */

@@ -139,6 +139,10 @@ SIGNATURES = {
     "OrionHipSetStream": ([c_void_p], None),
     "OrionHipGetStream": ([], c_void_p),
     "OrionHipSynchronize": ([], c_int),
+    "OrionHipGraphBegin": ([], c_int),
+    "OrionHipGraphEnd": ([], c_int),
+    "OrionHipGraphLaunch": ([c_int], c_int),
+    "OrionHipGraphDestroy": ([c_int], None),
     "OrionHipLogN": ([], c_int),
     "OrionHipNumQ": ([], c_int),
     "OrionHipNumP": ([], c_int),

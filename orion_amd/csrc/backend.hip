@@ -74,34 +74,88 @@ static thread_local std::string g_last_error;
 // ---------------------------------------------------------------------------
 // device memory: size-class cache (no hipMalloc/hipFree on the op path)
 // ---------------------------------------------------------------------------
+// A captured hipGraph replays into the buffers its capture used, so every
+// buffer handed out while capturing is pinned for the graph's lifetime: a
+// pinned buffer that is released is parked instead of returning to the free
+// lists, and nothing allocated later can alias a graph's temporaries.
 class DevicePool {
  public:
   void* alloc(size_t bytes) {
+    void* p = nullptr;
     auto it = free_.find(bytes);
     if (it != free_.end() && !it->second.empty()) {
-      void* p = it->second.back();
+      p = it->second.back();
       it->second.pop_back();
-      return p;
+    } else {
+      hipError_t e = hipMalloc(&p, bytes);
+      if (e != hipSuccess) {  // release the cache once and retry (not while capturing: trim synchronises)
+        if (tracking_) throw std::runtime_error("device memory exhausted during graph capture");
+        trim();
+        HIPCHK(hipMalloc(&p, bytes));
+      }
     }
-    void* p = nullptr;
-    hipError_t e = hipMalloc(&p, bytes);
-    if (e != hipSuccess) {  // release the cache once and retry
-      trim();
-      HIPCHK(hipMalloc(&p, bytes));
-    }
+    if (tracking_) touched_[p] = bytes;
     return p;
   }
-  void release(void* p, size_t bytes) { free_[bytes].push_back(p); }
+  void release(void* p, size_t bytes) {
+    if (pins_.count(p))
+      parked_[p] = bytes;
+    else
+      free_[bytes].push_back(p);
+  }
   void trim() {
     hipDeviceSynchronize();
     for (auto& kv : free_)
       for (void* p : kv.second) hipFree(p);
     free_.clear();
   }
-  ~DevicePool() { trim(); }
+  // graph capture: record every buffer handed out until end_track()
+  void begin_track() {
+    touched_.clear();
+    tracking_ = true;
+  }
+  std::vector<std::pair<void*, size_t>> end_track() {
+    tracking_ = false;
+    std::vector<std::pair<void*, size_t>> v(touched_.begin(), touched_.end());
+    touched_.clear();
+    return v;
+  }
+  void pin(const std::vector<std::pair<void*, size_t>>& v) {
+    for (auto& pb : v) {
+      if (pins_[pb.first]++) continue;
+      auto& fl = free_[pb.second];  // released during the capture: park it
+      for (size_t i = 0; i < fl.size(); ++i)
+        if (fl[i] == pb.first) {
+          fl[i] = fl.back();
+          fl.pop_back();
+          parked_[pb.first] = pb.second;
+          break;
+        }
+    }
+  }
+  void unpin(const std::vector<std::pair<void*, size_t>>& v) {
+    for (auto& pb : v) {
+      auto it = pins_.find(pb.first);
+      if (it == pins_.end() || --it->second > 0) continue;
+      pins_.erase(it);
+      auto pk = parked_.find(pb.first);
+      if (pk != parked_.end()) {
+        free_[pk->second].push_back(pk->first);
+        parked_.erase(pk);
+      }
+    }
+  }
+  ~DevicePool() {
+    for (auto& kv : parked_) free_[kv.second].push_back(kv.first);
+    parked_.clear();
+    trim();
+  }
 
  private:
   std::unordered_map<size_t, std::vector<void*>> free_;
+  bool tracking_ = false;
+  std::unordered_map<void*, size_t> touched_, parked_;
+  std::unordered_map<void*, int> pins_;
 };
 
 struct Buffer {
@@ -263,6 +317,17 @@ struct Context {
   HandlePool<Ciphertext> cts;
   HandlePool<LinTrans> lts;
 
+  // hipGraphs captured from the library stream (OrionHipGraphBegin/End)
+  struct GraphRec {
+    hipGraph_t g = nullptr;
+    hipGraphExec_t x = nullptr;
+    std::vector<std::pair<void*, size_t>> pins;
+  };
+  std::map<int, GraphRec> graphs;
+  int next_graph = 0;
+  bool capturing = false;
+  unsigned prof_saved = 0;
+
   unsigned prof = 0;  // bit mask of profiled kernel categories
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> ev_free;
@@ -270,6 +335,16 @@ struct Context {
 
   ~Context() {
     hipDeviceSynchronize();
+    if (capturing) {
+      hipGraph_t gr = nullptr;
+      hipStreamEndCapture(stream, &gr);
+      if (gr) hipGraphDestroy(gr);
+    }
+    for (auto& kv : graphs) {
+      hipGraphExecDestroy(kv.second.x);
+      hipGraphDestroy(kv.second.g);
+    }
+    graphs.clear();
     gks.clear();
     sk = pk = rlk = Poly();
     pts.reset();
@@ -333,6 +408,85 @@ struct Context {
       ev_free.push_back(r.e1);
     }
     prof_recs.clear();
+  }
+
+  // -- graph capture ---------------------------------------------------------------
+  // Every op issued between graph_begin and graph_end is recorded (not run)
+  // into one hipGraph; a replay re-runs all its kernels on the library stream
+  // with one launch.  The captured ops must not synchronise (keys, tables and
+  // LT plans are made by a warm-up pass first); profiling is off meanwhile.
+  void graph_begin() {
+    if (capturing) throw std::runtime_error("a graph capture is already open");
+    HIPCHK(hipStreamSynchronize(stream));
+    prof_flush();
+    prof_saved = prof;
+    prof = 0;
+    pool.begin_track();
+    HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
+    capturing = true;
+  }
+  int graph_end() {
+    if (!capturing) throw std::runtime_error("no graph capture is open");
+    capturing = false;
+    prof = prof_saved;
+    hipGraph_t gr = nullptr;
+    const hipError_t e = hipStreamEndCapture(stream, &gr);
+    auto touched = pool.end_track();
+    if (e != hipSuccess || !gr) {
+      if (gr) hipGraphDestroy(gr);
+      // an invalidated capture leaves its stream unusable: end whatever is
+      // still open and, for the library's own stream, start a fresh one
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+        hipGraph_t g2 = nullptr;
+        hipStreamEndCapture(stream, &g2);
+        if (g2) hipGraphDestroy(g2);
+      }
+      (void)hipGetLastError();
+      if (own_stream) {
+        hipStreamDestroy(stream);
+        HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+      }
+      throw std::runtime_error(std::string("graph capture failed (an op synchronised or left the stream?): ") +
+                               hipGetErrorString(e));
+    }
+    GraphRec r;
+    r.g = gr;
+    const hipError_t ei = hipGraphInstantiate(&r.x, gr, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+      hipGraphDestroy(gr);
+      throw std::runtime_error(std::string("graph instantiation failed: ") + hipGetErrorString(ei));
+    }
+    pool.pin(touched);
+    r.pins = std::move(touched);
+    const int id = next_graph++;
+    graphs[id] = std::move(r);
+    return id;
+  }
+  void graph_launch(int id) {
+    auto it = graphs.find(id);
+    if (it == graphs.end()) throw std::runtime_error("graph not found: " + std::to_string(id));
+    if (capturing) throw std::runtime_error("graph launch while capturing");
+    HIPCHK(hipGraphLaunch(it->second.x, stream));
+  }
+  void graph_destroy(int id) {
+    auto it = graphs.find(id);
+    if (it == graphs.end()) return;
+    HIPCHK(hipStreamSynchronize(stream));
+    hipGraphExecDestroy(it->second.x);
+    hipGraphDestroy(it->second.g);
+    pool.unpin(it->second.pins);
+    graphs.erase(it);
+  }
+
+  // lazily built tables, keys and host transfers synchronise, which would
+  // invalidate an open capture (and leave HIP's stream state unusable): refuse
+  // them first
+  void no_capture(const char* what) const {
+    if (capturing)
+      throw std::runtime_error(std::string(what) +
+                               " needs a host synchronisation, not allowed while capturing a graph (run the op "
+                               "stream once before capturing it)");
   }
 
   // -- allocation --------------------------------------------------------------
@@ -434,16 +588,24 @@ struct Context {
   // rule; 2: every forward launch that needs no scratch (not an in-place tail)
   int ntt2_tail_fwd = getenv("ORION_NTT2_TAIL_FWD") ? atoi(getenv("ORION_NTT2_TAIL_FWD")) : 1;
   int n_cu = 0;
-  bool ntt2_tail(int jobs) {
-    if (jobs > ntt2_tail_max || ntt2_tail_eff <= 0) return false;
+  int cus() {
     if (n_cu == 0) {
       int dev = 0;
       HIPCHK(hipGetDevice(&dev));
       HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
     }
+    return n_cu;
+  }
+  bool ntt2_tail(int jobs) {
+    if (jobs > ntt2_tail_max || ntt2_tail_eff <= 0) return false;
+    cus();
     const int rounds = (jobs + n_cu - 1) / n_cu;
     return (double)jobs / ((double)rounds * n_cu) < ntt2_tail_eff;
   }
+  // timing switches: s_sleep(127) iterations (~3.4 us each) before the first
+  // job of every other CU in persistent launches of >= ntt_stagger_min rounds
+  int ntt_stagger = getenv("ORION_NTT_STAGGER") ? atoi(getenv("ORION_NTT_STAGGER")) : 0;
+  int ntt_stagger_min = getenv("ORION_NTT_STAGGER_MIN") ? atoi(getenv("ORION_NTT_STAGGER_MIN")) : 2;
   void ntt_io(NttIO io, bool inv) {
     io.order = ntt_order;
     io.ci = ci ? 1 : 0;
@@ -482,6 +644,9 @@ struct Context {
       Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, per * io.jobs);
       if (orion_launch_ntt2(logN, io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
       return;
+    }
+    if (ntt_stagger > 0) {
+      io.stagger = io.jobs >= ntt_stagger_min * cus() ? ntt_stagger : 0;
     }
     // algorithmic bytes per limb-transform: read + write the limb (16 N), + 8 N
     // for the epilogue's second operand
@@ -699,6 +864,7 @@ struct Context {
   }
 
   BasisExtTable* make_betab(const std::vector<int>& src, const std::vector<int>& dst) {
+    no_capture("a basis extension table");
     BasisExtTable T;
     memset(&T, 0, sizeof(T));
     T.ns = (int)src.size();
@@ -753,6 +919,7 @@ struct Context {
   BasisExtTable* const* modup_tabs(int level) {
     auto it = modup_arr.find(level);
     if (it != modup_arr.end()) return it->second;
+    no_capture("the ModUp table array");
     const int beta = (level + 1 + K - 1) / K;
     std::vector<BasisExtTable*> h;
     std::vector<int> tpos;
@@ -780,6 +947,7 @@ struct Context {
   const u32* aut_index(u64 g) {
     auto it = autidx.find(g);
     if (it != autidx.end()) return it->second;
+    no_capture("an automorphism index table");
     // CI: the index over the degree-2N NTT; the ring keeps its first half,
     // which every g = 5^k (= 1 mod 4) maps onto itself
     std::vector<u32> idx(N);
@@ -805,10 +973,12 @@ struct Context {
 
   // -- upload of host residues (coefficient domain) + NTT -------------------------------
   void upload(const Poly& P, const std::vector<u64>& host) {
+    no_capture("a host upload");
     HIPCHK(hipMemcpyAsync(P.ptr(), host.data(), host.size() * sizeof(u64), hipMemcpyHostToDevice, stream));
     HIPCHK(hipStreamSynchronize(stream));
   }
   void download(const Poly& P, std::vector<u64>& host) {
+    no_capture("a host download");
     host.resize((size_t)P.ncomp * P.nlimb * P.B * N);
     HIPCHK(hipMemcpyAsync(host.data(), P.ptr(), host.size() * sizeof(u64), hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
@@ -887,6 +1057,7 @@ struct Context {
   // layout [beta][2][level+1+K][N] (beta = ceil((level+1)/K) digits); a
   // full-chain key (level L - 1) is [dnum][2][L+K][N]
   Poly gen_evk(const Poly& s_in, const Poly& s_out, int level) {
+    no_capture("evaluation key generation");
     const int beta = (level + 1 + K - 1) / K, nl = level + 1 + K;
     const std::vector<int> md = key_mods(level), kp = iota(0, nl);
     Poly k = alloc(2 * beta, nl, 1);
@@ -1222,6 +1393,7 @@ struct Context {
   // device plan of a BSGS transform: register slot of each baby, giant order,
   // and the diagonal plane of every (giant, slot) term
   void build_plan(LinTrans& T) {
+    no_capture("building a linear transform's BSGS plan");
     T.slots.clear();
     T.gorder.clear();
     bool b0 = false, g0 = false;
@@ -1442,6 +1614,7 @@ struct Context {
   const u64* garner_table(int level) {
     auto it = garner.find(level);
     if (it != garner.end()) return it->second;
+    no_capture("a decode CRT table");
     const int nl = level + 1;
     std::vector<u64> t((size_t)nl * nl + nl, 0);
     for (int j = 0; j < nl; ++j)
@@ -2008,9 +2181,29 @@ using namespace orion;
 // ---------------------------------------------------------------------------
 // C-ABI
 // ---------------------------------------------------------------------------
+// C-ABI calls that only enqueue device work (or read host metadata) may be
+// recorded into a graph; every other call is refused while a capture is open
+static bool capture_ok(const char* fn) {
+  static const std::set<std::string> ok = {
+      "Negate", "Rotate", "RotateNew", "Rescale", "RescaleNew", "ModDropCiphertext", "AddScalar", "AddScalarNew",
+      "SubScalar", "SubScalarNew", "MulScalarInt", "MulScalarIntNew", "MulScalarFloat", "MulScalarFloatNew",
+      "AddPlaintext", "AddPlaintextNew", "SubPlaintext", "SubPlaintextNew", "MulPlaintext", "MulPlaintextNew",
+      "AddCiphertext", "AddCiphertextNew", "SubCiphertext", "SubCiphertextNew", "MulRelinCiphertext",
+      "MulRelinCiphertextNew", "EvaluateLinearTransform", "EvaluatePolynomial", "CloneCiphertext",
+      "DeleteCiphertext", "DeletePlaintext", "SetCiphertextScale", "SetPlaintextScale", "GetCiphertextScale",
+      "GetPlaintextScale", "GetCiphertextScaleF", "GetCiphertextLevel", "GetPlaintextLevel", "GetCiphertextSlots",
+      "GetPlaintextSlots", "GetCiphertextDegree", "GetCiphertextBatch", "GetPlaintextBatch", "GetLiveCiphertexts",
+      "GetLivePlaintexts", "GetModuliChain", "GaloisElement", "OrionHipGraphEnd"};
+  return ok.count(fn) != 0;
+}
+static void capture_guard(const char* fn) {
+  if (g && g->capturing && !capture_ok(fn))
+    throw std::runtime_error(std::string(fn) + " is not allowed while capturing a graph");
+}
 #define API_BEGIN                                  \
   std::lock_guard<std::recursive_mutex> lk_(g_mu); \
-  try {
+  try {                                            \
+    capture_guard(__func__);
 #define API_END(errval)          \
   }                              \
   catch (const std::exception& e) { \
@@ -2083,6 +2276,30 @@ int OrionHipSynchronize(void) {
   HIPCHK(hipStreamSynchronize(ctx().stream));
   return 0;
   API_END(-1)
+}
+
+// ---- hipGraph capture of op streams (see Context::graph_begin) ----
+int OrionHipGraphBegin(void) {
+  API_BEGIN
+  ctx().graph_begin();
+  return 0;
+  API_END(-1)
+}
+int OrionHipGraphEnd(void) {
+  API_BEGIN
+  return ctx().graph_end();
+  API_END(-1)
+}
+int OrionHipGraphLaunch(int graph) {
+  API_BEGIN
+  ctx().graph_launch(graph);
+  return 0;
+  API_END(-1)
+}
+void OrionHipGraphDestroy(int graph) {
+  API_BEGIN
+  ctx().graph_destroy(graph);
+  API_END_VOID
 }
 
 int OrionHipLogN(void) { return g ? g->logN : -1; }

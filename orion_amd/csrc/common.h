@@ -300,6 +300,7 @@ struct NttIO {
                 // 2 = image fastest, then component, limbs in the order lord[] (slow integer-path limbs first)
   int jobs;     // ncomp * nlimb * nbatch of dst
   int pro, epi;
+  int stagger;  // persistent kernels: s_sleep(127) iterations before the first job of every other CU (timing switch)
   int ci;       // ConjugateInvariant ring: the forward folds its input, the inverse unfolds its output (ModConst::ciw)
   // two-pass kernels, chunked: this launch covers jobs [job0, job0 + njob) and
   // mid is a compact scratch of njob rows (row = job - job0), reused by every

@@ -451,6 +451,15 @@ __device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int 
 // with one.
 // The subtract-and-scale epilogue variants keep one job per workgroup: as a
 // loop their extra live values spill (36-41 VGPRs at N = 2^15).
+// Desynchronise the CUs of a persistent launch: half of each XCD's
+// workgroups (blockIdx bit 3; workgroups go round-robin over the 8 XCDs)
+// start late, so their memory phases fall into the other half's compute
+// phases instead of all 256 CUs contending for HBM at once.
+__device__ __forceinline__ void ntt_stagger(const NttIO& io) {
+  if (io.stagger > 0 && (blockIdx.x & 8))
+    for (int i = 0; i < io.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+}
+
 template <int EPI>
 struct FwdPersist {
   static constexpr bool value = EPI == NTT_EPI_STORE;
@@ -476,6 +485,7 @@ template <int LOGN, int PRO, int EPI, bool CI>
 __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_fwd_kernel(NttIO io, const DeviceTables* __restrict__ tb) {
   extern __shared__ u32 lds[];
   if constexpr (FwdPersist<EPI>::value) {
+    ntt_stagger(io);
 #pragma nounroll
     for (int job = blockIdx.x; job < io.jobs; job += gridDim.x) ntt_fwd_job<LOGN, PRO, EPI, CI>(io, job, tb, lds);
   } else {
@@ -487,6 +497,7 @@ template <int LOGN, bool CI>
 __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_inv_kernel(NttIO io, const DeviceTables* __restrict__ tb) {
   constexpr int N = 1 << LOGN;
   extern __shared__ u32 lds[];
+  ntt_stagger(io);
 #pragma nounroll
   for (int job = blockIdx.x; job < io.jobs; job += gridDim.x) {
     int c, l, b;
@@ -591,5 +602,6 @@ int orion_ntt_init() {
     g_ntt_grid = per_cu * ncu;
   else
     g_ntt_grid = 0;
+  if (getenv("ORION_NTT_GRID")) g_ntt_grid = atoi(getenv("ORION_NTT_GRID"));  // timing switch: workgroups
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

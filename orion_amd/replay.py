@@ -195,6 +195,27 @@ class OrionStream:
                 lib.DeleteCiphertext(h)
         return out
 
+    def capture(self, ct_in):
+        """Record forward(clone(ct_in)) into one hipGraph (OrionHipGraphBegin/End):
+        returns (graph id, output handle).  Each OrionHipGraphLaunch(graph)
+        re-runs every kernel of the pass on ct_in's current contents and
+        rewrites the output handle; the clone keeps in-place ops off ct_in.
+        Run forward() once first (keys, tables and LT plans are made then)."""
+        lib = self.lib
+        lib.OrionHipGraphBegin()
+        try:
+            x = lib.CloneCiphertext(ct_in)
+            out = self.forward(x)
+            if out != x:
+                lib.DeleteCiphertext(x)
+        except Exception:
+            try:
+                lib.OrionHipGraphEnd()
+            except RuntimeError:
+                pass
+            raise
+        return lib.OrionHipGraphEnd(), out
+
     def decrypt_output(self, ct, n_out=None):
         """Decrypt + decode a batch output; returns (B, n_out) floats."""
         lib = self.lib

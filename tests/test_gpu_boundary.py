@@ -283,3 +283,52 @@ def test_level_scoped_galois_keys(torch_cuda, oracle_mod):
         assert lib.GetGaloisKeyLevel(e) == levels[e]
         assert np.array_equal(lib.export_galois_key(e), keys[e])
     lib.DeleteScheme()
+
+
+def test_graph_capture_replay(torch_cuda):
+    """OrionHipGraphBegin/End/Launch: the LoLA N=2^13 forward pass captured
+    into one hipGraph replays bit for bit like the stream-launched pass, again
+    and again; ciphertexts made after the capture (the pool pins the graph's
+    buffers) are not touched by a replay; a capture that would synchronise
+    (an upload) fails with an error instead of recording a broken graph."""
+    from orion_amd.replay import OrionStream
+    st = OrionStream("lola_n13", seed=77)
+    st.keygen()
+    st.compile()
+    lib = st.lib
+    rng = np.random.default_rng(5)
+    imgs = rng.standard_normal((3,) + st.reference_input().shape[1:]).astype(np.float32)
+    imgs[0] = st.reference_input()[0]
+    ct = st.encrypt_batch(imgs)
+    ref_h = st.forward(ct)
+    ref = lib.export_ciphertext(ref_h)
+    gid, out = st.capture(ct)
+    assert gid >= 0
+    x = lib.export_ciphertext(ct)
+    bystander = lib.import_ciphertext(x, 2.0 ** 26)  # allocated after the capture
+    for _ in range(3):
+        lib.OrionHipGraphLaunch(gid)
+        lib.OrionHipSynchronize()
+        assert np.array_equal(lib.export_ciphertext(out), ref)
+        assert np.array_equal(lib.export_ciphertext(bystander), x)
+        assert np.array_equal(lib.export_ciphertext(ct), x)  # the input is not consumed
+    res = st.decrypt_output(out)
+    assert np.abs(res[0] - st.arrays["expected_output"].reshape(-1)).mean() < 0.005
+    lib.OrionHipGraphDestroy(gid)
+    # calls that synchronise are refused inside a capture, before they reach
+    # HIP, so the capture stays valid and the library stays usable
+    ref_r = lib.export_ciphertext(lib.RotateNew(ct, 5))  # makes the key before the capture
+    lib.OrionHipGraphBegin()
+    with pytest.raises(RuntimeError, match="not allowed while capturing"):
+        lib.import_ciphertext(x, 2.0 ** 26)
+    with pytest.raises(RuntimeError, match="not allowed while capturing"):
+        lib.Decrypt(ct)
+    r = lib.RotateNew(ct, 5)  # recorded, not run
+    g2 = lib.OrionHipGraphEnd()
+    lib.OrionHipGraphLaunch(g2)
+    lib.OrionHipSynchronize()
+    assert np.array_equal(lib.export_ciphertext(r), ref_r)
+    lib.OrionHipGraphDestroy(g2)
+    again = st.forward(ct)
+    assert np.array_equal(lib.export_ciphertext(again), ref)
+    lib.DeleteScheme()
