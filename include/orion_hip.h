@@ -129,9 +129,11 @@ void RemovePlaintextDiagonals(int transformId);                            /* li
 void RemoveRotationKeys(void);                                             /* lineartransform.go:204 */
 
 /* ---------------- polynomial evaluator / bootstrapping ----------------
- * Implemented on the GPU: Lattigo's polynomial-evaluator
- * contract (level - bitlen(degree), exact target scale) and a bootstrapper
- * that extends the modulus chain above the residual one.  */
+ * Implemented on the GPU: Lattigo's polynomial evaluator
+ * (power basis + Paterson-Stockmeyer, level and target-scale contract) and
+ * one bootstrapper per slot count under bootstrapping parameters of its own
+ * (residual Q + 15 circuit primes, P primes of the bit sizes logPs), with
+ * Orion's post-scale 2^(LogMaxSlots - LogSlots).  */
 void NewPolynomialEvaluator(void);                                         /* polyeval.go:33 */
 int GenerateMonomial(float *coeffs, int n);                                /* polyeval.go:38 */
 int GenerateChebyshev(float *coeffs, int n);                               /* polyeval.go:50 */
@@ -167,6 +169,11 @@ int OrionHipLogN(void);                                   /* log2 of the ring de
 int OrionHipNumQ(void);
 int OrionHipNumP(void);
 unsigned long OrionHipModulus(int idx);                   /* QP index space */
+/* the bootstrapping chain of the circuit for `slots` (NewBootstrapper):
+ * Q primes (residual + circuit), then P primes; -1 / 0 when there is none */
+int OrionHipBootstrapNumQ(int slots);
+int OrionHipBootstrapNumP(int slots);
+unsigned long OrionHipBootstrapModulus(int slots, int idx);
 
 /* batch ciphertexts: one handle holds B images; ops act on the whole batch */
 int EncodeBatch(float *values, int lenPerImage, int batch, int level, unsigned long scale);

@@ -147,6 +147,9 @@ SIGNATURES = {
     "OrionHipNumQ": ([], c_int),
     "OrionHipNumP": ([], c_int),
     "OrionHipModulus": ([c_int], c_ulong),
+    "OrionHipBootstrapNumQ": ([c_int], c_int),
+    "OrionHipBootstrapNumP": ([c_int], c_int),
+    "OrionHipBootstrapModulus": ([c_int, c_int], c_ulong),
     "EncodeBatch": ([P(c_float), c_int, c_int, c_int, c_ulong], c_int),
     "EncodeBatchDevice": ([c_void_p, c_int, c_int, c_int, c_double], c_int),
     "DecodeDevice": ([c_int, c_void_p], c_int),
@@ -311,6 +314,14 @@ class HipLibrary:
 
     def moduli(self):
         return [int(self.OrionHipModulus(i)) for i in range(self.L + self.K)]
+
+    def bootstrap_moduli(self, slots):
+        """(Q primes, P primes) of the bootstrapping chain of the circuit for `slots`."""
+        nq, npr = self.OrionHipBootstrapNumQ(slots), self.OrionHipBootstrapNumP(slots)
+        if nq < 0:
+            raise RuntimeError(f"no bootstrapper found for slot count: {slots}")
+        m = [int(self.OrionHipBootstrapModulus(slots, i)) for i in range(nq + npr)]
+        return m[:nq], m[nq:]
 
     def export_ciphertext(self, ct):
         B, lvl = self.GetCiphertextBatch(ct), self.GetCiphertextLevel(ct)

@@ -335,6 +335,8 @@ struct Context {
 
   ~Context() {
     hipDeviceSynchronize();
+    btps.clear();  // circuits first: their buffers belong to the bootstrapping contexts' pools
+    btp_ctx.clear();
     if (capturing) {
       hipGraph_t gr = nullptr;
       hipStreamEndCapture(stream, &gr);
@@ -672,6 +674,17 @@ struct Context {
   // -- tables ---------------------------------------------------------------------
   void setup(int logN_, const std::vector<int>& logQ, const std::vector<int>& logP, int logScale_, int h_,
              bool ci_ = false) {
+    if ((int)(logQ.size() + logP.size()) > ORION_MAXMOD) throw std::runtime_error("too many moduli");
+    for (int b : logQ)
+      if (b > 61) throw std::runtime_error("moduli must be <= 61 bits");
+    for (int b : logP)
+      if (b > 61) throw std::runtime_error("moduli must be <= 61 bits");
+    if (logN_ < 13 || logN_ > 16) throw std::runtime_error("logN must be 13..16 in this build");
+    init_moduli(logN_, gen_moduli(logN_ + (ci_ ? 1 : 0), logQ, logP), logQ, logP, logScale_, h_, ci_);  // q = 1 mod NthRoot
+  }
+  // tables for explicit moduli m = [Q..., P...] (|Q| = |logQ|, |P| = |logP|)
+  void init_moduli(int logN_, const std::vector<u64>& m, const std::vector<int>& logQ, const std::vector<int>& logP,
+                   int logScale_, int h_, bool ci_) {
     logN = logN_;
     N = 1 << logN;
     ci = ci_;
@@ -683,13 +696,8 @@ struct Context {
     dnum = (L + K - 1) / K;
     logScale = logScale_;
     h = h_;
-    if (logN < 13 || logN > 16) throw std::runtime_error("logN must be 13..16 in this build");
-    if (L + K > ORION_MAXMOD) throw std::runtime_error("too many moduli");
-    for (int b : logQ)
-      if (b > 61) throw std::runtime_error("moduli must be <= 61 bits");
-    for (int b : logP)
-      if (b > 61) throw std::runtime_error("moduli must be <= 61 bits");
-    mods = gen_moduli(logN + (ci ? 1 : 0), logQ, logP);  // q = 1 mod NthRoot
+    if (L + K > ORION_MAXMOD || L + K > ORION_MAXLIMB) throw std::runtime_error("too many moduli");
+    mods = m;
     logQ_bits = logQ;
     logP_bits = logP;
     if (!stream) {
@@ -797,58 +805,6 @@ struct Context {
     const u64 q0 = mods[0];
     for (int i = 0; i < N; ++i) s[i] = host[i] > q0 / 2 ? -(int64_t)(q0 - host[i]) : (int64_t)host[i];
     return s;
-  }
-  // append Q primes above the current top (Lattigo's bootstrapping chain sits
-  // above the residual chain).  P keeps its primes (the generator allocates
-  // per bit size in list order, so P is listed before the extension) and
-  // moves to the end of the index space; the secret key is re-expanded, the
-  // public/relinearisation keys are regenerated and Galois keys are dropped
-  // (regenerated on first use).  QP plaintexts stay valid: their P limbs hold
-  // the same primes and are addressed as L + k at use time.
-  void extend_chain(const std::vector<int>& ext) {
-    if (!have_sk) throw std::runtime_error("extending the modulus chain needs the secret key");
-    const int Lold = L, Lnew = L + (int)ext.size();
-    if (Lnew + K > ORION_MAXMOD || Lnew + K > ORION_MAXLIMB) throw std::runtime_error("modulus chain too long");
-    std::vector<int> bits = logQ_bits;
-    bits.insert(bits.end(), logP_bits.begin(), logP_bits.end());
-    bits.insert(bits.end(), ext.begin(), ext.end());
-    const std::vector<u64> g = gen_moduli(logN, bits, {});
-    std::vector<u64> nm(g.begin(), g.begin() + Lold);
-    nm.insert(nm.end(), g.begin() + Lold + K, g.end());
-    nm.insert(nm.end(), g.begin() + Lold, g.begin() + Lold + K);
-    for (int i = 0; i < Lold; ++i)
-      if (nm[i] != mods[i]) throw std::runtime_error("chain extension changed a Q prime");
-    for (int k = 0; k < K; ++k)
-      if (nm[Lnew + k] != mods[Lold + k]) throw std::runtime_error("chain extension changed a P prime");
-    const std::vector<int64_t> s = secret_coeffs();
-    HIPCHK(hipStreamSynchronize(stream));
-    const DeviceTables old = host_tb;
-    mods = nm;
-    L = Lnew;
-    dnum = (L + K - 1) / K;
-    logQ_bits.insert(logQ_bits.end(), ext.begin(), ext.end());
-    for (int k = 0; k < K; ++k) {
-      host_tb.mc[L + k] = old.mc[Lold + k];
-      host_tb.fwd[L + k] = old.fwd[Lold + k];
-      host_tb.inv[L + k] = old.inv[Lold + k];
-      host_tb.fwd_d[L + k] = old.fwd_d[Lold + k];
-      host_tb.inv_d[L + k] = old.inv_d[Lold + k];
-    }
-    for (int m = Lold; m < L; ++m) build_mod_tables(m);
-    HIPCHK(hipMemcpy(d_tb, &host_tb, sizeof(DeviceTables), hipMemcpyHostToDevice));
-    for (auto& kv : betab) hipFree(kv.second);
-    betab.clear();
-    betab_pos.clear();
-    for (auto& kv : modup_arr) hipFree(kv.second);
-    modup_arr.clear();
-    sk = alloc(1, L + K, 1);
-    std::vector<u64> host((size_t)(L + K) * N);
-    small_residues(s, iota(0, L + K), host.data());
-    upload(sk, host);
-    ntt(ls(sk, 0, 1, iota(0, L + K), iota(0, L + K)), false);
-    gks.clear();
-    if (have_pk) gen_public();
-    if (have_rlk) gen_relin();
   }
   // encryption randomness: ChaCha20 key from the seed, encryption index 0
   void seed_encryption(u64 seed) {
@@ -1019,8 +975,9 @@ struct Context {
   // ---------------------------------------------------------------------------
   // keys
   // ---------------------------------------------------------------------------
-  void gen_secret() {
-    auto s = sample_ternary_h(h);
+  void gen_secret() { import_secret(sample_ternary_h(h)); }
+  // the secret with these (ternary) coefficients, expanded over QP
+  void import_secret(const std::vector<int64_t>& s) {
     sk = alloc(1, L + K, 1);
     std::vector<u64> host((size_t)(L + K) * N);
     small_residues(s, iota(0, L + K), host.data());
@@ -1880,18 +1837,36 @@ struct Context {
   HandlePool<PolyFn> polys;
 
   // ---------------------------------------------------------------------------
-  // bootstrapping (bootstrapper.go:19-80), full slots:
-  //   ModRaise (level 0 -> top, t = m + q0 I) -> CoeffsToSlots (the special
-  //   inverse FFT's butterfly stages, merged into 3 BSGS transforms with
-  //   complex diagonals; the final bit reversal is skipped because EvalMod is
-  //   slot-wise and SlotsToCoeffs starts with the matching one) -> real and
-  //   imaginary parts (conjugation key) -> EvalMod (Chebyshev approximation of
-  //   cos(2 pi (x - 1/4) / 2^r) on [-(K+1), K+1], then r double angles, giving
-  //   sin(2 pi x) = 2 pi m / q0 + O(m^3)) -> recombination (x i as X^(N/2)) ->
-  //   SlotsToCoeffs (forward FFT stages, 3 transforms) -> the input scale.
-  // NewBootstrapper extends the chain above the residual one by the 15 levels
-  // the circuit consumes (3 CoeffsToSlots, depth(poly) + r EvalMod, 3
-  // SlotsToCoeffs), so the output lands on the residual chain's top level.
+  // bootstrapping (bootstrapper.go:15-87).  As in Lattigo, a
+  // bootstrapper is made per slot count (NewBootstrapper(logPs, slots)), and
+  // its circuit runs under bootstrapping parameters of its own: the residual Q
+  // chain extended by the 15 levels the circuit consumes, with key-switching P
+  // primes of the bit sizes logPs (bootstrapping.ParametersLiteral{LogP}).
+  // Those parameters live in a second Context -- the bootstrapping context,
+  // one per distinct logPs, shared by the slot counts -- that holds the same
+  // secret and its own relinearisation and Galois keys.  The scheme's context,
+  // its chain and its keys are not touched.  The circuit, for n slots
+  // (gap = N / 2n):
+  //   ModRaise (level 0 -> top of the bootstrapping chain, t = m + q0 I)
+  //   -> Trace, n < N/2 only: multiply by gap^-1 mod Q, then add the
+  //      log2(gap) rotations by n 2^i (ModUp's SubSum): the exact projection
+  //      on Z[X^gap], whose slots are the n-periodic average of the input's
+  //   -> CoeffsToSlots: the n-point special inverse FFT's butterfly stages
+  //      merged into 3 BSGS transforms with complex diagonals (n-periodic);
+  //      the final bit reversal is skipped because EvalMod is slot-wise and
+  //      SlotsToCoeffs starts with the matching one.  For n < N/2 the last
+  //      transform also packs: real parts into slots [0, n) and imaginary
+  //      parts into [n, 2n) of every 2n-period, so that one EvalMod serves both
+  //   -> EvalMod: Chebyshev approximation of cos(2 pi (x - 1/4) / 2^r) on
+  //      [-(K+1), K+1], then r double angles, giving sin(2 pi x) =
+  //      2 pi m / q0 + O(m^3); once (n < N/2) or on the real and the
+  //      imaginary part (n = N/2, recombined with x i = X^(N/2))
+  //   -> SlotsToCoeffs: the forward stages, 3 transforms (for n < N/2 the
+  //      first one also unpacks real + i imag) -> the residual top level,
+  //      copied back into the scheme's context at the input's scale.
+  // Bootstrap then applies Orion's post-scale 2^(LogMaxSlots - LogSlots)
+  // (bootstrapper.go:73-74): an input whose slots >= n are zero comes back with
+  // its n slots replicated over all N/2 (Lattigo's sparse packing).
   // ---------------------------------------------------------------------------
   typedef std::complex<double> cplx;
   typedef std::map<int, std::vector<cplx>> DiagMap;  // rotation offset -> diagonal (n slots)
@@ -1992,20 +1967,29 @@ struct Context {
     return C;
   }
   struct Bootstrapper {
-    int K = 0, r = 3, degree = 63;
+    static constexpr int kDegree = 63, kR = 3, kDepthPoly = 6;  // EvalMod: cos degree, double angles, depth(63)
+    Context* bc = nullptr;  // the bootstrapping context (owned by the scheme's btp_ctx)
+    int slots = 0, gap = 1, K = 0, r = kR, degree = kDegree;
     PolyFn cosp;
     std::vector<LinTrans> cts, stc;  // in application order
+    std::vector<u64> trace_gal;      // Galois elements of the trace (rotations by slots * 2^i)
     int top = 0;
-    Poly mono_i;      // NTT of X^(N/2) (x i on every slot), all Q limbs
+    Poly mono_i;          // n = N/2: NTT of X^(N/2) (x i on every slot), all Q limbs
     long double s_y = 0;  // scale of the EvalMod output
-    u64 F = 1;        // message pre-scaling before ModRaise: F m <= q0 / 2^9 at the default scale
+    u64 F = 1;            // message pre-scaling before ModRaise: F m <= q0 / 2^9 at the default scale
   };
-  std::unique_ptr<Bootstrapper> btp;
+  // declared in this order so that the circuits (whose buffers belong to a
+  // bootstrapping context's pool) are destroyed before the contexts
+  std::map<std::vector<int>, std::unique_ptr<Context>> btp_ctx;  // logPs -> bootstrapping context
+  std::map<int, std::unique_ptr<Bootstrapper>> btps;             // slot count -> circuit
 
-  void new_bootstrapper() {
-    if (ci) throw std::runtime_error("bootstrapping needs the Standard ring (Lattigo has no ConjugateInvariant bootstrapper)");
-    const int n = N / 2, logn = logN - 1;
+  // (on the bootstrapping context) the circuit for `ns` slots
+  std::unique_ptr<Bootstrapper> make_circuit(int ns) {
+    const int n = N / 2;
     auto B = std::unique_ptr<Bootstrapper>(new Bootstrapper());
+    B->bc = this;
+    B->slots = ns;
+    B->gap = n / ns;
     // EvalMod range from the secret's Hamming weight: I ~ N(0, (h+1)/12) per coefficient
     B->K = (int)ceil(6.0 * sqrt((h + 1) / 12.0)) + 2;
     // Chebyshev interpolation of cos(2 pi ((K+1) u - 1/4) / 2^r) at degree+1 nodes on [-1, 1]
@@ -2025,28 +2009,21 @@ struct Context {
       B->cosp.cheb = true;
       B->cosp.c = c;
     }
-    int depth_poly = 0;
-    while ((1 << depth_poly) <= B->degree) ++depth_poly;
-    // Lattigo's bootstrapping parameters extend the residual chain (bootstrapper.go:33-41):
-    // SlotsToCoeffs 3 x 40-bit, EvalMod depth(poly) + r x 60-bit, CoeffsToSlots 3 x 55-bit,
-    // so the refreshed ciphertext comes out at the residual chain's top level
-    {
-      std::vector<int> ext(3, 40);
-      ext.insert(ext.end(), depth_poly + B->r, 60);
-      ext.insert(ext.end(), 3, 55);
-      extend_chain(ext);
-    }
     B->top = L - 1;
     {  // EvalMod sees x = F m / q0 + I: raise the message to <= 2^-9 of q0 (sin 2 pi x ~ 2 pi x to 3e-5)
       const int lg = (63 - __builtin_clzll(mods[0])) - logScale - 9;
       B->F = lg > 0 ? (1ull << lg) : 1;
     }
-    // merged FFT stage groups: 3 groups, stages split as evenly as possible
-    const std::vector<Cplx> twi = special_fft_twiddles(logN, true), twf = special_fft_twiddles(logN, false);
-    auto groups = [&](bool inverse) {
+    for (int s = ns; s < n; s *= 2) B->trace_gal.push_back(galois_element(s));
+    int logns = 0;
+    while ((1 << logns) < ns) ++logns;
+    // the n-point special FFT (slots of Z[Y]/(Y^2n + 1), Y = X^gap); its
+    // diagonals act n-periodically on the N/2 slots
+    const std::vector<Cplx> twi = special_fft_twiddles(logns + 1, true), twf = special_fft_twiddles(logns + 1, false);
+    auto groups = [&](bool inverse) {  // 3 groups of stages, split as evenly as possible
       std::vector<std::vector<int>> g(3);
       std::vector<int> lens;
-      for (int len = inverse ? n : 2; inverse ? len >= 2 : len <= n; len = inverse ? len / 2 : len * 2) lens.push_back(len);
+      for (int len = inverse ? ns : 2; inverse ? len >= 2 : len <= ns; len = inverse ? len / 2 : len * 2) lens.push_back(len);
       int at = 0;
       for (int k = 0; k < 3; ++k) {
         const int cnt = (int)(lens.size() - at) / (3 - k);
@@ -2054,6 +2031,7 @@ struct Context {
       }
       return g;
     };
+    const bool packed = ns < n;
     // CoeffsToSlots: slots of t / q0 -> bitrev((t_j + i t_{j+n}) / q0) / (2 (K+1)).  The 1/n of
     // the inverse transform and EvalMod's 1 / (2 (K+1)) are spread over the groups (2^-r per
     // group of r stages, the cube root of 1 / (2 (K+1)) each), so no diagonal is small against
@@ -2066,13 +2044,20 @@ struct Context {
         DiagMap M;
         M[0] = std::vector<cplx>(n, cplx(ldexp(kf, -(int)g[k].size()), 0));
         for (int len : g[k]) M = diag_compose(fft_stage(len, true, twi), M);
+        if (packed && k == 2) {
+          // w -> a w, a = 1 on [0, n) and -i on [n, 2n) of every 2n-period: then
+          // a w + conj(a w) = 2 Re w on the first half, 2 Im w on the second
+          DiagMap A;
+          A[0] = std::vector<cplx>(n);
+          for (int p = 0; p < n; ++p) A[0][p] = (p % (2 * ns)) < ns ? cplx(1, 0) : cplx(0, -1);
+          M = diag_compose(A, M);
+        }
         B->cts.push_back(make_lt_complex(M, level--));
       }
-      (void)logn;
     }
     // scale of the EvalMod output (simulated: CtS keeps scale q0, poly lands on 2^60 exactly)
     {
-      const int lvl_poly = B->top - 3 - depth_poly;
+      const int lvl_poly = B->top - 3 - Bootstrapper::kDepthPoly;
       long double sc = ldexpl(1.0L, 60);
       int lv = lvl_poly;
       for (int k = 0; k < B->r; ++k) sc = sc * sc / (long double)mods[lv--];
@@ -2086,25 +2071,36 @@ struct Context {
       const double cf = cbrt(cst);  // spread like CoeffsToSlots' constant
       for (int k = 0; k < 3; ++k) {
         DiagMap M;
-        M[0] = std::vector<cplx>(n, cplx(cf, 0));
+        if (packed && k == 0) {
+          // unpack: y_p + i y_{p+n} on the first half of a 2n-period, i y_p + y_{p-n}
+          // (= y_{p+n}: y is 2n-periodic) on the second, so the result is n-periodic
+          M[0] = std::vector<cplx>(n);
+          M[ns] = std::vector<cplx>(n);
+          for (int p = 0; p < n; ++p) {
+            const bool lo = (p % (2 * ns)) < ns;
+            M[0][p] = lo ? cplx(cf, 0) : cplx(0, cf);
+            M[ns][p] = lo ? cplx(0, cf) : cplx(cf, 0);
+          }
+        } else {
+          M[0] = std::vector<cplx>(n, cplx(cf, 0));
+        }
         for (int len : g[k]) M = diag_compose(fft_stage(len, false, twf), M);
         B->stc.push_back(make_lt_complex(M, level--));
       }
     }
-    // x i on every slot = multiplication by X^(N/2)
-    {
+    if (!packed) {  // x i on every slot = multiplication by X^(N/2)
       B->mono_i = alloc(1, L, 1);
       std::vector<u64> host((size_t)L * N, 0);
       for (int l = 0; l < L; ++l) host[(size_t)l * N + N / 2] = 1;
       upload(B->mono_i, host);
       ntt(lsq(B->mono_i, 0, 1, L - 1), false);
     }
-    btp = std::move(B);
+    return B;
   }
 
-  Ciphertext mul_i(const Ciphertext& a) {
+  Ciphertext mul_i(const Bootstrapper& bt, const Ciphertext& a) {
     Ciphertext o = new_ct(a.level, a.poly.B, a.scale);
-    LimbSet mi = ls(btp->mono_i, 0, 1, iota(0, a.level + 1), iota(0, a.level + 1), a.poly.B);
+    LimbSet mi = ls(bt.mono_i, 0, 1, iota(0, a.level + 1), iota(0, a.level + 1), a.poly.B);
     mi.ncomp = 2;
     mi.comp_stride = 0;  // one plaintext for both components
     ew(EW_MUL, lsq(o.poly, 0, 2, a.level), lsq(a.poly, 0, 2, a.level), mi);
@@ -2116,9 +2112,9 @@ struct Context {
     y.scale = x.scale;  // diagonals at scale q_level
     return y;
   }
-  Ciphertext eval_mod(const Ciphertext& u) {
-    Ciphertext y = eval_poly(u, btp->cosp, ldexpl(1.0L, 60));
-    for (int k = 0; k < btp->r; ++k) {  // cos(2a) = 2 cos(a)^2 - 1
+  Ciphertext eval_mod(const Bootstrapper& bt, const Ciphertext& u) {
+    Ciphertext y = eval_poly(u, bt.cosp, ldexpl(1.0L, 60));
+    for (int k = 0; k < bt.r; ++k) {  // cos(2a) = 2 cos(a)^2 - 1
       Ciphertext t = mul_relin(y, y);
       rescale_inplace(t);
       const LimbSet lt = lsq(t.poly, 0, 2, t.level);
@@ -2129,40 +2125,122 @@ struct Context {
     }
     return y;
   }
-  Ciphertext bootstrap(const Ciphertext& in) {
-    if (!btp) throw std::runtime_error("no bootstrapper: call NewBootstrapper first");
-    const int B = in.poly.B;
+  // (on the bootstrapping context) c0: the level-0 residues mod q0 of a batch
+  // of B ciphertexts, coefficient domain, already pre-scaled by F
+  Ciphertext run_circuit(Bootstrapper& bt, const Poly& c0, int B) {
     // ModRaise: level-0 residues (coefficient domain) lifted to every Q limb
-    Poly c0 = alloc(2, 1, B);
-    ntt_io(nio(lsq(c0, 0, 2, 0), lsq(in.poly, 0, 2, 0)), true);
-    if (btp->F > 1) {
-      std::vector<u64> f{btp->F % mods[0]};
-      ew1(EW_SCALE, lsq(c0, 0, 2, 0), lsq(c0, 0, 2, 0), &f);
-    }
     Ciphertext t = new_ct(L - 1, B, (long double)mods[0]);
     const LimbSet tl = lsq(t.poly, 0, 2, L - 1);
     if (orion_launch_modraise(tl, lsq(c0, 0, 2, 0), d_tb, N, stream)) throw std::runtime_error("modraise failed");
     ntt(tl, false);
+    if (bt.gap > 1) {  // Trace: (gap^-1 t) summed over the rotations by slots * 2^i
+      std::vector<u64> gi(L);
+      for (int l = 0; l < L; ++l) gi[l] = hm_invmod((u64)bt.gap % mods[l], mods[l]);
+      ew1(EW_SCALE, tl, tl, &gi);
+      for (u64 gel : bt.trace_gal) {
+        Ciphertext r = apply_galois(t, gel);
+        ew(EW_ADD, tl, tl, lsq(r.poly, 0, 2, L - 1));
+      }
+    }
     // CoeffsToSlots
-    Ciphertext z = lt_rescale(btp->cts[0], t);
-    z = lt_rescale(btp->cts[1], z);
-    z = lt_rescale(btp->cts[2], z);
-    // real and imaginary parts: z + conj z, -i (z - conj z)
+    Ciphertext z = lt_rescale(bt.cts[0], t);
+    z = lt_rescale(bt.cts[1], z);
+    z = lt_rescale(bt.cts[2], z);
     Ciphertext zc = apply_galois(z, 2 * (u64)N - 1);
-    Ciphertext re = new_ct(z.level, B, z.scale), im = new_ct(z.level, B, z.scale);
-    ew(EW_ADD, lsq(re.poly, 0, 2, z.level), lsq(z.poly, 0, 2, z.level), lsq(zc.poly, 0, 2, z.level));
-    ew(EW_SUB, lsq(im.poly, 0, 2, z.level), lsq(zc.poly, 0, 2, z.level), lsq(z.poly, 0, 2, z.level));
-    im = mul_i(im);  // (conj z - z) i = -i (z - conj z)
-    // EvalMod on both
-    Ciphertext yr = eval_mod(re), yi = eval_mod(im);
-    Ciphertext y = mul_i(yi);
-    ew(EW_ADD, lsq(y.poly, 0, 2, y.level), lsq(y.poly, 0, 2, y.level), lsq(yr.poly, 0, 2, y.level));
+    Ciphertext y;
+    if (bt.gap > 1) {
+      // packed real | imaginary parts: z + conj z
+      Ciphertext u = new_ct(z.level, B, z.scale);
+      ew(EW_ADD, lsq(u.poly, 0, 2, z.level), lsq(z.poly, 0, 2, z.level), lsq(zc.poly, 0, 2, z.level));
+      y = eval_mod(bt, u);
+    } else {
+      // real and imaginary parts: z + conj z, -i (z - conj z)
+      Ciphertext re = new_ct(z.level, B, z.scale), im = new_ct(z.level, B, z.scale);
+      ew(EW_ADD, lsq(re.poly, 0, 2, z.level), lsq(z.poly, 0, 2, z.level), lsq(zc.poly, 0, 2, z.level));
+      ew(EW_SUB, lsq(im.poly, 0, 2, z.level), lsq(zc.poly, 0, 2, z.level), lsq(z.poly, 0, 2, z.level));
+      im = mul_i(bt, im);  // (conj z - z) i = -i (z - conj z)
+      Ciphertext yr = eval_mod(bt, re), yi = eval_mod(bt, im);
+      y = mul_i(bt, yi);
+      ew(EW_ADD, lsq(y.poly, 0, 2, y.level), lsq(y.poly, 0, 2, y.level), lsq(yr.poly, 0, 2, y.level));
+    }
     // SlotsToCoeffs
-    Ciphertext o = lt_rescale(btp->stc[0], y);
-    o = lt_rescale(btp->stc[1], o);
-    o = lt_rescale(btp->stc[2], o);
-    o.scale = in.scale;
+    Ciphertext o = lt_rescale(bt.stc[0], y);
+    o = lt_rescale(bt.stc[1], o);
+    o = lt_rescale(bt.stc[2], o);
     return o;
+  }
+
+  // bootstrapper.go:19-58: one circuit per slot count (made once); logPs
+  // empty = the scheme's own P bit sizes
+  void new_bootstrapper(std::vector<int> logPs, int ns) {
+    if (ci) throw std::runtime_error("bootstrapping needs the Standard ring (Lattigo has no ConjugateInvariant bootstrapper)");
+    if (ns < 2 || ns > N / 2 || (ns & (ns - 1)))
+      throw std::runtime_error("slots must be a power of two in [2, " + std::to_string(N / 2) + "]");
+    if (btps.count(ns)) return;
+    if (!have_sk) throw std::runtime_error("bootstrapping keys need the secret key");
+    if (logPs.empty()) logPs = logP_bits;
+    for (int b : logPs)
+      if (b < 20 || b > 61) throw std::runtime_error("bootstrapping P primes must be 20..61 bits");
+    auto it = btp_ctx.find(logPs);
+    if (it == btp_ctx.end()) {
+      // Lattigo's bootstrapping chain: the residual Q, then SlotsToCoeffs 3 x 40-bit,
+      // EvalMod depth(poly) + r x 60-bit, CoeffsToSlots 3 x 55-bit (bottom to top), so the
+      // refreshed ciphertext comes out at the residual chain's top level; P from logPs.
+      // New primes skip every prime of the scheme.
+      std::vector<int> ext(3, 40);
+      ext.insert(ext.end(), Bootstrapper::kDepthPoly + Bootstrapper::kR, 60);
+      ext.insert(ext.end(), 3, 55);
+      std::vector<int> bits = ext;
+      bits.insert(bits.end(), logPs.begin(), logPs.end());
+      const std::vector<u64> fresh = gen_moduli_excluding(logN, bits, mods);
+      std::vector<u64> m(mods.begin(), mods.begin() + L);
+      m.insert(m.end(), fresh.begin(), fresh.end());
+      std::vector<int> qb = logQ_bits;
+      qb.insert(qb.end(), ext.begin(), ext.end());
+      if ((int)m.size() > ORION_MAXMOD || (int)m.size() > ORION_MAXLIMB)
+        throw std::runtime_error("bootstrapping chain too long");
+      HIPCHK(hipStreamSynchronize(stream));
+      std::unique_ptr<Context> bc(new Context());
+      bc->stream = stream;  // shared, not owned
+      bc->prng = Prng(prng.next());
+      bc->init_moduli(logN, m, qb, logPs, logScale, h, false);
+      bc->import_secret(secret_coeffs());
+      bc->gen_relin();
+      it = btp_ctx.emplace(logPs, std::move(bc)).first;
+    }
+    btps[ns] = it->second->make_circuit(ns);
+  }
+  // bootstrapper.go:61-80: a new ciphertext at the residual top level, at the
+  // input's scale, times the post-scale N / (2 slots)
+  Ciphertext bootstrap(const Ciphertext& in, int ns) {
+    auto it = btps.find(ns);
+    if (it == btps.end()) throw std::runtime_error("no bootstrapper found for slot count: " + std::to_string(ns));
+    Bootstrapper& bt = *it->second;
+    const int B = in.poly.B;
+    Poly c0 = alloc(2, 1, B);
+    ntt_io(nio(lsq(c0, 0, 2, 0), lsq(in.poly, 0, 2, 0)), true);
+    if (bt.F > 1) {
+      std::vector<u64> f{bt.F % mods[0]};
+      ew1(EW_SCALE, lsq(c0, 0, 2, 0), lsq(c0, 0, 2, 0), &f);
+    }
+    Ciphertext o = bt.bc->run_circuit(bt, c0, B);
+    if (o.level != L - 1) throw std::logic_error("bootstrapping circuit did not end at the residual top level");
+    Ciphertext out = new_ct(L - 1, B, in.scale);
+    // the residual limbs hold the same primes in both contexts
+    const LimbSet ol = lsq(out.poly, 0, 2, L - 1);
+    if (bt.gap > 1) {  // post-scale (an integer: no level)
+      std::vector<u64> ps(L);
+      for (int l = 0; l < L; ++l) ps[l] = (u64)bt.gap % mods[l];
+      ew1(EW_SCALE, ol, lsq(o.poly, 0, 2, L - 1), &ps);
+    } else {
+      copy(ol, lsq(o.poly, 0, 2, L - 1));
+    }
+    return out;
+  }
+  void delete_bootstrappers() {
+    if (stream) HIPCHK(hipStreamSynchronize(stream));
+    btps.clear();
+    btp_ctx.clear();
   }
 };
 
@@ -2265,6 +2343,7 @@ void OrionHipSetStream(void* s) {
       HIPCHK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
       g->own_stream = true;
     }
+    for (auto& kv : g->btp_ctx) kv.second->stream = g->stream;
   }
   API_END_VOID
 }
@@ -3165,42 +3244,47 @@ ArrayResultDouble GenerateMinimaxSignCoeffs(int* degrees, int n, int prec, int l
   return r;
   API_END(r)
 }
-// bootstrapper.go:19-58.  Like Lattigo's bootstrapping parameters, the modulus
-// chain is extended above the residual chain by the 15 levels the circuit uses
-// (keys regenerated for it); the key-switching P primes stay those of the
-// scheme, so logPs is not used.
-// Sparse slot counts (tensors.py:294-305 passes 2^ceil(log2(elements)) <= N/2)
-// share the one full-slot circuit: Orion's inputs are full-slot encodings whose
-// unused slots are zeroed before the bootstrap (operations.py:76-84), and the
-// full circuit returns every slot as it came in, so no post-scale is needed
-// (Lattigo's sparse circuit leaves replicas there and multiplies by
-// 2^(LogMaxSlots - LogSlots), bootstrapper.go:73-74).
-static void check_slots(const Context& c, int slots) {
-  if (slots < 1 || slots > c.slots || (slots & (slots - 1)))
-    throw std::runtime_error("slots must be a power of two <= " + std::to_string(c.slots));
-}
+// bootstrapper.go:19-58: one bootstrapper per slot count, made once, under
+// bootstrapping parameters with P primes of the bit sizes logPs
+// (Context::new_bootstrapper)
 void NewBootstrapper(int* logPs, int n, int slots) {
   API_BEGIN
-  (void)logPs;
-  (void)n;
   Context& c = ctx();
-  check_slots(c, slots);
-  if (!c.btp) c.new_bootstrapper();
+  std::vector<int> lp;
+  if (logPs && n > 0) lp.assign(logPs, logPs + n);
+  c.new_bootstrapper(lp, slots);
   API_END_VOID
 }
-// bootstrapper.go:61-80: a new ciphertext refreshed to the level below the
-// bootstrapping circuit, at the input's scale
+// bootstrapper.go:61-80: a new ciphertext refreshed to the residual top level,
+// at the input's scale, post-scaled by 2^(LogMaxSlots - LogSlots)
 int Bootstrap(int ct, int slots) {
   API_BEGIN
   Context& c = ctx();
-  check_slots(c, slots);
-  return c.cts.add(c.bootstrap(c.cts.get(ct)));
+  return c.cts.add(c.bootstrap(c.cts.get(ct), slots));
   API_END(-1)
 }
 void DeleteBootstrappers(void) {
   API_BEGIN
-  if (g) g->btp.reset();
+  if (g) g->delete_bootstrappers();
   API_END_VOID
+}
+// the bootstrapping chain of the circuit for `slots` (its Q primes, then its P primes)
+static Context* btp_context(int slots) {
+  if (!g) return nullptr;
+  auto it = g->btps.find(slots);
+  return it == g->btps.end() ? nullptr : it->second->bc;
+}
+int OrionHipBootstrapNumQ(int slots) {
+  Context* b = btp_context(slots);
+  return b ? b->L : -1;
+}
+int OrionHipBootstrapNumP(int slots) {
+  Context* b = btp_context(slots);
+  return b ? b->K : -1;
+}
+unsigned long OrionHipBootstrapModulus(int slots, int i) {
+  Context* b = btp_context(slots);
+  return (b && i >= 0 && i < (int)b->mods.size()) ? b->mods[i] : 0;
 }
 
 // ---- import / export ----

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <map>
+#include <set>
 #include <stdexcept>
 
 namespace orion {
@@ -103,6 +104,27 @@ std::vector<u64> gen_moduli(int logN, const std::vector<int>& logQ, const std::v
   std::vector<u64> out;
   for (int b : logQ) out.push_back(pool[b][used[b]++]);
   for (int b : logP) out.push_back(pool[b][used[b]++]);
+  return out;
+}
+
+// Lattigo bootstrapping.NewParametersFromLiteral: the circuit's new primes
+// (and its P primes) come from the same per-bit-size streams, skipping any
+// prime of the residual parameters, so the residual Q chain is kept as is
+std::vector<u64> gen_moduli_excluding(int logN, const std::vector<int>& bits, const std::vector<u64>& exclude) {
+  const u64 nthroot = 2ull << logN;
+  std::set<u64> taken(exclude.begin(), exclude.end());
+  std::map<int, PrimeStream> streams;
+  std::vector<u64> out;
+  for (int b : bits) {
+    auto it = streams.find(b);
+    if (it == streams.end()) it = streams.emplace(b, PrimeStream(b, nthroot)).first;
+    u64 q;
+    do {
+      q = b == 61 ? it->second.below() : it->second.alternate();
+    } while (taken.count(q));
+    taken.insert(q);
+    out.push_back(q);
+  }
   return out;
 }
 

@@ -21,6 +21,8 @@ u64 hm_bitrev(u64 x, int bits);
 
 // Lattigo ckks GenModuli (Standard ring, NthRoot = 2N); throws on exhaustion
 std::vector<u64> gen_moduli(int logN, const std::vector<int>& logQ, const std::vector<int>& logP);
+// primes of the given bit sizes (in list order) from the same streams, none in `exclude`
+std::vector<u64> gen_moduli_excluding(int logN, const std::vector<int>& bits, const std::vector<u64>& exclude);
 u64 primitive_root(u64 q);
 
 // CKKS canonical embedding helpers (n = N/2 slots, M = 2N)

@@ -115,8 +115,8 @@ class OrionStream:
                 coeffs = self.arrays[ev["arrays"] + "_coeffs"]
                 self.poly_map[ret] = (lib.GenerateChebyshev(list(coeffs), len(coeffs)) if op == "GenerateChebyshev"
                                       else lib.GenerateMonomial(list(coeffs)))
-            elif op == "NewBootstrapper":  # bootstrapper.py:9-13 (extends the chain, regenerates keys)
-                lib.NewBootstrapper([61], args[1])
+            elif op == "NewBootstrapper":  # bootstrapper.py:9-13 (boot_logp of the config)
+                lib.NewBootstrapper(list(self.meta["config"].get("boot_logp") or []), args[1])
         # rotation amounts used by the forward pass (hybrid output rotations)
         if gen_keys:
             for ev in self._events:

@@ -364,17 +364,21 @@ def test_n16_ops_parity(torch_cuda, oracle_mod):
     lib.DeleteScheme()
 
 
-BTP_LOGQ = [60] + [40] * 5  # the residual chain; NewBootstrapper extends it by 15 levels
+BTP_LOGQ = [60] + [40] * 5  # the residual chain; the bootstrapping chain adds 15 levels above it
 
 
 @pytest.mark.parametrize("h", [32, 192])
 def test_bootstrap_functional(torch_cuda, h):
-    """Bootstrap (bootstrapper.go:19-80) of a level-0 batch.  As with Lattigo's
-    bootstrapping parameters, NewBootstrapper extends the modulus chain above
-    the residual one (3 CoeffsToSlots + 6 polynomial + 3 double-angle + 3
-    SlotsToCoeffs levels), so the refreshed ciphertext sits on the residual
-    top level, at the input scale exactly, and decrypts to the input.  A
-    ciphertext and a linear transform made before the extension keep working.
+    """Bootstrap (bootstrapper.go:19-80) of a level-0 batch.  As in Lattigo,
+    each slot count gets its own bootstrapper, made once, under bootstrapping
+    parameters of its own: the residual Q chain plus the circuit's 15 levels
+    (3 CoeffsToSlots + 6 polynomial + 3 double-angle + 3 SlotsToCoeffs), and
+    P primes of the bit sizes logPs.  The scheme's chain and keys are not
+    touched.  The refreshed ciphertext sits on the residual top level at the
+    input scale.  A sparse slot count n runs the n-point circuit (trace, one
+    packed EvalMod) and Orion's post-scale 2^(LogMaxSlots - LogSlots)
+    (bootstrapper.go:73-74): an input whose slots >= n are zero comes back with
+    its n slots replicated over all N/2, as Lattigo's sparse packing leaves it.
     Parity with Lattigo's bootstrapper is unpinned (different circuit
     parameters); the bar is the functional one."""
     from orion_amd.backend import HipLibrary
@@ -393,9 +397,14 @@ def test_bootstrap_functional(torch_cuda, h):
     with pytest.raises(RuntimeError, match="power of two"):
         lib.NewBootstrapper([61, 61], 3 * n // 4)
     lib.NewBootstrapper([61, 61], n)
-    q_after = list(lib.GetModuliChain())
-    assert q_after[:len(q_before)] == q_before and len(q_after) == len(q_before) + 15
-    # state from before the extension: decrypt, and the transform
+    lib.NewBootstrapper([55], n)  # bootstrapper.go:25-27: made once per slot count
+    assert list(lib.GetModuliChain()) == q_before  # the scheme's parameters are unchanged
+    bq, bp = lib.bootstrap_moduli(n)
+    assert bq[:len(BTP_LOGQ)] == q_before[:len(BTP_LOGQ)] and len(bq) == len(BTP_LOGQ) + 15
+    assert [int(p).bit_length() for p in bp] == [61, 61]  # logPs
+    assert len(set(bq + bp + q_before)) == len(bq) + len(bp) + len(q_before) - len(BTP_LOGQ)
+    assert all(p % (2 * lib.N) == 1 for p in bq + bp)
+    # state from before NewBootstrapper: decrypt, and the transform
     assert np.abs(lib.decode_f64(lib.Decrypt(pre)) - vals).max() < 1e-5
     y = lib.EvaluateLinearTransform(lt, pre)
     lib.Rescale(y)
@@ -413,11 +422,23 @@ def test_bootstrap_functional(torch_cuda, h):
     lib.Rescale(sq)
     d2 = lib.decode_f64(lib.Decrypt(sq))
     assert np.abs(d2 - vals.astype(np.float64) ** 2).max() < 1e-4
-    # sparse slot count (tensors.py bootstrap): unused slots zeroed, they stay zero
-    sp = vals.copy()
-    sp[:, n // 4:] = 0
-    out_s = lib.Bootstrap(lib.Encrypt(lib.encode_batch(sp, 0, 1 << 40)), n // 4)
-    assert np.abs(lib.decode_f64(lib.Decrypt(out_s)) - sp).max() < 1e-5
+    # sparse slot counts (tensors.py:294-305 passes 2^ceil(log2(elements))): slots >= ns
+    # zeroed (operations.py:76-84); the output holds the ns slots replicated
+    with pytest.raises(RuntimeError, match="no bootstrapper found for slot count"):
+        lib.Bootstrap(ct, n // 4)
+    for ns, logp in ((n // 4, [61, 61, 61]), (64, [])):
+        lib.NewBootstrapper(logp, ns)
+        bq2, bp2 = lib.bootstrap_moduli(ns)
+        assert [int(p).bit_length() for p in bp2] == (logp or [60, 60])
+        sp = vals.copy()
+        sp[:, ns:] = 0
+        cs = lib.Encrypt(lib.encode_batch(sp, 0, 1 << 40))
+        out_s = lib.Bootstrap(cs, ns)
+        assert lib.GetCiphertextLevel(out_s) == len(BTP_LOGQ) - 1
+        assert lib.GetCiphertextScaleF(out_s) == 2.0 ** 40
+        exp_s = np.tile(sp[:, :ns], (1, n // ns)).astype(np.float64)
+        err = np.abs(lib.decode_f64(lib.Decrypt(out_s)) - exp_s)
+        assert err.max() < 1e-4 and err.mean() < 1e-5, (ns, err.max(), err.mean())
     lib.DeleteBootstrappers()
     with pytest.raises(RuntimeError, match="no bootstrapper"):
         lib.Bootstrap(ct, n)

@@ -3,7 +3,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-r01}
-ARGS="--steps 2 --warmup 1 --no-cpu-baseline"
+ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-extras"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o kt --output-format csv -- python bench.py $ARGS > gpurun_out/prof_${TAG}_kt.log 2>&1 || { echo "kt failed"; tail -20 gpurun_out/prof_${TAG}_kt.log; exit 1; }
 echo "kt ok"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "ntt" -d gpurun_out/prof_$TAG -o pmc_fetch --output-format csv -- python bench.py $ARGS > gpurun_out/prof_${TAG}_fetch.log 2>&1 || { echo "fetch failed"; tail -20 gpurun_out/prof_${TAG}_fetch.log; exit 1; }
