@@ -1306,9 +1306,9 @@ static pct pct_mul_relin(const oracle_ctx *c, const pct *a, const pct *b, const 
 typedef struct {
   const oracle_ctx *c;
   const pct *x;
-  int cheb, max_baby;
+  int cheb;
   pct pw[17];   /* pw[k] = T_{2^k}, k >= 1 */
-  pct baby[64]; /* T_j, j not a power of two (v == NULL until computed) */
+  pct baby[256]; /* T_j, j < 2^logSplit not a power of two (v == NULL until computed) */
   const u64 *rlk;
 } poly_run;
 
@@ -1363,66 +1363,100 @@ static const pct *poly_T(poly_run *R, int j) {
   return &R->baby[j];
 }
 
-static int poly_leaf(const poly_run *R, const long double *cf, int n, int lam) {
-  const int deg = n - 1;
-  if (deg <= 1) return 1;
-  if (deg >= R->max_baby) return 0;
-  for (int j = 2; j <= deg; j++)
-    if (cf[j] != 0 && R->x->level - ceil_log2i(j) < lam) return 0;
-  return 1;
+static int bitlen_i(int v) {
+  int k = 0;
+  while (v >> k) k++;
+  return k;
+}
+/* leaf (Lattigo EvaluatePolynomialVectorFromPowerBasis): c_0 S + sum_j
+ * round(c_j S / scale(T_j)) T_j, at the lowest level among lam and the T_j
+ * used (MulThenAdd takes the lower level) */
+static pct poly_leaf(poly_run *R, const long double *cf, int n, int lam, long double S) {
+  const oracle_ctx *c = R->c;
+  const int N = c->N, deg = n - 1;
+  u64 k[MAXMOD];
+  int lv = lam;
+  for (int j = 1; j <= deg; j++)
+    if (cf[j] != 0) {
+      const pct *T = poly_T(R, j);
+      if (T->level < lv) lv = T->level;
+    }
+  const size_t P = (size_t)(lv + 1) * N;
+  pct o = pct_alloc(c, lv, S);
+  for (int j = 1; j <= deg; j++) {
+    if (cf[j] == 0) continue;
+    const pct *T = poly_T(R, j);
+    big_const_res(c, cf[j] * S / T->scale, lv, k);
+    u64 *x = pct_at(c, T, lv);
+    for (int comp = 0; comp < 2; comp++)
+      for (int l = 0; l <= lv; l++)
+        for (int i = 0; i < N; i++) {
+          size_t at = comp * P + (size_t)l * N + i;
+          o.v[at] = addmod(o.v[at], mulmod(x[at], k[l], c->mod[l]), c->mod[l]);
+        }
+    free(x);
+  }
+  if (cf[0] != 0) {
+    big_const_res(c, cf[0] * S, lv, k);
+    for (int l = 0; l <= lv; l++)
+      for (int i = 0; i < N; i++) o.v[(size_t)l * N + i] = addmod(o.v[(size_t)l * N + i], k[l], c->mod[l]);
+  }
+  return o;
 }
 
-static pct poly_acc(poly_run *R, const long double *cf, int n, int lam, long double S) {
+/* Lattigo v6 recursePS (he/polynomial.go) with the ckks simEvaluator's
+ * UpdateLevelAndScale{Baby,Giant}Step: a node of degree < 2^logSplit is a
+ * leaf unless it is a lead node (on the quotient chain from the top) with
+ * maxdeg > 2^bitlen(maxdeg) - 2^(logSplit-1), which is re-split with
+ * logSplit = OptimalSplit(bitlen(deg)); otherwise p = q X^m + r with m the
+ * smallest power of two >= 2^logSplit and >= deg/2 + 1 (splitCoeffs; the
+ * Chebyshev split uses T_{m+j} = 2 T_m T_j - T_{m-j}).  The q branch runs one
+ * level up at S q_i / scale(X^m) (q_i = q_lam for a lead node, q_{lam+1}
+ * otherwise), is rescaled and multiplied by X^m; the r branch runs at that
+ * product's scale; a lead leaf is evaluated at S q_lam. */
+static pct poly_ps(poly_run *R, const long double *cf, int n, int lead, int maxdeg, int logSplit, int lam,
+                   long double S) {
   const oracle_ctx *c = R->c;
   const int N = c->N, deg = n - 1, cheb = R->cheb;
-  const size_t P = (size_t)(lam + 1) * N;
-  u64 k[MAXMOD];
-  if (poly_leaf(R, cf, n, lam)) {
-    pct o = pct_alloc(c, lam, S);
-    for (int j = 1; j <= deg; j++) {
-      if (cf[j] == 0) continue;
-      const pct *T = poly_T(R, j);
-      big_const_res(c, cf[j] * S / T->scale, lam, k);
-      u64 *x = pct_at(c, T, lam);
-      for (int comp = 0; comp < 2; comp++)
-        for (int l = 0; l <= lam; l++)
-          for (int i = 0; i < N; i++) {
-            size_t at = comp * P + (size_t)l * N + i;
-            o.v[at] = addmod(o.v[at], mulmod(x[at], k[l], c->mod[l]), c->mod[l]);
-          }
-      free(x);
-    }
-    if (cf[0] != 0) {
-      big_const_res(c, cf[0] * S, lam, k);
-      for (int l = 0; l <= lam; l++)
-        for (int i = 0; i < N; i++) o.v[(size_t)l * N + i] = addmod(o.v[(size_t)l * N + i], k[l], c->mod[l]);
-    }
-    return o;
+  if (deg < (1 << logSplit)) {
+    if (lead && logSplit > 1 && maxdeg > (1 << bitlen_i(maxdeg)) - (1 << (logSplit - 1)))
+      return poly_ps(R, cf, n, lead, maxdeg, optimal_split(bitlen_i(deg)), lam, S);
+    return poly_leaf(R, cf, n, lam, lead ? S * (long double)c->mod[lam] : S);
   }
-  int s = 1, ks = 0;
-  while (2 * s <= deg) s *= 2, ks++;
-  /* split p = q T_s + r (Chebyshev: T_{s+j} = 2 T_s T_j - T_{s-j}) */
-  long double *q = (long double *)malloc(sizeof(long double) * (deg - s + 1));
-  long double *r = (long double *)malloc(sizeof(long double) * s);
-  for (int j = 0; j <= deg - s; j++) q[j] = cf[s + j];
-  for (int j = 0; j < s; j++) r[j] = cf[j];
+  int m = 1 << logSplit;
+  while (m < (deg >> 1) + 1) m <<= 1;
+  long double *q = (long double *)malloc(sizeof(long double) * (deg - m + 1));
+  long double *r = (long double *)malloc(sizeof(long double) * m);
+  for (int j = 0; j <= deg - m; j++) q[j] = cf[m + j];
+  for (int j = 0; j < m; j++) r[j] = cf[j];
   if (cheb)
-    for (int j = 1; j <= deg - s; j++) {
-      q[j] = 2 * cf[s + j];
-      r[s - j] -= cf[s + j];
+    for (int j = 1; j <= deg - m; j++) {
+      q[j] = 2 * cf[m + j];
+      r[m - j] -= cf[m + j];
     }
-  const pct *G = &R->pw[ks];
-  pct qc = poly_acc(R, q, deg - s + 1, lam + 1, S * (long double)c->mod[lam + 1] / G->scale);
+  const int rmax = maxdeg == deg ? m - 1 : maxdeg - (deg - m + 1);
+  const pct *X = &R->pw[ceil_log2i(m)];
+  const long double qi = (long double)c->mod[lead ? lam : lam + 1];
+  pct qc = poly_ps(R, q, deg - m + 1, lead, maxdeg, logSplit, lam + 1, S * qi / X->scale);
   pct_rescale(c, &qc);
-  pct o = pct_mul_relin(c, &qc, G, R->rlk);
-  o.scale = S;
-  pct rc = poly_acc(R, r, s, lam, S);
+  pct o = pct_mul_relin(c, &qc, X, R->rlk);
+  pct rc = poly_ps(R, r, m, 0, rmax, logSplit, lam, o.scale);
+  const int lv = o.level < rc.level ? o.level : rc.level; /* Add takes the lower level */
+  if (lv < o.level) {
+    u64 *v = pct_at(c, &o, lv);
+    free(o.v);
+    o.v = v;
+    o.level = lv;
+  }
+  u64 *y = pct_at(c, &rc, lv);
+  const size_t P = (size_t)(lv + 1) * N;
   for (int comp = 0; comp < 2; comp++)
-    for (int l = 0; l <= lam; l++)
+    for (int l = 0; l <= lv; l++)
       for (int i = 0; i < N; i++) {
         size_t at = comp * P + (size_t)l * N + i;
-        o.v[at] = addmod(o.v[at], rc.v[at], c->mod[l]);
+        o.v[at] = addmod(o.v[at], y[at], c->mod[l]);
       }
+  free(y);
   free(qc.v);
   free(rc.v);
   free(q);
@@ -1437,7 +1471,7 @@ int oracle_eval_poly(const oracle_ctx *c, int level, const u64 *ct, long double 
   const int deg = n - 1;
   int depth = 0;
   while ((1 << depth) <= deg) depth++;
-  if (level < depth) return -1;
+  if (level < depth || depth > 16) return -1;
   pct x = {level, xscale, (u64 *)ct};
   poly_run R;
   memset(&R, 0, sizeof(R));
@@ -1445,8 +1479,6 @@ int oracle_eval_poly(const oracle_ctx *c, int level, const u64 *ct, long double 
   R.x = &x;
   R.rlk = rlk;
   R.cheb = cheb;
-  R.max_baby = depth >= 2 ? (1 << optimal_split(depth)) : 2;
-  if (R.max_baby > 64) R.max_baby = 64;
   long double *cf = (long double *)malloc(sizeof(long double) * n);
   for (int i = 0; i < n; i++) cf[i] = (long double)coeffs[i];
   u64 k[MAXMOD];
@@ -1469,10 +1501,9 @@ int oracle_eval_poly(const oracle_ctx *c, int level, const u64 *ct, long double 
   }
   pct o;
   if (deg == 0) {
-    o = poly_acc(&R, cf, n, level, target);
+    o = poly_leaf(&R, cf, n, level, target);
   } else {
-    const int lo = level - depth;
-    o = poly_acc(&R, cf, n, lo + 1, target * (long double)c->mod[lo + 1]);
+    o = poly_ps(&R, cf, n, 1, deg, optimal_split(depth), level - depth + 1, target);
     pct_rescale(c, &o);
     o.scale = target;
   }
@@ -1480,7 +1511,7 @@ int oracle_eval_poly(const oracle_ctx *c, int level, const u64 *ct, long double 
   *out_scale = o.scale;
   free(o.v);
   for (int i = 1; i < 17; i++) free(R.pw[i].v);
-  for (int i = 0; i < 64; i++) free(R.baby[i].v);
+  for (int i = 0; i < 256; i++) free(R.baby[i].v);
   free(cf);
   return o.level;
 }

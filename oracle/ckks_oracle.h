@@ -149,7 +149,9 @@ void oracle_encrypt_pk(const oracle_ctx *ctx, const uint32_t key[8], uint32_t en
                        uint32_t image, int level, const uint64_t *pk,
                        const uint64_t *pt, uint64_t *ct);
 
-/* ---- polynomial evaluation of the HIP backend (backend.hip eval_poly) ----
+/* ---- polynomial evaluation: Lattigo v6 he.EvaluatePolynomial restated
+ * (power basis + the recursePS Paterson-Stockmeyer tree and its scale rules,
+ * as backend.hip eval_poly; parity with Lattigo itself unpinned) ----
  * p(x) (monomial or Chebyshev basis, coefficients lowest degree first) of a
  * [2][level+1][N] ciphertext at scale xscale; writes [2][out_level+1][N] at
  * scale *out_scale (= target) and returns out_level = level - bitlen(n-1),

@@ -1682,24 +1682,34 @@ struct Context {
   }
 
   // ---------------------------------------------------------------------------
-  // polynomial evaluation (polyeval.go:63-84 -> Lattigo polynomial.Evaluator):
-  // p(x) in the monomial or Chebyshev basis, consuming exactly bitlen(degree)
-  // levels (orion/nn/activation.py:22-23,106-107 plans for that) and returning
-  // exactly the requested scale.
-  //   * power basis (Lattigo genPower): T_{2s} = T_s^2 (Chebyshev 2 T_s^2 - 1);
-  //     baby steps T_j, j < 2^OptimalSplit(bitlen(deg)), from the split
-  //     a = 2^k - 1, b = j + 1 - 2^k (Chebyshev 2 T_a T_b - T_|a-b|, the T_c
-  //     term scaled by round(s_a s_b / s_c) before the rescale), computed on
-  //     first use; T_j sits at level(x) - ceil(log2 j);
-  //   * recursion p = q T_s + r, s the largest power of two <= deg p (the
-  //     Chebyshev split uses T_{s+j} = 2 T_s T_j - T_{s-j}).  A node at level
-  //     lam is accumulated at scale S without rescaling; its q-branch is
-  //     accumulated one level up at scale S q_{lam+1} / scale(T_s), rescaled
-  //     once and multiplied by T_s.  A node is a leaf sum c0 + sum c_j T_j when
-  //     its degree is 1, or below the baby-step bound with every T_j it needs
-  //     at level >= lam.  Leaf constants are integers round(c_j S / scale(T_j)),
-  //     so every term of a node carries the same nominal scale and the final
-  //     rescale lands exactly on the target.
+  // polynomial evaluation (polyeval.go:63-84 -> Lattigo v6 he.EvaluatePolynomial,
+  // restated): p(x) in the monomial or Chebyshev basis, consuming exactly
+  // bitlen(degree) levels (orion/nn/activation.py:22-23,106-107 plans for that)
+  // and returning exactly the requested scale.
+  //   * power basis (PowerBasis.GenPower): T_{2s} = T_s^2 (Chebyshev
+  //     2 T_s^2 - 1); baby steps T_j from a = 2^k - 1, b = j + 1 - 2^k
+  //     (Chebyshev 2 T_a T_b - T_|a-b|, T_c scaled by round(s_a s_b / s_c)
+  //     before the rescale); every stored power is rescaled once.  Babies are
+  //     made on first use (Lattigo makes all j < 2^logSplit up front; the
+  //     values are the same);
+  //   * Paterson-Stockmeyer tree (GetPatersonStockmeyerPolynomial /
+  //     recursePS): logSplit = OptimalSplit(bitlen(deg)), top target level
+  //     level(x) - bitlen(deg) + 1.  A node of degree < 2^logSplit is a leaf,
+  //     except that a lead node (the chain of quotients from the top) whose
+  //     MaxDeg > 2^bitlen(MaxDeg) - 2^(logSplit-1) is re-split with
+  //     logSplit = OptimalSplit(bitlen(deg)), passed down to its subtree.
+  //     Otherwise p = q X^m + r, m = the smallest power of two >= 2^logSplit
+  //     and >= deg/2 + 1 (Chebyshev: T_{m+j} = 2 T_m T_j - T_{m-j});
+  //   * scales (ckks simEvaluator.UpdateLevelAndScale{Baby,Giant}Step): the q
+  //     branch runs one level up at scale S q_i / scale(X^m), q_i = q_level
+  //     for a lead node and q_{level+1} otherwise; its result is rescaled and
+  //     multiplied by X^m, and the r branch runs at that product's scale; a
+  //     lead leaf is evaluated at S q_level.  The top result is rescaled once,
+  //     landing on the target scale;
+  //   * a leaf (EvaluatePolynomialVectorFromPowerBasis) is c_0 S + sum_j
+  //     round(c_j S / scale(T_j)) T_j (MulThenAdd: half away from zero), at
+  //     the lowest level among its target and the powers it uses, as
+  //     MulThenAdd and Add take the lower level of their operands.
   // ---------------------------------------------------------------------------
   struct PolyFn {
     bool cheb = false;
@@ -1708,7 +1718,6 @@ struct Context {
   struct PolyRun {
     const Ciphertext* x;
     bool cheb;
-    int max_baby;                    // leaves may use T_j, j < max_baby
     std::map<int, Ciphertext> pw;    // T_{2^k}, k >= 1
     std::map<int, Ciphertext> baby;  // T_j, j not a power of two
   };
@@ -1760,61 +1769,71 @@ struct Context {
     }
     return {q, r};
   }
-  bool poly_leaf(const PolyRun& R, const std::vector<long double>& c, int lam) const {
-    const int deg = (int)c.size() - 1;
-    if (deg <= 1) return true;
-    if (deg >= R.max_baby) return false;
-    for (int j = 2; j <= deg; ++j)
-      if (c[j] != 0 && R.x->level - ceil_log2(j) < lam) return false;
-    return true;
-  }
-  Ciphertext poly_acc(PolyRun& R, const std::vector<long double>& c, int lam, long double S) {
-    const Ciphertext& x = *R.x;
-    const int deg = (int)c.size() - 1, B = x.poly.B;
-    if (poly_leaf(R, c, lam)) {
-      Ciphertext o = new_ct(lam, B, S);
-      const LimbSet lo = lsq(o.poly, 0, 2, lam);
-      bool first = true;
-      for (int j = 1; j <= deg; ++j) {
-        if (c[j] == 0) continue;
-        const Ciphertext& T = poly_T(R, j);
-        std::vector<u64> k = big_const_residues(c[j] * S / T.scale, lam);
-        ew1(first ? EW_SCALE : EW_ADDSCALE, lo, lsq(T.poly, 0, 2, lam), &k);
-        first = false;
-      }
-      if (first) HIPCHK(hipMemsetAsync(o.poly.ptr(), 0, (size_t)2 * (lam + 1) * B * N * sizeof(u64), stream));
-      if (c[0] != 0) {
-        std::vector<u64> k = big_const_residues(c[0] * S, lam);
-        ew1(EW_ADDC, lsq(o.poly, 0, 1, lam), lsq(o.poly, 0, 1, lam), &k);
-      }
-      return o;
+  // leaf: c_0 S + sum_j round(c_j S / scale(T_j)) T_j at level min(lam, level(T_j))
+  Ciphertext poly_leaf(PolyRun& R, const std::vector<long double>& c, int lam, long double S) {
+    const int deg = (int)c.size() - 1, B = R.x->poly.B;
+    int lv = lam;
+    for (int j = 1; j <= deg; ++j)
+      if (c[j] != 0) lv = std::min(lv, poly_T(R, j).level);
+    Ciphertext o = new_ct(lv, B, S);
+    const LimbSet lo = lsq(o.poly, 0, 2, lv);
+    bool first = true;
+    for (int j = 1; j <= deg; ++j) {
+      if (c[j] == 0) continue;
+      const Ciphertext& T = poly_T(R, j);
+      std::vector<u64> k = big_const_residues(c[j] * S / T.scale, lv);
+      ew1(first ? EW_SCALE : EW_ADDSCALE, lo, lsq(T.poly, 0, 2, lv), &k);
+      first = false;
     }
-    int s = 1;
-    while (2 * s <= deg) s *= 2;
-    auto qr = poly_split(c, s, R.cheb);
-    const Ciphertext& G = R.pw.at(s);
-    if (G.level < lam || lam + 1 > x.level) throw std::runtime_error("polynomial evaluation: level plan violated");
-    Ciphertext qc = poly_acc(R, qr.first, lam + 1, S * (long double)mods[lam + 1] / G.scale);
+    if (first) HIPCHK(hipMemsetAsync(o.poly.ptr(), 0, (size_t)2 * (lv + 1) * B * N * sizeof(u64), stream));
+    if (c[0] != 0) {
+      std::vector<u64> k = big_const_residues(c[0] * S, lv);
+      ew1(EW_ADDC, lsq(o.poly, 0, 1, lv), lsq(o.poly, 0, 1, lv), &k);
+    }
+    return o;
+  }
+  static int bitlen(int v) {
+    int k = 0;
+    while (v >> k) ++k;
+    return k;
+  }
+  // recursePS: node c (lead: on the quotient chain from the top; maxdeg as
+  // splitCoeffs propagates it) evaluated for target level lam and scale S
+  Ciphertext poly_ps(PolyRun& R, const std::vector<long double>& c, bool lead, int maxdeg, int logSplit, int lam,
+                     long double S) {
+    const int deg = (int)c.size() - 1;
+    if (deg < (1 << logSplit)) {
+      if (lead && logSplit > 1 && maxdeg > (1 << bitlen(maxdeg)) - (1 << (logSplit - 1)))
+        return poly_ps(R, c, lead, maxdeg, optimal_split(bitlen(deg)), lam, S);
+      return poly_leaf(R, c, lam, lead ? S * (long double)mods[lam] : S);
+    }
+    int m = 1 << logSplit;
+    while (m < (deg >> 1) + 1) m <<= 1;
+    auto qr = poly_split(c, m, R.cheb);
+    const int rmax = maxdeg == deg ? m - 1 : maxdeg - (deg - m + 1);
+    const Ciphertext& X = R.pw.at(m);
+    if (lam + 1 > R.x->level) throw std::runtime_error("polynomial evaluation: level plan violated");
+    const long double qi = (long double)mods[lead ? lam : lam + 1];
+    Ciphertext qc = poly_ps(R, qr.first, lead, maxdeg, logSplit, lam + 1, S * qi / X.scale);
     rescale_inplace(qc);
-    Ciphertext o = mul_relin(qc, G);
-    o.scale = S;
-    Ciphertext rc = poly_acc(R, qr.second, lam, S);
-    const LimbSet lo = lsq(o.poly, 0, 2, lam);
-    ew(EW_ADD, lo, lo, lsq(rc.poly, 0, 2, lam));
+    Ciphertext o = mul_relin(qc, X);
+    Ciphertext rc = poly_ps(R, qr.second, false, rmax, logSplit, lam, o.scale);
+    const int lv = std::min(o.level, rc.level);  // Add takes the lower level
+    o.level = lv;
+    const LimbSet lo = lsq(o.poly, 0, 2, lv);
+    ew(EW_ADD, lo, lo, lsq(rc.poly, 0, 2, lv));
     return o;
   }
   Ciphertext eval_poly(const Ciphertext& x, const PolyFn& p, long double target) {
     const int deg = (int)p.c.size() - 1;
     if (deg < 0) throw std::runtime_error("empty polynomial");
-    int depth = 0;
-    while ((1 << depth) <= deg) ++depth;  // bits.Len64(degree)
+    const int depth = bitlen(deg);  // bits.Len64(degree)
     if (x.level < depth)
       throw std::runtime_error(std::to_string(x.level) + " levels < " + std::to_string(depth) +
                                " log(d) -> cannot evaluate poly");
     PolyRun R;
     R.x = &x;
     R.cheb = p.cheb;
-    R.max_baby = depth >= 2 ? std::min(64, 1 << optimal_split(depth)) : 2;
     for (int s = 1; 2 * s <= deg; s *= 2) {
       const Ciphertext& a = s == 1 ? x : R.pw.at(s);
       Ciphertext t = mul_relin(a, a);
@@ -1827,9 +1846,8 @@ struct Context {
       }
       R.pw.emplace(2 * s, std::move(t));
     }
-    if (deg == 0) return poly_acc(R, p.c, x.level, target);
-    const int lo = x.level - depth;
-    Ciphertext out = poly_acc(R, p.c, lo + 1, target * (long double)mods[lo + 1]);
+    if (deg == 0) return poly_leaf(R, p.c, x.level, target);
+    Ciphertext out = poly_ps(R, p.c, true, deg, optimal_split(depth), x.level - depth + 1, target);
     rescale_inplace(out);
     out.scale = target;
     return out;

@@ -364,6 +364,50 @@ def test_n16_ops_parity(torch_cuda, oracle_mod):
     lib.DeleteScheme()
 
 
+@pytest.mark.parametrize("cheb,deg,odd", [
+    (True, 63, False),   # logSplit 3; the lead node of degree 7 is re-split with logSplit 1
+    (True, 27, True),    # odd (a minimax sign stage): even coefficients zero
+    (True, 100, False),  # depth 7, non-power-of-two degree
+    (False, 40, False),  # monomial basis, depth 6
+])
+def test_polynomial_parity_deep(torch_cuda, cheb, deg, odd):
+    """Deeper Paterson-Stockmeyer trees (recursePS: lead re-split, non-lead
+    leaves at several levels, babies up to 2^logSplit - 1) vs the oracle, bit
+    for bit, on a 45-bit chain; level - bitlen(degree), the exact target
+    scale, decrypt ~ p(x)."""
+    from oracle.oracle import Oracle
+    from orion_amd.backend import HipLibrary
+    logq = [60] + [45] * 9
+    lib = HipLibrary().new_scheme(13, logq, [60, 60], 45, h=192, seed=21)
+    orc = Oracle(13, lib.moduli(), len(logq), 2)
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    rng = np.random.default_rng(deg)
+    level, B = 9, 1
+    xs = rng.uniform(-1, 1, (B, orc.N // 2)).astype(np.float32)
+    ct = lib.Encrypt(lib.encode_batch(xs, level, 1 << 45))
+    x = lib.export_ciphertext(ct)
+    cf = (rng.uniform(-1, 1, deg + 1) / (1 + np.arange(deg + 1))).astype(np.float32)
+    if odd:
+        cf[0::2] = 0
+    poly = lib.GenerateChebyshev(list(cf), len(cf)) if cheb else lib.GenerateMonomial(list(cf))
+    out = lib.EvaluatePolynomial(ct, poly, 1 << 45)
+    depth = int(deg).bit_length()
+    assert lib.GetCiphertextLevel(out) == level - depth
+    assert lib.GetCiphertextScaleF(out) == 2.0 ** 45
+    got = lib.export_ciphertext(out)
+    ref, lv, sc = orc.eval_poly(x[0], level, 2.0 ** 45, cf.astype(np.float64), cheb, 2.0 ** 45,
+                                lib.export_relin_key())
+    assert lv == level - depth and sc == 2.0 ** 45
+    assert np.array_equal(got[0], ref)
+    dec = lib.decode_f64(lib.Decrypt(out))
+    xd = xs.astype(np.float64)
+    exp = np.polynomial.chebyshev.chebval(xd, cf) if cheb else np.polynomial.polynomial.polyval(xd, cf)
+    assert np.abs(dec - exp).max() < 1e-4
+    lib.DeleteScheme()
+
+
 BTP_LOGQ = [60] + [40] * 5  # the residual chain; the bootstrapping chain adds 15 levels above it
 
 
