@@ -364,6 +364,7 @@ struct Context {
     }
     for (auto e : ev_free) hipEventDestroy(e);
     if (own_stream && stream) hipStreamDestroy(stream);
+    if (ntt_log) fclose(ntt_log);
   }
 
   // -- profiling -----------------------------------------------------------
@@ -608,6 +609,21 @@ struct Context {
   // job of every other CU in persistent launches of >= ntt_stagger_min rounds
   int ntt_stagger = getenv("ORION_NTT_STAGGER") ? atoi(getenv("ORION_NTT_STAGGER")) : 0;
   int ntt_stagger_min = getenv("ORION_NTT_STAGGER_MIN") ? atoi(getenv("ORION_NTT_STAGGER_MIN")) : 2;
+  // ORION_NTT_LOG=path: one line per NTT call ("<impl> <jobs> <sub>": impl 1 =
+  // one dispatch of ntt.hip, 2 = a two-pass pair of ntt2.hip; sub = the
+  // subtract-and-scale epilogue), so tools/pmc_summary.py can price each
+  // dispatch of a rocprofv3 pass with its limb-transform count (persistent
+  // launches have fewer workgroups than jobs)
+  FILE* ntt_log = nullptr;
+  bool ntt_log_init = false;
+  void log_ntt(int impl, const NttIO& io) {
+    if (!ntt_log_init) {
+      ntt_log_init = true;
+      const char* p = getenv("ORION_NTT_LOG");
+      if (p && *p) ntt_log = fopen(p, "a");
+    }
+    if (ntt_log) fprintf(ntt_log, "%d %d %d\n", impl, io.jobs, io.epi == NTT_EPI_SUBSCALE ? 1 : 0);
+  }
   void ntt_io(NttIO io, bool inv) {
     io.order = ntt_order;
     io.ci = ci ? 1 : 0;
@@ -634,6 +650,9 @@ struct Context {
           io.job0 = j0;
           io.njob = std::min(chunk, io.jobs - j0);
           if (orion_launch_ntt2(logN, io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
+          NttIO lio = io;
+          lio.jobs = io.njob;
+          log_ntt(2, lio);
         }
         return;
       }
@@ -645,6 +664,7 @@ struct Context {
       const double per = 16.0 * N + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
       Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, per * io.jobs);
       if (orion_launch_ntt2(logN, io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
+      log_ntt(2, io);
       return;
     }
     if (ntt_stagger > 0) {
@@ -655,6 +675,7 @@ struct Context {
     const double per = 16.0 * N + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
     Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, per * io.dst.ncomp * io.dst.nlimb * io.dst.nbatch);
     if (orion_launch_ntt_io(logN, io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
+    log_ntt(1, io);
   }
   void ntt(const LimbSet& s, bool inv) { ntt_io(nio(s, s), inv); }
   void ew(int op, const LimbSet& o, const LimbSet& a, const LimbSet& b, const std::vector<u64>* sc = nullptr) {

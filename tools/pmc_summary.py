@@ -9,10 +9,13 @@ and SQ counter passes) and writes
 
 HBM bytes follow MI355X_MICROARCH.md (HBM/rocprofv3): FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide
-coalesced reads, so it is doubled.  Algorithmic bytes of an NTT launch =
-16 N per limb-transform (24 N with the subtract-and-scale epilogue), for the
-one-pass kernels (one workgroup of N/32 threads per limb) and the two-pass
-pairs (ntt2.hip) alike.
+coalesced reads, so it is doubled.  Algorithmic bytes of an NTT call = 16 N
+per limb-transform (24 N with the subtract-and-scale epilogue), for the
+one-pass kernels and the two-pass pairs (ntt2.hip) alike.  The one-pass
+kernels are persistent (one workgroup per CU walks the jobs), so the
+limb-transform count of a dispatch comes from the library's call log
+(ORION_NTT_LOG, one file per pass: gpurun_out/prof_<tag>/ntt_log_<pass>.txt),
+paired with the pass's NTT dispatches in issue order.
 """
 import collections
 import csv
@@ -37,71 +40,80 @@ def main(tag, workload="lola_n15", batch=64, logn=15):
     N = 1 << logn
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     ntt_alg = ntt_fetch = ntt_write = 0.0
+    def ntt_log(name):
+        """The pass's NTT calls in order (bench.py run with ORION_NTT_LOG):
+        (dispatches, jobs, subtract-and-scale epilogue)."""
+        p = os.path.join(d, f"ntt_log_{name}.txt")
+        if not os.path.exists(p):
+            return None
+        with open(p) as f:
+            return [(int(a), int(j), int(s)) for a, j, s in (ln.split() for ln in f if ln.strip())]
+
+    def priced(dispatches, log):
+        """Pair the pass's NTT dispatches (in issue order) with its logged calls:
+        yields (call index, dispatch, algorithmic bytes of the call or None for
+        the 2nd dispatch of a two-pass pair, jobs of the call)."""
+        i = 0
+        for call, (nd, jobs, sub) in enumerate(log):
+            for k in range(nd):
+                if i >= len(dispatches):
+                    raise RuntimeError("NTT log longer than the dispatch list")
+                alg = jobs * (24.0 if sub else 16.0) * N if k == 0 else None
+                yield call, dispatches[i], alg, jobs
+                i += 1
+        if i != len(dispatches):
+            raise RuntimeError(f"{len(dispatches)} NTT dispatches vs {i} logged")
+
     for name in ("pmc_fetch", "pmc_write", "pmc_sq"):
         p = os.path.join(d, f"{name}_counter_collection.csv")
         if not os.path.exists(p):
             continue
-        for r in rows(p):
+        rs = rows(p)
+        for r in rs:
             k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
             v = float(r["Counter_Value"])
             per[k][r["Counter_Name"]] += v
             per[k]["_dispatches_" + name] += 1
-            # algorithmic bytes of this dispatch (batched launches only, >= 64
-            # jobs): one-pass kernel = jobs * 16 N (24 N with the subtract-and-
-            # scale epilogue); a two-pass call's 16 N per job is booked on its
-            # cols kernel, the epilogue's extra 8 N on its rows kernel
-            wgs = int(r["Grid_Size"]) // max(1, int(r.get("Workgroup_Size") or 1))
-            tmpl = k.split("<")[1].split(">")[0].replace(" ", "") if "<" in k else ""
-            alg = None
-            if "ntt2_" in k:
-                jobs = wgs // 16 if "_cols" in k else wgs // (1 << (logn - 12))
-                if jobs >= 64:
-                    alg = jobs * 16.0 * N if "_cols" in k else (
-                        jobs * 8.0 * N if ("ntt2_fwd_rows" in k and tmpl.endswith(",1")) else 0.0)
-            elif "ntt_" in k and wgs >= 64:
-                alg = wgs * (24.0 if ("ntt_fwd_kernel" in k and tmpl.endswith(",1")) else 16.0) * N
-            if alg is not None:
-                if r["Counter_Name"] == "FETCH_SIZE":
-                    ntt_fetch += 2 * v * 1024
-                    ntt_alg += alg
-                elif r["Counter_Name"] == "WRITE_SIZE":
-                    ntt_write += v * 1024
-    ratio = (ntt_fetch + ntt_write) / ntt_alg if ntt_alg else None
-    # the batched NTT launches of the kernel trace, counted the way bench.py's
-    # HIP events count them: one launch per transform call, i.e. one one-pass
-    # kernel (jobs = workgroups) or one two-pass pair (ntt2.hip: cols kernel
-    # jobs*16 workgroups + rows kernel jobs*BTILES, BTILES = 2^(logn-12)),
-    # duration = the kernels' summed time; setup launches (keygen, < 64 jobs)
-    # are excluded
-    tr = sorted(rows(os.path.join(d, "kt_kernel_trace.csv")), key=lambda r: int(r["Start_Timestamp"]))
-    btiles = 1 << (logn - 12)
-    n_l = 0
-    n_us = n_b = 0.0
-    for r in tr:
-        k = r["Kernel_Name"]
-        if "ntt" not in k:
+        if name == "pmc_sq":
             continue
-        wgs = int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"])
-        dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        tmpl = k.split("<")[1].split(">")[0].replace(" ", "") if "<" in k else ""
-        if "ntt2_" in k:
-            cols = "_cols" in k
-            jobs = wgs // 16 if cols else wgs // btiles
+        # HBM bytes of the batched NTT calls (>= 64 limb-transforms) per
+        # algorithmic byte: each call's counters (both dispatches of a two-pass
+        # pair) against 16 N per limb-transform (24 N with the epilogue)
+        disp = {}
+        for r in rs:
+            disp.setdefault(int(r["Dispatch_Id"]), []).append(r)
+        order = [disp[i] for i in sorted(disp)]
+        log = ntt_log(name)
+        if log is None:
+            continue
+        cnt = "FETCH_SIZE" if name == "pmc_fetch" else "WRITE_SIZE"
+        for call, drs, alg, jobs in priced(order, log):
             if jobs < 64:
                 continue
-            n_us += dur
-            if cols:
+            v = sum(float(r["Counter_Value"]) for r in drs if r["Counter_Name"] == cnt)
+            if cnt == "FETCH_SIZE":
+                ntt_fetch += 2 * v * 1024  # gfx950 counts half the bytes of wide reads
+                ntt_alg += alg or 0.0
+            else:
+                ntt_write += v * 1024
+    ratio = (ntt_fetch + ntt_write) / ntt_alg if ntt_alg else None
+    # the batched NTT calls of the kernel trace, counted the way bench.py's HIP
+    # events count them: one call = one one-pass dispatch or one two-pass pair,
+    # duration = the dispatches' summed time, priced with the logged
+    # limb-transform counts; setup calls (keygen, < 64 jobs) are excluded
+    tr = sorted(rows(os.path.join(d, "kt_kernel_trace.csv")), key=lambda r: int(r["Start_Timestamp"]))
+    tr = [r for r in tr if "ntt" in r["Kernel_Name"]]
+    n_l = 0
+    n_us = n_b = 0.0
+    klog = ntt_log("kt")
+    if klog is not None:
+        for call, r, alg, jobs in priced(tr, klog):
+            if jobs < 64:
+                continue
+            n_us += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            if alg is not None:
                 n_l += 1
-                n_b += jobs * 16.0 * N
-            elif "ntt2_fwd_rows" in k and tmpl.endswith(",1"):  # subtract-and-scale epilogue
-                n_b += jobs * 8.0 * N
-            continue
-        if "ntt_" not in k or wgs < 64:
-            continue
-        n_l += 1
-        n_us += dur
-        sub = "ntt_fwd_kernel<" in k and tmpl.endswith(",1")
-        n_b += wgs * (24.0 if sub else 16.0) * N
+                n_b += alg
     trace = {"launches": n_l, "avg_launch_us": n_us / n_l if n_l else None,
              "algorithmic_bytes_per_launch": n_b / n_l if n_l else None,
              "achieved_GBps": n_b / (n_us * 1e-6) / 1e9 if n_us else None}
