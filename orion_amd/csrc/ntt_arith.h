@@ -133,11 +133,23 @@ __device__ __forceinline__ T from_bits(u64 x) {
   return __builtin_bit_cast(T, x);
 }
 
+// byte i (wave-uniform) of a small table in the kernel arguments, read as its
+// aligned dword: scalar loads are dword-granular, so a byte load at a dynamic
+// index would be a vector load followed by vmcnt(0) -- and vector memory
+// operations retire in order, so that wait also drains every load and store
+// still in flight (a persistent kernel decodes its next job while the
+// previous job's stores drain)
+__device__ __forceinline__ int arg_byte(const unsigned char* a, int i) {
+  i = __builtin_amdgcn_readfirstlane(i);
+  const unsigned w = reinterpret_cast<const unsigned*>(a)[i >> 2];
+  return (int)((w >> ((i & 3) * 8)) & 0xff);
+}
+
 // wave-uniform pointer to row (c, l, b) of a LimbSet: the limb tables are
 // indexed dynamically, so force the results into SGPRs so that every element
 // address is SGPR base + lane offset
 __device__ __forceinline__ u64* row_ptr(const LimbSet& s, int c, int l, int b) {
-  const int pos = __builtin_amdgcn_readfirstlane(s.pos[l]);
+  const int pos = __builtin_amdgcn_readfirstlane(arg_byte(s.pos, l));
   const long long off = c * s.comp_stride + pos * s.limb_stride + b * s.batch_stride;
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(off & 0xffffffffll));
   const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(off >> 32));
@@ -150,7 +162,7 @@ __device__ __forceinline__ void job_of(const NttIO& io, int job, int& c, int& l,
     b = job % d.nbatch;
     const int r = job / d.nbatch;
     c = r % d.ncomp;
-    l = io.lord[r / d.ncomp];
+    l = arg_byte(io.lord, r / d.ncomp);
   } else if (io.order == 1) {
     l = job % d.nlimb;
     const int r = job / d.nlimb;
