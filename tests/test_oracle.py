@@ -221,6 +221,28 @@ def test_eval_poly_functional(ckks, cheb, deg):
     assert np.abs(dec - exp).max() < 1e-4
 
 
+@pytest.mark.parametrize("cheb,deg", [(True, 63), (True, 27), (False, 40)])
+def test_eval_poly_deep_functional(oracle_mod, cheb, deg):
+    """Deeper Paterson-Stockmeyer trees on the CPU (recursePS: degree 63 has
+    logSplit 3 and re-splits its lead node of degree 7 with logSplit 1):
+    decrypts to p(x), consumes bitlen(deg) levels, exact target scale."""
+    o = oracle_mod.Oracle.from_logs(12, [55] + [45] * 8, [60, 60])
+    sk = o.gen_secret(6, 64)
+    rng = np.random.default_rng(deg)
+    v = rng.uniform(-1, 1, o.N // 2)
+    lvl = 8
+    ct = o.encrypt_sk(22, sk, o.encode(v, 2.0 ** 45, list(range(lvl + 1))), lvl)
+    rlk = o.gen_evk(8, o.mul_coeffs(sk, sk, list(range(o.L + o.K))), sk)
+    cf = (rng.uniform(-1, 1, deg + 1) / (1 + np.arange(deg + 1))).astype(np.float32).astype(np.float64)
+    if deg == 27:
+        cf[0::2] = 0  # odd, as a minimax sign stage
+    out, lv, sc = o.eval_poly(ct, lvl, 2.0 ** 45, cf, cheb, 2.0 ** 45, rlk)
+    assert lv == lvl - int(deg).bit_length() and sc == 2.0 ** 45
+    dec = o.decode(o.decrypt(out, sk, lv), lv, 2.0 ** 45)
+    exp = np.polynomial.chebyshev.chebval(v, cf) if cheb else np.polynomial.polynomial.polyval(v, cf)
+    assert np.abs(dec - exp).max() < 1e-4
+
+
 def test_encode_matches_canonical_embedding(ckks):
     """Encoding by definition: slot j = m(zeta^(5^j)), zeta = exp(i*pi/N)."""
     o, _ = ckks
