@@ -866,6 +866,14 @@ struct Context {
         const u64 vs = hm_mulmod((u64)v, T.S_t[t], tm);
         T.vS_t[t][v] = vs ? tm - vs : 0;
       }
+      u128 bound = 1;  // (sum s_i + 1) t
+      bool narrow = tm < (1ull << 32);
+      for (int i = 0; i < T.ns; ++i) {
+        narrow = narrow && mods[src[i]] < (1ull << 32);
+        bound += mods[src[i]];
+      }
+      T.narrow[t] = narrow && bound * tm < ((u128)1 << 63) ? 1 : 0;
+      T.tinv[t] = 1.0 / (double)tm;
     }
     BasisExtTable* d;
     HIPCHK(hipMalloc(&d, sizeof(T)));

@@ -149,6 +149,10 @@ struct BasisExtTable {
   u64 qhat_ts[ORION_MAXLIMB][ORION_MAXSRC];   // its Shoup companion
   u64 S_t[ORION_MAXLIMB];
   u64 vS_t[ORION_MAXLIMB][ORION_MAXSRC + 1];  // (t - v*S mod t) mod t, v = 0..ns (Lattigo vtimesqmodp)
+  // narrow targets: sources and t below 2^32 and (sum s_i + 1) t < 2^63, so the
+  // target sum is exact in one u64 of 32x32-bit products (bext_target_sel)
+  int narrow[ORION_MAXLIMB];
+  double tinv[ORION_MAXLIMB];  // 1 / t
 };
 
 // ---------------------------------------------------------------------------

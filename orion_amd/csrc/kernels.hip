@@ -117,6 +117,20 @@ __device__ __forceinline__ u64 bext_target_sel(const BasisExtTable* __restrict__
     if (j > ns) break;
     acc = v == (u64)j ? T->vS_t[t][j] : acc;
   }
+  if (T->narrow[t]) {  // wave-uniform: sources and target < 2^32 (ResNet's 30-bit chains)
+    // the whole sum in one u64: one 32x32 -> 64 multiply-add per source,
+    // then a single reduction with a float64 quotient (off by at most one)
+#pragma unroll
+    for (int i = 0; i < ORION_MAXSRC; ++i) {
+      if (i >= ns) break;
+      acc += (u64)(u32)y[i] * (u32)T->qhat_t[t][i];
+    }
+    const u64 k = (u64)((double)acc * T->tinv[t]);
+    long long r = (long long)(acc - k * q);
+    r = r < 0 ? r + (long long)q : r;
+    r = r >= (long long)q ? r - (long long)q : r;
+    return (u64)r;
+  }
   // lazy: each Shoup product is in [0, 2q) and the running sum is kept in
   // [0, 2q) by one conditional subtraction (4q < 2^63 for q < 2^61)
   const u64 q2 = q << 1, nq = 0 - q;
