@@ -315,28 +315,51 @@ struct NttIO {
 };
 
 // ---------------------------------------------------------------------------
-// multiply-accumulate for moduli below 2^48: operands split at bit 24 and kept
-// as (lo 24 bits | hi part << 32), so one product is 4 v_mad_u64_u32 with no
-// carry handling (every partial sum stays below 2^63 for up to 2^14 terms).
+// operands of moduli below 2^48 split at bit 24 and kept as (lo 24 bits | hi
+// part << 32) (lt_bsgs's diagonal copies); the partial sums of split products
+// are folded by macs_reduce.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ u64 split24(u64 x) { return (x & 0xffffffull) | ((x >> 24) << 32); }
 struct MacS {
   u64 lo, mid, hi;
 };
-__device__ __forceinline__ void macs_zero(MacS& a) { a.lo = a.mid = a.hi = 0; }
-__device__ __forceinline__ void macs_add(MacS& a, u64 xs, u64 ys) {
-  const u32 xb = (u32)xs, xa = (u32)(xs >> 32), yb = (u32)ys, ya = (u32)(ys >> 32);
-  a.lo += (u64)xb * yb;
-  a.mid += (u64)xa * yb;
-  a.mid += (u64)xb * ya;
-  a.hi += (u64)xa * ya;
-}
 // x = hi 2^48 + mid 2^24 + lo  (< 128 q^2)  ->  x mod q
 __device__ __forceinline__ u64 macs_reduce(const MacS& a, const ModConst& m) {
   const u64 L1 = a.lo + (a.mid << 24);
   const u64 L2 = L1 + (a.hi << 48);
   const u64 H = (a.mid >> 40) + (a.hi >> 16) + (L1 < a.lo) + (L2 < L1);
   return barrett_256q2(H, L2, m);
+}
+
+// ---------------------------------------------------------------------------
+// the same split products in float64 (moduli below 2^48): the 24-bit pieces
+// convert to doubles exactly, each piece product is below 2^48 and the sums
+// of up to 16 operand pairs stay below 2^53, so every FMA is exact.  FP64 FMA
+// issues at full rate, the 32-bit integer multiplies at quarter rate.
+// ---------------------------------------------------------------------------
+struct MacD {
+  double lo, mid, hi;
+};
+__device__ __forceinline__ void macd_zero(MacD& a) { a.lo = a.mid = a.hi = 0.0; }
+// x = xa 2^24 + xb, y = ya 2^24 + yb
+__device__ __forceinline__ void macd_add(MacD& a, double xb, double xa, double yb, double ya) {
+  a.lo = __builtin_fma(xb, yb, a.lo);
+  a.mid = __builtin_fma(xa, yb, a.mid);
+  a.mid = __builtin_fma(xb, ya, a.mid);
+  a.hi = __builtin_fma(xa, ya, a.hi);
+}
+// exact integer double in [0, 2^53) -> u64
+__device__ __forceinline__ u64 d53_to_u64(double d) {
+  const double h = __builtin_floor(d * 0x1p-32);
+  const double l = __builtin_fma(-h, 0x1p32, d);
+  return ((u64)(u32)h << 32) | (u32)l;
+}
+__device__ __forceinline__ u64 macd_reduce(const MacD& a, const ModConst& m) {
+  MacS s;
+  s.lo = d53_to_u64(a.lo);
+  s.mid = d53_to_u64(a.mid);
+  s.hi = d53_to_u64(a.hi);
+  return macs_reduce(s, m);
 }
 
 // ---------------------------------------------------------------------------

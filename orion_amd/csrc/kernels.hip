@@ -8,6 +8,12 @@
 // batch_stride = 0 and are read once per row from L2.
 #include "common.h"
 
+// timing-only ablation of lt_bsgs (0 in the product): bit 0 skips the giant
+// inner products, bit 1 skips the baby gadget products
+#ifndef LT_ABLATE
+#define LT_ABLATE 0
+#endif
+
 namespace {
 
 __device__ __forceinline__ long long row_off(const LimbSet& s, int c, int l, int b) {
@@ -383,7 +389,7 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
   for (int s = 0; s < MB; ++s) {
     x0[s] = x1[s] = 0;
     if (s < Bb.nb) {
-      if (Bb.key[s]) {
+      if (Bb.key[s] && !(LT_ABLATE & 2)) {
         const int j = jx[s];
         u64 r0, r1;
         gadget_at(dp, D.comp_stride, c1p, owndigit, Bb.key[s], Bb.beta, Bb.L, Bb.K, Bb.klvl[s], m, N, j, mc, r0, r1);
@@ -398,8 +404,41 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
   }
   const bool small = mc.bar_k <= 48;  // block-uniform
   if (small) {
+    // < 2^48 moduli: float64 split products (MacD), one reduction per giant;
+    // the baby rotations as 24-bit pieces in doubles
+    double xb0[MB], xa0[MB], xb1[MB], xa1[MB];
 #pragma unroll
-    for (int s = 0; s < MB; ++s) x0[s] = split24(x0[s]), x1[s] = split24(x1[s]);
+    for (int s = 0; s < MB; ++s) {
+      xb0[s] = (double)(u32)(x0[s] & 0xffffffull), xa0[s] = (double)(u32)(x0[s] >> 24);
+      xb1[s] = (double)(u32)(x1[s] & 0xffffffull), xa1[s] = (double)(u32)(x1[s] >> 24);
+    }
+    for (int g = g0; g < g1; ++g) {
+      const unsigned long long mask = P->mask[g] >> Bb.s0;
+      u64 r0 = 0, r1 = 0;
+      if (accumulate) {
+        r0 = t0.p[(long long)(g - g0) * t0.comp_stride + ro];
+        r1 = t1.p[(long long)(g - g0) * t1.comp_stride + ro];
+      }
+      u64 pv[MB];
+#pragma unroll
+      for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? P->pt[g][Bb.s0 + s][po] : 0;
+      MacD a0, a1;
+      macd_zero(a0), macd_zero(a1);
+#pragma unroll
+      for (int s = 0; s < MB; ++s) {
+        if (((mask >> s) & 1ull) && !(LT_ABLATE & 1)) {
+          // the plan's diagonal copies are stored split (EW_SPLIT24): pieces in the two dwords
+          const double pb = (double)(u32)pv[s], pa = (double)(u32)(pv[s] >> 32);
+          macd_add(a0, xb0[s], xa0[s], pb, pa);
+          macd_add(a1, xb1[s], xa1[s], pb, pa);
+        }
+      }
+      r0 = add_mod(r0, macd_reduce(a0, mc), mc.q);
+      r1 = add_mod(r1, macd_reduce(a1, mc), mc.q);
+      t0.p[(long long)(g - g0) * t0.comp_stride + ro] = r0;
+      t1.p[(long long)(g - g0) * t1.comp_stride + ro] = r1;
+    }
+    return;
   }
   for (int g = g0; g < g1; ++g) {
     const unsigned long long mask = P->mask[g] >> Bb.s0;
@@ -413,33 +452,18 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
     u64 pv[MB];
 #pragma unroll
     for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? P->pt[g][Bb.s0 + s][po] : 0;
-    if (small) {  // < 2^48 moduli: carry-free split products, one reduction per giant
-      MacS a0, a1;
-      macs_zero(a0), macs_zero(a1);
+    MacAcc a0, a1;
+    mac_zero(a0), mac_zero(a1);
 #pragma unroll
-      for (int s = 0; s < MB; ++s) {
-        if ((mask >> s) & 1ull) {
-          const u64 ps = pv[s];  // the plan's diagonal copies are stored split (EW_SPLIT24)
-          macs_add(a0, ps, x0[s]);
-          macs_add(a1, ps, x1[s]);
-        }
+    for (int s = 0; s < MB; ++s) {
+      if ((mask >> s) & 1ull) {
+        mac_add(a0, pv[s], x0[s]);
+        mac_add(a1, pv[s], x1[s]);
       }
-      r0 = add_mod(r0, macs_reduce(a0, mc), mc.q);
-      r1 = add_mod(r1, macs_reduce(a1, mc), mc.q);
-    } else {
-      MacAcc a0, a1;
-      mac_zero(a0), mac_zero(a1);
-#pragma unroll
-      for (int s = 0; s < MB; ++s) {
-        if ((mask >> s) & 1ull) {
-          mac_add(a0, pv[s], x0[s]);
-          mac_add(a1, pv[s], x1[s]);
-        }
-        if ((s & 3) == 3) {
-          r0 = add_mod(r0, mac_reduce(a0, mc), mc.q);
-          r1 = add_mod(r1, mac_reduce(a1, mc), mc.q);
-          mac_zero(a0), mac_zero(a1);
-        }
+      if ((s & 3) == 3) {
+        r0 = add_mod(r0, mac_reduce(a0, mc), mc.q);
+        r1 = add_mod(r1, mac_reduce(a1, mc), mc.q);
+        mac_zero(a0), mac_zero(a1);
       }
     }
     t0.p[(long long)(g - g0) * t0.comp_stride + ro] = r0;
