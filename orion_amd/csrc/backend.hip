@@ -34,7 +34,7 @@ int orion_launch_tensor(const LimbSet& d, const LimbSet& a, const LimbSet& b, co
                         hipStream_t st);
 int orion_launch_basis_ext(const LimbSet& out, const LimbSet& in, const BasisExtTable* T, const DeviceTables* tb,
                            int N, hipStream_t st);
-int orion_launch_modup_all(const LimbSet& D, const LimbSet& in, const BasisExtTable* const* Ts, int beta, int K,
+int orion_launch_modup_all(const LimbSet& D, const LimbSet& in, const BasisExtTable* Ts, int beta, int K,
                            int nqp, const DeviceTables* tb, int N, hipStream_t st);
 int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const LimbSet& own, const MacGroups& G, int ngroup,
                         int beta, const DeviceTables* tb, int N, hipStream_t st);
@@ -311,7 +311,7 @@ struct Context {
   std::map<u64, u32*> autidx;
   std::map<std::pair<int, int>, BasisExtTable*> betab;
   std::map<std::pair<int, int>, std::vector<int>> betab_pos;  // target positions (QP order)
-  std::map<int, BasisExtTable**> modup_arr;  // level -> device array of the digits' ModUp tables
+  std::map<int, BasisExtTable*> modup_arr;  // level -> the digits' ModUp tables, contiguous (one device array)
 
   HandlePool<Plaintext> pts;
   HandlePool<Ciphertext> cts;
@@ -901,17 +901,19 @@ struct Context {
     betab_pos[key] = tpos;
     return d;
   }
-  BasisExtTable* const* modup_tabs(int level) {
+  // copies of the digits' ModUp tables in one array, so that modup_all_kernel
+  // indexes them off a kernel argument (noalias: wave-uniform table reads
+  // become scalar loads; through an array of pointers they were vector loads)
+  const BasisExtTable* modup_tabs(int level) {
     auto it = modup_arr.find(level);
     if (it != modup_arr.end()) return it->second;
     no_capture("the ModUp table array");
     const int beta = (level + 1 + K - 1) / K;
-    std::vector<BasisExtTable*> h;
+    BasisExtTable* d;
+    HIPCHK(hipMalloc(&d, sizeof(BasisExtTable) * beta));
     std::vector<int> tpos;
-    for (int i = 0; i < beta; ++i) h.push_back(modup_tab(level, i, tpos));
-    BasisExtTable** d;
-    HIPCHK(hipMalloc(&d, sizeof(BasisExtTable*) * beta));
-    HIPCHK(hipMemcpy(d, h.data(), sizeof(BasisExtTable*) * beta, hipMemcpyHostToDevice));
+    for (int i = 0; i < beta; ++i)
+      HIPCHK(hipMemcpy(d + i, modup_tab(level, i, tpos), sizeof(BasisExtTable), hipMemcpyDeviceToDevice));
     modup_arr[level] = d;
     return d;
   }

@@ -16,6 +16,14 @@
 
 namespace {
 
+// p[i] through a global-address-space pointer: for a pointer read from device
+// memory (a plan's diagonal table) the compiler cannot infer the address
+// space and emits a flat load, whose completion is only trackable with
+// vmcnt(0) lgkmcnt(0) -- every product would wait for all loads in flight
+__device__ __forceinline__ u64 gld(const u64* p, long long i) {
+  return ((const __attribute__((address_space(1))) u64*)p)[i];
+}
+
 __device__ __forceinline__ long long row_off(const LimbSet& s, int c, int l, int b) {
   return c * s.comp_stride + s.pos[l] * s.limb_stride + b * s.batch_stride;
 }
@@ -182,7 +190,7 @@ __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in,
 // (consumers read the own limbs from the NTT-domain input, and the NTT that
 // follows covers only the target positions).
 // D: comps c*beta + i, limb pos j at D.pos[j]; Ts[i] = digit i's table.
-__global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, const BasisExtTable* const* Ts,
+__global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, const BasisExtTable* __restrict__ Ts,
                                                         int beta, int K, int nqp, const DeviceTables* __restrict__ tb,
                                                         int N, int tchunk) {
   const int row = blockIdx.y;
@@ -192,7 +200,7 @@ __global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, c
   const int c = r / beta;
   const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
   if (n >= N) return;
-  const BasisExtTable* __restrict__ T = Ts[i];
+  const BasisExtTable* __restrict__ T = Ts + i;
   const int ns = T->ns, lo = i * K;
   u64 x0[ORION_MAXSRC], x1[ORION_MAXSRC], y0[ORION_MAXSRC], y1[ORION_MAXSRC];
 #pragma unroll
@@ -421,7 +429,7 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
       }
       u64 pv[MB];
 #pragma unroll
-      for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? P->pt[g][Bb.s0 + s][po] : 0;
+      for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? gld(P->pt[g][Bb.s0 + s], po) : 0;
       MacD a0, a1;
       macd_zero(a0), macd_zero(a1);
 #pragma unroll
@@ -451,7 +459,7 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
     // their latencies overlap (the branches are wave-uniform)
     u64 pv[MB];
 #pragma unroll
-    for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? P->pt[g][Bb.s0 + s][po] : 0;
+    for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? gld(P->pt[g][Bb.s0 + s], po) : 0;
     MacAcc a0, a1;
     mac_zero(a0), mac_zero(a1);
 #pragma unroll
@@ -562,7 +570,7 @@ int orion_launch_basis_ext(const LimbSet& out, const LimbSet& in, const BasisExt
   return 0;
 }
 
-int orion_launch_modup_all(const LimbSet& D, const LimbSet& in, const BasisExtTable* const* Ts, int beta, int K,
+int orion_launch_modup_all(const LimbSet& D, const LimbSet& in, const BasisExtTable* Ts, int beta, int K,
                            int nqp, const DeviceTables* tb, int N, hipStream_t st) {
   if (beta < 1 || nqp > ORION_MAXLIMB || D.ncomp != in.ncomp * beta) return -1;
   const int rows = D.ncomp * D.nbatch;

@@ -19,3 +19,11 @@ for rep in 1 2; do
     echo "$v $rep: $(python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['roofline']['frac'])" gpurun_out/bench_${TAG}_${v}_$rep.log)"
   done
 done
+# optional: ResNet-20 N=2^16 batch 1 per library (RESNET=1)
+if [ "${RESNET:-0}" = 1 ]; then
+  for v in product "$@"; do
+    lib=orion_amd/liborion_hip.so; [ $v != product ] && lib=orion_amd/_build/liborion_hip_$v.so
+    ORION_LIB=$lib WORKLOAD=resnet20_n16 BATCH=1 timeout -k 10 400 python -u tools/resnet_bench.py > gpurun_out/resnet_${TAG}_$v.log 2>&1 || { tail -20 gpurun_out/resnet_${TAG}_$v.log; exit 1; }
+    echo "$v resnet: $(grep workload gpurun_out/resnet_${TAG}_$v.log | tail -1 | cut -c1-200)"
+  done
+fi
