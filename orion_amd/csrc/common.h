@@ -63,6 +63,20 @@ struct LimbSet {
   unsigned char pos[ORION_MAXLIMB];  // limb l lives at p + pos[l]*limb_stride
 };
 
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
+// byte i (wave-uniform) of a small table in the kernel arguments, read as its
+// aligned dword: scalar loads are dword-granular, so a byte load at a dynamic
+// index would be a vector load followed by vmcnt(0) -- and vector memory
+// operations retire in order, so that wait also drains every load and store
+// still in flight (a persistent kernel decodes its next job while the
+// previous job's stores drain)
+__device__ __forceinline__ int arg_byte(const unsigned char* a, int i) {
+  i = __builtin_amdgcn_readfirstlane(i);
+  const unsigned w = reinterpret_cast<const unsigned*>(a)[i >> 2];
+  return (int)((w >> ((i & 3) * 8)) & 0xff);
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // modular arithmetic (q < 2^62)
 // ---------------------------------------------------------------------------

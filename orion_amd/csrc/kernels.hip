@@ -25,7 +25,7 @@ __device__ __forceinline__ u64 gld(const u64* p, long long i) {
 }
 
 __device__ __forceinline__ long long row_off(const LimbSet& s, int c, int l, int b) {
-  return c * s.comp_stride + s.pos[l] * s.limb_stride + b * s.batch_stride;
+  return c * s.comp_stride + arg_byte(s.pos, l) * s.limb_stride + b * s.batch_stride;
 }
 
 enum EwOp : int {
@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(256) ew_kernel(LimbSet o, LimbSet a, LimbSet b
   const int c = r / o.nlimb;
   const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
   if (n >= N) return;
-  const ModConst mc = tb->mc[o.mod[l]];
+  const ModConst mc = tb->mc[arg_byte(o.mod, l)];
   const u64 q = mc.q;
   ulonglong2* po = (ulonglong2*)(o.p + row_off(o, c, l, bi) + n);
   const ulonglong2 x = *(const ulonglong2*)(a.p + row_off(a, c, l, bi) + n);
@@ -101,7 +101,7 @@ __global__ void __launch_bounds__(256) tensor_kernel(LimbSet d, LimbSet a, LimbS
   const int l = row / d.nbatch;
   const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
   if (n >= N) return;
-  const ModConst mc = tb->mc[d.mod[l]];
+  const ModConst mc = tb->mc[arg_byte(d.mod, l)];
   const u64 q = mc.q;
   const ulonglong2 a0 = *(const ulonglong2*)(a.p + row_off(a, 0, l, bi) + n);
   const ulonglong2 a1 = *(const ulonglong2*)(a.p + row_off(a, 1, l, bi) + n);
@@ -243,7 +243,7 @@ __global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, Lim
   const int g = r / out.nlimb;
   const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
   if (n >= N) return;
-  const int m = out.mod[l];
+  const int m = arg_byte(out.mod, l);
   const ModConst mc = tb->mc[m];
   const u64 q = mc.q;
   const u64* key = G.key[g];
@@ -310,7 +310,7 @@ __global__ void __launch_bounds__(256) automorph_kernel(LimbSet o, LimbSet a, co
   const int c = r / o.nlimb;
   const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
   if (n >= N) return;
-  const u64 q = tb->mc[o.mod[l]].q;
+  const u64 q = tb->mc[arg_byte(o.mod, l)].q;
   const u64* src = a.p + row_off(a, c, l, bi);
   u64* dst = o.p + row_off(o, c, l, bi) + n;
   const uint2 ix = *(const uint2*)(idx + n);
@@ -379,11 +379,11 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
   const int n = blockIdx.y * blockDim.x + threadIdx.x;
   const int l = blockIdx.z;
   if (n >= N) return;
-  const int m = t0.mod[l];
+  const int m = arg_byte(t0.mod, l);
   const ModConst mc = tb->mc[m];
   const bool isq = l <= Bb.level;
   const long long ro = row_off(t0, 0, l, bi) + n;
-  const long long po = (long long)ptl.pos[l] * ptl.limb_stride + n;
+  const long long po = (long long)arg_byte(ptl.pos, l) * ptl.limb_stride + n;
   const u64* c0p = ct.p + row_off(ct, 0, isq ? l : 0, bi);
   const u64* c1p = ct.p + row_off(ct, 1, isq ? l : 0, bi);
   const u64* dp = D.p + row_off(D, 0, l, bi);
@@ -490,7 +490,7 @@ __global__ void __launch_bounds__(256) lt_giant_kernel(LimbSet acc, LimbSet D, L
   const int n = blockIdx.y * blockDim.x + threadIdx.x;
   const int l = blockIdx.z;
   if (n >= N) return;
-  const int m = acc.mod[l];
+  const int m = arg_byte(acc.mod, l);
   const ModConst mc = tb->mc[m];
   const bool isq = l <= G.level;
   const int owndigit = isq ? l / G.K : -1;

@@ -133,18 +133,6 @@ __device__ __forceinline__ T from_bits(u64 x) {
   return __builtin_bit_cast(T, x);
 }
 
-// byte i (wave-uniform) of a small table in the kernel arguments, read as its
-// aligned dword: scalar loads are dword-granular, so a byte load at a dynamic
-// index would be a vector load followed by vmcnt(0) -- and vector memory
-// operations retire in order, so that wait also drains every load and store
-// still in flight (a persistent kernel decodes its next job while the
-// previous job's stores drain)
-__device__ __forceinline__ int arg_byte(const unsigned char* a, int i) {
-  i = __builtin_amdgcn_readfirstlane(i);
-  const unsigned w = reinterpret_cast<const unsigned*>(a)[i >> 2];
-  return (int)((w >> ((i & 3) * 8)) & 0xff);
-}
-
 // wave-uniform pointer to row (c, l, b) of a LimbSet: the limb tables are
 // indexed dynamically, so force the results into SGPRs so that every element
 // address is SGPR base + lane offset
