@@ -249,7 +249,7 @@ __device__ __forceinline__ void ntt_fwd_job(const NttIO& io, int job, const Devi
   constexpr int N = 1 << LOGN;
   int c, l, b;
   job_of(io, job, c, l, b);
-  const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
+  const int mod = arg_byte(io.dst.mod, l);
   const ModConst mc = tb->mc[mod];
   if (mc.f64) {
     const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->fwd_d[mod], 0, N * 8, 0x00020000);
@@ -281,7 +281,7 @@ __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_inv_kernel(NttIO io, con
   for (int job = blockIdx.x; job < io.jobs; job += gridDim.x) {
     int c, l, b;
     job_of(io, job, c, l, b);
-    const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
+    const int mod = arg_byte(io.dst.mod, l);
     const ModConst mc = tb->mc[mod];
     if (mc.f64) {
       const __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void*)tb->inv_d[mod], 0, N * 8, 0x00020000);

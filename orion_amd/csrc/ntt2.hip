@@ -271,7 +271,7 @@ __global__ void __launch_bounds__(N2<LOGN>::ATHREADS) ntt2_fwd_cols(NttIO io, co
   int c, l, b;
   const int job = io.job0 + (blockIdx.x >> 4);
   job_of(io, job, c, l, b);
-  const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
+  const int mod = arg_byte(io.dst.mod, l);
   const ModConst mc = tb->mc[mod];
   const bool lazy = mc.bar_k <= 41;
   if (mc.f64)
@@ -289,7 +289,7 @@ __global__ void __launch_bounds__(256) ntt2_fwd_rows(NttIO io, const DeviceTable
   int c, l, b;
   const int job = io.job0 + blockIdx.x / T;
   job_of(io, job, c, l, b);
-  const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
+  const int mod = arg_byte(io.dst.mod, l);
   const ModConst mc = tb->mc[mod];
   if (mc.f64)
     fwd_rows<F64Arith, LOGN, EPI>(io, job, c, l, b, blockIdx.x % T, mc, F64Arith(mc), twr(tb->fwd_d[mod], (8 << LOGN)),
@@ -306,7 +306,7 @@ __global__ void __launch_bounds__(256) ntt2_inv_rows(NttIO io, const DeviceTable
   int c, l, b;
   const int job = io.job0 + blockIdx.x / T;
   job_of(io, job, c, l, b);
-  const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
+  const int mod = arg_byte(io.dst.mod, l);
   const ModConst mc = tb->mc[mod];
   if (mc.f64)
     inv_rows<F64Arith, LOGN>(io, job, c, l, b, blockIdx.x % T, F64Arith(mc), twr(tb->inv_d[mod], (8 << LOGN)), lds);
@@ -320,7 +320,7 @@ __global__ void __launch_bounds__(N2<LOGN>::ATHREADS) ntt2_inv_cols(NttIO io, co
   int c, l, b;
   const int job = io.job0 + (blockIdx.x >> 4);
   job_of(io, job, c, l, b);
-  const int mod = __builtin_amdgcn_readfirstlane(io.dst.mod[l]);
+  const int mod = arg_byte(io.dst.mod, l);
   const ModConst mc = tb->mc[mod];
   if (mc.f64)
     inv_cols<F64Arith, LOGN>(io, job, c, l, b, blockIdx.x & 15, F64Arith(mc), twr(tb->inv_d[mod], (8 << LOGN)), lds);
