@@ -19,6 +19,7 @@ launcher and the collective flow on the CPU (no GPU, no number reported as a
 measurement) -- both are for tests, never for a reported value.
 """
 import argparse
+import faulthandler
 import json
 import os
 import socket
@@ -211,7 +212,24 @@ def dryrun(args, world, rank):
         dist.destroy_process_group()
 
 
+def dump_maps(tag):
+    """ORION_DUMP_MAPS=<prefix>: write /proc/self/maps to <prefix>_<tag>.txt, so
+    that the PCs of a native crash report (e.g. a profiler's signal handler)
+    can be resolved to library + offset afterwards."""
+    prefix = os.environ.get("ORION_DUMP_MAPS")
+    if prefix:
+        with open("/proc/self/maps") as f, open(f"{prefix}_{tag}.txt", "w") as o:
+            o.write(f.read())
+
+
+def stage(name):
+    """ORION_BENCH_STAGES=1: name each phase on stderr (locates a crash)"""
+    if os.environ.get("ORION_BENCH_STAGES") == "1":
+        print(f"bench stage: {name} t={time.perf_counter():.3f}", file=sys.stderr, flush=True)
+
+
 def main():
+    faulthandler.enable()  # a native crash prints the Python frames of every thread
     args = parse()
     from orion_amd import dist as odist
     world, rank, local = odist.env_ranks()
@@ -281,10 +299,14 @@ def main():
     def step():
         return st.forward(ct)
 
+    dump_maps("setup")
+    stage("warmup")
+
     for _ in range(args.warmup):
         lib.DeleteCiphertext(step())
     lib.OrionHipSynchronize()
 
+    stage("timed")
     lib.OrionHipProfileReset()
     lib.OrionHipProfile(0b11)  # HIP events around the NTT launches only (the roofline kernel)
     if dist:
@@ -340,6 +362,8 @@ def main():
     breakdown = lib.profile_read()
 
     client_ms, b1_ms, graph_step = None, None, None
+    dump_maps("extras")
+    stage("extras: client")
     if rank == 0 and not args.no_extras:
         # client side on the GPU (outside the timed region): encode + encrypt of
         # the batch from HBM-resident slots, and decrypt + decode of the output
@@ -376,6 +400,7 @@ def main():
         # BASELINE configs[2] (LoLA N=2^15, batch=1): single-image latency of the
         # same op stream, outside the timed region (one image per launch leaves
         # most CUs idle; the throughput line above is the batched shard)
+        stage("extras: batch-1 stream")
         ct1 = st.encrypt_batch(imgs[:1])
         lib.DeleteCiphertext(st.forward(ct1))
         lib.OrionHipSynchronize()
@@ -387,6 +412,7 @@ def main():
         b1_stream_ms = (time.perf_counter() - t1) / reps1 * 1e3
         # the same pass captured once into a hipGraph and replayed: one launch
         # per image instead of ~900 (launch-bound at one image per launch)
+        stage("extras: batch-1 graph capture + replay")
         gid, g_out = st.capture(ct1)
         lib.OrionHipGraphLaunch(gid)
         lib.OrionHipSynchronize()
@@ -401,6 +427,7 @@ def main():
         lib.DeleteCiphertext(ct1)
         # the batched step as a hipGraph replay (reported beside the line; the
         # value above is the stream-launched step the NTT events are timed on)
+        stage("extras: batched graph capture + replay")
         gid, g_out = st.capture(ct)
         lib.OrionHipGraphLaunch(gid)
         lib.OrionHipSynchronize()
@@ -413,6 +440,7 @@ def main():
         lib.OrionHipGraphDestroy(gid)
         lib.DeleteCiphertext(g_out)
 
+    stage("report")
     images = args.batch * world * args.steps
     value = images / dt
     ntt = [prof.get("ntt_fwd", {}), prof.get("ntt_inv", {})]

@@ -354,14 +354,23 @@ void oracle_intt(const oracle_ctx *c, int mi, u64 *a) {
 /* ------------------------------------------------------------------ */
 /* exact basis extension (Lattigo ModUpExact restated, App. A.5)        */
 /*   y_i = x_i * (S/s_i)^-1 mod s_i                                     */
-/*   v   = (u64) sum_i (double)y_i * (1.0/(double)s_i)   (ordered, no FMA) */
+/*   v   = (u64) sum_i (double)y_i / (double)s_i   (source order)       */
 /*   out_t = sum_i y_i * (S/s_i mod t) - v * (S mod t)   mod t          */
+/* The quotient is Lattigo v6's reconstructRNS (ring/basis_extension.go */
+/* [U], lattigo/v6 v6.2.0 per orion/backend/lattigo/go.mod:5):          */
+/* `vi += float64(y_i) / float64(Q[i])`, a correctly rounded division   */
+/* accumulated in source order, then truncated by uint64(vi).  It is    */
+/* not always floor(x / S): near an integer the rounding decides, and   */
+/* a reciprocal multiply (y_i * (1/s_i)) can truncate to another v      */
+/* (tests/golden/kat_ckks.json "bext_quotient" holds such coefficients).*/
+/* centered (DecomposeAndSplit's single-prime digit, decompLvl == -1):  */
+/*   x >= s >> 1 is extended as x - s (v = 1), else as x (v = 0).       */
 /* ------------------------------------------------------------------ */
-void oracle_basis_extend(const oracle_ctx *c, const u64 *x, const int *src, int ns,
-                         u64 *out, const int *dst, int nt) {
+static void basis_extend_impl(const oracle_ctx *c, const u64 *x, const int *src, int ns,
+                              u64 *out, const int *dst, int nt, int centered) {
   const int N = c->N;
   u64 qhatinv[MAXMOD];
-  double qinvf[MAXMOD];
+  double qf[MAXMOD];
   u64 qhat_t[MAXMOD][MAXMOD]; /* [t][i] */
   u64 S_t[MAXMOD];
   for (int i = 0; i < ns; i++) {
@@ -370,7 +379,7 @@ void oracle_basis_extend(const oracle_ctx *c, const u64 *x, const int *src, int 
     for (int k = 0; k < ns; k++)
       if (k != i) prod = mulmod(prod, c->mod[src[k]] % si, si);
     qhatinv[i] = invmod(prod, si);
-    qinvf[i] = 1.0 / (double)si;
+    qf[i] = (double)si;
   }
   for (int t = 0; t < nt; t++) {
     u64 tm = c->mod[dst[t]];
@@ -385,15 +394,22 @@ void oracle_basis_extend(const oracle_ctx *c, const u64 *x, const int *src, int 
     }
   }
   u64 y[MAXMOD];
+  const u64 half0 = c->mod[src[0]] >> 1;
   for (int n = 0; n < N; n++) {
-    double vf = 0.0;
-    for (int i = 0; i < ns; i++) {
-      u64 si = c->mod[src[i]];
-      y[i] = mulmod(x[(size_t)i * N + n] % si, qhatinv[i], si);
-      volatile double prod = (double)y[i] * qinvf[i];
-      vf = vf + prod;
+    u64 v;
+    if (centered && ns == 1) {
+      y[0] = x[n] % c->mod[src[0]];
+      v = y[0] >= half0 ? 1 : 0;
+    } else {
+      double vf = 0.0;
+      for (int i = 0; i < ns; i++) {
+        u64 si = c->mod[src[i]];
+        y[i] = mulmod(x[(size_t)i * N + n] % si, qhatinv[i], si);
+        volatile double quo = (double)y[i] / qf[i];
+        vf = vf + quo;
+      }
+      v = (u64)vf;
     }
-    u64 v = (u64)vf;
     for (int t = 0; t < nt; t++) {
       u64 tm = c->mod[dst[t]];
       u128 acc = 0;
@@ -403,6 +419,19 @@ void oracle_basis_extend(const oracle_ctx *c, const u64 *x, const int *src, int 
       out[(size_t)t * N + n] = submod(r, vs, tm);
     }
   }
+}
+
+void oracle_basis_extend(const oracle_ctx *c, const u64 *x, const int *src, int ns,
+                         u64 *out, const int *dst, int nt) {
+  basis_extend_impl(c, x, src, ns, out, dst, nt, 0);
+}
+
+/* ModUp of one gadget digit (Lattigo Decomposer.DecomposeAndSplit [U]): a */
+/* single-prime digit is extended from its centered representative, a     */
+/* wider one by ModUpExact                                                  */
+void oracle_modup_digit(const oracle_ctx *c, const u64 *x, const int *src, int ns,
+                        u64 *out, const int *dst, int nt) {
+  basis_extend_impl(c, x, src, ns, out, dst, nt, 1);
 }
 
 /* ------------------------------------------------------------------ */
@@ -490,7 +519,7 @@ void oracle_gadget_product_lazy(const oracle_ctx *c, int level, const u64 *cx,
       pos[nt++] = j;
     }
     u64 *ext = (u64 *)malloc(sizeof(u64) * N * (nt ? nt : 1));
-    oracle_basis_extend(c, cinv + (size_t)lo * N, src, hi - lo, ext, dst, nt);
+    oracle_modup_digit(c, cinv + (size_t)lo * N, src, hi - lo, ext, dst, nt);
     for (int t = 0; t < nt; t++) {
       oracle_ntt(c, dst[t], ext + (size_t)t * N);
       memcpy(d + (size_t)pos[t] * N, ext + (size_t)t * N, sizeof(u64) * N);

@@ -59,11 +59,19 @@ uint64_t oracle_primitive_root(uint64_t q);
 void oracle_ntt(const oracle_ctx *ctx, int m, uint64_t *a);
 void oracle_intt(const oracle_ctx *ctx, int m, uint64_t *a);
 
-/* Exact basis extension (Lattigo ModUpExact): x holds ns coefficient-domain
- * limbs (moduli src[0..ns)); writes nt limbs (moduli dst[0..nt)) to out. */
+/* Basis extension (Lattigo ModUpExact / reconstructRNS): x holds ns
+ * coefficient-domain limbs (moduli src[0..ns)); writes nt limbs (moduli
+ * dst[0..nt)) to out.  The quotient v is Lattigo's float64 sum of correctly
+ * rounded divisions y_i / s_i in source order, truncated. */
 void oracle_basis_extend(const oracle_ctx *ctx, const uint64_t *x,
                          const int *src, int ns, uint64_t *out,
                          const int *dst, int nt);
+/* ModUp of one gadget digit (Lattigo Decomposer.DecomposeAndSplit): as
+ * oracle_basis_extend, except that a single-prime digit (ns == 1) extends
+ * its centered representative (x >= s >> 1 becomes x - s). */
+void oracle_modup_digit(const oracle_ctx *ctx, const uint64_t *x,
+                        const int *src, int ns, uint64_t *out,
+                        const int *dst, int nt);
 
 /* Rescale (DivRoundByLastModulusNTT): ct has ncomp components, each
  * [level+1][N] (NTT).  out gets [level][N] per component. */

@@ -41,6 +41,7 @@ def _load():
         "oracle_ntt": (None, [vp, ctypes.c_int, _u64p]),
         "oracle_intt": (None, [vp, ctypes.c_int, _u64p]),
         "oracle_basis_extend": (None, [vp, _u64p, _intp, ctypes.c_int, _u64p, _intp, ctypes.c_int]),
+        "oracle_modup_digit": (None, [vp, _u64p, _intp, ctypes.c_int, _u64p, _intp, ctypes.c_int]),
         "oracle_rescale": (None, [vp, ctypes.c_int, ctypes.c_int, _u64p, _u64p]),
         "oracle_moddown": (None, [vp, ctypes.c_int, _u64p, _u64p]),
         "oracle_gadget_product_lazy": (None, [vp, ctypes.c_int, _u64p, _u64p, _u64p, _u64p]),
@@ -151,6 +152,13 @@ class Oracle:
         x = np.ascontiguousarray(x, dtype=np.uint64)
         out = np.zeros((len(dst), self.N), dtype=np.uint64)
         lib().oracle_basis_extend(self._h, _p(x), _ip(src), len(src), _p(out), _ip(dst), len(dst))
+        return out
+
+    def modup_digit(self, x, src, dst):
+        """ModUp of one gadget digit (DecomposeAndSplit: centered if one prime)."""
+        x = np.ascontiguousarray(x, dtype=np.uint64)
+        out = np.zeros((len(dst), self.N), dtype=np.uint64)
+        lib().oracle_modup_digit(self._h, _p(x), _ip(src), len(src), _p(out), _ip(dst), len(dst))
         return out
 
     def rescale(self, ct, level):

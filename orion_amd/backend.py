@@ -276,6 +276,13 @@ class HipFunction:
         return res
 
 
+# The scheme is process-global, like Lattigo's (scheme.go:32): every
+# HipLibrary of a process drives the same one.  A generation number, bumped by
+# each NewScheme / DeleteScheme, lets a holder tell whether the scheme it set
+# up is still the live one (scheme_current).
+_SCHEME_GEN = [0]
+
+
 class HipLibrary:
     """Drop-in replacement for LattigoLibrary (bindings.py:94-139)."""
 
@@ -283,6 +290,24 @@ class HipLibrary:
         self.lib = load_library(path)
         for name in SIGNATURES:
             setattr(self, name, HipFunction(self.lib, name))
+        self._scheme_gen = None
+        new, delete = self.NewScheme, self.DeleteScheme
+
+        def new_scheme_call(*args):
+            _SCHEME_GEN[0] += 1
+            self._scheme_gen = None
+            new(*args)
+            self._scheme_gen = _SCHEME_GEN[0]
+
+        def delete_scheme_call(*args):
+            _SCHEME_GEN[0] += 1
+            delete(*args)
+
+        self.NewScheme, self.DeleteScheme = new_scheme_call, delete_scheme_call
+
+    def scheme_current(self):
+        """True while the scheme this object created is the process's live one."""
+        return self._scheme_gen is not None and self._scheme_gen == _SCHEME_GEN[0]
 
     # evaluator.py:30-41 calls the HEonGPU binding's private
     # _ModDropCiphertext(arithmeticoperator_handle, ct, None)

@@ -98,6 +98,9 @@ class DevicePool {
     return p;
   }
   void release(void* p, size_t bytes) {
+    // a buffer that predates a capture and is released inside it may still be
+    // read by the captured work: pin it with the graph's own buffers
+    if (tracking_) touched_[p] = bytes;
     if (pins_.count(p))
       parked_[p] = bytes;
     else
@@ -206,7 +209,8 @@ struct LinTrans {
   // device BSGS plan (built at first evaluation, rebuilt when diagonals change)
   std::vector<int> slots;   // baby of each register slot: nonzero babies, then 0
   std::vector<int> gorder;  // giants in evaluation order: nonzero giants, then 0
-  LtPlan* d_plan = nullptr;
+  LtPlan* d_plan = nullptr;            // = plan.get()
+  std::shared_ptr<void> plan;          // owns d_plan (hipFree); captured graphs hold a reference
   int n_plan = 0;
   bool plan_dirty = true;
   LinTrans() = default;
@@ -218,13 +222,11 @@ struct LinTrans {
     idx = std::move(o.idx), diags = std::move(o.diags), giants = std::move(o.giants), babies = std::move(o.babies);
     sdiags = std::move(o.sdiags);
     index = std::move(o.index), slots = std::move(o.slots), gorder = std::move(o.gorder);
-    std::swap(d_plan, o.d_plan), std::swap(n_plan, o.n_plan);
+    std::swap(d_plan, o.d_plan), std::swap(plan, o.plan), std::swap(n_plan, o.n_plan);
     plan_dirty = o.plan_dirty;
     return *this;
   }
-  ~LinTrans() {
-    if (d_plan) hipFree(d_plan);
-  }
+  ~LinTrans() = default;
 };
 
 template <class T>
@@ -239,8 +241,10 @@ class HandlePool {  // lowest-free-id reuse (minheap.go:46-64)
       id = next_++;
     }
     map_[id] = std::make_unique<T>(std::move(v));
+    if (born) born->insert(id);
     return id;
   }
+  std::set<int>* born = nullptr;  // while set: ids handed out (graph capture)
   T& get(int id) {
     auto it = map_.find(id);
     if (it == map_.end()) throw std::runtime_error("handle not found: " + std::to_string(id));
@@ -322,7 +326,14 @@ struct Context {
     hipGraph_t g = nullptr;
     hipGraphExec_t x = nullptr;
     std::vector<std::pair<void*, size_t>> pins;
+    // every buffer the context's handles, keys and transforms referenced when
+    // the capture ended: none of them returns to the pool (and can be handed
+    // out again) while the graph may replay, whatever is deleted or replaced
+    // meanwhile (DeleteCiphertext, a Galois key made again for a higher level,
+    // LoadRotationKey, new LT diagonals or plans, DeleteLinearTransform)
+    std::vector<std::shared_ptr<void>> holds;
   };
+  std::set<int> capture_born;  // ciphertext ids created inside the open capture
   std::map<int, GraphRec> graphs;
   int next_graph = 0;
   bool capturing = false;
@@ -425,12 +436,15 @@ struct Context {
     prof_saved = prof;
     prof = 0;
     pool.begin_track();
+    capture_born.clear();
+    cts.born = &capture_born;
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
     capturing = true;
   }
   int graph_end() {
     if (!capturing) throw std::runtime_error("no graph capture is open");
     capturing = false;
+    cts.born = nullptr;
     prof = prof_saved;
     hipGraph_t gr = nullptr;
     const hipError_t e = hipStreamEndCapture(stream, &gr);
@@ -462,6 +476,7 @@ struct Context {
     }
     pool.pin(touched);
     r.pins = std::move(touched);
+    r.holds = graph_holds();
     const int id = next_graph++;
     graphs[id] = std::move(r);
     return id;
@@ -480,6 +495,36 @@ struct Context {
     hipGraphDestroy(it->second.g);
     pool.unpin(it->second.pins);
     graphs.erase(it);
+  }
+
+  std::vector<std::shared_ptr<void>> graph_holds() {
+    std::vector<std::shared_ptr<void>> h;
+    auto add = [&h](const Poly& p) {
+      if (p.buf) h.push_back(p.buf);
+    };
+    add(sk), add(pk), add(rlk);
+    for (auto& kv : gks) add(kv.second.k);
+    for (int id : cts.live()) add(cts.get(id).poly);
+    for (int id : pts.live()) add(pts.get(id).poly);
+    for (int id : lts.live()) {
+      LinTrans& t = lts.get(id);
+      for (auto& kv : t.diags) add(kv.second.poly);
+      for (auto& kv : t.sdiags) add(kv.second);
+      if (t.plan) h.push_back(t.plan);
+    }
+    return h;
+  }
+  // in-place ops inside a capture only on ciphertexts made inside it: on an
+  // older handle a replay would apply the op again to its own output, and the
+  // handle's level and scale would advance once (at capture) while its data
+  // changes at every launch
+  Ciphertext& inplace_ct(int id) {
+    Ciphertext& a = cts.get(id);
+    if (capturing && !capture_born.count(id))
+      throw std::runtime_error("in-place op on ciphertext " + std::to_string(id) +
+                               ", which predates the graph capture (a replay would reapply it): clone it inside the "
+                               "capture first");
+    return a;
   }
 
   // lazily built tables, keys and host transfers synchronise, which would
@@ -840,19 +885,24 @@ struct Context {
     return r;
   }
 
-  BasisExtTable* make_betab(const std::vector<int>& src, const std::vector<int>& dst) {
+  // centered: a gadget digit (Lattigo DecomposeAndSplit extends a one-prime
+  // digit from its centered representative; ModDown's ModUpExact does not)
+  BasisExtTable* make_betab(const std::vector<int>& src, const std::vector<int>& dst, bool centered = false) {
     no_capture("a basis extension table");
     BasisExtTable T;
     memset(&T, 0, sizeof(T));
     T.ns = (int)src.size();
     T.nt = (int)dst.size();
+    T.centered = centered && T.ns == 1 ? 1 : 0;
+    T.chalf = mods[src[0]] >> 1;
     if (T.ns > ORION_MAXSRC || T.nt > ORION_MAXLIMB) throw std::runtime_error("basis extension too large");
     for (int i = 0; i < T.ns; ++i) {
       const u64 si = mods[src[i]];
       T.src_mod[i] = src[i];
       T.qhatinv[i] = hm_invmod(prod_mod(src, i, si), si);
       T.qhatinv_s[i] = hm_shoup(T.qhatinv[i], si);
-      T.qinv_f[i] = 1.0 / (double)si;
+      T.qf[i] = (double)si;
+      T.qinv_f[i] = 1.0 / T.qf[i];
     }
     for (int t = 0; t < T.nt; ++t) {
       const u64 tm = mods[dst[t]];
@@ -896,7 +946,7 @@ struct Context {
       tpos.push_back(j);
       dst.push_back(qp_mod(level, j));
     }
-    BasisExtTable* d = make_betab(src, dst);
+    BasisExtTable* d = make_betab(src, dst, true);
     betab[key] = d;
     betab_pos[key] = tpos;
     return d;
@@ -1418,11 +1468,14 @@ struct Context {
         P.pt[gg][sl] = T.sdiags.at((j + b) & (slots - 1)).ptr();
       }
     }
-    if (T.d_plan && T.n_plan != nplan) {
-      HIPCHK(hipFree(T.d_plan));
-      T.d_plan = nullptr;
+    // a plan that a captured graph still holds is never rewritten: the graph
+    // keeps replaying the plan (and the diagonals) it was captured with
+    if (!T.plan || T.n_plan != nplan || T.plan.use_count() > 1) {
+      void* d = nullptr;
+      HIPCHK(hipMalloc(&d, nplan * sizeof(LtPlan)));
+      T.plan = std::shared_ptr<void>(d, [](void* q) { hipFree(q); });
+      T.d_plan = (LtPlan*)d;
     }
-    if (!T.d_plan) HIPCHK(hipMalloc(&T.d_plan, nplan * sizeof(LtPlan)));
     HIPCHK(hipMemcpy(T.d_plan, plans.data(), nplan * sizeof(LtPlan), hipMemcpyHostToDevice));
     T.n_plan = nplan;
     T.plan_dirty = false;
@@ -2759,7 +2812,7 @@ int Negate(int id) {
 int Rotate(int id, int k) {
   API_BEGIN
   Context& c = ctx();
-  Ciphertext& a = c.cts.get(id);
+  Ciphertext& a = c.inplace_ct(id);
   a = c.rotate(a, k);
   return id;
   API_END(-1)
@@ -2773,14 +2826,14 @@ int RotateNew(int id, int k) {
 int Rescale(int id) {
   API_BEGIN
   Context& c = ctx();
-  c.rescale_inplace(c.cts.get(id));
+  c.rescale_inplace(c.inplace_ct(id));
   return id;
   API_END(-1)
 }
 int RescaleNew(int id) {  // evaluator.go:92-99: rescales the input in place, returns a copy
   API_BEGIN
   Context& c = ctx();
-  Ciphertext& a = c.cts.get(id);
+  Ciphertext& a = c.inplace_ct(id);
   c.rescale_inplace(a);
   return c.cts.add(c.clone(a));
   API_END(-1)
@@ -2790,7 +2843,7 @@ int RescaleNew(int id) {  // evaluator.go:92-99: rescales the input in place, re
 // in place, scale unchanged; returns the input id
 int ModDropCiphertext(int id) {
   API_BEGIN
-  Ciphertext& a = ctx().cts.get(id);
+  Ciphertext& a = ctx().inplace_ct(id);
   if (a.level < 1) throw std::runtime_error("cannot drop the last modulus");
   a.level -= 1;
   return id;
@@ -2811,7 +2864,7 @@ static Ciphertext add_scalar(Context& c, const Ciphertext& a, float v, bool inpl
 int AddScalar(int id, float v) {
   API_BEGIN
   Context& c = ctx();
-  Ciphertext& a = c.cts.get(id);
+  Ciphertext& a = c.inplace_ct(id);
   add_scalar(c, a, v, true, &a);
   return id;
   API_END(-1)
@@ -2831,7 +2884,7 @@ static void mul_const(Context& c, const Ciphertext& a, Ciphertext& out, const st
 int MulScalarInt(int id, int v) {
   API_BEGIN
   Context& c = ctx();
-  Ciphertext& a = c.cts.get(id);
+  Ciphertext& a = c.inplace_ct(id);
   mul_const(c, a, a, c.const_residues((long double)v, a.level));
   return id;
   API_END(-1)
@@ -2862,7 +2915,7 @@ static void mul_float(Context& c, const Ciphertext& a, Ciphertext& out, float v)
 int MulScalarFloat(int id, float v) {
   API_BEGIN
   Context& c = ctx();
-  Ciphertext& a = c.cts.get(id);
+  Ciphertext& a = c.inplace_ct(id);
   mul_float(c, a, a, v);
   return id;
   API_END(-1)
@@ -2880,7 +2933,7 @@ int MulScalarFloatNew(int id, float v) {
 // ct (+/-) pt
 static int ct_pt_op(int id, int pid, int op, bool inplace) {
   Context& c = ctx();
-  Ciphertext& a = c.cts.get(id);
+  Ciphertext& a = inplace ? c.inplace_ct(id) : c.cts.get(id);
   const Plaintext& p = c.pts.get(pid);
   const int level = std::min(a.level, p.level);
   const int B = c.batch_of(a.poly.B, p.poly.B);
@@ -2917,7 +2970,7 @@ int SubPlaintextNew(int id, int pt) {
 }
 static int ct_pt_mul(int id, int pid, bool inplace) {
   Context& c = ctx();
-  Ciphertext& a = c.cts.get(id);
+  Ciphertext& a = inplace ? c.inplace_ct(id) : c.cts.get(id);
   const Plaintext& p = c.pts.get(pid);
   const int level = std::min(a.level, p.level);
   const int B = c.batch_of(a.poly.B, p.poly.B);
@@ -2948,7 +3001,7 @@ int MulPlaintextNew(int id, int pt) {
 }
 static int ct_ct_op(int i0, int i1, int op, bool inplace) {
   Context& c = ctx();
-  Ciphertext& a = c.cts.get(i0);
+  Ciphertext& a = inplace ? c.inplace_ct(i0) : c.cts.get(i0);
   const Ciphertext& b = c.cts.get(i1);
   const int level = std::min(a.level, b.level);
   const int B = c.batch_of(a.poly.B, b.poly.B);
@@ -2986,6 +3039,7 @@ int SubCiphertextNew(int a, int b) {
 int MulRelinCiphertext(int a, int b) {
   API_BEGIN
   Context& c = ctx();
+  c.inplace_ct(a);
   Ciphertext r = c.mul_relin(c.cts.get(a), c.cts.get(b));
   if (r.poly.B != c.cts.get(a).poly.B) throw std::runtime_error("in-place op cannot grow the batch");
   c.cts.get(a) = std::move(r);

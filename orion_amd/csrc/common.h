@@ -148,17 +148,24 @@ __host__ __device__ static inline void mac128(Acc128& a, u64 x, u64 y) {
 // ---------------------------------------------------------------------------
 // host-side tables for basis extension (ModUp / ModDown), device-resident
 //   y_i  = x_i * qhatinv[i] mod s_i
-//   v    = (u64) sum_i (double)y_i * qinv_f[i]       (ordered, no FMA)
+//   v    = (u64) sum_i (double)y_i / (double)s_i    (Lattigo reconstructRNS:
+//          correctly rounded divisions summed in source order, truncated)
 //   out_t = sum_i y_i * qhat_t[t][i] - v * S_t[t]   mod t
+// centered (a gadget digit of one prime, Lattigo DecomposeAndSplit's
+// decompLvl == -1 branch): v = (x >= s >> 1), i.e. x - s is extended
 // ---------------------------------------------------------------------------
 #define ORION_MAXSRC 8
 #define ORION_MAXBABY 64  // baby steps fused into one BSGS giant-step MAC launch
 struct BasisExtTable {
   int ns, nt;
+  int centered;
+  int pad0;
+  u64 chalf;  // s_0 >> 1 (centered tables)
   int src_mod[ORION_MAXSRC];
   int dst_mod[ORION_MAXLIMB];
   u64 qhatinv[ORION_MAXSRC], qhatinv_s[ORION_MAXSRC];
-  double qinv_f[ORION_MAXSRC];
+  double qinv_f[ORION_MAXSRC];  // RN(1 / (double)s_i)
+  double qf[ORION_MAXSRC];      // (double)s_i (rounded, as Lattigo's float64(Q[i]))
   u64 qhat_t[ORION_MAXLIMB][ORION_MAXSRC];    // (S/s_i) mod t
   u64 qhat_ts[ORION_MAXLIMB][ORION_MAXSRC];   // its Shoup companion
   u64 S_t[ORION_MAXLIMB];
@@ -282,12 +289,20 @@ __device__ __forceinline__ u64 mac_reduce(const MacAcc& a, const ModConst& m) {
 // ---------------------------------------------------------------------------
 // exact basis extension of one coefficient (Lattigo ModUpExact restated;
 // SURVEY App. A.5): sources x_i (i < ns, coefficient domain) -> target t.
-// The float64 quotient is accumulated in source order with explicit
-// round-to-nearest multiply and add (no FMA contraction) so that it matches
-// the CPU restatement bit for bit.  y[] and v are shared by every target.
+// The float64 quotient is Lattigo reconstructRNS's: vi += float64(y_i) /
+// float64(s_i) in source order.  Each correctly rounded division is formed
+// as q0 = RN(y * RN(1/s)), r = y - q0 s (exact by FMA), RN(q0 + r RN(1/s))
+// (Markstein: with RN(1/s) and q0 within an ulp of y/s this is RN(y/s) in
+// round-to-nearest; checked on 4e8 adversarial pairs against IEEE division,
+// and the GPU parity tests compare with the oracle's plain division).
+// y[] and v are shared by every target.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ u64 bext_prep(const BasisExtTable* __restrict__ T, const DeviceTables* __restrict__ tb,
                                          const u64* x, u64* y) {
+  if (T->centered) {  // one source, qhatinv = 1 (wave-uniform)
+    y[0] = x[0];
+    return x[0] >= T->chalf ? 1 : 0;
+  }
   double vf = 0.0;
   const int ns = T->ns;
 #pragma unroll
@@ -295,7 +310,10 @@ __device__ __forceinline__ u64 bext_prep(const BasisExtTable* __restrict__ T, co
     if (i >= ns) break;
     const u64 si = tb->mc[T->src_mod[i]].q;
     y[i] = shoup_mul(x[i], T->qhatinv[i], T->qhatinv_s[i], si);
-    vf = __dadd_rn(vf, __dmul_rn((double)y[i], T->qinv_f[i]));
+    const double yd = (double)y[i], rc = T->qinv_f[i];
+    const double q0 = __dmul_rn(yd, rc);
+    const double r = __builtin_fma(-q0, T->qf[i], yd);
+    vf = __dadd_rn(vf, __builtin_fma(r, rc, q0));
   }
   return (u64)vf;
 }

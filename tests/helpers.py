@@ -16,3 +16,19 @@ def rand_ct(rng, moduli, level, N, B=1):
 
 
 SMALL = dict(logn=13, logq=[55, 40, 40, 40, 40, 40], logp=[60, 60])
+
+
+class SchemeCache:
+    """A GPU scheme shared by the tests of a module, rebuilt whenever another
+    test has replaced or deleted the process-global scheme since (the library
+    keeps one scheme per process, like Lattigo's scheme.go:32), so the tests
+    pass in any order or -k selection."""
+
+    def __init__(self):
+        self.val = None
+
+    def get(self, make):
+        if self.val is None or not self.val[0].scheme_current():
+            self.val = None
+            self.val = make()
+        return self.val

@@ -9,7 +9,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from tests.helpers import rand_ct
+from tests.helpers import rand_ct, SchemeCache
 
 pytestmark = pytest.mark.gpu
 
@@ -24,20 +24,29 @@ def torch_cuda():
     return torch
 
 
-@pytest.fixture(scope="module")
+_ci_small_cache = SchemeCache()
+
+
+@pytest.fixture
 def ci_small(torch_cuda, oracle_mod):
-    from orion_amd.backend import HipLibrary
-    p = CI_SMALL
-    lib = HipLibrary().new_scheme(p["logn"], p["logq"], p["logp"], 40, h=192, seed=4321,
-                                  ringtype="ConjugateInvariant")
-    mods = lib.moduli()
-    assert mods == oracle_mod.gen_moduli(p["logn"] + 1, p["logq"], p["logp"])  # q = 1 mod 4N
-    orc = oracle_mod.Oracle(p["logn"], mods, len(p["logq"]), len(p["logp"]), ci=True)
-    assert lib.N == orc.N == 1 << p["logn"] and lib.slots == orc.slots == orc.N
-    lib.GenerateSecretKey()
-    lib.GeneratePublicKey()
-    lib.GenerateRelinearizationKey()
-    return lib, orc
+    """function-scoped view of a module-wide scheme, rebuilt if another test
+    replaced the process-global scheme (order-independent)"""
+
+    def make():
+        from orion_amd.backend import HipLibrary
+        p = CI_SMALL
+        lib = HipLibrary().new_scheme(p["logn"], p["logq"], p["logp"], 40, h=192, seed=4321,
+                                      ringtype="ConjugateInvariant")
+        mods = lib.moduli()
+        assert mods == oracle_mod.gen_moduli(p["logn"] + 1, p["logq"], p["logp"])  # q = 1 mod 4N
+        orc = oracle_mod.Oracle(p["logn"], mods, len(p["logq"]), len(p["logp"]), ci=True)
+        assert lib.N == orc.N == 1 << p["logn"] and lib.slots == orc.slots == orc.N
+        lib.GenerateSecretKey()
+        lib.GeneratePublicKey()
+        lib.GenerateRelinearizationKey()
+        return lib, orc
+
+    return _ci_small_cache.get(make)
 
 
 def _ntt_roundtrip(torch, lib, orc, host):

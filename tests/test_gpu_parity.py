@@ -3,7 +3,7 @@ the same inputs.  Integer ring arithmetic must match bit for bit."""
 import numpy as np
 import pytest
 
-from tests.helpers import SMALL, rand_ct
+from tests.helpers import SMALL, rand_ct, SchemeCache
 
 pytestmark = pytest.mark.gpu
 
@@ -16,16 +16,25 @@ def torch_cuda():
     return torch
 
 
-@pytest.fixture(scope="module")
+_small_cache = SchemeCache()
+
+
+@pytest.fixture
 def small(torch_cuda, oracle_mod):
-    from orion_amd.backend import HipLibrary
-    lib = HipLibrary().new_scheme(SMALL["logn"], SMALL["logq"], SMALL["logp"], 40, h=192, seed=1234)
-    mods = lib.moduli()
-    orc = oracle_mod.Oracle(SMALL["logn"], mods, len(SMALL["logq"]), len(SMALL["logp"]))
-    lib.GenerateSecretKey()
-    lib.GeneratePublicKey()
-    lib.GenerateRelinearizationKey()
-    return lib, orc
+    """function-scoped view of a module-wide scheme, rebuilt if another test
+    replaced the process-global scheme (order-independent)"""
+
+    def make():
+        from orion_amd.backend import HipLibrary
+        lib = HipLibrary().new_scheme(SMALL["logn"], SMALL["logq"], SMALL["logp"], 40, h=192, seed=1234)
+        mods = lib.moduli()
+        orc = oracle_mod.Oracle(SMALL["logn"], mods, len(SMALL["logq"]), len(SMALL["logp"]))
+        lib.GenerateSecretKey()
+        lib.GeneratePublicKey()
+        lib.GenerateRelinearizationKey()
+        return lib, orc
+
+    return _small_cache.get(make)
 
 
 @pytest.mark.parametrize("logn", [13, 14, 15, 16])

@@ -50,6 +50,25 @@ def test_basis_extension_exact(kat, oracle_mod):
     c = kat["basisext"]
     got = o.basis_extend(np.array(c["x"], dtype=np.uint64), c["src"], c["dst"])
     assert got.tolist() == c["out"]
+    # the float64 quotient: Lattigo's division form, on coefficients where it
+    # differs from floor(x / S) and from a reciprocal multiply
+    for c in kat["bext_quotient"]:
+        assert any(a != b for a, b in zip(c["v_div"], c["v_rcp"]))
+        assert any(a != b for a, b in zip(c["v_div"], c["v_floor"]))
+        got = o.basis_extend(np.array(c["x"], dtype=np.uint64), c["src"], c["dst"])
+        assert got.tolist() == c["out"], c["src"]
+
+
+def test_modup_single_prime_digit_centered(kat, oracle_mod):
+    """DecomposeAndSplit's single-prime digit extends x - s for x >= s >> 1"""
+    o = _chain(kat, oracle_mod)
+    c = kat["modup_single"]
+    got = o.modup_digit(np.array(c["x"], dtype=np.uint64), c["src"], c["dst"])
+    assert got.tolist() == c["out"]
+    # wider digits: the same as ModUpExact
+    c = kat["bext_quotient"][0]
+    x = np.array(c["x"], dtype=np.uint64)
+    assert np.array_equal(o.modup_digit(x, c["src"], c["dst"]), o.basis_extend(x, c["src"], c["dst"]))
 
 
 def test_rescale_round(kat, oracle_mod):

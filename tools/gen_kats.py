@@ -7,6 +7,13 @@ backend.  The reference holds no golden vectors for this path (SURVEY.md §4,
   * rescale:   round(x / q_l) of the CRT-reconstructed, centered integer
   * moddown:   floor(x / P) of x in [0, Q*P)
   * basisext:  exact residues of x in [0, S) modulo other primes
+  * bext_quotient: Lattigo's reconstructRNS quotient v = trunc(sum_i
+               float64(y_i) / float64(s_i)) (correctly rounded divisions in
+               source order), on coefficients x near 0 and near S where it
+               is not floor(x / S) and where a reciprocal multiply
+               y_i * (1/s_i) truncates to a different v
+  * modup_single: DecomposeAndSplit's single-prime digit, extended from the
+               centered representative (x >= s >> 1 -> x - s)
   * automorph: a(X^g) mod (X^N + 1) in the coefficient domain
   * primes:    NTT-friendly prime walk around 2^b (Lattigo GenModuli rule)
 
@@ -132,6 +139,57 @@ def crt(res, mods):
     return x % Q, Q
 
 
+def lattigo_v(ys, srcm):
+    """reconstructRNS: vi += float64(y_i) / float64(Q[i]); v = uint64(vi)"""
+    vf = 0.0
+    for y, q in zip(ys, srcm):
+        vf += float(y) / float(q)
+    return int(vf)
+
+
+def reciprocal_v(ys, srcm):
+    """the same sum with y_i * (1/s_i) (the builder's round-2 form)"""
+    vf = 0.0
+    for y, q in zip(ys, srcm):
+        vf += float(y) * (1.0 / float(q))
+    return int(vf)
+
+
+def bext_quotient_case(rng, mods, src, n):
+    """n coefficients x of the sources' product S, at least half of them ones
+    where the division form and the reciprocal form truncate differently;
+    expected outputs follow the division form"""
+    srcm = [mods[i] for i in src]
+    dst = [j for j in range(len(mods)) if j not in src]
+    S = 1
+    for q in srcm:
+        S *= q
+    qhinv = [pow(S // q, -1, q) for q in srcm]
+
+    def ys_of(x):
+        return [(x % q) * h % q for q, h in zip(srcm, qhinv)]
+
+    diff, same = [], []
+    while len(diff) < n // 2 or len(same) < n - n // 2:
+        k = rng.randrange(1 << 24)
+        x = k if rng.random() < 0.5 else S - 1 - k
+        ys = ys_of(x)
+        vd, vr = lattigo_v(ys, srcm), reciprocal_v(ys, srcm)
+        (diff if vd != vr else same).append(x)
+    xs = diff[:n // 2] + same[:n - n // 2]
+    outs, vds, vrs, vex = [], [], [], []
+    for x in xs:
+        ys = ys_of(x)
+        vd = lattigo_v(ys, srcm)
+        X = sum(y * (S // q) for y, q in zip(ys, srcm))
+        vds.append(vd)
+        vrs.append(reciprocal_v(ys, srcm))
+        vex.append(X // S)
+        outs.append([(X - vd * S) % mods[t] for t in dst])
+    return dict(src=src, dst=dst, x=[[x % q for x in xs] for q in srcm],
+                out=[[o[t] for o in outs] for t in range(len(dst))], v_div=vds, v_rcp=vrs, v_floor=vex)
+
+
 def main():
     rng = random.Random(20251016)
     os.makedirs(OUT, exist_ok=True)
@@ -166,6 +224,16 @@ def main():
     xs = [rng.randrange(S) for _ in range(n)]
     kats["basisext"] = dict(src=src, dst=dst, x=[[x % mods[i] for x in xs] for i in src],
                             out=[[x % mods[t] for x in xs] for t in dst])
+    # the float64 quotient of ModUpExact (Lattigo reconstructRNS [U]):
+    # near-integer sums, where the division form decides the bits
+    kats["bext_quotient"] = [bext_quotient_case(rng, mods, src, n)
+                             for src in ([1, 2], [0, 1, 2], [4, 5], [1, 2, 3])]
+    # single-prime digit (K = 1 digits, or the last digit of an odd level)
+    src, dst = [1], [0, 2, 3, 4, 5]
+    s1 = mods[1]
+    xs = [rng.randrange(s1) for _ in range(n - 4)] + [s1 >> 1, (s1 >> 1) - 1, 0, s1 - 1]
+    kats["modup_single"] = dict(src=src, dst=dst, x=[xs],
+                                out=[[(x - s1 if x >= s1 >> 1 else x) % mods[t] for x in xs] for t in dst])
     # rescale at level 3: coefficient-domain residues of x, expected round(xc / q3) for centered xc
     lvl = 3
     Q = 1
