@@ -390,7 +390,7 @@ def main():
 
         def dec_once():
             pt = lib.Decrypt(out_ct)
-            lib.DecodeDevice(pt, dout.data_ptr())
+            lib.decode_device(pt, dout)
             lib.DeletePlaintext(pt)
 
         client_ms = {"encode_encrypt_ms_per_batch": round(client(enc_once), 3),

@@ -199,7 +199,14 @@ int ExportCiphertext(int ct, unsigned long *out, unsigned long n);
 int ImportPlaintext(const unsigned long *data, int batch, int level, double scale);
 int ExportPlaintext(int pt, unsigned long *out, unsigned long n);
 /* the same canonical layout in device memory (e.g. a torch.uint64/int64 tensor
- * on the library's GPU): no host round trip, asynchronous on the library stream */
+ * on the library's GPU): no host round trip, asynchronous on the library stream.
+ * Ordering is the caller's: the library stream (OrionHipGetStream) must wait
+ * for the work that writes dptr before an import (and the buffer must not be
+ * freed or reused until the copy has run), and a consumer of an export must
+ * wait for the library stream.  orion_amd/backend.py does this with stream
+ * waits and record_stream; the same holds for EncodeBatchDevice's dvalues and
+ * DecodeDevice's dout.  Residues must be fully reduced in [0, q_l): kernels
+ * assume it and the import does not check. */
 int ImportCiphertextDevice(const unsigned long *dptr, int batch, int level, double scale);
 int ExportCiphertextDevice(int ct, unsigned long *dptr, unsigned long n);
 int ExportSecretKey(unsigned long *out, unsigned long n);                  /* [L+K][N]           */

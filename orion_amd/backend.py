@@ -362,16 +362,51 @@ class HipLibrary:
         h = self.lib.ImportCiphertext(arr.ctypes.data_as(P(c_ulong)), B, nl - 1, float(scale))
         return self._chk(h, "ImportCiphertext")
 
+    # Device-pointer calls run asynchronously on the library stream, which
+    # torch does not know about: order them against the tensor's stream both
+    # ways, and keep an input tensor from being recycled by torch's caching
+    # allocator before the copy that reads it has run.
+    def _streams(self, t):
+        import torch
+        cur = torch.cuda.current_stream(t.device)
+        ptr = self.OrionHipGetStream()
+        lib_s = torch.cuda.ExternalStream(ptr, device=t.device) if ptr else torch.cuda.default_stream(t.device)
+        return cur, lib_s
+
+    def _before_read(self, t):
+        cur, lib_s = self._streams(t)
+        lib_s.wait_stream(cur)  # the producer of t runs first
+        return lib_s
+
+    def _before_write(self, t):
+        cur, lib_s = self._streams(t)
+        lib_s.wait_stream(cur)  # earlier torch work on t (allocation, readers) first
+        return cur, lib_s
+
     def import_ciphertext_device(self, t, scale):
-        """t: a contiguous [B][2][level+1][N] int64/uint64 device tensor (torch), NTT domain."""
+        """t: a contiguous [B][2][level+1][N] int64/uint64 device tensor (torch),
+        NTT domain, every residue fully reduced."""
         assert t.is_cuda and t.is_contiguous() and t.dim() == 4 and t.shape[3] == self.N and t.element_size() == 8
-        return self._chk(self.lib.ImportCiphertextDevice(t.data_ptr(), t.shape[0], t.shape[2] - 1, float(scale)),
-                         "ImportCiphertextDevice")
+        lib_s = self._before_read(t)
+        h = self._chk(self.lib.ImportCiphertextDevice(t.data_ptr(), t.shape[0], t.shape[2] - 1, float(scale)),
+                      "ImportCiphertextDevice")
+        t.record_stream(lib_s)
+        return h
 
     def export_ciphertext_device(self, ct, out):
         """Copy ciphertext `ct` into the device tensor `out` ([B][2][level+1][N], 8-byte elements)."""
         assert out.is_cuda and out.is_contiguous() and out.element_size() == 8
+        cur, lib_s = self._before_write(out)
         self._chk(self.lib.ExportCiphertextDevice(ct, out.data_ptr(), out.numel()), "ExportCiphertextDevice")
+        cur.wait_stream(lib_s)  # torch's readers of out follow the copy
+        return out
+
+    def decode_device(self, pt, out):
+        """Real parts of every slot of every image into the float64 device tensor out [B][slots]."""
+        assert out.is_cuda and out.is_contiguous() and out.dtype.itemsize == 8
+        cur, lib_s = self._before_write(out)
+        self._chk(self.lib.DecodeDevice(pt, out.data_ptr()), "DecodeDevice")
+        cur.wait_stream(lib_s)
         return out
 
     def export_plaintext(self, pt):
@@ -426,8 +461,11 @@ class HipLibrary:
     def encode_batch_device(self, dvalues, level, scale):
         """dvalues: a contiguous float32 [B][n] device tensor (torch, HBM resident)."""
         B, n = dvalues.shape
-        return self._chk(self.lib.EncodeBatchDevice(dvalues.data_ptr(), n, B, level, float(scale)),
-                         "EncodeBatchDevice")
+        lib_s = self._before_read(dvalues)
+        h = self._chk(self.lib.EncodeBatchDevice(dvalues.data_ptr(), n, B, level, float(scale)),
+                      "EncodeBatchDevice")
+        dvalues.record_stream(lib_s)
+        return h
 
     def decode_f64(self, pt):
         """Slots of every image of a plaintext, float64 [B][slots] (GPU decode)."""

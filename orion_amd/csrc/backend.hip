@@ -98,13 +98,30 @@ class DevicePool {
     return p;
   }
   void release(void* p, size_t bytes) {
-    // a buffer that predates a capture and is released inside it may still be
-    // read by the captured work: pin it with the graph's own buffers
-    if (tracking_) touched_[p] = bytes;
-    if (pins_.count(p))
+    if (pins_.count(p)) {
       parked_[p] = bytes;
-    else
-      free_[bytes].push_back(p);
+      return;
+    }
+    if (tracking_ && !touched_.count(p)) {
+      // predates the open capture: the captured work may read it at every
+      // replay, so nothing recorded later in the capture may reuse it; it is
+      // parked now and pinned with the graph's buffers at the end
+      touched_[p] = bytes;
+      parked_[p] = bytes;
+      return;
+    }
+    free_[bytes].push_back(p);
+  }
+  // a capture that failed: buffers parked for it that no graph pins go back
+  void unpark_unpinned(const std::vector<std::pair<void*, size_t>>& v) {
+    for (auto& pb : v) {
+      if (pins_.count(pb.first)) continue;
+      auto pk = parked_.find(pb.first);
+      if (pk != parked_.end()) {
+        free_[pk->second].push_back(pk->first);
+        parked_.erase(pk);
+      }
+    }
   }
   void trim() {
     hipDeviceSynchronize();
@@ -451,6 +468,7 @@ struct Context {
     auto touched = pool.end_track();
     if (e != hipSuccess || !gr) {
       if (gr) hipGraphDestroy(gr);
+      pool.unpark_unpinned(touched);
       // an invalidated capture leaves its stream unusable: end whatever is
       // still open and, for the library's own stream, start a fresh one
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -472,6 +490,7 @@ struct Context {
     const hipError_t ei = hipGraphInstantiate(&r.x, gr, nullptr, nullptr, 0);
     if (ei != hipSuccess) {
       hipGraphDestroy(gr);
+      pool.unpark_unpinned(touched);
       throw std::runtime_error(std::string("graph instantiation failed: ") + hipGetErrorString(ei));
     }
     pool.pin(touched);
@@ -3176,7 +3195,9 @@ void GenerateConsolidatedRotationKeys(int* galEls, int n) {
   API_END_VOID
 }
 // lineartransform.go:131-142: a fresh key, serialised and NOT kept (the
-// save path stores it to HDF5 and LoadRotationKey brings it back per layer)
+// save path stores it to HDF5 and LoadRotationKey brings it back per layer).
+// Like Lattigo's GenGaloisKeyNew the blob is a full-chain key (every digit over
+// every Q limb); LoadRotationKey scopes it to the level its transforms need.
 ArrayResultByte GenerateAndSerializeRotationKey(int galEl) {
   ArrayResultByte r{nullptr, 0};
   API_BEGIN
@@ -3188,7 +3209,7 @@ ArrayResultByte GenerateAndSerializeRotationKey(int galEl) {
     saved = kept->second;
     c.gks.erase(kept);
   }
-  const int level = c.hinted_level(g);
+  const int level = c.L - 1;
   c.gen_galois(g, level);
   std::vector<u64> host;
   c.download(c.gks.at(g).k, host);
@@ -3197,7 +3218,11 @@ ArrayResultByte GenerateAndSerializeRotationKey(int galEl) {
   return to_bytes(galois_key_bytes(c, g, host, level));
   API_END(r)
 }
-// lineartransform.go:145-164: unmarshal an rlwe.GaloisKey into the key set under galEl
+// lineartransform.go:145-164: unmarshal an rlwe.GaloisKey into the key set under
+// galEl.  A key asked for by a linear transform is kept only over the limbs and
+// digits of the highest level that uses it (key_hint): the digits 0..beta-1 of
+// a key made for a higher level, restricted to q_0..q_level and P, are exactly
+// the key Lattigo's gadget product reads at that level.
 void LoadRotationKey(char* data, unsigned long len, unsigned long galEl) {
   API_BEGIN
   Context& c = ctx();
@@ -3223,9 +3248,21 @@ void LoadRotationKey(char* data, unsigned long len, unsigned long galEl) {
     for (int k = 0; k < 2; ++k) get_qp(body, c, host.data() + (2 * (size_t)i + k) * qp, level + 1, "rotation key");
   }
   if (body.left()) throw std::runtime_error("rotation key blob has trailing bytes");
-  Poly k = c.alloc(2 * beta, level + 1 + c.K, 1);
+  const int tl = std::min(level, c.hinted_level(galEl)), tbeta = (tl + 1 + c.K - 1) / c.K;
+  if (tl < level) {  // keep digits < tbeta over limbs q_0..q_tl, p_0..p_{K-1}
+    const size_t tqp = (size_t)(tl + 1 + c.K) * c.N;
+    std::vector<u64> sc(2 * (size_t)tbeta * tqp);
+    for (int r = 0; r < 2 * tbeta; ++r) {
+      const u64* src = host.data() + (size_t)r * qp;
+      u64* dst = sc.data() + (size_t)r * tqp;
+      memcpy(dst, src, sizeof(u64) * (size_t)(tl + 1) * c.N);
+      memcpy(dst + (size_t)(tl + 1) * c.N, src + (size_t)(level + 1) * c.N, sizeof(u64) * (size_t)c.K * c.N);
+    }
+    host.swap(sc);
+  }
+  Poly k = c.alloc(2 * tbeta, tl + 1 + c.K, 1);
   c.upload(k, host);
-  c.gks[galEl] = EvKey{k, level};
+  c.gks[galEl] = EvKey{k, tl};
   API_END_VOID
 }
 // lineartransform.go:167-183: the diagonal's ringqp.Poly (Q at the transform's

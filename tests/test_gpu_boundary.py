@@ -115,6 +115,20 @@ def test_device_import_export(small, torch_cuda):
     lib.export_ciphertext_device(h, out)
     lib.OrionHipSynchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint64), ref)
+    # no manual synchronisation -- the wrappers order the library
+    # stream after the torch work that produces the input (a kernel on the
+    # current stream, freed right away: record_stream keeps its memory from
+    # being reused before the copy), and torch's readers after the export
+    for _ in range(3):
+        d2 = d.clone()
+        h2 = lib.import_ciphertext_device(d2, 2.0 ** 80)
+        del d2
+        junk = torch.full_like(d, -1)  # would take d2's memory if the allocator recycled it early
+        out2 = torch.zeros_like(d)
+        lib.export_ciphertext_device(h2, out2)
+        assert np.array_equal((out2 + 0).cpu().numpy().view(np.uint64), x)
+        del junk
+        lib.DeleteCiphertext(h2)
     with pytest.raises(RuntimeError, match="size mismatch"):
         lib.export_ciphertext_device(h, torch.empty((B, 2, level + 1, orc.N), dtype=torch.int64, device="cuda"))
 
@@ -212,6 +226,20 @@ def test_wire_format_rotation_key_and_diagonals(small):
     for d in idx:
         lib.LoadPlaintextDiagonal(blobs[d], lt2, d)
     assert np.array_equal(lib.export_ciphertext(lib.EvaluateLinearTransform(lt2, ct)), ref)
+
+    # a transform's key is serialised full-chain, as Lattigo's
+    # GenGaloisKeyNew marshals it, and scoped to the transform's level at load
+    gels = [ge for ge in lib.GetLinearTransformRotationKeys(lt) if ge != 1]
+    for ge in gels:
+        kb, _ = lib.GenerateAndSerializeRotationKey(ge)
+        kw = kb.view(np.uint64)
+        assert list(kw[:4]) == [ge, 2 * N, 0, dnum] and kw[6] == L
+        lib.LoadRotationKey(kb, ge)
+        assert lib.GetGaloisKeyLevel(ge) == level
+    x = lib.export_ciphertext(ct)[0]
+    got = lib.export_ciphertext(lib.EvaluateLinearTransform(lt, ct))[0]
+    gkeys = {ge: lib.export_galois_key(ge) for ge in gels}
+    assert np.array_equal(got, orc.lt_bsgs(x, level, idx, [pts[d] for d in idx], lib.GetLinearTransformN1(lt), gkeys))
 
 
 def test_key_bundle_header_checks(torch_cuda):
@@ -340,4 +368,30 @@ def test_graph_capture_replay(torch_cuda):
     lib.OrionHipGraphDestroy(g2)
     again = st.forward(ct)
     assert np.array_equal(lib.export_ciphertext(again), ref)
+    # buffers a graph reads stay its own: a handle made before the capture and
+    # deleted inside it, or deleted after it, does not hand its buffer to a
+    # later allocation while the graph can replay
+    ref_add = lib.export_ciphertext(lib.AddCiphertextNew(ct, ct))
+    y = lib.export_ciphertext(lib.MulScalarIntNew(ct, 3))
+    pre, pre2 = lib.CloneCiphertext(ct), lib.CloneCiphertext(ct)
+    lib.OrionHipGraphBegin()
+    r3 = lib.AddCiphertextNew(pre, pre)
+    lib.DeleteCiphertext(pre)  # predates the capture, released inside it
+    r4 = lib.AddCiphertextNew(pre2, pre2)
+    # in-place ops on handles older than the capture would be reapplied by every replay
+    with pytest.raises(RuntimeError, match="predates the graph capture"):
+        lib.Rescale(ct)
+    with pytest.raises(RuntimeError, match="predates the graph capture"):
+        lib.AddCiphertext(pre2, ct)
+    g3 = lib.OrionHipGraphEnd()
+    lib.DeleteCiphertext(pre2)  # deleted after the capture
+    bys = [lib.import_ciphertext(y, 2.0 ** 26) for _ in range(3)]
+    for _ in range(2):
+        lib.OrionHipGraphLaunch(g3)
+        lib.OrionHipSynchronize()
+        assert np.array_equal(lib.export_ciphertext(r3), ref_add)
+        assert np.array_equal(lib.export_ciphertext(r4), ref_add)
+        for b in bys:
+            assert np.array_equal(lib.export_ciphertext(b), y)
+    lib.OrionHipGraphDestroy(g3)
     lib.DeleteScheme()
