@@ -174,6 +174,25 @@ unsigned long OrionHipModulus(int idx);                   /* QP index space */
 int OrionHipBootstrapNumQ(int slots);
 int OrionHipBootstrapNumP(int slots);
 unsigned long OrionHipBootstrapModulus(int slots, int idx);
+/* parity access to the shared inputs of the circuit for `slots` (keys,
+ * diagonals, constants), so that the CPU oracle can restate the circuit on
+ * the same inputs (tests only).  Returns the element count written, or needed
+ * when out is NULL; -1 on error.  Items (element type):
+ *   PARAMS (long double): F, gap, K, r, degree, slots, s_y, top, L, K_P,
+ *          #trace rotations, #transforms, #cosine coefficients
+ *   COS (long double): EvalMod's Chebyshev coefficients, lowest first
+ *   TRACE (unsigned long): Galois elements of the trace
+ *   RLK / GALOIS (arg = galEl) (unsigned long): key in the full-chain layout
+ *          [dnum][2][L+K][N] of the bootstrapping chain
+ *   GALOIS_KEYS (unsigned long): every Galois element with a key
+ *   LT_INFO (arg = transform 0..5, CoeffsToSlots then SlotsToCoeffs) (long):
+ *          level, N1, #diagonals, diagonal indices
+ *   LT_DIAG (arg = transform << 32 | k) (unsigned long): k-th diagonal,
+ *          [level+1+K_P][N] NTT domain
+ *   MONO_I (unsigned long): X^(N/2) over the Q limbs, NTT domain (full slots) */
+enum { ORION_BTX_PARAMS = 0, ORION_BTX_COS, ORION_BTX_TRACE, ORION_BTX_RLK, ORION_BTX_GALOIS_KEYS,
+       ORION_BTX_GALOIS, ORION_BTX_LT_INFO, ORION_BTX_LT_DIAG, ORION_BTX_MONO_I };
+long OrionHipBootstrapExport(int slots, int what, long arg, void *out, unsigned long n);
 
 /* batch ciphertexts: one handle holds B images; ops act on the whole batch */
 int EncodeBatch(float *values, int lenPerImage, int batch, int level, unsigned long scale);

@@ -1497,6 +1497,16 @@ static pct poly_ps(poly_run *R, const long double *cf, int n, int lead, int maxd
  * out: [2][out_level+1][N]; returns out_level (-1 if level < depth). */
 int oracle_eval_poly(const oracle_ctx *c, int level, const u64 *ct, long double xscale, const double *coeffs,
                      int n, int cheb, long double target, const u64 *rlk, u64 *out, long double *out_scale) {
+  long double *cf = (long double *)malloc(sizeof(long double) * (n > 0 ? n : 1));
+  for (int i = 0; i < n; i++) cf[i] = (long double)coeffs[i];
+  int r = oracle_eval_poly_ld(c, level, ct, xscale, cf, n, cheb, target, rlk, out, out_scale);
+  free(cf);
+  return r;
+}
+
+/* the same with long double coefficients (the bootstrapping cosine's) */
+int oracle_eval_poly_ld(const oracle_ctx *c, int level, const u64 *ct, long double xscale, const long double *coeffs,
+                        int n, int cheb, long double target, const u64 *rlk, u64 *out, long double *out_scale) {
   const int deg = n - 1;
   int depth = 0;
   while ((1 << depth) <= deg) depth++;
@@ -1509,7 +1519,7 @@ int oracle_eval_poly(const oracle_ctx *c, int level, const u64 *ct, long double 
   R.rlk = rlk;
   R.cheb = cheb;
   long double *cf = (long double *)malloc(sizeof(long double) * n);
-  for (int i = 0; i < n; i++) cf[i] = (long double)coeffs[i];
+  for (int i = 0; i < n; i++) cf[i] = coeffs[i];
   u64 k[MAXMOD];
   for (int ks = 0; (2 << ks) <= deg; ks++) {
     const pct *a = ks == 0 ? &x : &R.pw[ks];
@@ -1543,4 +1553,197 @@ int oracle_eval_poly(const oracle_ctx *c, int level, const u64 *ct, long double 
   for (int i = 0; i < 256; i++) free(R.baby[i].v);
   free(cf);
   return o.level;
+}
+
+/* ------------------------------------------------------------------ */
+/* bootstrapping circuit of the HIP backend (backend.hip                 */
+/* Context::bootstrap / run_circuit; bootstrapper.go:19-80 is the call   */
+/* site, the circuit itself is this backend's), restated   */
+/* on the shared inputs in P (keys, diagonals, constants exported by     */
+/* OrionHipBootstrapExport):                                             */
+/*   c0 = F * INTT(limb 0)  (scheme context, mod q0)                     */
+/*   t  = NTT(centered lift of c0 to every Q limb of the boot chain),    */
+/*        scale q0                                                       */
+/*   gap > 1: t = gap^-1 t, then t += sigma_g(t) for each trace element  */
+/*   z  = three CoeffsToSlots transforms, each followed by a rescale     */
+/*        (the scale stays q0)                                           */
+/*   zc = sigma_{2N-1}(z)                                                */
+/*   gap > 1: y = EvalMod(z + zc)                                        */
+/*   else:    y = i EvalMod(i (zc - z)) + EvalMod(z + zc), i = X^(N/2)   */
+/*   EvalMod(u) = cosine polynomial at target 2^60, then r double angles */
+/*        y <- 2 rescale(y^2) - 1                                        */
+/*   o  = three SlotsToCoeffs transforms with rescales                   */
+/*   out = gap * o (residual top level, scheme primes)                   */
+/* ------------------------------------------------------------------ */
+static const u64 *btp_key(const oracle_btp *P, u64 g) {
+  for (int i = 0; i < P->ngk; i++)
+    if (P->galEls[i] == g) return P->gks[i];
+  return NULL;
+}
+/* sigma_g of a [2][level+1][N] ciphertext; returns -1 without a key */
+static int btp_galois(const oracle_ctx *bc, const oracle_btp *P, pct *a, u64 g) {
+  const u64 *gk = btp_key(P, g);
+  if (!gk) return -1;
+  pct o = pct_alloc(bc, a->level, a->scale);
+  oracle_rotate(bc, a->level, a->v, g, gk, o.v);
+  free(a->v);
+  *a = o;
+  return 0;
+}
+static pct pct_clone(const oracle_ctx *c, const pct *a) {
+  pct o = pct_alloc(c, a->level, a->scale);
+  memcpy(o.v, a->v, sizeof(u64) * 2 * (size_t)(a->level + 1) * c->N);
+  return o;
+}
+/* a (+ or -) b at a's level and scale */
+static void pct_addsub(const oracle_ctx *c, pct *a, const pct *b, int sub) {
+  const size_t P = (size_t)(a->level + 1) * c->N, B = (size_t)(b->level + 1) * c->N;
+  for (int comp = 0; comp < 2; comp++)
+    for (int l = 0; l <= a->level; l++)
+      for (int i = 0; i < c->N; i++) {
+        u64 *x = a->v + comp * P + (size_t)l * c->N + i;
+        const u64 y = b->v[comp * B + (size_t)l * c->N + i];
+        *x = sub ? submod(*x, y, c->mod[l]) : addmod(*x, y, c->mod[l]);
+      }
+}
+static void pct_mul_pt(const oracle_ctx *c, pct *a, const u64 *pt) {
+  const size_t P = (size_t)(a->level + 1) * c->N;
+  for (int comp = 0; comp < 2; comp++)
+    for (int l = 0; l <= a->level; l++)
+      for (int i = 0; i < c->N; i++) {
+        u64 *x = a->v + comp * P + (size_t)l * c->N + i;
+        *x = mulmod(*x, pt[(size_t)l * c->N + i], c->mod[l]);
+      }
+}
+static int btp_lt_rescale(const oracle_ctx *bc, const oracle_btp *P, int k, pct *x) {
+  if (P->lt_level[k] != x->level) return -1;
+  pct y = pct_alloc(bc, x->level, x->scale);
+  oracle_lt_bsgs(bc, x->level, x->v, P->lt_ndiag[k], P->lt_idx[k], P->lt_pts[k], P->lt_n1[k], P->ngk, P->galEls,
+                 P->gks, y.v);
+  free(x->v);
+  const long double s = x->scale;
+  *x = y;
+  pct_rescale(bc, x);
+  x->scale = s; /* diagonals at scale q_level: the rescale restores the input scale */
+  return 0;
+}
+static int btp_eval_mod(const oracle_ctx *bc, const oracle_btp *P, const pct *u, pct *y) {
+  pct o = pct_alloc(bc, u->level, 0);
+  long double sc = 0;
+  const int lv = oracle_eval_poly_ld(bc, u->level, u->v, u->scale, P->cos, P->ncos, 1, P->poly_scale, P->rlk, o.v,
+                                     &sc);
+  if (lv < 0) {
+    free(o.v);
+    return -1;
+  }
+  pct t = pct_alloc(bc, lv, sc);
+  memcpy(t.v, o.v, sizeof(u64) * 2 * (size_t)(lv + 1) * bc->N);
+  free(o.v);
+  u64 k[MAXMOD];
+  for (int j = 0; j < P->r; j++) { /* cos(2a) = 2 cos(a)^2 - 1 */
+    pct s2 = pct_mul_relin(bc, &t, &t, P->rlk);
+    free(t.v);
+    pct_rescale(bc, &s2);
+    const size_t L = (size_t)(s2.level + 1) * bc->N;
+    for (size_t i = 0; i < 2 * L; i++) {
+      const int l = (int)((i % L) / bc->N);
+      s2.v[i] = addmod(s2.v[i], s2.v[i], bc->mod[l]);
+    }
+    big_const_res(bc, -s2.scale, s2.level, k);
+    for (int l = 0; l <= s2.level; l++)
+      for (int i = 0; i < bc->N; i++) s2.v[(size_t)l * bc->N + i] = addmod(s2.v[(size_t)l * bc->N + i], k[l], bc->mod[l]);
+    t = s2;
+  }
+  *y = t;
+  return 0;
+}
+
+int oracle_bootstrap(const oracle_ctx *sc, const oracle_ctx *bc, const oracle_btp *P, int level, const u64 *ct,
+                     u64 *out) {
+  const int N = bc->N, Ls = sc->L, top = bc->L - 1;
+  if (sc->N != N || sc->mod[0] != bc->mod[0]) return -1;
+  const u64 q0 = bc->mod[0];
+  /* c0: level-0 residues of both components, coefficient domain, times F */
+  u64 *c0 = (u64 *)malloc(sizeof(u64) * 2 * N);
+  for (int comp = 0; comp < 2; comp++) {
+    memcpy(c0 + (size_t)comp * N, ct + (size_t)comp * (level + 1) * N, sizeof(u64) * N);
+    oracle_intt(sc, 0, c0 + (size_t)comp * N);
+    if (P->F > 1)
+      for (int i = 0; i < N; i++) c0[(size_t)comp * N + i] = mulmod(c0[(size_t)comp * N + i], P->F % q0, q0);
+  }
+  /* ModRaise: the centered lift (x > q0 / 2 is x - q0) to every Q limb */
+  pct t = pct_alloc(bc, top, (long double)q0);
+  for (int comp = 0; comp < 2; comp++)
+    for (int l = 0; l <= top; l++) {
+      const u64 q = bc->mod[l];
+      u64 *o = t.v + ((size_t)comp * (top + 1) + l) * N;
+      for (int i = 0; i < N; i++) {
+        const u64 x = c0[(size_t)comp * N + i];
+        const int neg = x > (q0 >> 1);
+        const u64 r = (neg ? q0 - x : x) % q;
+        o[i] = neg ? (r ? q - r : 0) : r;
+      }
+      oracle_ntt(bc, l, o);
+    }
+  free(c0);
+  int rc = 0;
+  if (P->gap > 1) { /* trace: gap^-1 t + its rotations by slots * 2^i */
+    for (int l = 0; l <= top; l++) {
+      const u64 q = bc->mod[l], gi = invmod((u64)P->gap % q, q);
+      for (int comp = 0; comp < 2; comp++)
+        for (int i = 0; i < N; i++) {
+          u64 *x = t.v + ((size_t)comp * (top + 1) + l) * N + i;
+          *x = mulmod(*x, gi, q);
+        }
+    }
+    for (int j = 0; j < P->ntrace && !rc; j++) {
+      pct r = pct_clone(bc, &t);
+      rc = btp_galois(bc, P, &r, P->trace_gal[j]);
+      if (!rc) pct_addsub(bc, &t, &r, 0);
+      free(r.v);
+    }
+  }
+  for (int k = 0; k < 3 && !rc; k++) rc = btp_lt_rescale(bc, P, k, &t); /* CoeffsToSlots */
+  pct y = {0, 0, NULL};
+  if (!rc) {
+    pct zc = pct_clone(bc, &t);
+    rc = btp_galois(bc, P, &zc, 2 * (u64)N - 1);
+    if (!rc && P->gap > 1) {
+      pct u = pct_clone(bc, &t);
+      pct_addsub(bc, &u, &zc, 0);
+      rc = btp_eval_mod(bc, P, &u, &y);
+      free(u.v);
+    } else if (!rc) {
+      pct re = pct_clone(bc, &t), im = pct_clone(bc, &zc);
+      pct_addsub(bc, &re, &zc, 0);
+      pct_addsub(bc, &im, &t, 1);
+      pct_mul_pt(bc, &im, P->mono_i);
+      pct yr, yi;
+      rc = btp_eval_mod(bc, P, &re, &yr);
+      if (!rc) rc = btp_eval_mod(bc, P, &im, &yi);
+      if (!rc) {
+        pct_mul_pt(bc, &yi, P->mono_i);
+        if (yr.level != yi.level) rc = -1;
+        else pct_addsub(bc, &yi, &yr, 0);
+        y = yi;
+        free(yr.v);
+      }
+      free(re.v);
+      free(im.v);
+    }
+    free(zc.v);
+  }
+  free(t.v);
+  for (int k = 3; k < 6 && !rc; k++) rc = btp_lt_rescale(bc, P, k, &y); /* SlotsToCoeffs */
+  if (!rc && y.level != Ls - 1) rc = -1;
+  if (!rc) { /* post-scale gap (Orion bootstrapper.go:73-74), on the scheme's primes */
+    for (int comp = 0; comp < 2; comp++)
+      for (int l = 0; l < Ls; l++) {
+        const u64 q = bc->mod[l], g = (u64)P->gap % q;
+        for (int i = 0; i < N; i++)
+          out[((size_t)comp * Ls + l) * N + i] = mulmod(y.v[((size_t)comp * (y.level + 1) + l) * N + i], g, q);
+      }
+  }
+  free(y.v);
+  return rc;
 }

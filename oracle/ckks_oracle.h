@@ -169,6 +169,37 @@ int oracle_eval_poly(const oracle_ctx *ctx, int level, const uint64_t *ct,
                      long double target, const uint64_t *rlk, uint64_t *out,
                      long double *out_scale);
 
+int oracle_eval_poly_ld(const oracle_ctx *ctx, int level, const uint64_t *ct,
+                        long double xscale, const long double *coeffs, int n, int cheb,
+                        long double target, const uint64_t *rlk, uint64_t *out,
+                        long double *out_scale);
+
+/* ---- bootstrapping: the HIP backend's circuit (backend.hip run_circuit,
+ * reached from bootstrapper.go:61-80), restated on shared inputs exported
+ * by OrionHipBootstrapExport.  sc: the scheme's context (its Q primes are the
+ * first L primes of bc); bc: the bootstrapping chain.  ct: [2][level+1][N]
+ * (scheme); out: [2][L_scheme][N] at the residual top level.  Returns 0, or
+ * -1 when an input is missing or a level does not match. ---- */
+typedef struct oracle_btp {
+  int gap, K, r;                    /* gap = N / (2 slots) */
+  uint64_t F;                       /* message pre-scale before ModRaise */
+  int ncos;
+  const long double *cos;           /* EvalMod Chebyshev coefficients */
+  long double poly_scale;           /* EvalMod polynomial target scale (2^60) */
+  int ntrace;
+  const uint64_t *trace_gal;
+  int lt_level[6], lt_n1[6], lt_ndiag[6]; /* 0..2 CoeffsToSlots, 3..5 SlotsToCoeffs */
+  const int *lt_idx[6];
+  const uint64_t *const *lt_pts[6];
+  const uint64_t *mono_i;           /* X^(N/2) over the Q limbs (NTT), full slots */
+  int ngk;
+  const uint64_t *galEls;
+  const uint64_t *const *gks;       /* Galois keys of bc, layout as evk */
+  const uint64_t *rlk;              /* relinearisation key of bc */
+} oracle_btp;
+int oracle_bootstrap(const oracle_ctx *sc, const oracle_ctx *bc, const oracle_btp *P,
+                     int level, const uint64_t *ct, uint64_t *out);
+
 /* coefficient-wise helpers used by tests */
 void oracle_mul_coeffs(const oracle_ctx *ctx, const int *mods, int nl,
                        const uint64_t *a, const uint64_t *b, uint64_t *out);

@@ -22,6 +22,16 @@ _dblp = ctypes.POINTER(ctypes.c_double)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
 
 
+class OracleBtp(ctypes.Structure):
+    """oracle_btp (ckks_oracle.h): the bootstrapping circuit's shared inputs."""
+    _fields_ = [("gap", ctypes.c_int), ("K", ctypes.c_int), ("r", ctypes.c_int), ("F", ctypes.c_uint64),
+                ("ncos", ctypes.c_int), ("cos", ctypes.POINTER(ctypes.c_longdouble)),
+                ("poly_scale", ctypes.c_longdouble), ("ntrace", ctypes.c_int), ("trace_gal", _u64p),
+                ("lt_level", ctypes.c_int * 6), ("lt_n1", ctypes.c_int * 6), ("lt_ndiag", ctypes.c_int * 6),
+                ("lt_idx", _intp * 6), ("lt_pts", ctypes.POINTER(_u64p) * 6), ("mono_i", _u64p),
+                ("ngk", ctypes.c_int), ("galEls", _u64p), ("gks", ctypes.POINTER(_u64p)), ("rlk", _u64p)]
+
+
 def build():
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
 
@@ -64,6 +74,7 @@ def _load():
         "oracle_eval_poly": (ctypes.c_int, [vp, ctypes.c_int, _u64p, ctypes.c_longdouble, _dblp, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_longdouble, _u64p, _u64p,
                                             ctypes.POINTER(ctypes.c_longdouble)]),
+        "oracle_bootstrap": (ctypes.c_int, [vp, vp, ctypes.POINTER(OracleBtp), ctypes.c_int, _u64p, _u64p]),
         "oracle_chacha20_block": (None, [_u32p, ctypes.c_uint32, _u32p, _u32p]),
         "oracle_enc_key": (None, [ctypes.c_uint64, _u32p]),
         "oracle_gauss_cdt": (None, [ctypes.c_double, ctypes.c_int, _u64p]),
@@ -284,6 +295,44 @@ class Oracle:
         if lv < 0:
             raise ValueError("level < depth")
         return out[:2 * (lv + 1) * self.N].reshape(2, lv + 1, self.N).copy(), lv, osc.value
+
+    def bootstrap(self, boot, inputs, ct, level):
+        """The HIP backend's bootstrapping circuit restated (oracle_bootstrap):
+        self = the scheme's oracle, boot = the bootstrapping chain's oracle,
+        inputs = the circuit's shared inputs (tests: HipLibrary.bootstrap_export),
+        ct [2][level+1][N].  Returns [2][L][N] at the residual top level."""
+        keep = []
+
+        def u64arr(a):
+            a = np.ascontiguousarray(a, dtype=np.uint64)
+            keep.append(a)
+            return _p(a)
+
+        P = OracleBtp()
+        P.gap, P.K, P.r, P.F = inputs["gap"], inputs["K"], inputs["r"], inputs["F"]
+        cos = np.ascontiguousarray(inputs["cos"], dtype=np.longdouble)  # the 80-bit values, not via double
+        keep.append(cos)
+        P.ncos, P.cos = len(cos), cos.ctypes.data_as(ctypes.POINTER(ctypes.c_longdouble))
+        P.poly_scale = inputs["poly_scale"]
+        P.ntrace, P.trace_gal = len(inputs["trace"]), u64arr(inputs["trace"] if len(inputs["trace"]) else [0])
+        for k, lt in enumerate(inputs["lts"]):
+            P.lt_level[k], P.lt_n1[k], P.lt_ndiag[k] = lt["level"], lt["N1"], len(lt["idx"])
+            ia = _ip(lt["idx"])
+            pa = (_u64p * len(lt["pts"]))(*[u64arr(x) for x in lt["pts"]])
+            keep += [ia, pa]
+            P.lt_idx[k], P.lt_pts[k] = ia, pa
+        P.mono_i = u64arr(inputs["mono_i"]) if inputs.get("mono_i") is not None else None
+        gels = list(inputs["gks"].keys())
+        P.ngk, P.galEls = len(gels), u64arr(gels)
+        ka = (_u64p * len(gels))(*[u64arr(inputs["gks"][g]) for g in gels])
+        keep.append(ka)
+        P.gks, P.rlk = ka, u64arr(inputs["rlk"])
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        out = np.zeros((2, self.L, self.N), dtype=np.uint64)
+        rc = lib().oracle_bootstrap(self._h, boot._h, ctypes.byref(P), level, _p(ct), _p(out))
+        if rc != 0:
+            raise ValueError("oracle_bootstrap: missing input or level mismatch")
+        return out
 
     def encrypt_pk(self, seed, enc, image, pk, pt, level):
         """The HIP backend's public-key encryption of image `image` in

@@ -150,6 +150,7 @@ SIGNATURES = {
     "OrionHipBootstrapNumQ": ([c_int], c_int),
     "OrionHipBootstrapNumP": ([c_int], c_int),
     "OrionHipBootstrapModulus": ([c_int, c_int], c_ulong),
+    "OrionHipBootstrapExport": ([c_int, c_int, ctypes.c_long, c_void_p, c_ulong], ctypes.c_long),
     "EncodeBatch": ([P(c_float), c_int, c_int, c_int, c_ulong], c_int),
     "EncodeBatchDevice": ([c_void_p, c_int, c_int, c_int, c_double], c_int),
     "DecodeDevice": ([c_int, c_void_p], c_int),
@@ -347,6 +348,18 @@ class HipLibrary:
             raise RuntimeError(f"no bootstrapper found for slot count: {slots}")
         m = [int(self.OrionHipBootstrapModulus(slots, i)) for i in range(nq + npr)]
         return m[:nq], m[nq:]
+
+    BTX = dict(params=0, cos=1, trace=2, rlk=3, galois_keys=4, galois=5, lt_info=6, lt_diag=7, mono_i=8)
+
+    def bootstrap_export(self, slots, what, arg=0):
+        """A bootstrapper's shared inputs for the CPU oracle (OrionHipBootstrapExport)."""
+        w = self.BTX[what]
+        n = self._chk(self.lib.OrionHipBootstrapExport(slots, w, arg, None, 0), "OrionHipBootstrapExport")
+        dt = {0: np.longdouble, 1: np.longdouble, 6: np.int64}.get(w, np.uint64)
+        out = np.zeros(n, dtype=dt)
+        self._chk(self.lib.OrionHipBootstrapExport(slots, w, arg, out.ctypes.data_as(c_void_p), n),
+                  "OrionHipBootstrapExport")
+        return out
 
     def export_ciphertext(self, ct):
         B, lvl = self.GetCiphertextBatch(ct), self.GetCiphertextLevel(ct)

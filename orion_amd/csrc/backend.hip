@@ -3427,6 +3427,127 @@ unsigned long OrionHipBootstrapModulus(int slots, int i) {
   return (b && i >= 0 && i < (int)b->mods.size()) ? b->mods[i] : 0;
 }
 
+// an evaluation key in the full-chain layout [dnum][2][L+K][N]: a key made for
+// a lower level fills its digits and limbs, the rest is zero
+static void export_evk_full(Context& c, const EvKey& k, unsigned long* out, unsigned long n) {
+  if (n != (unsigned long)2 * c.dnum * (c.L + c.K) * c.N) throw std::runtime_error("export buffer size mismatch");
+  std::vector<u64> host;
+  c.download(k.k, host);
+  memset(out, 0, n * 8);
+  const int beta = k.k.ncomp / 2, nl = k.k.nlimb;
+  for (int i = 0; i < 2 * beta; ++i)
+    for (int x = 0; x < nl; ++x) {
+      const int m = x <= k.level ? x : c.L + (x - k.level - 1);
+      memcpy(out + ((size_t)i * (c.L + c.K) + m) * c.N, host.data() + ((size_t)i * nl + x) * c.N, (size_t)c.N * 8);
+    }
+}
+
+// Parity access to a bootstrapper's shared inputs (tests/test_gpu_parity.py
+// bootstrapping parity; the CPU oracle restates the circuit from them):
+// returns the element count written (or needed, out = NULL), -1 on error.
+long OrionHipBootstrapExport(int slots, int what, long arg, void* out, unsigned long n) {
+  API_BEGIN
+  Context& c = ctx();
+  auto it = c.btps.find(slots);
+  if (it == c.btps.end()) throw std::runtime_error("no bootstrapper found for slot count: " + std::to_string(slots));
+  Context::Bootstrapper& bt = *it->second;
+  Context& b = *bt.bc;
+  auto lt_of = [&](long i) -> LinTrans& {
+    if (i < 0 || i >= (long)(bt.cts.size() + bt.stc.size())) throw std::runtime_error("bootstrap LT index out of range");
+    return i < (long)bt.cts.size() ? bt.cts[i] : bt.stc[i - bt.cts.size()];
+  };
+  switch (what) {
+    case ORION_BTX_PARAMS: {  // long double: F, gap, K, r, degree, slots, s_y, top, L, K_P, ntrace, nlt, degree+1
+      const long double v[] = {(long double)bt.F, (long double)bt.gap, (long double)bt.K, (long double)bt.r,
+                               (long double)bt.degree, (long double)bt.slots, bt.s_y, (long double)bt.top,
+                               (long double)b.L, (long double)b.K, (long double)bt.trace_gal.size(),
+                               (long double)(bt.cts.size() + bt.stc.size()), (long double)bt.cosp.c.size()};
+      const long cnt = (long)(sizeof(v) / sizeof(v[0]));
+      if (out) {
+        if (n < (unsigned long)cnt) throw std::runtime_error("export buffer too small");
+        memcpy(out, v, sizeof(v));
+      }
+      return cnt;
+    }
+    case ORION_BTX_COS: {
+      const long cnt = (long)bt.cosp.c.size();
+      if (out) {
+        if (n < (unsigned long)cnt) throw std::runtime_error("export buffer too small");
+        for (long i = 0; i < cnt; ++i) ((long double*)out)[i] = bt.cosp.c[i];
+      }
+      return cnt;
+    }
+    case ORION_BTX_TRACE: {
+      const long cnt = (long)bt.trace_gal.size();
+      if (out) {
+        if (n < (unsigned long)cnt) throw std::runtime_error("export buffer too small");
+        for (long i = 0; i < cnt; ++i) ((unsigned long*)out)[i] = bt.trace_gal[i];
+      }
+      return cnt;
+    }
+    case ORION_BTX_RLK: {
+      const long cnt = 2L * b.dnum * (b.L + b.K) * b.N;
+      if (out) export_evk_full(b, EvKey{b.rlk, b.L - 1}, (unsigned long*)out, n);
+      return cnt;
+    }
+    case ORION_BTX_GALOIS_KEYS: {  // the Galois elements with a key in the bootstrapping context
+      const long cnt = (long)b.gks.size();
+      if (out) {
+        if (n < (unsigned long)cnt) throw std::runtime_error("export buffer too small");
+        long i = 0;
+        for (auto& kv : b.gks) ((unsigned long*)out)[i++] = kv.first;
+      }
+      return cnt;
+    }
+    case ORION_BTX_GALOIS: {
+      auto kt = b.gks.find((u64)arg);
+      if (kt == b.gks.end()) throw std::runtime_error("no galois key for element " + std::to_string(arg));
+      const long cnt = 2L * b.dnum * (b.L + b.K) * b.N;
+      if (out) export_evk_full(b, kt->second, (unsigned long*)out, n);
+      return cnt;
+    }
+    case ORION_BTX_LT_INFO: {  // long: level, N1, ndiag, then the diagonal indices
+      LinTrans& T = lt_of(arg);
+      const long cnt = 3 + (long)T.idx.size();
+      if (out) {
+        if (n < (unsigned long)cnt) throw std::runtime_error("export buffer too small");
+        long* o = (long*)out;
+        o[0] = T.level, o[1] = T.N1, o[2] = (long)T.idx.size();
+        for (size_t k = 0; k < T.idx.size(); ++k) o[3 + k] = T.idx[k];
+      }
+      return cnt;
+    }
+    case ORION_BTX_LT_DIAG: {  // arg = lt * 2^32 + k: the k-th diagonal (QP plaintext [level+1+K][N])
+      LinTrans& T = lt_of(arg >> 32);
+      const long k = arg & 0xffffffffl;
+      if (k < 0 || k >= (long)T.idx.size()) throw std::runtime_error("bootstrap LT diagonal index out of range");
+      const Poly& p = T.diags.at(T.idx[k] & (b.N / 2 - 1)).poly;
+      const long cnt = (long)p.nlimb * b.N;
+      if (out) {
+        if (n != (unsigned long)cnt) throw std::runtime_error("export buffer size mismatch");
+        std::vector<u64> host;
+        b.download(p, host);
+        memcpy(out, host.data(), (size_t)cnt * 8);
+      }
+      return cnt;
+    }
+    case ORION_BTX_MONO_I: {
+      if (!bt.mono_i.buf) throw std::runtime_error("sparse-slot circuit: no X^(N/2) plaintext");
+      const long cnt = (long)bt.mono_i.nlimb * b.N;
+      if (out) {
+        if (n != (unsigned long)cnt) throw std::runtime_error("export buffer size mismatch");
+        std::vector<u64> host;
+        b.download(bt.mono_i, host);
+        memcpy(out, host.data(), (size_t)cnt * 8);
+      }
+      return cnt;
+    }
+    default:
+      throw std::runtime_error("unknown bootstrap export item " + std::to_string(what));
+  }
+  API_END(-1)
+}
+
 // ---- import / export ----
 static void to_canonical(const std::vector<u64>& dev, int ncomp, int nl, int B, int N, unsigned long* out) {
   // device [c][l][b][n] -> host [b][c][l][n]
@@ -3562,19 +3683,7 @@ int ExportGaloisKey(unsigned long galEl, unsigned long* out, unsigned long n) {
   Context& c = ctx();
   auto it = c.gks.find(galEl);
   if (it == c.gks.end()) throw std::runtime_error("no galois key for element " + std::to_string(galEl));
-  // always the full-chain layout [dnum][2][L+K][N]: a key made for a lower
-  // level fills its digits and limbs, the rest is zero
-  if (n != (unsigned long)2 * c.dnum * (c.L + c.K) * c.N) throw std::runtime_error("export buffer size mismatch");
-  const EvKey& k = it->second;
-  std::vector<u64> host;
-  c.download(k.k, host);
-  memset(out, 0, n * 8);
-  const int beta = k.k.ncomp / 2, nl = k.k.nlimb;
-  for (int i = 0; i < 2 * beta; ++i)
-    for (int x = 0; x < nl; ++x) {
-      const int m = x <= k.level ? x : c.L + (x - k.level - 1);
-      memcpy(out + ((size_t)i * (c.L + c.K) + m) * c.N, host.data() + ((size_t)i * nl + x) * c.N, (size_t)c.N * 8);
-    }
+  export_evk_full(c, it->second, out, n);  // the full-chain layout [dnum][2][L+K][N]
   return 0;
   API_END(-1)
 }

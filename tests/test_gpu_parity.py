@@ -498,6 +498,60 @@ def test_bootstrap_functional(torch_cuda, h):
     lib.DeleteScheme()
 
 
+def _bootstrap_inputs(lib, ns):
+    """The circuit's shared inputs (keys, diagonals, constants) for the oracle."""
+    F, gap, K, r, _deg, _slots, _sy, _top, _lb, _kb, _nt, nlt, _nc = lib.bootstrap_export(ns, "params")
+    inp = dict(F=int(F), gap=int(gap), K=int(K), r=int(r), cos=lib.bootstrap_export(ns, "cos"),
+               poly_scale=2.0 ** 60, trace=lib.bootstrap_export(ns, "trace"), rlk=lib.bootstrap_export(ns, "rlk"))
+    inp["lts"] = []
+    for k in range(int(nlt)):
+        info = lib.bootstrap_export(ns, "lt_info", k)
+        level, n1, nd = (int(v) for v in info[:3])
+        inp["lts"].append(dict(level=level, N1=n1, idx=[int(v) for v in info[3:]],
+                               pts=[lib.bootstrap_export(ns, "lt_diag", (k << 32) | j) for j in range(nd)]))
+    inp["gks"] = {int(g): lib.bootstrap_export(ns, "galois", int(g)) for g in lib.bootstrap_export(ns, "galois_keys")}
+    inp["mono_i"] = lib.bootstrap_export(ns, "mono_i") if int(gap) == 1 else None
+    return inp
+
+
+@pytest.mark.parametrize("sparse", [False, True])
+def test_bootstrap_parity(torch_cuda, oracle_mod, sparse):
+    """Bootstrap bit for bit against the oracle's restatement of
+    the same circuit (oracle_bootstrap: F pre-scale, centered ModRaise, trace,
+    3 CoeffsToSlots transforms, conjugation, EvalMod = Chebyshev cosine +
+    double angles, 3 SlotsToCoeffs transforms, Orion's post-scale) on shared
+    inputs: the bootstrapping chain's keys, the transforms' diagonals and the
+    cosine coefficients, exported through OrionHipBootstrapExport.  Full slots
+    (real and imaginary EvalMod) and a sparse slot count (trace, one packed
+    EvalMod); a batch of two images."""
+    from orion_amd.backend import HipLibrary
+    logp = [60, 60]
+    lib = HipLibrary().new_scheme(13, BTP_LOGQ, logp, 40, h=192, seed=21)
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    n = lib.N // 2
+    ns = n // 8 if sparse else n
+    lib.NewBootstrapper([61, 61], ns)
+    rng = np.random.default_rng(40 + sparse)
+    vals = rng.uniform(-1, 1, (2, n)).astype(np.float32)
+    vals[:, ns:] = 0
+    ct = lib.Encrypt(lib.encode_batch(vals, 0, 1 << 40))
+    lib.DeleteCiphertext(lib.Bootstrap(ct, ns))  # every key made at the level it ends at
+    out = lib.Bootstrap(ct, ns)
+    got, x = lib.export_ciphertext(out), lib.export_ciphertext(ct)
+    inputs = _bootstrap_inputs(lib, ns)
+    orc = oracle_mod.Oracle(13, lib.moduli(), len(BTP_LOGQ), len(logp))
+    bq, bp = lib.bootstrap_moduli(ns)
+    borc = oracle_mod.Oracle(13, bq + bp, len(bq), len(bp))
+    for b in range(2):
+        ref = orc.bootstrap(borc, inputs, x[b], 0)
+        assert np.array_equal(got[b], ref), b
+    exp = np.tile(vals[:, :ns], (1, n // ns)).astype(np.float64)
+    assert np.abs(lib.decode_f64(lib.Decrypt(out)) - exp).max() < 1e-4
+    lib.DeleteScheme()
+
+
 def test_error_contract(torch_cuda):
     """SURVEY §8b errors: where Lattigo panics (aborting the process), the
     C-ABI returns an error with a last-error string; the library stays usable
