@@ -257,7 +257,9 @@ void OrionHipProfileReset(void);
 
 /* raw kernel entry for the roofline microbenchmark and parity tests:
  * in-place NTT/INTT of `nlimb` limbs x `batch` images at device pointer
- * (layout [limb][batch][N]), limb l under QP modulus index mods[l] */
+ * (layout [limb][batch][N]), limb l under QP modulus index mods[l];
+ * inverse bit 0: INTT; bit 1: out of place, into the nlimb x batch limbs
+ * that follow the input */
 int OrionHipNTT(unsigned long *dptr, int nlimb, int batch, const int *mods, int inverse);
 
 #ifdef __cplusplus

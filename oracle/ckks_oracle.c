@@ -1504,6 +1504,13 @@ int oracle_eval_poly(const oracle_ctx *c, int level, const u64 *ct, long double 
   return r;
 }
 
+/* long double scales passed by address (80-bit values through ctypes) */
+int oracle_eval_poly_ldp(const oracle_ctx *c, int level, const u64 *ct, const long double *xscale,
+                         const double *coeffs, int n, int cheb, const long double *target, const u64 *rlk, u64 *out,
+                         long double *out_scale) {
+  return oracle_eval_poly(c, level, ct, *xscale, coeffs, n, cheb, *target, rlk, out, out_scale);
+}
+
 /* the same with long double coefficients (the bootstrapping cosine's) */
 int oracle_eval_poly_ld(const oracle_ctx *c, int level, const u64 *ct, long double xscale, const long double *coeffs,
                         int n, int cheb, long double target, const u64 *rlk, u64 *out, long double *out_scale) {

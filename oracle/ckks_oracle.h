@@ -169,6 +169,10 @@ int oracle_eval_poly(const oracle_ctx *ctx, int level, const uint64_t *ct,
                      long double target, const uint64_t *rlk, uint64_t *out,
                      long double *out_scale);
 
+int oracle_eval_poly_ldp(const oracle_ctx *ctx, int level, const uint64_t *ct,
+                         const long double *xscale, const double *coeffs, int n, int cheb,
+                         const long double *target, const uint64_t *rlk, uint64_t *out,
+                         long double *out_scale);
 int oracle_eval_poly_ld(const oracle_ctx *ctx, int level, const uint64_t *ct,
                         long double xscale, const long double *coeffs, int n, int cheb,
                         long double target, const uint64_t *rlk, uint64_t *out,

@@ -74,6 +74,9 @@ def _load():
         "oracle_eval_poly": (ctypes.c_int, [vp, ctypes.c_int, _u64p, ctypes.c_longdouble, _dblp, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_longdouble, _u64p, _u64p,
                                             ctypes.POINTER(ctypes.c_longdouble)]),
+        "oracle_eval_poly_ldp": (ctypes.c_int, [vp, ctypes.c_int, _u64p, ctypes.POINTER(ctypes.c_longdouble), _dblp,
+                                                ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_longdouble), _u64p,
+                                                _u64p, ctypes.POINTER(ctypes.c_longdouble)]),
         "oracle_bootstrap": (ctypes.c_int, [vp, vp, ctypes.POINTER(OracleBtp), ctypes.c_int, _u64p, _u64p]),
         "oracle_chacha20_block": (None, [_u32p, ctypes.c_uint32, _u32p, _u32p]),
         "oracle_enc_key": (None, [ctypes.c_uint64, _u32p]),
@@ -333,6 +336,22 @@ class Oracle:
         if rc != 0:
             raise ValueError("oracle_bootstrap: missing input or level mismatch")
         return out
+
+    def eval_poly_ld(self, ct, level, scale, coeffs, cheb, target, rlk):
+        """eval_poly with 80-bit scales (numpy longdouble in and out, not via double)."""
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        cf = np.ascontiguousarray(coeffs, dtype=np.float64)
+        out = np.zeros(2 * (level + 1) * self.N, dtype=np.uint64)
+        xs = np.array([scale], dtype=np.longdouble)
+        tg = np.array([target], dtype=np.longdouble)
+        osc = np.zeros(1, dtype=np.longdouble)
+        ldp = ctypes.POINTER(ctypes.c_longdouble)
+        lv = lib().oracle_eval_poly_ldp(self._h, level, _p(ct), xs.ctypes.data_as(ldp), cf.ctypes.data_as(_dblp),
+                                        len(cf), int(cheb), tg.ctypes.data_as(ldp), _p(np.ascontiguousarray(rlk)),
+                                        _p(out), osc.ctypes.data_as(ldp))
+        if lv < 0:
+            raise ValueError("level < depth")
+        return out[:2 * (lv + 1) * self.N].reshape(2, lv + 1, self.N).copy(), lv, osc[0]
 
     def encrypt_pk(self, seed, enc, image, pk, pt, level):
         """The HIP backend's public-key encryption of image `image` in

@@ -144,16 +144,20 @@ class OrionStream:
         return self.arrays["input"]
 
     # -- forward: the timed net(ct) ------------------------------------------------
-    def forward(self, ct_in, hook=None):
-        """hook(event, handle): called after every replayed op (debugging)."""
+    def forward(self, ct_in, hook=None, stop_after=None):
+        """hook(event, handle): called after every replayed op (debugging).
+        stop_after: index of a forward event; the handle that event produced is
+        returned (the stream's other temporaries are deleted)."""
         lib = self.lib
         in_ids = self.meta["input_ids"]
         ct_map = {in_ids[0]: ct_in}
         skipped_pts = set()
         owned = set()
+        fi = -1
         for ev in self._events:
             if ev["phase"] != "forward":
                 continue
+            fi += 1
             op, args, ret = ev["op"], ev["args"], ev["ret"]
             if op in ("Decrypt", "Decode"):  # debug decryptions of the fork: not operator semantics
                 if op == "Decrypt":
@@ -188,8 +192,9 @@ class OrionStream:
                 if op.endswith("New") or op in _NEW_CT:
                     owned.add(h)
                 ct_map[ret] = h
-        out_ids = self.meta["output_ids"]
-        out = ct_map[out_ids[0]]
+            if stop_after is not None and fi == stop_after:
+                break
+        out = ct_map[ret] if stop_after is not None else ct_map[self.meta["output_ids"][0]]
         for rid, h in ct_map.items():
             if h != out and h in owned:
                 lib.DeleteCiphertext(h)

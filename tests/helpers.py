@@ -32,3 +32,19 @@ class SchemeCache:
             self.val = None
             self.val = make()
         return self.val
+
+
+def bootstrap_inputs(lib, ns):
+    """The circuit's shared inputs (keys, diagonals, constants) for the oracle."""
+    F, gap, K, r, _deg, _slots, _sy, _top, _lb, _kb, _nt, nlt, _nc = lib.bootstrap_export(ns, "params")
+    inp = dict(F=int(F), gap=int(gap), K=int(K), r=int(r), cos=lib.bootstrap_export(ns, "cos"),
+               poly_scale=2.0 ** 60, trace=lib.bootstrap_export(ns, "trace"), rlk=lib.bootstrap_export(ns, "rlk"))
+    inp["lts"] = []
+    for k in range(int(nlt)):
+        info = lib.bootstrap_export(ns, "lt_info", k)
+        level, n1, nd = (int(v) for v in info[:3])
+        inp["lts"].append(dict(level=level, N1=n1, idx=[int(v) for v in info[3:]],
+                               pts=[lib.bootstrap_export(ns, "lt_diag", (k << 32) | j) for j in range(nd)]))
+    inp["gks"] = {int(g): lib.bootstrap_export(ns, "galois", int(g)) for g in lib.bootstrap_export(ns, "galois_keys")}
+    inp["mono_i"] = lib.bootstrap_export(ns, "mono_i") if int(gap) == 1 else None
+    return inp

@@ -15,7 +15,7 @@ streams at the BASELINE configs.
 import numpy as np
 import pytest
 
-from tests.helpers import SMALL, rand_ct, SchemeCache
+from tests.helpers import SMALL, rand_ct, SchemeCache, bootstrap_inputs
 
 pytestmark = pytest.mark.gpu
 
@@ -308,6 +308,44 @@ def test_resnet20_end_to_end(torch_cuda):
     exp = st.arrays["expected_output"].reshape(-1)
     assert np.abs(res - exp).mean() < 0.005, (res, exp)
     assert np.argmax(res) == np.argmax(exp)
+    st.lib.DeleteScheme()
+
+
+def test_resnet20_n13_prefix_matches_cpu_oracle_replay(torch_cuda, oracle_mod):
+    """the ResNet-20 N=2^13 op stream (configs/resnet.yml) from
+    the input through its first Bootstrap -- 20 linear transforms, 12
+    composite-minimax polynomial stages, plaintext/scalar ops with scale
+    matching, the bootstrap -- replayed on the GPU and on the CPU oracle
+    (oracle/replay_cpu.py, scales tracked in long double like the backend's)
+    with the same keys, bootstrapping inputs and input ciphertext: bit for bit,
+    same level and scale."""
+    from orion_amd.replay import OrionStream
+    from oracle.replay_cpu import CpuStream
+    st = OrionStream("resnet20_n13", seed=31)
+    st.keygen()
+    st.compile()
+    lib = st.lib
+    fwd = [e for e in st.trace["events"] if e["phase"] == "forward"]
+    stop = next(i for i, e in enumerate(fwd) if e["op"] == "Bootstrap")
+    ct = st.encrypt_batch(st.reference_input())
+    x = lib.export_ciphertext(ct)[0]
+    # first pass: every Galois key is made at the level it ends at
+    lib.DeleteCiphertext(st.forward(lib.CloneCiphertext(ct), stop_after=stop))
+    out_h = st.forward(lib.CloneCiphertext(ct), stop_after=stop)
+    out = lib.export_ciphertext(out_h)[0]
+    cpu = CpuStream("resnet20_n13")
+    cpu.sk = lib.export_secret_key()
+    cpu.rlk = lib.export_relin_key()
+    cpu.key_source = lib.export_galois_key
+    cpu.compile(keys=False, lazy=True)
+    slots = fwd[stop]["args"][1]
+    bq, bp = lib.bootstrap_moduli(slots)
+    cpu.bootstrappers[slots] = (oracle_mod.Oracle(13, bq + bp, len(bq), len(bp)), bootstrap_inputs(lib, slots))
+    enc = [e for e in cpu.trace["events"] if e["phase"] == "input" and e["op"] == "Encode"][0]
+    ref, lvl, scale = cpu.forward((x, x.shape[1] - 1, enc["args"][2]), stop_after=stop)
+    assert lib.GetCiphertextLevel(out_h) == lvl
+    assert lib.GetCiphertextScaleF(out_h) == float(scale)
+    assert np.array_equal(out, ref)
     st.lib.DeleteScheme()
 
 

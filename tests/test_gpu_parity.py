@@ -3,7 +3,7 @@ the same inputs.  Integer ring arithmetic must match bit for bit."""
 import numpy as np
 import pytest
 
-from tests.helpers import SMALL, rand_ct, SchemeCache
+from tests.helpers import SMALL, rand_ct, SchemeCache, bootstrap_inputs
 
 pytestmark = pytest.mark.gpu
 
@@ -498,22 +498,6 @@ def test_bootstrap_functional(torch_cuda, h):
     lib.DeleteScheme()
 
 
-def _bootstrap_inputs(lib, ns):
-    """The circuit's shared inputs (keys, diagonals, constants) for the oracle."""
-    F, gap, K, r, _deg, _slots, _sy, _top, _lb, _kb, _nt, nlt, _nc = lib.bootstrap_export(ns, "params")
-    inp = dict(F=int(F), gap=int(gap), K=int(K), r=int(r), cos=lib.bootstrap_export(ns, "cos"),
-               poly_scale=2.0 ** 60, trace=lib.bootstrap_export(ns, "trace"), rlk=lib.bootstrap_export(ns, "rlk"))
-    inp["lts"] = []
-    for k in range(int(nlt)):
-        info = lib.bootstrap_export(ns, "lt_info", k)
-        level, n1, nd = (int(v) for v in info[:3])
-        inp["lts"].append(dict(level=level, N1=n1, idx=[int(v) for v in info[3:]],
-                               pts=[lib.bootstrap_export(ns, "lt_diag", (k << 32) | j) for j in range(nd)]))
-    inp["gks"] = {int(g): lib.bootstrap_export(ns, "galois", int(g)) for g in lib.bootstrap_export(ns, "galois_keys")}
-    inp["mono_i"] = lib.bootstrap_export(ns, "mono_i") if int(gap) == 1 else None
-    return inp
-
-
 @pytest.mark.parametrize("sparse", [False, True])
 def test_bootstrap_parity(torch_cuda, oracle_mod, sparse):
     """Bootstrap bit for bit against the oracle's restatement of
@@ -540,7 +524,7 @@ def test_bootstrap_parity(torch_cuda, oracle_mod, sparse):
     lib.DeleteCiphertext(lib.Bootstrap(ct, ns))  # every key made at the level it ends at
     out = lib.Bootstrap(ct, ns)
     got, x = lib.export_ciphertext(out), lib.export_ciphertext(ct)
-    inputs = _bootstrap_inputs(lib, ns)
+    inputs = bootstrap_inputs(lib, ns)
     orc = oracle_mod.Oracle(13, lib.moduli(), len(BTP_LOGQ), len(logp))
     bq, bp = lib.bootstrap_moduli(ns)
     borc = oracle_mod.Oracle(13, bq + bp, len(bq), len(bp))

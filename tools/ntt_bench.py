@@ -1,7 +1,7 @@
 """NTT kernel microbenchmark (GPU): per-launch time and algorithmic GB/s
 (16 N bytes per limb-transform) for the float64 path (40-bit moduli), the
 integer path (60-bit moduli) and a LoLA-like mix, at several job counts.
-Usage: python tools/ntt_bench.py   (env: LOGN, JOBS, ORION_LIB, TAG;
+Usage: python tools/ntt_bench.py   (env: LOGN, JOBS, ORION_LIB, TAG, OOP=1 out-of-place forward;
 ORION_NTT_ORDER selects the job order of the library under test)"""
 import ctypes
 import os
@@ -26,18 +26,21 @@ def main():
     only = os.environ.get("KINDS")
     if only:
         kinds = [k for k in kinds if k[0].split("(")[0] in only.split(",")]
+    oop = os.environ.get("OOP") == "1"  # forward out of place (the half-limb kernel's launches)
     for kind, mset in kinds:
         for jobs in [int(j) for j in os.environ.get("JOBS", "256,1024,4096").split(",")]:
             nl = len(mset)
             B = jobs // nl
             rng = np.random.default_rng(0)
             host = np.stack([rng.integers(0, mods[m], (B, N), dtype=np.uint64) for m in mset])
+            if oop:  # out of place: results into a second buffer right after the input
+                host = np.concatenate([host, np.zeros_like(host)])
             dev = torch.from_numpy(host.view(np.int64)).cuda()
             ptr = ctypes.cast(dev.data_ptr(), ctypes.POINTER(ctypes.c_ulong))
             mc = (ctypes.c_int * nl)(*mset)
             for inv in (0, 1):
                 for _ in range(3):
-                    lib.lib.OrionHipNTT(ptr, nl, B, mc, inv)
+                    lib.lib.OrionHipNTT(ptr, nl, B, mc, inv | (2 if oop and not inv else 0))
                 lib.OrionHipSynchronize()
                 s = torch.cuda.Stream(device=0)
                 e0 = torch.cuda.Event(enable_timing=True)
@@ -47,7 +50,7 @@ def main():
                 with torch.cuda.stream(s):
                     e0.record(s)
                     for _ in range(reps):
-                        lib.lib.OrionHipNTT(ptr, nl, B, mc, inv)
+                        lib.lib.OrionHipNTT(ptr, nl, B, mc, inv | (2 if oop and not inv else 0))
                     e1.record(s)
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / reps
