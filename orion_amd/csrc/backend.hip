@@ -648,7 +648,7 @@ struct Context {
   // moduli, inverse: 192 jobs 61 vs 76 us, 384 jobs 98 vs 127 us).  Forward
   // launches keep the one-pass kernel: their fused epilogues cost the
   // two-pass kernels a scratch round trip, and the LoLA bench measured them
-  // slower (tools/ntt2_tail_ab.sh)
+  // slower (profiles/r01z_ntt2_tailfwd_ab.txt)
   double ntt2_tail_eff = getenv("ORION_NTT2_TAIL_EFF") ? atof(getenv("ORION_NTT2_TAIL_EFF")) : 0.9;
   int ntt2_tail_max = getenv("ORION_NTT2_TAIL_MAX") ? atoi(getenv("ORION_NTT2_TAIL_MAX")) : 1024;
   // 1: plain forward launches (load prologue, store epilogue) follow the same

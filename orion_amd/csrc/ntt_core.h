@@ -6,12 +6,12 @@
 
 #include "ntt_arith.h"
 
-// timing-only ablation builds (tools/ntt_ablate.sh); 0 in the product:
+// timing-only ablation builds (tools/build_ablation.py + tools/ab.sh); 0 in the product:
 // bit 0 skips the butterfly rounds, bit 1 skips the LDS exchanges
 #ifndef NTT_ABLATE
 #define NTT_ABLATE 0
 #endif
-// timing switch (tools/ntt_exp.sh): NTT_LAZY skips the forward round
+// timing switch: NTT_LAZY skips the forward round
 // reductions for small float64 moduli
 #ifndef NTT_LAZY
 #define NTT_LAZY 1

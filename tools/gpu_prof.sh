@@ -13,4 +13,7 @@ ORION_NTT_LOG=gpurun_out/prof_$TAG/ntt_log_pmc_write.txt timeout -k 10 600 rocpr
 echo "write ok"
 timeout -k 10 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_SALU GRBM_GUI_ACTIVE --kernel-include-regex "ntt|lt_bsgs|lt_giant|basis_ext|ks_mac|modup_all" -d gpurun_out/prof_$TAG -o pmc_sq --output-format csv -- python bench.py $ARGS > gpurun_out/prof_${TAG}_sq.log 2>&1 || { echo "sq failed"; tail -20 gpurun_out/prof_${TAG}_sq.log; exit 1; }
 echo "sq ok"
-find gpurun_out/prof_$TAG -name "*.csv" | head -20
+
+# summarise on the box (only gpurun_out/ comes back, <= 64 MiB): the summaries go to
+# gpurun_out/summ_<tag>/ (copied into profiles/ afterwards), the raw traces are dropped
+python tools/pmc_summary.py $TAG gpurun_out/summ_$TAG && rm -f gpurun_out/prof_$TAG/*_kernel_trace.csv gpurun_out/prof_$TAG/*_counter_collection.csv

@@ -32,10 +32,16 @@ def rows(path):
         return list(csv.DictReader(f))
 
 
-def main(tag, workload="lola_n15", batch=64, logn=15):
-    d = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
-    out = os.path.join(ROOT, "profiles")
+def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
+    """resnet: the ResNet-20 N=2^16 passes of tools/gpu_resnet_prof.sh (no NTT
+    call log, no shared roofline files); out: output directory (default
+    profiles/; on the GPU box a directory under gpurun_out/, since only that
+    is copied back)."""
+    d = os.path.join(ROOT, "gpurun_out", f"prof_rn16_{tag}" if resnet else f"prof_{tag}")
+    out = out or os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
+    if resnet:
+        workload, batch, logn, tag = "resnet20_n16", 1, 16, f"{tag}_rn16"
     shutil.copy(os.path.join(d, "kt_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
     N = 1 << logn
     per = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -101,7 +107,8 @@ def main(tag, workload="lola_n15", batch=64, logn=15):
     # events count them: one call = one one-pass dispatch or one two-pass pair,
     # duration = the dispatches' summed time, priced with the logged
     # limb-transform counts; setup calls (keygen, < 64 jobs) are excluded
-    tr = sorted(rows(os.path.join(d, "kt_kernel_trace.csv")), key=lambda r: int(r["Start_Timestamp"]))
+    kt = os.path.join(d, "kt_kernel_trace.csv")
+    tr = sorted(rows(kt), key=lambda r: int(r["Start_Timestamp"])) if os.path.exists(kt) else []
     tr = [r for r in tr if "ntt" in r["Kernel_Name"]]
     n_l = 0
     n_us = n_b = 0.0
@@ -135,8 +142,10 @@ def main(tag, workload="lola_n15", batch=64, logn=15):
                    "valu_insts_per_simd_cycle": v["SQ_INSTS_VALU"] / (cyc * 1024),
                    "frac_of_single_pass_peak": v["SQ_INSTS_VALU"] / (cyc * 1024) * 2.0,
                    "wait_inst_any_per_wave_cycle": v["SQ_WAIT_INST_ANY"] / v["SQ_WAVE_CYCLES"]
-                   if v.get("SQ_WAVE_CYCLES") else None}
-    if valu:
+                   if v.get("SQ_WAVE_CYCLES") else None,
+                   "salu_per_valu_inst": v["SQ_INSTS_SALU"] / v["SQ_INSTS_VALU"]
+                   if v.get("SQ_INSTS_SALU") and v.get("SQ_INSTS_VALU") else None}
+    if valu and not resnet:
         with open(os.path.join(out, "valu_roofline.json"), "w") as f:
             json.dump({"tag": tag, "workload": workload, "batch": batch,
                        "definition": "valu_busy = sum SQ_ACTIVE_INST_VALU*4 / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs)",
@@ -146,7 +155,7 @@ def main(tag, workload="lola_n15", batch=64, logn=15):
                "kernels": {k: dict(v) for k, v in per.items()}}
     with open(os.path.join(out, f"{tag}_pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    if ratio:
+    if ratio and not resnet:
         with open(os.path.join(out, "ntt_traffic.json"), "w") as f:
             json.dump({"tag": tag, "workload": workload, "batch": batch,
                        "hbm_bytes_per_algorithmic_byte": round(ratio, 4)}, f, indent=1)
@@ -154,4 +163,7 @@ def main(tag, workload="lola_n15", batch=64, logn=15):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    a = sys.argv[1:]
+    rn = "--resnet" in a
+    a = [x for x in a if x != "--resnet"]
+    main(a[0], resnet=rn, out=a[1] if len(a) > 1 else None)

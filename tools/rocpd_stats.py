@@ -1,5 +1,7 @@
-"""Per-kernel totals from a rocprofv3 rocpd database (the default output format
-when --output-format is not given): python tools/rocpd_stats.py DB [TOP]."""
+"""Per-kernel totals from a rocprofv3 run:
+  python tools/rocpd_stats.py DB [TOP]            rocpd database (the default output format)
+  python tools/rocpd_stats.py --csv STATS [TOP]   a --stats kernel_stats.csv"""
+import csv
 import sqlite3
 import sys
 
@@ -12,9 +14,16 @@ def stats(db):
     return [(n, k, t) for n, k, t in c.execute(q)]
 
 
+def stats_csv(path):
+    with open(path) as f:
+        return [(r["Name"], int(r["Calls"]), float(r["TotalDurationNs"])) for r in csv.DictReader(f)]
+
+
 if __name__ == "__main__":
-    rows = stats(sys.argv[1])
-    top = int(sys.argv[2]) if len(sys.argv) > 2 else 12
+    args = sys.argv[1:]
+    rows = stats_csv(args[1]) if args[0] == "--csv" else stats(args[0])
+    rest = args[2:] if args[0] == "--csv" else args[1:]
+    top = int(rest[0]) if rest else 12
     tot = sum(t for _, _, t in rows)
     print(f"total {tot / 1e6:.2f} ms")
     for n, k, t in sorted(rows, key=lambda r: -r[2])[:top]:
