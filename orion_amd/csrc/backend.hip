@@ -3358,8 +3358,10 @@ int EvaluatePolynomial(int ct, int poly, unsigned long outScale) {
 }
 // polyeval.go:91-167: composite minimax sign coefficients (compile-time, host),
 // cached per (degrees, prec, logalpha, logerr) like minimaxSignMap; the last
-// polynomial is mapped from [-1, 1] to [0, 1] (halved, + 0.5).  The Remez
-// restatement works in long double, whatever `prec` asks for.
+// polynomial is mapped from [-1, 1] to [0, 1] (halved, + 0.5, inside
+// minimax_sign_composite).  The Remez restatement works in binary128 whatever
+// `prec` asks for: at prec >= 113 (orion's default is 128) the doubles are the
+// prec-bit computation's (tests/golden/minimax_sign.json).
 static std::map<std::string, std::vector<double>> g_minimax_cache;
 ArrayResultDouble GenerateMinimaxSignCoeffs(int* degrees, int n, int prec, int logalpha, int logerr, int debug) {
   ArrayResultDouble r{nullptr, 0};
@@ -3374,8 +3376,6 @@ ArrayResultDouble GenerateMinimaxSignCoeffs(int* degrees, int n, int prec, int l
   auto it = g_minimax_cache.find(key);
   if (it == g_minimax_cache.end()) {
     std::vector<std::vector<double>> polys = minimax_sign_composite(deg, logalpha);
-    for (double& c : polys.back()) c /= 2;
-    polys.back()[0] += 0.5;
     std::vector<double> flat;
     for (auto& p : polys) flat.insert(flat.end(), p.begin(), p.end());
     it = g_minimax_cache.emplace(key, flat).first;

@@ -248,150 +248,207 @@ int64_t Prng::gaussian(double sigma, double bound) {
 namespace orion {
 // ---------------------------------------------------------------------------
 // composite minimax approximation of sign (polyeval.go:91-167 ->
-// Lattigo minimax.GenMinimaxCompositePolynomial), restated with the classic
-// Remez exchange in long double.  sign is odd, so each stage is an odd
-// Chebyshev series p(x) = sum_k c_k T_{2k+1}(x) fitted to 1 on [a, 1]; every
-// stage but the last is divided by its maximum on [-1, 1] (times 1 + 2^-10),
-// so the next stage's inputs stay inside [-1, 1], and the next stage is
-// fitted on [min over [a, 1] of the scaled stage, 1].
+// Lattigo v6 bignum.GenMinimaxCompositePolynomial [U], restated; the fixture
+// tests/golden/minimax_sign.json is the same construction at `prec` = 128
+// bits in mpmath, tools/gen_minimax.py):
+//   stage i: p_i = the odd minimax fit of 1 on [a_i, 1] (= the minimax
+//   approximation of sign on [-1, -a_i] U [a_i, 1], whose even Chebyshev
+//   coefficients vanish), degree d_i, error E_i; p_i /= 1 + E_i;
+//   a_{i+1} = (1 - E_i) / (1 + E_i); a_0 = 2^-logalpha.
+// The Remez exchange runs in binary128 (__float128, 113 bits: every stage's
+// minimax polynomial is unique, so once converged far below float64
+// resolution each coefficient rounds to the same double as the 128-bit
+// computation).
 // ---------------------------------------------------------------------------
 namespace {
-typedef long double ld;
+typedef __float128 qf;
 
-ld cheb_odd_eval(const std::vector<ld>& c, ld x) {  // sum_k c_k T_{2k+1}(x)
-  ld t0 = 1, t1 = x, s = 0;
-  for (size_t n = 1, k = 0; k < c.size(); ++n) {
-    if (n & 1) s += c[k++] * t1;
-    const ld t2 = 2 * x * t1 - t0;
-    t0 = t1;
-    t1 = t2;
+qf qabs(qf x) { return x < 0 ? -x : x; }
+// sum_k c_k T_{2k+1}(x) and its derivative (T_m' = m U_{m-1})
+void cheb_odd_eval(const std::vector<qf>& c, qf x, qf& s, qf& ds) {
+  qf t0 = 1, t1 = x, u0 = 1, u1 = 2 * x;
+  s = ds = 0;
+  size_t k = 0;
+  for (int m = 1; k < c.size(); ++m) {
+    if (m & 1) {
+      s += c[k] * t1;
+      ds += c[k] * m * u0;
+      ++k;
+    }
+    const qf t2 = 2 * x * t1 - t0, u2 = 2 * x * u1 - u0;
+    t0 = t1, t1 = t2, u0 = u1, u1 = u2;
   }
-  return s;
 }
-ld cheb_T(int n, ld x) {
-  ld t0 = 1, t1 = x;
+// double-binary128 (~226 bits) for the Remez linear system alone: the last
+// stages fit 1 on a short interval near 1 (a = 0.952 for orion's ReLU), where
+// the Chebyshev columns are nearly dependent and binary128 loses the float64
+// digits of the coefficients (mpmath at 128, 192 and 256 bits agree; binary128
+// alone differs in 13 of 28 doubles).  Error-free transformations (Dekker
+// split at 57 bits for the 113-bit significand).
+struct dq {
+  qf hi, lo;
+};
+inline dq qsum(qf a, qf b) {
+  const qf s = a + b, bb = s - a;
+  return {s, (a - (s - bb)) + (b - bb)};
+}
+inline dq qfast(qf a, qf b) {
+  const qf s = a + b;
+  return {s, b - (s - a)};
+}
+inline dq qprod(qf a, qf b) {
+  const qf p = a * b, C = (qf)144115188075855873.0L;  // 2^57 + 1
+  const qf ca = C * a, ah = ca - (ca - a), al = a - ah;
+  const qf cb = C * b, bh = cb - (cb - b), bl = b - bh;
+  return {p, ((ah * bh - p) + ah * bl + al * bh) + al * bl};
+}
+inline dq operator+(dq a, dq b) {
+  dq s = qsum(a.hi, b.hi);
+  return qfast(s.hi, s.lo + a.lo + b.lo);
+}
+inline dq operator-(dq a) { return {-a.hi, -a.lo}; }
+inline dq operator-(dq a, dq b) { return a + (-b); }
+inline dq operator*(dq a, dq b) {
+  dq p = qprod(a.hi, b.hi);
+  return qfast(p.hi, p.lo + a.hi * b.lo + a.lo * b.hi);
+}
+inline dq operator/(dq a, dq b) {
+  const qf q1 = a.hi / b.hi;
+  dq r = a - b * dq{q1, 0};
+  const qf q2 = r.hi / b.hi;
+  r = r - b * dq{q2, 0};
+  const qf q3 = r.hi / b.hi;
+  return qfast(q1, q2) + dq{q3, 0};
+}
+inline dq to_dq(qf x) { return {x, 0}; }
+dq cheb_T_dq(int n, qf x) {
+  const dq x2 = to_dq(2 * x);
+  dq t0 = to_dq(1), t1 = to_dq(x);
   if (n == 0) return t0;
   for (int i = 1; i < n; ++i) {
-    const ld t2 = 2 * x * t1 - t0;
-    t0 = t1;
-    t1 = t2;
+    const dq t2 = x2 * t1 - t0;
+    t0 = t1, t1 = t2;
   }
   return t1;
 }
 // Gaussian elimination with partial pivoting, A is n x (n+1) augmented
-std::vector<ld> solve(std::vector<std::vector<ld>> A) {
+std::vector<dq> solve(std::vector<std::vector<dq>> A) {
   const int n = (int)A.size();
   for (int col = 0; col < n; ++col) {
     int piv = col;
     for (int r = col + 1; r < n; ++r)
-      if (fabsl(A[r][col]) > fabsl(A[piv][col])) piv = r;
+      if (qabs(A[r][col].hi) > qabs(A[piv][col].hi)) piv = r;
     std::swap(A[col], A[piv]);
-    if (A[col][col] == 0) throw std::runtime_error("minimax: singular Remez system");
-    for (int r = 0; r < n; ++r) {
-      if (r == col) continue;
-      const ld f = A[r][col] / A[col][col];
-      for (int k = col; k <= n; ++k) A[r][k] -= f * A[col][k];
+    if (A[col][col].hi == 0) throw std::runtime_error("minimax: singular Remez system");
+    for (int r = col + 1; r < n; ++r) {
+      const dq f = A[r][col] / A[col][col];
+      for (int k = col; k <= n; ++k) A[r][k] = A[r][k] - f * A[col][k];
     }
   }
-  std::vector<ld> x(n);
-  for (int i = 0; i < n; ++i) x[i] = A[i][n] / A[i][i];
+  std::vector<dq> x(n);
+  for (int i = n - 1; i >= 0; --i) {
+    dq v = A[i][n];
+    for (int k = i + 1; k < n; ++k) v = v - A[i][k] * x[k];
+    x[i] = v / A[i][i];
+  }
   return x;
 }
-// best odd approximation of degree <= deg of 1 on [a, 1]; returns coefficients, sets err
-std::vector<ld> remez_sign(int deg, ld a, ld& err) {
-  const int n = (deg - 1) / 2 + 1;  // odd terms T_1, T_3, ..., T_{2n-1}
-  std::vector<ld> xs(n + 1);
-  for (int i = 0; i <= n; ++i) xs[i] = (a + 1) / 2 - (1 - a) / 2 * cosl(3.14159265358979323846264338327950288L * i / n);
-  std::vector<ld> c(n, 0);
-  const int G = 4000 * n;
-  std::vector<ld> grid(G), eg(G);
-  for (int j = 0; j < G; ++j) grid[j] = (a + 1) / 2 - (1 - a) / 2 * cosl(3.14159265358979323846264338327950288L * j / (G - 1));
-  ld E = 0;
-  for (int it = 0; it < 100; ++it) {
-    std::vector<std::vector<ld>> A(n + 1, std::vector<ld>(n + 2));
+// Chebyshev-spaced point j of m on [a, 1] (the starting reference and the scan grid)
+qf cheb_pt(qf a, int j, int m) {
+  return (a + 1) / 2 - (1 - a) / 2 * (qf)cosl(3.14159265358979323846264338327950288L * j / m);
+}
+// odd minimax fit of 1 on [a, 1] with n odd terms T_1 .. T_{2n-1}:
+// coefficients (double-binary128), sets err
+std::vector<dq> remez_sign(int n, qf a, qf& err) {
+  std::vector<qf> xs(n + 1), c(n, 0);
+  std::vector<dq> cd(n);
+  for (int i = 0; i <= n; ++i) xs[i] = cheb_pt(a, i, n);
+  const int G = 64 * n;
+  std::vector<qf> grid(G + 1), dg(G + 1);
+  for (int j = 0; j <= G; ++j) grid[j] = cheb_pt(a, j, G);
+  const qf tol_rel = 1 / (qf)18446744073709551616.0L;  // 2^-64
+  const qf tol_abs = tol_rel * tol_rel * 65536 * 2;    // 2^-111: binary128's floor
+  int done = 0;
+  for (int it = 0; it < 60; ++it) {
+    std::vector<std::vector<dq>> A(n + 1, std::vector<dq>(n + 2));
     for (int i = 0; i <= n; ++i) {
-      for (int k = 0; k < n; ++k) A[i][k] = cheb_T(2 * k + 1, xs[i]);
-      A[i][n] = (i & 1) ? -1 : 1;
-      A[i][n + 1] = 1;
+      for (int k = 0; k < n; ++k) A[i][k] = cheb_T_dq(2 * k + 1, xs[i]);
+      A[i][n] = to_dq((i & 1) ? -1 : 1);
+      A[i][n + 1] = to_dq(1);
     }
-    std::vector<ld> sol = solve(A);
-    for (int k = 0; k < n; ++k) c[k] = sol[k];
-    E = fabsl(sol[n]);
-    // local extrema of e(x) = p(x) - 1 on the grid, refined by ternary search
-    for (int j = 0; j < G; ++j) eg[j] = cheb_odd_eval(c, grid[j]) - 1;
-    std::vector<ld> ex, ev;
+    std::vector<dq> sol = solve(A);
+    for (int k = 0; k < n; ++k) cd[k] = sol[k], c[k] = sol[k].hi + sol[k].lo;
+    const qf E = qabs(sol[n].hi + sol[n].lo);
+    // extrema of e = p - 1: the endpoints and the zeros of p' (bisection)
+    qf s, ds;
+    for (int j = 0; j <= G; ++j) cheb_odd_eval(c, grid[j], s, dg[j]);
+    std::vector<qf> ex{grid[0]};
     for (int j = 0; j < G; ++j) {
-      const bool l = j == 0 || fabsl(eg[j]) >= fabsl(eg[j - 1]);
-      const bool r = j == G - 1 || fabsl(eg[j]) >= fabsl(eg[j + 1]);
-      if (!(l && r)) continue;
-      ld x = grid[j];
-      if (j > 0 && j < G - 1) {
-        ld lo = grid[j - 1], hi = grid[j + 1];
-        const ld sg = eg[j] >= 0 ? 1 : -1;
-        for (int t = 0; t < 60; ++t) {
-          const ld m1 = lo + (hi - lo) / 3, m2 = hi - (hi - lo) / 3;
-          if (sg * (cheb_odd_eval(c, m1) - 1) < sg * (cheb_odd_eval(c, m2) - 1))
-            lo = m1;
-          else
-            hi = m2;
-        }
-        x = (lo + hi) / 2;
+      if (!(dg[j] == 0 || (dg[j] > 0) != (dg[j + 1] > 0))) continue;
+      qf lo = grid[j], hi = grid[j + 1];
+      const bool up = dg[j] > 0;
+      for (int b = 0; b < 90; ++b) {
+        const qf m = (lo + hi) / 2;
+        cheb_odd_eval(c, m, s, ds);
+        if ((ds > 0) == up) lo = m; else hi = m;
       }
-      const ld v = cheb_odd_eval(c, x) - 1;
-      if (!ex.empty() && ((v >= 0) == (ev.back() >= 0))) {  // same sign: keep the larger
-        if (fabsl(v) > fabsl(ev.back())) ex.back() = x, ev.back() = v;
+      ex.push_back((lo + hi) / 2);
+    }
+    ex.push_back(grid[G]);
+    std::vector<qf> px, pv;  // alternating points, the larger of equal-sign neighbours
+    for (qf x : ex) {
+      cheb_odd_eval(c, x, s, ds);
+      const qf v = s - 1;
+      if (!px.empty() && (v >= 0) == (pv.back() >= 0)) {
+        if (qabs(v) > qabs(pv.back())) px.back() = x, pv.back() = v;
         continue;
       }
-      ex.push_back(x);
-      ev.push_back(v);
+      px.push_back(x);
+      pv.push_back(v);
     }
-    while ((int)ex.size() > n + 1) {  // drop the smaller end extremum
-      if (fabsl(ev.front()) < fabsl(ev.back()))
-        ex.erase(ex.begin()), ev.erase(ev.begin());
+    while ((int)px.size() > n + 1) {  // drop the smaller end extremum
+      if (qabs(pv.front()) < qabs(pv.back()))
+        px.erase(px.begin()), pv.erase(pv.begin());
       else
-        ex.pop_back(), ev.pop_back();
+        px.pop_back(), pv.pop_back();
     }
-    ld emax = 0;
-    for (ld v : ev) emax = std::max(emax, fabsl(v));
+    if ((int)px.size() < n + 1) throw std::runtime_error("minimax: Remez lost the alternation");
+    qf emax = 0;
+    for (qf v : pv) emax = qabs(v) > emax ? qabs(v) : emax;
     err = emax;
-    if ((int)ex.size() < n + 1) break;  // cannot alternate further: keep the current solution
-    xs = ex;
-    if (emax - E <= 1e-12L * emax) break;
+    xs = px;
+    // converged: the levelled error E matches the true maximum (relative,
+    // or absolute for stages whose error is far below float64); two more
+    // exchanges after the threshold (quadratic convergence)
+    if (emax - E <= tol_rel * emax || emax - E <= tol_abs) {
+      if (++done == 3) return cd;
+    }
   }
-  return c;
+  throw std::runtime_error("minimax: Remez did not converge");
 }
 }  // namespace
 
 std::vector<std::vector<double>> minimax_sign_composite(const std::vector<int>& degrees, int logalpha) {
   std::vector<std::vector<double>> out;
-  ld a = ldexpl(1.0L, -logalpha);
+  qf a = (qf)ldexpl(1.0L, -logalpha);
   for (size_t i = 0; i < degrees.size(); ++i) {
     const int d = degrees[i];
     if (d < 1) throw std::runtime_error("minimax: degrees must be >= 1");
-    ld err = 0;
-    std::vector<ld> c = remez_sign(d, a, err);
+    qf err = 0;
+    std::vector<dq> c = remez_sign((d - 1) / 2 + 1, a, err);
     if (!(err < 1)) throw std::runtime_error("minimax: degree too small for the interval");
-    const bool last = i + 1 == degrees.size();
-    // a stage's image must stay inside the next stage's Chebyshev domain for
-    // every input in [-1, 1], including the gap (-a, a) it is not fitted on,
-    // with room for the float32 coefficients and the homomorphic noise: scale
-    // by the true maximum of |p| on [0, 1] (p is odd), times 1 + 2^-10
-    ld norm = 1;
-    if (!last) {
-      ld mx = 0, mn_fit = 2;
-      const int G = 200000;
-      for (int j = 0; j <= G; ++j) {
-        const ld x = (ld)j / G;
-        const ld v = fabsl(cheb_odd_eval(c, x));
-        mx = std::max(mx, v);
-        if (x >= a) mn_fit = std::min(mn_fit, v);
-      }
-      norm = mx * (1 + ldexpl(1.0L, -10));
-      a = mn_fit / norm;
+    const dq s = to_dq(1) + to_dq(err);
+    std::vector<dq> p(d + 1, to_dq(0));
+    for (size_t k = 0; k < c.size(); ++k) p[2 * k + 1] = c[k] / s;
+    const dq an = (to_dq(1) - to_dq(err)) / s;
+    a = an.hi + an.lo;
+    if (i + 1 == degrees.size()) {  // orion (polyeval.go:136-143): halved, + 0.5 (in prec bits, then rounded)
+      for (dq& v : p) v = v / to_dq(2);
+      p[0] = p[0] + to_dq(0.5);
     }
-    std::vector<double> p(d + 1, 0.0);
-    for (size_t k = 0; k < c.size(); ++k) p[2 * k + 1] = (double)(c[k] / norm);
-    out.push_back(p);
+    std::vector<double> pd(d + 1);
+    for (int k = 0; k <= d; ++k) pd[k] = (double)(p[k].hi + p[k].lo);
+    out.push_back(pd);
   }
   return out;
 }

@@ -38,8 +38,9 @@ std::vector<Cplx> special_fft_twiddles(int logN, bool inverse);
 // i < 2 bound, P(x) proportional to exp(-x^2 / (2 sigma^2)) on |x| <= bound
 void gauss_cdt(double sigma, int bound, u64* t);
 // composite minimax sign approximation on [-1, -2^-logalpha] U [2^-logalpha, 1]:
-// one Chebyshev coefficient vector (T_0..T_d) per degree; every stage but the
-// last is normalised into [-1, 1]
+// one Chebyshev coefficient vector (T_0..T_d) per degree; every stage is
+// divided by 1 + its minimax error (Lattigo's construction), the last one is
+// then mapped to [0, 1] (halved, + 0.5: orion's polyeval.go:136-143)
 std::vector<std::vector<double>> minimax_sign_composite(const std::vector<int>& degrees, int logalpha);
 // 256-bit ChaCha20 key of the encryption sampler, from the scheme seed
 void enc_key_from_seed(u64 seed, uint32_t key[8]);

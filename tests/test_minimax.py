@@ -1,10 +1,16 @@
 """GenerateMinimaxSignCoeffs (polyeval.go:91-167): composite minimax
 approximation of sign on [-1, -2^-logalpha] U [2^-logalpha, 1], host-side
-compile-time work, so it runs on the CPU.  Lattigo's own coefficients are not
-available here (parity unpinned): the checks are the contract the caller
-(orion/nn/activation.py:201-260, _Sign / ReLU) relies on -- one Chebyshev
-coefficient vector per degree, intermediate stages inside [-1, 1], the last
-stage mapped to [0, 1] -- and the approximation quality of the composite."""
+compile-time work, so it runs on the CPU.  Lattigo v6's
+GenMinimaxCompositePolynomial is restated [U] and pinned by the same
+construction computed at `prec` bits in mpmath (tools/gen_minimax.py ->
+tests/golden/minimax_sign.json): the doubles must be equal.  The other checks
+are the contract the caller (orion/nn/activation.py:201-260, _Sign / ReLU)
+relies on -- one Chebyshev coefficient vector per degree, intermediate stages
+inside [-1, 1], the last stage mapped to [0, 1] -- and the approximation
+quality of the composite."""
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -14,6 +20,18 @@ from orion_amd.backend import HipLibrary
 @pytest.fixture(scope="module")
 def lib():
     return HipLibrary()
+
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "minimax_sign.json")
+
+
+@pytest.mark.parametrize("case", range(3))
+def test_minimax_sign_matches_prec_bit_fixture(lib, case):
+    c = json.load(open(GOLDEN))["cases"][case]
+    got = np.array(lib.GenerateMinimaxSignCoeffs(c["degrees"], c["prec"], c["logalpha"], c["logerr"], 0))
+    exp = np.concatenate([np.array(p, dtype=np.float64) for p in c["coeffs"]])
+    assert got.shape == exp.shape
+    assert np.array_equal(got, exp), (np.abs(got - exp).max(), int(np.sum(got != exp)))
 
 
 def _composite(polys, x):

@@ -300,7 +300,9 @@ class Recorder:
 
     # ---- polynomials (polyeval.go) and bootstrapping (bootstrapper.go) ----------
     def GenerateMinimaxSignCoeffs(self, degrees, prec, logalpha, logerr, debug):
-        # the coefficients come from this build's own generator (host code, CPU)
+        # the coefficients come from this build's generator (host code, CPU): Lattigo's composite
+        # construction restated [U] and pinned to the prec-bit mpmath computation of the same
+        # (tools/gen_minimax.py -> tests/golden/minimax_sign.json, tests/test_minimax.py)
         from orion_amd.backend import HipLibrary
         out = HipLibrary().GenerateMinimaxSignCoeffs(list(degrees), prec, logalpha, logerr, debug)
         self._rec("GenerateMinimaxSignCoeffs", [list(map(int, degrees)), int(prec), int(logalpha), int(logerr)])

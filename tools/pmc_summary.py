@@ -32,6 +32,31 @@ def rows(path):
         return list(csv.DictReader(f))
 
 
+def in_window(rs, key):
+    """The rows strictly between the first and the last torch fill kernel (the
+    PROF_MARK markers around the timed inference of tools/resnet_bench.py), in
+    dispatch order."""
+    rs = sorted(rs, key=lambda r: int(r[key]))
+    marks = [i for i, r in enumerate(rs) if "FillFunctor" in r["Kernel_Name"]]
+    if len(marks) < 2:
+        raise RuntimeError("no PROF_MARK markers in the trace")
+    return [r for r in rs[marks[0] + 1:marks[-1]] if "FillFunctor" not in r["Kernel_Name"]]
+
+
+def window_stats(d, path):
+    """rocprofv3 --stats columns for the kernels of the timed inference only."""
+    tr = in_window(rows(os.path.join(d, "kt_kernel_trace.csv")), key="Dispatch_Id")
+    agg = collections.defaultdict(list)
+    for r in tr:
+        agg[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    tot = sum(sum(v) for v in agg.values())
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f, quoting=csv.QUOTE_NONNUMERIC)
+        w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"])
+        for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
+            w.writerow([k, len(v), sum(v), sum(v) / len(v), round(100.0 * sum(v) / tot, 2), min(v), max(v)])
+
+
 def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
     """resnet: the ResNet-20 N=2^16 passes of tools/gpu_resnet_prof.sh (no NTT
     call log, no shared roofline files); out: output directory (default
@@ -42,7 +67,9 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
     os.makedirs(out, exist_ok=True)
     if resnet:
         workload, batch, logn, tag = "resnet20_n16", 1, 16, f"{tag}_rn16"
-    shutil.copy(os.path.join(d, "kt_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
+        window_stats(d, os.path.join(out, f"{tag}_kernel_stats.csv"))
+    else:
+        shutil.copy(os.path.join(d, "kt_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
     N = 1 << logn
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     ntt_alg = ntt_fetch = ntt_write = 0.0
@@ -75,6 +102,8 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
         if not os.path.exists(p):
             continue
         rs = rows(p)
+        if resnet:
+            rs = in_window(rs, key="Dispatch_Id")
         for r in rs:
             k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
             v = float(r["Counter_Value"])

@@ -24,6 +24,15 @@ def _heartbeat():
     threading.Thread(target=beat, daemon=True).start()
 
 
+def mark():
+    """PROF_MARK=1: a torch fill kernel before and after the timed forward, so a
+    rocprofv3 trace can be cut to the inference (tools/pmc_summary.py --resnet)."""
+    if os.environ.get("PROF_MARK") == "1":
+        import torch
+        torch.empty(1, device="cuda").fill_(1.0)
+        torch.cuda.synchronize()
+
+
 def main():
     _heartbeat()
     name = os.environ.get("WORKLOAD", "resnet20_n13")
@@ -41,10 +50,12 @@ def main():
         ct = st.encrypt_batch(np.repeat(img, B, axis=0))
         st.lib.DeleteCiphertext(st.forward(ct))  # warm (rotation keys, buffers)
         st.lib.OrionHipSynchronize()
+        mark()
         t0 = time.perf_counter()
         out = st.forward(ct)
         st.lib.OrionHipSynchronize()
         dt = time.perf_counter() - t0
+        mark()
         res = st.decrypt_output(out)
         mae = float(np.abs(res - exp[None]).mean())
         print(json.dumps({"workload": f"ResNet-20 CIFAR-10 (reference op stream {name}, "
