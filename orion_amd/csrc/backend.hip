@@ -673,20 +673,26 @@ struct Context {
   // job of every other CU in persistent launches of >= ntt_stagger_min rounds
   int ntt_stagger = getenv("ORION_NTT_STAGGER") ? atoi(getenv("ORION_NTT_STAGGER")) : 0;
   int ntt_stagger_min = getenv("ORION_NTT_STAGGER_MIN") ? atoi(getenv("ORION_NTT_STAGGER_MIN")) : 2;
-  // ORION_NTT_LOG=path: one line per NTT call ("<impl> <jobs> <sub>": impl 1 =
-  // one dispatch of ntt.hip, 2 = a two-pass pair of ntt2.hip; sub = the
-  // subtract-and-scale epilogue), so tools/pmc_summary.py can price each
-  // dispatch of a rocprofv3 pass with its limb-transform count (persistent
-  // launches have fewer workgroups than jobs)
+  // ORION_NTT_LOG=path: one line per NTT call ("<impl> <jobs> <sub> <inv>
+  // <pro> <intjobs>": impl 1 = one dispatch of ntt.hip, 2 = a two-pass pair of
+  // ntt2.hip; sub = the subtract-and-scale epilogue; pro = the prologue;
+  // intjobs = limb-transforms on integer-path (>= 2^46) moduli), so
+  // tools/pmc_summary.py can price each dispatch of a rocprofv3 pass with its
+  // limb-transform count (persistent launches have fewer workgroups than
+  // jobs) and break the NTT time down by launch class
   FILE* ntt_log = nullptr;
   bool ntt_log_init = false;
-  void log_ntt(int impl, const NttIO& io) {
+  void log_ntt(int impl, const NttIO& io, bool inv) {
     if (!ntt_log_init) {
       ntt_log_init = true;
       const char* p = getenv("ORION_NTT_LOG");
       if (p && *p) ntt_log = fopen(p, "a");
     }
-    if (ntt_log) fprintf(ntt_log, "%d %d %d\n", impl, io.jobs, io.epi == NTT_EPI_SUBSCALE ? 1 : 0);
+    if (!ntt_log) return;
+    int nint = 0;
+    for (int l = 0; l < io.dst.nlimb; ++l) nint += host_tb.mc[io.dst.mod[l]].f64 ? 0 : 1;
+    fprintf(ntt_log, "%d %d %d %d %d %d\n", impl, io.jobs, io.epi == NTT_EPI_SUBSCALE ? 1 : 0, inv ? 1 : 0, io.pro,
+            io.jobs / std::max(1, io.dst.nlimb) * nint);
   }
   void ntt_io(NttIO io, bool inv) {
     io.order = ntt_order;
@@ -716,7 +722,7 @@ struct Context {
           if (orion_launch_ntt2(logN, io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
           NttIO lio = io;
           lio.jobs = io.njob;
-          log_ntt(2, lio);
+          log_ntt(2, lio, inv);
         }
         return;
       }
@@ -728,7 +734,7 @@ struct Context {
       const double per = 16.0 * N + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
       Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, per * io.jobs);
       if (orion_launch_ntt2(logN, io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
-      log_ntt(2, io);
+      log_ntt(2, io, inv);
       return;
     }
     if (ntt_stagger > 0) {
@@ -739,7 +745,7 @@ struct Context {
     const double per = 16.0 * N + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
     Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, per * io.dst.ncomp * io.dst.nlimb * io.dst.nbatch);
     if (orion_launch_ntt_io(logN, io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
-    log_ntt(1, io);
+    log_ntt(1, io, inv);
   }
   void ntt(const LimbSet& s, bool inv) { ntt_io(nio(s, s), inv); }
   void ew(int op, const LimbSet& o, const LimbSet& a, const LimbSet& b, const std::vector<u64>* sc = nullptr) {
@@ -844,6 +850,8 @@ struct Context {
         fw[k] = make_ulonglong2(tf[src], hm_shoup(tf[src], q));
         iv[k] = make_ulonglong2(ti[src], hm_shoup(ti[src], q));
       }
+      mc.wl = hm_mulmod(iv[1].x, mc.ninv, q);
+      mc.wl_s = hm_shoup(mc.wl, q);
       mc.ciw = ci ? tf[1] : 0;  // psi^N
       mc.ciw_s = ci ? hm_shoup(tf[1], q) : 0;
       // float64-path constants and centered twiddles for small moduli
@@ -851,6 +859,7 @@ struct Context {
       mc.qd = (double)q;
       mc.qinv_d = 1.0 / (double)q;
       mc.ninv_d = (double)(mc.ninv > q / 2 ? (long long)mc.ninv - (long long)q : (long long)mc.ninv);
+      mc.wl_d = (double)(mc.wl > q / 2 ? (long long)mc.wl - (long long)q : (long long)mc.wl);
       if (mc.f64) {
         std::vector<double> fd(N), id(N);
         for (int j = 0; j < N; ++j) {
@@ -2395,9 +2404,13 @@ static bool capture_ok(const char* fn) {
       "GetLivePlaintexts", "GetModuliChain", "GaloisElement", "OrionHipGraphEnd"};
   return ok.count(fn) != 0;
 }
+// debugging switch ORION_DEBUG_SYNC=1: drain the library stream at the start
+// of every C-ABI call (separates an ordering race from an arithmetic fault)
+static const bool g_debug_sync = getenv("ORION_DEBUG_SYNC") && atoi(getenv("ORION_DEBUG_SYNC")) != 0;
 static void capture_guard(const char* fn) {
   if (g && g->capturing && !capture_ok(fn))
     throw std::runtime_error(std::string(fn) + " is not allowed while capturing a graph");
+  if (g_debug_sync && g && !g->capturing && g->stream) (void)hipStreamSynchronize(g->stream);
 }
 #define API_BEGIN                                  \
   std::lock_guard<std::recursive_mutex> lk_(g_mu); \

@@ -38,6 +38,10 @@ struct ModConst {
   // unfolds a_e = (b_e + W b_{N-e}) / 2, with the 1/2 folded into ninv = (2N)^-1.
   // Zero in a Standard ring.
   u64 ciw, ciw_s;
+  // the inverse NTT's last stage with N^-1 folded in (ntt.hip NTT_INV_FOLD):
+  // X = (x + y) N^-1, Y = (x - y) w1 N^-1, w1 = the stage's twiddle (inv[1])
+  u64 wl, wl_s;
+  double wl_d;  // centered
 };
 #define ORION_F64_BITS 46
 
@@ -111,6 +115,21 @@ __device__ __forceinline__ u64 shoup_lazy_nq(u64 a, u64 w, u64 ws, u64 nq) {
   const u64 m1 = (u64)a1 * s0 + __umulhi(a0, s0);
   const u64 m2 = (u64)a0 * s1 + (u32)m1;
   const u64 qh = (u64)a1 * s1 + ((m1 >> 32) + (m2 >> 32));  // floor(a * ws / 2^64)
+  const u32 h0 = (u32)qh, h1 = (u32)(qh >> 32), w0 = (u32)w, w1 = (u32)(w >> 32);
+  const u32 n0 = (u32)nq, n1 = (u32)(nq >> 32);
+  const u64 lo = (u64)h0 * n0 + (u64)a0 * w0;
+  const u32 hi = (u32)(lo >> 32) + a0 * w1 + a1 * w0 + h0 * n1 + h1 * n0;
+  return ((u64)hi << 32) | (u32)lo;
+}
+
+// the same with the quotient cut: the high word of a0*s0 and the low carries
+// are dropped, so qh <= floor(a*ws/2^64) <= qh + 2 and the result is in
+// [0, 4q) (ntt_arith.h NTT_INT_CUT): 4 v_mad_u64_u32 + 4 v_mul_lo_u32
+__device__ __forceinline__ u64 shoup_cut_nq(u64 a, u64 w, u64 ws, u64 nq) {
+  const u32 a0 = (u32)a, a1 = (u32)(a >> 32), s0 = (u32)ws, s1 = (u32)(ws >> 32);
+  const u64 m1 = (u64)a1 * s0;
+  const u64 m2 = (u64)a0 * s1 + (u32)m1;
+  const u64 qh = (u64)a1 * s1 + ((m1 >> 32) + (m2 >> 32));
   const u32 h0 = (u32)qh, h1 = (u32)(qh >> 32), w0 = (u32)w, w1 = (u32)(w >> 32);
   const u32 n0 = (u32)nq, n1 = (u32)(nq >> 32);
   const u64 lo = (u64)h0 * n0 + (u64)a0 * w0;

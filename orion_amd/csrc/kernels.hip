@@ -13,6 +13,14 @@
 #ifndef LT_ABLATE
 #define LT_ABLATE 0
 #endif
+// 1: ks_mac reduces once per output on moduli below 2^52
+#ifndef KS_MAC_ACC
+#define KS_MAC_ACC 1
+#endif
+// 1: lt_giant accumulates all giants unreduced on moduli below 2^52
+#ifndef LT_GIANT_ACC
+#define LT_GIANT_ACC 1
+#endif
 
 namespace {
 
@@ -268,6 +276,11 @@ __global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, Lim
   const int kl = G.klvl[g];
   const long long kstride = (long long)(kl + 1 + G.K) * N;
   const u64* kp = key + (long long)key_pos(m, G.L, kl) * N + n;
+  // moduli below 2^52 (block-uniform): the digits' products are reduced once
+  // at the end (mac_reduce_small takes up to 128), not once per chunk of 4
+  const bool small = KS_MAC_ACC && mc.bar_k <= 52 && beta <= 120;
+  MacAcc s0x, s0y, s1x, s1y;
+  mac_zero(s0x), mac_zero(s0y), mac_zero(s1x), mac_zero(s1y);
   for (int i0 = 0; i0 < beta; i0 += 4) {  // chunks of 4 digits: 12 loads in flight
     ulonglong2 d[4], kb[4], ka[4];
 #pragma unroll
@@ -280,8 +293,6 @@ __global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, Lim
         ka[u] = *(const ulonglong2*)(kp + (2 * i + 1) * kstride);
       }
     }
-    MacAcc s0x, s0y, s1x, s1y;
-    mac_zero(s0x), mac_zero(s0y), mac_zero(s1x), mac_zero(s1y);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (i0 + u < beta) {
@@ -291,10 +302,19 @@ __global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, Lim
         mac_add(s1y, d[u].y, ka[u].y);
       }
     }
-    r0.x = add_mod(r0.x, mac_reduce(s0x, mc), q);
-    r0.y = add_mod(r0.y, mac_reduce(s0y, mc), q);
-    r1.x = add_mod(r1.x, mac_reduce(s1x, mc), q);
-    r1.y = add_mod(r1.y, mac_reduce(s1y, mc), q);
+    if (!small) {
+      r0.x = add_mod(r0.x, mac_reduce(s0x, mc), q);
+      r0.y = add_mod(r0.y, mac_reduce(s0y, mc), q);
+      r1.x = add_mod(r1.x, mac_reduce(s1x, mc), q);
+      r1.y = add_mod(r1.y, mac_reduce(s1y, mc), q);
+      mac_zero(s0x), mac_zero(s0y), mac_zero(s1x), mac_zero(s1y);
+    }
+  }
+  if (small) {
+    r0.x = add_mod(r0.x, mac_reduce_small(s0x, mc), q);
+    r0.y = add_mod(r0.y, mac_reduce_small(s0y, mc), q);
+    r1.x = add_mod(r1.x, mac_reduce_small(s1x, mc), q);
+    r1.y = add_mod(r1.y, mac_reduce_small(s1y, mc), q);
   }
   *(ulonglong2*)(op + row_off(out, 0, l, bi) + n) = r0;
   *(ulonglong2*)(op + row_off(out, 1, l, bi) + n) = r1;
@@ -358,6 +378,38 @@ __device__ __forceinline__ void gadget_at(const u64* __restrict__ dp, long long 
     r0 = add_mod(r0, mac_reduce(a0, mc), mc.q);
     r1 = add_mod(r1, mac_reduce(a1, mc), mc.q);
   }
+}
+
+// The same gadget product left unreduced: the products are added to (a0, a1)
+// (moduli below 2^52: mac_reduce_small takes up to 128 of them at once)
+__device__ __forceinline__ void gadget_acc(const u64* __restrict__ dp, long long dstride, const u64* ownp,
+                                           int owndigit, const u64* __restrict__ key, int beta, int L, int K, int klvl,
+                                           int m, int N, int j, MacAcc& a0, MacAcc& a1) {
+  const long long kstride = (long long)(klvl + 1 + K) * N;
+  const u64* kp = key + (long long)key_pos(m, L, klvl) * N + j;
+  for (int i0 = 0; i0 < beta; i0 += 4) {
+    u64 d[4], k0[4], k1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u;
+      if (i < beta) {
+        d[u] = i == owndigit ? ownp[j] : dp[i * dstride + j];
+        k0[u] = kp[(2 * i + 0) * kstride];
+        k1[u] = kp[(2 * i + 1) * kstride];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i0 + u < beta) {
+        mac_add(a0, d[u], k0[u]);
+        mac_add(a1, d[u], k1[u]);
+      }
+    }
+  }
+}
+__device__ __forceinline__ void mac_add1(MacAcc& a, u64 x) {
+  a.lo += x;
+  a.c += (a.lo < x);
 }
 
 // Hoisted BSGS linear transform, baby steps and giant inner products fused
@@ -497,15 +549,40 @@ __global__ void __launch_bounds__(256) lt_giant_kernel(LimbSet acc, LimbSet D, L
   const long long dro = row_off(D, 0, l, bi), oro = row_off(own, 0, isq ? l : 0, bi), tro = row_off(t0, 0, l, bi);
   u64 r0 = 0, r1 = 0;
   int jn = G.ng > 0 ? (int)G.idx[0][n] : 0;
-  for (int g = 0; g < G.ng; ++g) {
-    const int j = jn;
-    if (g + 1 < G.ng) jn = G.idx[g + 1][n];  // prefetch the next giant's index
-    u64 a0, a1;
-    gadget_at(D.p + g * G.d_gstride + dro, D.comp_stride, own.p + g * G.own_gstride + oro, owndigit, G.key[g],
-              G.beta, G.L, G.K, G.klvl[g], m, N, j, mc, a0, a1);
-    a0 = add_mod(a0, t0.p[g * G.t0_gstride + tro + j], mc.q);
-    r0 = add_mod(r0, a0, mc.q);
-    r1 = add_mod(r1, a1, mc.q);
+  if (LT_GIANT_ACC && mc.bar_k <= 52) {  // block-uniform
+    // moduli below 2^52: every giant's products and its t0 term go into one
+    // unreduced accumulator, reduced once per <= 120 products instead of once
+    // per giant (the Barrett reduction is ~40 VALU ops per component)
+    MacAcc a0, a1;
+    mac_zero(a0), mac_zero(a1);
+    int cnt = 0;
+    for (int g = 0; g < G.ng; ++g) {
+      const int j = jn;
+      if (g + 1 < G.ng) jn = G.idx[g + 1][n];  // prefetch the next giant's index
+      gadget_acc(D.p + g * G.d_gstride + dro, D.comp_stride, own.p + g * G.own_gstride + oro, owndigit, G.key[g],
+                 G.beta, G.L, G.K, G.klvl[g], m, N, j, a0, a1);
+      mac_add1(a0, t0.p[g * G.t0_gstride + tro + j]);
+      cnt += G.beta + 1;
+      if (cnt + G.beta + 1 > 120) {
+        r0 = add_mod(r0, mac_reduce_small(a0, mc), mc.q);
+        r1 = add_mod(r1, mac_reduce_small(a1, mc), mc.q);
+        mac_zero(a0), mac_zero(a1);
+        cnt = 0;
+      }
+    }
+    r0 = add_mod(r0, mac_reduce_small(a0, mc), mc.q);
+    r1 = add_mod(r1, mac_reduce_small(a1, mc), mc.q);
+  } else {
+    for (int g = 0; g < G.ng; ++g) {
+      const int j = jn;
+      if (g + 1 < G.ng) jn = G.idx[g + 1][n];  // prefetch the next giant's index
+      u64 a0, a1;
+      gadget_at(D.p + g * G.d_gstride + dro, D.comp_stride, own.p + g * G.own_gstride + oro, owndigit, G.key[g],
+                G.beta, G.L, G.K, G.klvl[g], m, N, j, mc, a0, a1);
+      a0 = add_mod(a0, t0.p[g * G.t0_gstride + tro + j], mc.q);
+      r0 = add_mod(r0, a0, mc.q);
+      r1 = add_mod(r1, a1, mc.q);
+    }
   }
   if (G.has_zero) {
     r0 = add_mod(r0, z.p[row_off(z, 0, l, bi) + n], mc.q);

@@ -42,6 +42,11 @@ namespace {
 // Thread t's element e = t + k S (S = N/32) pairs with N - e = (S - t) + (31 - k) S,
 // held at the same offsets of the mirrored thread, so the partner is one more
 // coalesced (descending) load of the same limb, served by L2.
+// 1: the subtract-and-scale epilogue loads its operand one group of 8 rows ahead
+#ifndef NTT_EPI_PF
+#define NTT_EPI_PF 1
+#endif
+
 __device__ __forceinline__ u64 ci_fold(u64 x, u64 y, const ModConst& mc) {
   return sub_mod(x, shoup_mul(y, mc.ciw, mc.ciw_s, mc.q), mc.q);
 }
@@ -133,11 +138,33 @@ __device__ __forceinline__ void ntt_fwd_body(const NttIO& io, int c, int l, int 
   } else {  // NTT_EPI_SUBSCALE: dst = (ex - y) * s_l  (ModDown / rescale tail)
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.ex, c, l, b), 0, N * 8, 0x00020000);
     const u64 s = io.s[l], ss = io.ss[l];
+    if constexpr (NTT_EPI_PF) {
+      // ex in groups of 8 rows, the next group's loads issued before the
+      // current group is consumed: one load latency per job instead of four
+      u64 xa[8], xb[8];
 #pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const u64 x = buf_ld(rx, t * 8, (k << B0) * 8);
-      buf_st(rd, shoup_mul(sub_mod(x, r[k], mc.q), s, ss, mc.q), t * 8, (k << B0) * 8);
-      if ((k & 7) == 7) NTT_FENCE();
+      for (int k = 0; k < 8; ++k) xa[k] = buf_ld(rx, t * 8, (k << B0) * 8);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (g < 3) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) xb[k] = buf_ld(rx, t * 8, ((8 * (g + 1) + k) << B0) * 8);
+        }
+        NTT_FENCE();
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          buf_st(rd, shoup_mul(sub_mod(xa[k], r[8 * g + k], mc.q), s, ss, mc.q), t * 8, ((8 * g + k) << B0) * 8);
+        NTT_FENCE();
+#pragma unroll
+        for (int k = 0; k < 8; ++k) xa[k] = xb[k];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        const u64 x = buf_ld(rx, t * 8, (k << B0) * 8);
+        buf_st(rd, shoup_mul(sub_mod(x, r[k], mc.q), s, ss, mc.q), t * 8, (k << B0) * 8);
+        if ((k & 7) == 7) NTT_FENCE();
+      }
     }
   }
 }
@@ -170,10 +197,10 @@ __device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int 
     }
   }
   inv_round<A, LOGN, 0, 0, B1 - 1>(a, ar, w, t);
-  reduce_all<A>(a, ar);
+  if (!NTT_INV_NORED) reduce_all<A>(a, ar);
   xchg<typename A::T, LOGN, 0, B1>(a, lds, t);
   inv_round<A, LOGN, B1, B1, B0 - 1>(a, ar, w, t);
-  reduce_all<A>(a, ar);
+  if (!NTT_INV_NORED) reduce_all<A>(a, ar);
   xchg<typename A::T, LOGN, B1, B0>(a, lds, t);
   inv_round<A, LOGN, B0, B0, LOGN - 1>(a, ar, w, t);
   const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.dst, c, l, b), 0, N * 8, 0x00020000);
@@ -188,7 +215,7 @@ __device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int 
     u64* const l64 = reinterpret_cast<u64*>(lds);
     u64 r[32];
 #pragma unroll
-    for (int k = 0; k < 32; ++k) r[k] = ar.final_inv(a[k]);
+    for (int k = 0; k < 32; ++k) r[k] = NTT_INV_FOLD ? ar.final_inv_folded(a[k]) : ar.final_inv(a[k]);
 #pragma unroll
     for (int k = 0; k < 16; ++k) l64[k * S + t] = r[k];
     __syncthreads();
@@ -216,7 +243,7 @@ __device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int 
   }
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
-    buf_st(rd, ar.final_inv(a[k]), t * 8, (k << B0) * 8);
+    buf_st(rd, NTT_INV_FOLD ? ar.final_inv_folded(a[k]) : ar.final_inv(a[k]), t * 8, (k << B0) * 8);
     if ((k & 3) == 3) NTT_FENCE();
   }
 }
@@ -239,9 +266,14 @@ __device__ __forceinline__ void ntt_stagger(const NttIO& io) {
     for (int i = 0; i < io.stagger; ++i) __builtin_amdgcn_s_sleep(127);
 }
 
+// 1: the subtract-and-scale (ModDown / rescale tail) variants are persistent
+// too (they no longer spill: 1 VGPR, outside the job loop)
+#ifndef NTT_PERSIST_ALL
+#define NTT_PERSIST_ALL 1
+#endif
 template <int EPI>
 struct FwdPersist {
-  static constexpr bool value = EPI == NTT_EPI_STORE;
+  static constexpr bool value = EPI == NTT_EPI_STORE || NTT_PERSIST_ALL;
 };
 
 template <int LOGN, int PRO, int EPI, bool CI>

@@ -40,12 +40,20 @@ __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, u64 v, int voff
 #ifndef NTT_INT_DIET
 #define NTT_INT_DIET 1
 #endif
+// 1: the forward (CT) butterfly's Shoup quotient drops the a0*s0 high word and
+// its carries (floor(a*ws/2^64) under-estimated by at most 2, so t < 4q) and
+// keeps values lazily in [0, 8q) instead of [0, 4q) (8q < 2^64 for q < 2^61)
+#ifndef NTT_INT_CUT
+#define NTT_INT_CUT 1
+#endif
 struct IntArith {
   typedef u64 T;
   typedef ulonglong2 W;
-  u64 q, q2, ninv, ninv_s, nq;
-  __device__ IntArith(const ModConst& m) : q(m.q), q2(m.q << 1), ninv(m.ninv), ninv_s(m.ninv_s), nq(0 - m.q) {}
+  u64 q, q2, q4, ninv, ninv_s, nq, wl, wl_s;
+  __device__ IntArith(const ModConst& m)
+      : q(m.q), q2(m.q << 1), q4(m.q << 2), ninv(m.ninv), ninv_s(m.ninv_s), nq(0 - m.q), wl(m.wl), wl_s(m.wl_s) {}
   __device__ __forceinline__ u64 smul(u64 a, u64 w, u64 ws) const {
+    if constexpr (NTT_INT_CUT) return shoup_cut_nq(a, w, ws, nq);
     if constexpr (NTT_INT_DIET) return shoup_lazy_nq(a, w, ws, nq);
     return shoup_lazy(a, w, ws, q);
   }
@@ -54,12 +62,19 @@ struct IntArith {
     return make_ulonglong2(((u64)v[1] << 32) | v[0], ((u64)v[3] << 32) | v[2]);
   }
   __device__ __forceinline__ T from_u64(u64 x) const { return x; }
-  // Harvey CT butterfly, values in [0, 4q)
+  // Harvey CT butterfly, values in [0, 4q) ([0, 8q) with the cut quotient)
   __device__ __forceinline__ void ct(T& X, T& Y, const W& w) const {
-    const u64 x = X >= q2 ? X - q2 : X;
-    const u64 t = smul(Y, w.x, w.y);
-    X = x + t;
-    Y = x - t + q2;
+    if constexpr (NTT_INT_CUT) {
+      const u64 x = X >= q4 ? X - q4 : X;
+      const u64 t = smul(Y, w.x, w.y);
+      X = x + t;
+      Y = x - t + q4;
+    } else {
+      const u64 x = X >= q2 ? X - q2 : X;
+      const u64 t = smul(Y, w.x, w.y);
+      X = x + t;
+      Y = x - t + q2;
+    }
   }
   // Harvey GS butterfly, values in [0, 2q)
   __device__ __forceinline__ void gs(T& X, T& Y, const W& w, bool) const {
@@ -68,8 +83,16 @@ struct IntArith {
     X = s >= q2 ? s - q2 : s;
     Y = shoup_lazy(x - y + q2, w.x, w.y, q);  // (the diet's extra live values spill the inverse kernel)
   }
+  // the last GS stage with N^-1 folded in (inputs in [0, 2q), outputs in [0, 2q))
+  __device__ __forceinline__ void gs_last(T& X, T& Y) const {
+    const u64 x = X, y = Y;
+    X = shoup_lazy(x + y, ninv, ninv_s, q);
+    Y = shoup_lazy(x - y + q2, wl, wl_s, q);
+  }
+  __device__ __forceinline__ u64 final_inv_folded(T x) const { return x >= q ? x - q : x; }
   __device__ __forceinline__ T reduce_round(T x) const { return x; }  // lazy range is invariant
   __device__ __forceinline__ u64 final_fwd(T x) const {
+    if constexpr (NTT_INT_CUT) x = x >= q4 ? x - q4 : x;
     x = x >= q2 ? x - q2 : x;
     return x >= q ? x - q : x;
   }
@@ -82,8 +105,8 @@ struct IntArith {
 struct F64Arith {
   typedef double T;
   typedef double W;
-  double q, qinv, ninv;
-  __device__ F64Arith(const ModConst& m) : q(m.qd), qinv(m.qinv_d), ninv(m.ninv_d) {}
+  double q, qinv, ninv, wl;
+  __device__ F64Arith(const ModConst& m) : q(m.qd), qinv(m.qinv_d), ninv(m.ninv_d), wl(m.wl_d) {}
   __device__ __forceinline__ W tw(__amdgpu_buffer_rsrc_t r, int vidx, int sidx) const {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vidx * 8, sidx * 8, 0));
   }
@@ -122,6 +145,13 @@ struct F64Arith {
   }
   __device__ __forceinline__ u64 final_fwd(T x) const { return to_u64(x); }
   __device__ __forceinline__ u64 final_inv(T x) const { return to_u64(mulmod(x, ninv)); }
+  // the last GS stage with N^-1 folded in (|x|, |y| < 8q: |x +- y| < 16q)
+  __device__ __forceinline__ void gs_last(T& X, T& Y) const {
+    const double x = X, y = Y;
+    X = mulmod(x + y, ninv);
+    Y = mulmod(x - y, wl);
+  }
+  __device__ __forceinline__ u64 final_inv_folded(T x) const { return to_u64(x); }
 };
 
 template <class T>

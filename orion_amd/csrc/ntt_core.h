@@ -35,6 +35,17 @@
 #ifndef NTT_FENCE_INV
 #define NTT_FENCE_INV 2
 #endif
+// 1: the inverse's last stage multiplies by N^-1 (X) and w1 N^-1 (Y) instead
+// of a separate N^-1 pass over every output (ntt.hip final_inv_folded)
+#ifndef NTT_INV_FOLD
+#define NTT_INV_FOLD 1
+#endif
+// 1: no float64 reductions between inverse rounds: a round of GS stages maps
+// inputs below 8q to outputs below 3q (the sums are reduced every other stage,
+// mulmod outputs are below 1.5q + ulp), so the bound holds round to round
+#ifndef NTT_INV_NORED
+#define NTT_INV_NORED 1
+#endif
 // 1: butterflies scheduled in pairs (see run_stage)
 #ifndef NTT_PAIR
 #define NTT_PAIR 0
@@ -191,7 +202,10 @@ __device__ __forceinline__ void run_stage(typename A::T (&a)[32], typename A::W 
       ar.ct(a[k0], a[k1], W);
       if ((pr & (NTT_FENCE_FWD - 1)) == NTT_FENCE_FWD - 1) NTT_FENCE();
     } else {
-      ar.gs(a[k0], a[k1], W, (S & 1) == 1);
+      if constexpr (NTT_INV_FOLD && d == LOGN - 1)
+        ar.gs_last(a[k0], a[k1]);
+      else
+        ar.gs(a[k0], a[k1], W, (S & 1) == 1);
       if ((pr & (NTT_FENCE_INV - 1)) == NTT_FENCE_INV - 1) NTT_FENCE();
     }
   }

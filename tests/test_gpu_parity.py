@@ -67,6 +67,48 @@ def test_ntt_roundtrip_and_parity(torch_cuda, oracle_mod, logn):
     lib.DeleteScheme()
 
 
+@pytest.mark.parametrize("B", [32, 64])
+def test_ntt_one_pass_launches(torch_cuda, oracle_mod, B):
+    """N = 2^15 launches of one or two full rounds of 256 limb-transforms take
+    the one-limb-per-workgroup kernels (smaller or partial-round launches take
+    the two-pass kernels): integer-path (60-bit) and float64-path (40-bit)
+    limbs in one launch, forward bit-exact with the oracle, inverse exact."""
+    torch = torch_cuda
+    from orion_amd.backend import HipLibrary
+    import ctypes
+    logn, logq = 15, [60] + [40] * 5
+    lib = HipLibrary().new_scheme(logn, logq, [60, 60], 40)
+    mods = lib.moduli()
+    orc = oracle_mod.Oracle(logn, mods, len(logq), 2)
+    N, nl = 1 << logn, len(mods)
+    assert nl * B in (256, 512)
+    rng = np.random.default_rng(B)
+    host = np.stack([rng.integers(0, mods[m], (B, N), dtype=np.uint64) for m in range(nl)])
+    host[:, 0, :8] = np.array([mods[m] - 1 for m in range(nl)], dtype=np.uint64)[:, None]
+    dev = torch.from_numpy(host.view(np.int64).copy()).cuda()
+    mods_c = (ctypes.c_int * nl)(*range(nl))
+    ptr = ctypes.cast(dev.data_ptr(), ctypes.POINTER(ctypes.c_ulong))
+    assert lib.lib.OrionHipNTT(ptr, nl, B, mods_c, 0) == 0
+    lib.OrionHipSynchronize()
+    fwd = dev.cpu().numpy().view(np.uint64).copy()
+    for m in range(nl):
+        for b in (0, B - 1):
+            assert np.array_equal(fwd[m, b], orc.ntt(m, host[m, b])), (m, b)
+    assert lib.lib.OrionHipNTT(ptr, nl, B, mods_c, 1) == 0
+    lib.OrionHipSynchronize()
+    back = dev.cpu().numpy().view(np.uint64)
+    bad = [(m, b) for m in range(nl) for b in range(B) if not np.array_equal(back[m, b], host[m, b])]
+    assert not bad, bad[:8]
+    # inverse on its own against the oracle (inputs: arbitrary NTT-domain rows)
+    dev.copy_(torch.from_numpy(host.view(np.int64).copy()))
+    assert lib.lib.OrionHipNTT(ptr, nl, B, mods_c, 1) == 0
+    lib.OrionHipSynchronize()
+    inv = dev.cpu().numpy().view(np.uint64)
+    for m in range(nl):
+        assert np.array_equal(inv[m, 0], orc.intt(m, host[m, 0])), m
+    lib.DeleteScheme()
+
+
 def test_encode_parity(small):
     lib, orc = small
     rng = np.random.default_rng(1)

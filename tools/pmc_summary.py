@@ -80,7 +80,15 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
         if not os.path.exists(p):
             return None
         with open(p) as f:
-            return [(int(a), int(j), int(s)) for a, j, s in (ln.split() for ln in f if ln.strip())]
+            return [tuple(int(v) for v in ln.split()[:3]) for ln in f if ln.strip()]
+
+    def ntt_log_full(name):
+        """(impl, jobs, sub, inv, pro, intjobs) per call (older logs: 3 fields)."""
+        p = os.path.join(d, f"ntt_log_{name}.txt")
+        if not os.path.exists(p):
+            return None
+        with open(p) as f:
+            return [tuple(int(v) for v in ln.split()) for ln in f if ln.strip()]
 
     def priced(dispatches, log):
         """Pair the pass's NTT dispatches (in issue order) with its logged calls:
@@ -150,6 +158,26 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
             if alg is not None:
                 n_l += 1
                 n_b += alg
+    # NTT time by launch class (kt pass): direction, kernel (one-pass / two-pass
+    # pair), epilogue, prologue, integer-path share, jobs in multiples of CUs
+    classes = {}
+    full = ntt_log_full("kt")
+    if klog is not None and full is not None and len(full[0]) >= 6:
+        for call, r, alg, jobs in priced(tr, klog):
+            f = full[call]
+            if jobs < 64:
+                continue
+            key = (f"{'inv' if f[3] else 'fwd'} {'1pass' if f[0] == 1 else '2pass'} "
+                   f"{'sub' if f[2] else 'store'} pro{f[4]} int{round(f[5] / f[1], 2)} jobs{f[1]}")
+            c = classes.setdefault(key, {"calls": 0, "us": 0.0, "bytes": 0.0})
+            c["us"] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            if alg is not None:
+                c["calls"] += 1
+                c["bytes"] += alg
+        for c in classes.values():
+            c["GBps"] = round(c["bytes"] / (c["us"] * 1e-6) / 1e9, 1) if c["us"] else None
+            c["us_per_call"] = round(c["us"] / max(c["calls"], 1), 1)
+            c["us"] = round(c["us"], 1)
     trace = {"launches": n_l, "avg_launch_us": n_us / n_l if n_l else None,
              "algorithmic_bytes_per_launch": n_b / n_l if n_l else None,
              "achieved_GBps": n_b / (n_us * 1e-6) / 1e9 if n_us else None}
@@ -179,7 +207,8 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
             json.dump({"tag": tag, "workload": workload, "batch": batch,
                        "definition": "valu_busy = sum SQ_ACTIVE_INST_VALU*4 / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs)",
                        "kernels": valu}, f, indent=1)
-    summary = {"tag": tag, "ntt_hbm_bytes_per_algorithmic_byte": ratio, "ntt_trace_batched": trace, "valu": valu,
+    summary = {"tag": tag, "ntt_hbm_bytes_per_algorithmic_byte": ratio, "ntt_trace_batched": trace,
+               "ntt_classes": dict(sorted(classes.items(), key=lambda kv: -kv[1]["us"])), "valu": valu,
                "ntt_fetch_bytes_per_algorithmic_byte": ntt_fetch / ntt_alg if ntt_alg else None,
                "kernels": {k: dict(v) for k, v in per.items()}}
     with open(os.path.join(out, f"{tag}_pmc_summary.json"), "w") as f:
