@@ -79,6 +79,10 @@ static thread_local std::string g_last_error;
 // pinned buffer that is released is parked instead of returning to the free
 // lists, and nothing allocated later can alias a graph's temporaries.
 class DevicePool {
+  // ORION_DEBUG_POISON=1: fill each allocation with 0xA5 bytes, so a kernel that
+  // reads memory nothing wrote fails deterministically
+  bool poison_ = getenv("ORION_DEBUG_POISON") && atoi(getenv("ORION_DEBUG_POISON")) != 0;
+
  public:
   void* alloc(size_t bytes) {
     void* p = nullptr;
@@ -95,6 +99,10 @@ class DevicePool {
       }
     }
     if (tracking_) touched_[p] = bytes;
+    if (poison_) {  // debugging: every buffer handed out holds garbage, not stale or zero pages
+      (void)hipDeviceSynchronize();
+      (void)hipMemset(p, 0xA5, bytes);
+    }
     return p;
   }
   void release(void* p, size_t bytes) {
@@ -555,6 +563,16 @@ struct Context {
                                " needs a host synchronisation, not allowed while capturing a graph (run the op "
                                "stream once before capturing it)");
   }
+  // tables and plans made on first use go to the device in the library
+  // stream's order: a blocking hipMemcpy runs on the legacy NULL stream, which
+  // the non-blocking library stream does not wait for (a device-to-device
+  // hipMemcpy can even return before the copy lands), so a kernel queued next
+  // could read a table the copy has not finished, and a rewritten plan could
+  // change under a kernel still queued on the stream
+  void h2d(void* d, const void* h, size_t n) {
+    HIPCHK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+  }
 
   // -- allocation --------------------------------------------------------------
   Poly alloc(int ncomp, int nlimb, int B) {
@@ -808,6 +826,10 @@ struct Context {
       static_bufs.push_back(d);
       (inv ? tw_inv : tw_fwd) = (double2*)d;
     }
+    // the blocking table copies above ran on the legacy NULL stream, which the
+    // library stream does not wait for: drain the device before any kernel
+    // reads a twiddle or constant table
+    HIPCHK(hipDeviceSynchronize());
     memset(&enc_sampler, 0, sizeof(enc_sampler));
     gauss_cdt(3.2, ORION_GAUSS_BOUND, enc_sampler.cdt);
   }
@@ -955,7 +977,7 @@ struct Context {
     }
     BasisExtTable* d;
     HIPCHK(hipMalloc(&d, sizeof(T)));
-    HIPCHK(hipMemcpy(d, &T, sizeof(T), hipMemcpyHostToDevice));
+    h2d(d, &T, sizeof(T));
     return d;
   }
   // ModUp of digit i at level: sources Q[lo,hi), targets = rest of QP in QP-position order
@@ -991,7 +1013,9 @@ struct Context {
     HIPCHK(hipMalloc(&d, sizeof(BasisExtTable) * beta));
     std::vector<int> tpos;
     for (int i = 0; i < beta; ++i)
-      HIPCHK(hipMemcpy(d + i, modup_tab(level, i, tpos), sizeof(BasisExtTable), hipMemcpyDeviceToDevice));
+      HIPCHK(hipMemcpyAsync(d + i, modup_tab(level, i, tpos), sizeof(BasisExtTable), hipMemcpyDeviceToDevice,
+                             stream));
+    HIPCHK(hipStreamSynchronize(stream));
     modup_arr[level] = d;
     return d;
   }
@@ -1026,7 +1050,7 @@ struct Context {
     }
     u32* d;
     HIPCHK(hipMalloc(&d, N * sizeof(u32)));
-    HIPCHK(hipMemcpy(d, idx.data(), N * sizeof(u32), hipMemcpyHostToDevice));
+    h2d(d, idx.data(), N * sizeof(u32));
     autidx[g] = d;
     return d;
   }
@@ -1504,7 +1528,7 @@ struct Context {
       T.plan = std::shared_ptr<void>(d, [](void* q) { hipFree(q); });
       T.d_plan = (LtPlan*)d;
     }
-    HIPCHK(hipMemcpy(T.d_plan, plans.data(), nplan * sizeof(LtPlan), hipMemcpyHostToDevice));
+    h2d(T.d_plan, plans.data(), nplan * sizeof(LtPlan));
     T.n_plan = nplan;
     T.plan_dirty = false;
   }
@@ -1696,7 +1720,7 @@ struct Context {
     }
     u64* d;
     HIPCHK(hipMalloc(&d, t.size() * sizeof(u64)));
-    HIPCHK(hipMemcpy(d, t.data(), t.size() * sizeof(u64), hipMemcpyHostToDevice));
+    h2d(d, t.data(), t.size() * sizeof(u64));
     garner[level] = d;
     return d;
   }

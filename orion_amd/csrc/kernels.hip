@@ -13,9 +13,13 @@
 #ifndef LT_ABLATE
 #define LT_ABLATE 0
 #endif
-// 1: ks_mac reduces once per output on moduli below 2^52
+// 1: ks_mac reduces once per output on moduli below 2^52 instead of once per
+// chunk of 4 digits.  Off: the accumulators live across the digit loop (84 ->
+// 102 VGPRs, 5 -> 4 waves per SIMD) and the LoLA bench measured ks_mac 1.31
+// -> 1.48 ms per step with it (profiles/r03n_ab.txt); LoLA's decompositions
+// have at most 3 digits, so there is one chunk anyway
 #ifndef KS_MAC_ACC
-#define KS_MAC_ACC 1
+#define KS_MAC_ACC 0
 #endif
 // 1: lt_giant accumulates all giants unreduced on moduli below 2^52
 #ifndef LT_GIANT_ACC

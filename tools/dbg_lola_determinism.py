@@ -7,6 +7,7 @@ output).  Run after the GPU suite's earlier modules in the same process:
 import hashlib
 
 import numpy as np
+import pytest
 
 
 def _run(st, ct):
@@ -27,6 +28,7 @@ def _run(st, ct):
     return log, res
 
 
+@pytest.mark.gpu
 def test_lola_n15_determinism():
     from orion_amd.replay import OrionStream
     st = OrionStream("lola_n15", seed=33)
@@ -45,6 +47,7 @@ def test_lola_n15_determinism():
     st.lib.DeleteScheme()
 
 
+@pytest.mark.gpu
 def test_lola_n15_batch_invariance_repeat():
     """The suite's batch-invariance scenario repeated (REPS, default 6) in one
     process; prints which repetitions differ."""
