@@ -32,20 +32,28 @@ def rows(path):
         return list(csv.DictReader(f))
 
 
-def in_window(rs, key):
-    """The rows strictly between the first and the last torch fill kernel (the
-    PROF_MARK markers around the timed inference of tools/resnet_bench.py), in
-    dispatch order."""
-    rs = sorted(rs, key=lambda r: int(r[key]))
-    marks = [i for i, r in enumerate(rs) if "FillFunctor" in r["Kernel_Name"]]
-    if len(marks) < 2:
-        raise RuntimeError("no PROF_MARK markers in the trace")
-    return [r for r in rs[marks[0] + 1:marks[-1]] if "FillFunctor" not in r["Kernel_Name"]]
+def window_positions(d):
+    """[i0, i1): dispatch positions (issue order) of the timed inference in the
+    kernel trace: the kernels between the last two idle gaps of > 0.4 s that
+    tools/resnet_bench.py leaves around it under PROF_MARK=1."""
+    tr = sorted(rows(os.path.join(d, "kt_kernel_trace.csv")), key=lambda r: int(r["Dispatch_Id"]))
+    gaps = [i for i in range(1, len(tr))
+            if int(tr[i]["Start_Timestamp"]) - int(tr[i - 1]["End_Timestamp"]) > 400_000_000]
+    if len(gaps) < 2:
+        raise RuntimeError("no PROF_MARK gaps in the kernel trace")
+    return gaps[-2], gaps[-1]
 
 
-def window_stats(d, path):
+def in_window(rs, key, pos):
+    """Rows whose dispatch (in issue order) falls in positions [pos[0], pos[1])."""
+    ids = sorted({int(r[key]) for r in rs})
+    keep = set(ids[pos[0]:pos[1]])
+    return [r for r in rs if int(r[key]) in keep]
+
+
+def window_stats(d, path, pos):
     """rocprofv3 --stats columns for the kernels of the timed inference only."""
-    tr = in_window(rows(os.path.join(d, "kt_kernel_trace.csv")), key="Dispatch_Id")
+    tr = in_window(rows(os.path.join(d, "kt_kernel_trace.csv")), "Dispatch_Id", pos)
     agg = collections.defaultdict(list)
     for r in tr:
         agg[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
@@ -67,7 +75,8 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
     os.makedirs(out, exist_ok=True)
     if resnet:
         workload, batch, logn, tag = "resnet20_n16", 1, 16, f"{tag}_rn16"
-        window_stats(d, os.path.join(out, f"{tag}_kernel_stats.csv"))
+        pos = window_positions(d)
+        window_stats(d, os.path.join(out, f"{tag}_kernel_stats.csv"), pos)
     else:
         shutil.copy(os.path.join(d, "kt_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
     N = 1 << logn
@@ -111,7 +120,7 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
             continue
         rs = rows(p)
         if resnet:
-            rs = in_window(rs, key="Dispatch_Id")
+            rs = in_window(rs, "Dispatch_Id", pos)
         for r in rs:
             k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
             v = float(r["Counter_Value"])
