@@ -405,7 +405,32 @@ __device__ __forceinline__ u64 d53_to_u64(double d) {
   const double l = __builtin_fma(-h, 0x1p32, d);
   return ((u64)(u32)h << 32) | (u32)l;
 }
+#ifndef LT_F64_RED
+#define LT_F64_RED 1
+#endif
+// a representative of x mod q for an exact integer double x (below 2^53, or a
+// reduced value times a power of two as below): x - rint(x RN(1/q)) q.  The
+// estimate x RN(1/q) is within (x/q) 2^-51 of x/q, so the exact remainder is
+// below q (1/2 + (x/q) 2^-51) in magnitude -- a small integer the FMA forms
+// without rounding
+__device__ __forceinline__ double f64_rem(double x, double q, double qi) {
+  return __builtin_fma(-__builtin_rint(x * qi), q, x);
+}
 __device__ __forceinline__ u64 macd_reduce(const MacD& a, const ModConst& m) {
+  if (LT_F64_RED) {
+    // x = hi 2^48 + mid 2^24 + lo reduced in float64: each piece (< 2^53) to
+    // |r| < 2.5 q, the two high ones scaled by their power of two (exact) and
+    // reduced again (r 2^48 / q < 2^50: the estimate is within 1/2 of the
+    // real quotient, |r| < q), the three summed exactly (< 2^51), reduced to
+    // |s| <= q/2 + 1 and brought to [0, q)
+    const double q = m.qd, qi = m.qinv_d;
+    const double rl = f64_rem(a.lo, q, qi);
+    const double rm = f64_rem(f64_rem(a.mid, q, qi) * 0x1p24, q, qi);
+    const double rh = f64_rem(f64_rem(a.hi, q, qi) * 0x1p48, q, qi);
+    double s = f64_rem((rl + rm) + rh, q, qi);
+    s = s < 0.0 ? s + q : s;
+    return d53_to_u64(s);
+  }
   MacS s;
   s.lo = d53_to_u64(a.lo);
   s.mid = d53_to_u64(a.mid);

@@ -6,6 +6,8 @@
 // y covers the (comp, limb, image) rows.  Operands that are shared by the
 // whole batch (plaintexts, LT diagonals, evaluation keys) are passed with
 // batch_stride = 0 and are read once per row from L2.
+#include <type_traits>
+
 #include "common.h"
 
 // timing-only ablation of lt_bsgs (0 in the product): bit 0 skips the giant
@@ -24,6 +26,10 @@
 // 1: lt_giant accumulates all giants unreduced on moduli below 2^52
 #ifndef LT_GIANT_ACC
 #define LT_GIANT_ACC 1
+#endif
+// images per lt_giant thread
+#ifndef LT_GIANT_IB
+#define LT_GIANT_IB 4
 #endif
 
 namespace {
@@ -476,32 +482,43 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
       xb0[s] = (double)(u32)(x0[s] & 0xffffffull), xa0[s] = (double)(u32)(x0[s] >> 24);
       xb1[s] = (double)(u32)(x1[s] & 0xffffffull), xa1[s] = (double)(u32)(x1[s] >> 24);
     }
-    for (int g = g0; g < g1; ++g) {
-      const unsigned long long mask = P->mask[g] >> Bb.s0;
-      u64 r0 = 0, r1 = 0;
-      if (accumulate) {
-        r0 = t0.p[(long long)(g - g0) * t0.comp_stride + ro];
-        r1 = t1.p[(long long)(g - g0) * t1.comp_stride + ro];
-      }
-      u64 pv[MB];
-#pragma unroll
-      for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? gld(P->pt[g][Bb.s0 + s], po) : 0;
-      MacD a0, a1;
-      macd_zero(a0), macd_zero(a1);
-#pragma unroll
-      for (int s = 0; s < MB; ++s) {
-        if (((mask >> s) & 1ull) && !(LT_ABLATE & 1)) {
-          // the plan's diagonal copies are stored split (EW_SPLIT24): pieces in the two dwords
-          const double pb = (double)(u32)pv[s], pa = (double)(u32)(pv[s] >> 32);
-          macd_add(a0, xb0[s], xa0[s], pb, pa);
-          macd_add(a1, xb1[s], xa1[s], pb, pa);
+    // the giant loop instantiated with and without accumulation (uniform)
+    auto giants = [&](auto acc_tag) {
+      constexpr bool ACC = decltype(acc_tag)::value;
+      for (int g = g0; g < g1; ++g) {
+        const unsigned long long mask = P->mask[g] >> Bb.s0;
+        u64 r0 = 0, r1 = 0;
+        if (ACC) {
+          r0 = t0.p[(long long)(g - g0) * t0.comp_stride + ro];
+          r1 = t1.p[(long long)(g - g0) * t1.comp_stride + ro];
         }
+        u64 pv[MB];
+#pragma unroll
+        for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? gld(P->pt[g][Bb.s0 + s], po) : 0;
+        MacD a0, a1;
+        macd_zero(a0), macd_zero(a1);
+#pragma unroll
+        for (int s = 0; s < MB; ++s) {
+          if (((mask >> s) & 1ull) && !(LT_ABLATE & 1)) {
+            // the plan's diagonal copies are stored split (EW_SPLIT24): pieces in the two dwords
+            // (signed conversions of the dwords: converting (u32)(pv >> 32) went
+            // through the u64 conversion and left an add of 0.0 * 2^32 behind)
+            u32 w[2];
+            __builtin_memcpy(w, &pv[s], 8);
+            const double pb = (double)(int)w[0], pa = (double)(int)w[1];  // pieces < 2^24
+            macd_add(a0, xb0[s], xa0[s], pb, pa);
+            macd_add(a1, xb1[s], xa1[s], pb, pa);
+          }
+        }
+        const u64 v0 = macd_reduce(a0, mc), v1 = macd_reduce(a1, mc);
+        r0 = ACC ? add_mod(r0, v0, mc.q) : v0;
+        r1 = ACC ? add_mod(r1, v1, mc.q) : v1;
+        t0.p[(long long)(g - g0) * t0.comp_stride + ro] = r0;
+        t1.p[(long long)(g - g0) * t1.comp_stride + ro] = r1;
       }
-      r0 = add_mod(r0, macd_reduce(a0, mc), mc.q);
-      r1 = add_mod(r1, macd_reduce(a1, mc), mc.q);
-      t0.p[(long long)(g - g0) * t0.comp_stride + ro] = r0;
-      t1.p[(long long)(g - g0) * t1.comp_stride + ro] = r1;
-    }
+    };
+    if (accumulate) giants(std::true_type{});
+    else giants(std::false_type{});
     return;
   }
   for (int g = g0; g < g1; ++g) {
@@ -540,60 +557,127 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
 // D_g: decomposition of ModDown(t1_g) (digit i of group g at D.p + g*d_gstride
 // + i*D.comp_stride; its own Q limbs read from `own`, the ModDown output);
 // z = the zero giant's (t0, t1), added without automorphism.
+// Each thread takes one coefficient of IB images: the automorphism index, the
+// key words and every pointer step are shared by the IB images, so the key
+// reads from L2 and the scalar address work per product drop IB-fold.
+template <int IB>
 __global__ void __launch_bounds__(256) lt_giant_kernel(LimbSet acc, LimbSet D, LimbSet own, LimbSet t0, LimbSet z,
                                                        LtGiants G, const DeviceTables* __restrict__ tb, int N) {
-  const int bi = blockIdx.x;
+  constexpr int CH = IB >= 4 ? 2 : 4;  // digits per load chunk
+  const int b0 = blockIdx.x * IB;
   const int n = blockIdx.y * blockDim.x + threadIdx.x;
   const int l = blockIdx.z;
   if (n >= N) return;
+  const int nb = acc.nbatch - b0 < IB ? acc.nbatch - b0 : IB;  // uniform
   const int m = arg_byte(acc.mod, l);
   const ModConst mc = tb->mc[m];
   const bool isq = l <= G.level;
   const int owndigit = isq ? l / G.K : -1;
-  const long long dro = row_off(D, 0, l, bi), oro = row_off(own, 0, isq ? l : 0, bi), tro = row_off(t0, 0, l, bi);
-  u64 r0 = 0, r1 = 0;
-  int jn = G.ng > 0 ? (int)G.idx[0][n] : 0;
-  if (LT_GIANT_ACC && mc.bar_k <= 52) {  // block-uniform
-    // moduli below 2^52: every giant's products and its t0 term go into one
-    // unreduced accumulator, reduced once per <= 120 products instead of once
-    // per giant (the Barrett reduction is ~40 VALU ops per component)
-    MacAcc a0, a1;
-    mac_zero(a0), mac_zero(a1);
+  const long long dro = row_off(D, 0, l, b0), oro = row_off(own, 0, isq ? l : 0, b0), tro = row_off(t0, 0, l, b0);
+  const long long dbs = D.batch_stride, obs = own.batch_stride, tbs = t0.batch_stride;
+  u64 r0[IB], r1[IB];
+#pragma unroll
+  for (int b = 0; b < IB; ++b) r0[b] = r1[b] = 0;
+  // the giant loop, instantiated for the two reduction schemes
+  auto giants = [&](auto small_tag) {
+    constexpr bool SMALL = decltype(small_tag)::value;
+    MacAcc a0[IB], a1[IB];
+    if (SMALL) {
+#pragma unroll
+      for (int b = 0; b < IB; ++b) mac_zero(a0[b]), mac_zero(a1[b]);
+    }
     int cnt = 0;
+    int jn = G.ng > 0 ? (int)G.idx[0][n] : 0;
     for (int g = 0; g < G.ng; ++g) {
       const int j = jn;
       if (g + 1 < G.ng) jn = G.idx[g + 1][n];  // prefetch the next giant's index
-      gadget_acc(D.p + g * G.d_gstride + dro, D.comp_stride, own.p + g * G.own_gstride + oro, owndigit, G.key[g],
-                 G.beta, G.L, G.K, G.klvl[g], m, N, j, a0, a1);
-      mac_add1(a0, t0.p[g * G.t0_gstride + tro + j]);
-      cnt += G.beta + 1;
-      if (cnt + G.beta + 1 > 120) {
-        r0 = add_mod(r0, mac_reduce_small(a0, mc), mc.q);
-        r1 = add_mod(r1, mac_reduce_small(a1, mc), mc.q);
-        mac_zero(a0), mac_zero(a1);
-        cnt = 0;
+      const int klvl = G.klvl[g];
+      const long long kstride = (long long)(klvl + 1 + G.K) * N;
+      const u64* kp = G.key[g] + (long long)key_pos(m, G.L, klvl) * N + j;
+      const u64* dp = D.p + g * G.d_gstride + dro + j;
+      const u64* op = own.p + g * G.own_gstride + oro + j;
+      for (int i0 = 0; i0 < G.beta; i0 += CH) {
+        u64 d[CH][IB], k0[CH], k1[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int i = i0 + u;
+          if (i < G.beta) {
+            k0[u] = kp[(2 * i + 0) * kstride];
+            k1[u] = kp[(2 * i + 1) * kstride];
+            const u64* src = i == owndigit ? op : dp + i * D.comp_stride;
+            const long long bs = i == owndigit ? obs : dbs;
+#pragma unroll
+            for (int b = 0; b < IB; ++b)
+              if (b < nb) d[u][b] = src[b * bs];
+          }
+        }
+        if (SMALL) {
+#pragma unroll
+          for (int u = 0; u < CH; ++u)
+            if (i0 + u < G.beta) {
+#pragma unroll
+              for (int b = 0; b < IB; ++b)
+                if (b < nb) mac_add(a0[b], d[u][b], k0[u]), mac_add(a1[b], d[u][b], k1[u]);
+            }
+        } else {
+#pragma unroll
+          for (int b = 0; b < IB; ++b) {
+            if (b >= nb) break;
+            MacAcc c0, c1;
+            mac_zero(c0), mac_zero(c1);
+#pragma unroll
+            for (int u = 0; u < CH; ++u)
+              if (i0 + u < G.beta) mac_add(c0, d[u][b], k0[u]), mac_add(c1, d[u][b], k1[u]);
+            r0[b] = add_mod(r0[b], mac_reduce(c0, mc), mc.q);
+            r1[b] = add_mod(r1[b], mac_reduce(c1, mc), mc.q);
+          }
+        }
+      }
+      const u64* tp = t0.p + g * G.t0_gstride + tro + j;
+#pragma unroll
+      for (int b = 0; b < IB; ++b)
+        if (b < nb) {
+          const u64 t = tp[b * tbs];
+          if (SMALL) mac_add1(a0[b], t);
+          else r0[b] = add_mod(r0[b], t, mc.q);
+        }
+      if (SMALL) {
+        cnt += G.beta + 1;
+        if (cnt + G.beta + 1 > 120) {
+#pragma unroll
+          for (int b = 0; b < IB; ++b) {
+            r0[b] = add_mod(r0[b], mac_reduce_small(a0[b], mc), mc.q);
+            r1[b] = add_mod(r1[b], mac_reduce_small(a1[b], mc), mc.q);
+            mac_zero(a0[b]), mac_zero(a1[b]);
+          }
+          cnt = 0;
+        }
       }
     }
-    r0 = add_mod(r0, mac_reduce_small(a0, mc), mc.q);
-    r1 = add_mod(r1, mac_reduce_small(a1, mc), mc.q);
-  } else {
-    for (int g = 0; g < G.ng; ++g) {
-      const int j = jn;
-      if (g + 1 < G.ng) jn = G.idx[g + 1][n];  // prefetch the next giant's index
-      u64 a0, a1;
-      gadget_at(D.p + g * G.d_gstride + dro, D.comp_stride, own.p + g * G.own_gstride + oro, owndigit, G.key[g],
-                G.beta, G.L, G.K, G.klvl[g], m, N, j, mc, a0, a1);
-      a0 = add_mod(a0, t0.p[g * G.t0_gstride + tro + j], mc.q);
-      r0 = add_mod(r0, a0, mc.q);
-      r1 = add_mod(r1, a1, mc.q);
+    if (SMALL) {
+#pragma unroll
+      for (int b = 0; b < IB; ++b) {
+        r0[b] = add_mod(r0[b], mac_reduce_small(a0[b], mc), mc.q);
+        r1[b] = add_mod(r1[b], mac_reduce_small(a1[b], mc), mc.q);
+      }
     }
+  };
+  // moduli below 2^52: every giant's products and its t0 term go into one
+  // unreduced accumulator per image, reduced once per <= 120 products instead
+  // of once per giant (the Barrett reduction is ~40 VALU ops per component)
+  if (LT_GIANT_ACC && mc.bar_k <= 52) giants(std::true_type{});  // block-uniform
+  else giants(std::false_type{});
+#pragma unroll
+  for (int b = 0; b < IB; ++b) {
+    if (b >= nb) break;
+    u64 x0 = r0[b], x1 = r1[b];
+    if (G.has_zero) {
+      x0 = add_mod(x0, z.p[row_off(z, 0, l, b0 + b) + n], mc.q);
+      x1 = add_mod(x1, z.p[row_off(z, 1, l, b0 + b) + n], mc.q);
+    }
+    acc.p[row_off(acc, 0, l, b0 + b) + n] = x0;
+    acc.p[row_off(acc, 1, l, b0 + b) + n] = x1;
   }
-  if (G.has_zero) {
-    r0 = add_mod(r0, z.p[row_off(z, 0, l, bi) + n], mc.q);
-    r1 = add_mod(r1, z.p[row_off(z, 1, l, bi) + n], mc.q);
-  }
-  acc.p[row_off(acc, 0, l, bi) + n] = r0;
-  acc.p[row_off(acc, 1, l, bi) + n] = r1;
 }
 
 inline dim3 ew_grid(int N, int rows) { return dim3((N / 2 + 255) / 256, rows); }
@@ -687,8 +771,9 @@ int orion_launch_lt_bsgs(const LimbSet& t0, const LimbSet& t1, const LimbSet& D,
 int orion_launch_lt_giant(const LimbSet& acc, const LimbSet& D, const LimbSet& own, const LimbSet& t0,
                           const LimbSet& z, const LtGiants& G, const DeviceTables* tb, int N, hipStream_t st) {
   if (G.ng > ORION_MAXGROUP) return -1;
-  dim3 g(acc.nbatch, (N + 255) / 256, acc.nlimb);
-  hipLaunchKernelGGL(lt_giant_kernel, g, dim3(256), 0, st, acc, D, own, t0, z, G, tb, N);
+  constexpr int IB = LT_GIANT_IB;
+  dim3 g((acc.nbatch + IB - 1) / IB, (N + 255) / 256, acc.nlimb);
+  hipLaunchKernelGGL(lt_giant_kernel<IB>, g, dim3(256), 0, st, acc, D, own, t0, z, G, tb, N);
   return 0;
 }
 
