@@ -316,6 +316,7 @@ __device__ __forceinline__ u64 mac_reduce(const MacAcc& a, const ModConst& m) {
 // and the GPU parity tests compare with the oracle's plain division).
 // y[] and v are shared by every target.
 // ---------------------------------------------------------------------------
+template <int MS = ORION_MAXSRC>  // MS >= ns: the register arrays' size
 __device__ __forceinline__ u64 bext_prep(const BasisExtTable* __restrict__ T, const DeviceTables* __restrict__ tb,
                                          const u64* x, u64* y) {
   if (T->centered) {  // one source, qhatinv = 1 (wave-uniform)
@@ -325,7 +326,7 @@ __device__ __forceinline__ u64 bext_prep(const BasisExtTable* __restrict__ T, co
   double vf = 0.0;
   const int ns = T->ns;
 #pragma unroll
-  for (int i = 0; i < ORION_MAXSRC; ++i) {
+  for (int i = 0; i < MS; ++i) {
     if (i >= ns) break;
     const u64 si = tb->mc[T->src_mod[i]].q;
     y[i] = shoup_mul(x[i], T->qhatinv[i], T->qhatinv_s[i], si);

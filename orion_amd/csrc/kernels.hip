@@ -141,11 +141,12 @@ __global__ void __launch_bounds__(256) tensor_kernel(LimbSet d, LimbSet a, LimbS
 // coefficients per thread (16-B accesses); the per-target constants are
 // wave-uniform (SGPR) and v*S mod t is selected from the ns+1 precomputed
 // values with v_cndmask instead of a per-lane table lookup.
+template <int MS>
 __device__ __forceinline__ u64 bext_target_sel(const BasisExtTable* __restrict__ T, int t, int ns, u64 q,
                                                const u64* y, u64 v) {
   u64 acc = T->vS_t[t][0];
 #pragma unroll
-  for (int j = 1; j <= ORION_MAXSRC; ++j) {
+  for (int j = 1; j <= MS; ++j) {
     if (j > ns) break;
     acc = v == (u64)j ? T->vS_t[t][j] : acc;
   }
@@ -153,7 +154,7 @@ __device__ __forceinline__ u64 bext_target_sel(const BasisExtTable* __restrict__
     // the whole sum in one u64: one 32x32 -> 64 multiply-add per source,
     // then a single reduction with a float64 quotient (off by at most one)
 #pragma unroll
-    for (int i = 0; i < ORION_MAXSRC; ++i) {
+    for (int i = 0; i < MS; ++i) {
       if (i >= ns) break;
       acc += (u64)(u32)y[i] * (u32)T->qhat_t[t][i];
     }
@@ -167,13 +168,14 @@ __device__ __forceinline__ u64 bext_target_sel(const BasisExtTable* __restrict__
   // [0, 2q) by one conditional subtraction (4q < 2^63 for q < 2^61)
   const u64 q2 = q << 1, nq = 0 - q;
 #pragma unroll
-  for (int i = 0; i < ORION_MAXSRC; ++i) {
+  for (int i = 0; i < MS; ++i) {
     if (i >= ns) break;
     acc += shoup_lazy_nq(y[i], T->qhat_t[t][i], T->qhat_ts[t][i], nq);
     acc = acc >= q2 ? acc - q2 : acc;
   }
   return acc >= q ? acc - q : acc;
 }
+template <int MS>
 __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in, const BasisExtTable* __restrict__ T,
                                                         const DeviceTables* __restrict__ tb, int N, int tchunk) {
   const int row = blockIdx.y;  // (comp, image)
@@ -182,21 +184,21 @@ __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in,
   const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
   if (n >= N) return;
   const int ns = T->ns, nt = T->nt;
-  u64 x0[ORION_MAXSRC], x1[ORION_MAXSRC], y0[ORION_MAXSRC], y1[ORION_MAXSRC];
+  u64 x0[MS], x1[MS], y0[MS], y1[MS];
 #pragma unroll
-  for (int i = 0; i < ORION_MAXSRC; ++i) {
+  for (int i = 0; i < MS; ++i) {
     if (i >= ns) break;
     const ulonglong2 v = *(const ulonglong2*)(in.p + row_off(in, c, i, bi) + n);
     x0[i] = v.x;
     x1[i] = v.y;
   }
-  const u64 v0 = bext_prep(T, tb, x0, y0), v1 = bext_prep(T, tb, x1, y1);
+  const u64 v0 = bext_prep<MS>(T, tb, x0, y0), v1 = bext_prep<MS>(T, tb, x1, y1);
   const int tend = min(nt, (int)(blockIdx.z + 1) * tchunk);
   for (int t = blockIdx.z * tchunk; t < tend; ++t) {
     const u64 q = tb->mc[T->dst_mod[t]].q;
     ulonglong2 o;
-    o.x = bext_target_sel(T, t, ns, q, y0, v0);
-    o.y = bext_target_sel(T, t, ns, q, y1, v1);
+    o.x = bext_target_sel<MS>(T, t, ns, q, y0, v0);
+    o.y = bext_target_sel<MS>(T, t, ns, q, y1, v1);
     *(ulonglong2*)(out.p + row_off(out, c, t, bi) + n) = o;
   }
 }
@@ -208,6 +210,7 @@ __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in,
 // (consumers read the own limbs from the NTT-domain input, and the NTT that
 // follows covers only the target positions).
 // D: comps c*beta + i, limb pos j at D.pos[j]; Ts[i] = digit i's table.
+template <int MS>
 __global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, const BasisExtTable* __restrict__ Ts,
                                                         int beta, int K, int nqp, const DeviceTables* __restrict__ tb,
                                                         int N, int tchunk) {
@@ -220,15 +223,15 @@ __global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, c
   if (n >= N) return;
   const BasisExtTable* __restrict__ T = Ts + i;
   const int ns = T->ns, lo = i * K;
-  u64 x0[ORION_MAXSRC], x1[ORION_MAXSRC], y0[ORION_MAXSRC], y1[ORION_MAXSRC];
+  u64 x0[MS], x1[MS], y0[MS], y1[MS];
 #pragma unroll
-  for (int s = 0; s < ORION_MAXSRC; ++s) {
+  for (int s = 0; s < MS; ++s) {
     if (s >= ns) break;
     const ulonglong2 v = *(const ulonglong2*)(in.p + row_off(in, c, lo + s, bi) + n);
     x0[s] = v.x;
     x1[s] = v.y;
   }
-  const u64 v0 = bext_prep(T, tb, x0, y0), v1 = bext_prep(T, tb, x1, y1);
+  const u64 v0 = bext_prep<MS>(T, tb, x0, y0), v1 = bext_prep<MS>(T, tb, x1, y1);
   const int jend = min(nqp, (int)(blockIdx.z + 1) * tchunk);
   for (int j = blockIdx.z * tchunk; j < jend; ++j) {
     // own limbs are not written: every consumer reads them from the NTT-domain
@@ -237,8 +240,8 @@ __global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, c
     const int t = j < lo ? j : j - ns;
     const u64 q = tb->mc[T->dst_mod[t]].q;
     ulonglong2 o;
-    o.x = bext_target_sel(T, t, ns, q, y0, v0);
-    o.y = bext_target_sel(T, t, ns, q, y1, v1);
+    o.x = bext_target_sel<MS>(T, t, ns, q, y0, v0);
+    o.y = bext_target_sel<MS>(T, t, ns, q, y1, v1);
     *(ulonglong2*)(D.p + row_off(D, c * beta + i, j, bi) + n) = o;
   }
 }
@@ -390,33 +393,6 @@ __device__ __forceinline__ void gadget_at(const u64* __restrict__ dp, long long 
   }
 }
 
-// The same gadget product left unreduced: the products are added to (a0, a1)
-// (moduli below 2^52: mac_reduce_small takes up to 128 of them at once)
-__device__ __forceinline__ void gadget_acc(const u64* __restrict__ dp, long long dstride, const u64* ownp,
-                                           int owndigit, const u64* __restrict__ key, int beta, int L, int K, int klvl,
-                                           int m, int N, int j, MacAcc& a0, MacAcc& a1) {
-  const long long kstride = (long long)(klvl + 1 + K) * N;
-  const u64* kp = key + (long long)key_pos(m, L, klvl) * N + j;
-  for (int i0 = 0; i0 < beta; i0 += 4) {
-    u64 d[4], k0[4], k1[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = i0 + u;
-      if (i < beta) {
-        d[u] = i == owndigit ? ownp[j] : dp[i * dstride + j];
-        k0[u] = kp[(2 * i + 0) * kstride];
-        k1[u] = kp[(2 * i + 1) * kstride];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (i0 + u < beta) {
-        mac_add(a0, d[u], k0[u]);
-        mac_add(a1, d[u], k1[u]);
-      }
-    }
-  }
-}
 __device__ __forceinline__ void mac_add1(MacAcc& a, u64 x) {
   a.lo += x;
   a.c += (a.lo < x);
@@ -731,7 +707,16 @@ int orion_launch_basis_ext(const LimbSet& out, const LimbSet& in, const BasisExt
   dim3 g = ew_grid(N, rows);
   const int nt = out.nlimb;
   g.z = target_chunks(g, nt);
-  hipLaunchKernelGGL(basis_ext_kernel, g, dim3(256), 0, st, out, in, T, tb, N, (nt + g.z - 1) / g.z);
+  const int tc = (nt + g.z - 1) / g.z;
+  // the kernel's source arrays sized for in.nlimb (= the table's ns)
+  if (in.nlimb <= 2)
+    hipLaunchKernelGGL(basis_ext_kernel<2>, g, dim3(256), 0, st, out, in, T, tb, N, tc);
+  else if (in.nlimb <= 4)
+    hipLaunchKernelGGL(basis_ext_kernel<4>, g, dim3(256), 0, st, out, in, T, tb, N, tc);
+  else if (in.nlimb <= ORION_MAXSRC)
+    hipLaunchKernelGGL(basis_ext_kernel<ORION_MAXSRC>, g, dim3(256), 0, st, out, in, T, tb, N, tc);
+  else
+    return -1;
   return 0;
 }
 
@@ -741,7 +726,15 @@ int orion_launch_modup_all(const LimbSet& D, const LimbSet& in, const BasisExtTa
   const int rows = D.ncomp * D.nbatch;
   dim3 g = ew_grid(N, rows);
   g.z = target_chunks(g, nqp);
-  hipLaunchKernelGGL(modup_all_kernel, g, dim3(256), 0, st, D, in, Ts, beta, K, nqp, tb, N, (nqp + g.z - 1) / g.z);
+  const int tc = (nqp + g.z - 1) / g.z;
+  if (K <= 2)  // every digit has at most K sources
+    hipLaunchKernelGGL(modup_all_kernel<2>, g, dim3(256), 0, st, D, in, Ts, beta, K, nqp, tb, N, tc);
+  else if (K <= 4)
+    hipLaunchKernelGGL(modup_all_kernel<4>, g, dim3(256), 0, st, D, in, Ts, beta, K, nqp, tb, N, tc);
+  else if (K <= ORION_MAXSRC)
+    hipLaunchKernelGGL(modup_all_kernel<ORION_MAXSRC>, g, dim3(256), 0, st, D, in, Ts, beta, K, nqp, tb, N, tc);
+  else
+    return -1;
   return 0;
 }
 
