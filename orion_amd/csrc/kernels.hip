@@ -23,6 +23,11 @@
 #ifndef KS_MAC_ACC
 #define KS_MAC_ACC 0
 #endif
+// ks_mac: digits per load chunk (4 -> 2: 84 -> 62 VGPRs, 5 -> 8 waves per
+// SIMD; ks_mac 104.3 -> 96.6 us per launch, profiles/r03z_ks_mac_chunk_ab.txt)
+#ifndef KS_CH
+#define KS_CH 2
+#endif
 // 1: lt_giant accumulates all giants unreduced on moduli below 2^52
 #ifndef LT_GIANT_ACC
 #define LT_GIANT_ACC 1
@@ -294,10 +299,10 @@ __global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, Lim
   const bool small = KS_MAC_ACC && mc.bar_k <= 52 && beta <= 120;
   MacAcc s0x, s0y, s1x, s1y;
   mac_zero(s0x), mac_zero(s0y), mac_zero(s1x), mac_zero(s1y);
-  for (int i0 = 0; i0 < beta; i0 += 4) {  // chunks of 4 digits: 12 loads in flight
-    ulonglong2 d[4], kb[4], ka[4];
+  for (int i0 = 0; i0 < beta; i0 += KS_CH) {  // chunks of KS_CH digits: 3 KS_CH loads in flight
+    ulonglong2 d[KS_CH], kb[KS_CH], ka[KS_CH];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < KS_CH; ++u) {
       const int i = i0 + u;
       if (i < beta) {
         d[u] = i == owndigit ? *(const ulonglong2*)(own.p + g * G.own_gstride + row_off(own, 0, l, bi) + n)
@@ -307,7 +312,7 @@ __global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, Lim
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < KS_CH; ++u) {
       if (i0 + u < beta) {
         mac_add(s0x, d[u].x, kb[u].x);
         mac_add(s0y, d[u].y, kb[u].y);
