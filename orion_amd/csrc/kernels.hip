@@ -36,6 +36,9 @@
 #ifndef LT_GIANT_IB
 #define LT_GIANT_IB 4
 #endif
+#ifndef LT_GIANT_CH
+#define LT_GIANT_CH 0  // lt_giant digits per load chunk (0: 2 at IB >= 4, else 4)
+#endif
 
 namespace {
 
@@ -544,7 +547,7 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
 template <int IB>
 __global__ void __launch_bounds__(256) lt_giant_kernel(LimbSet acc, LimbSet D, LimbSet own, LimbSet t0, LimbSet z,
                                                        LtGiants G, const DeviceTables* __restrict__ tb, int N) {
-  constexpr int CH = IB >= 4 ? 2 : 4;  // digits per load chunk
+  constexpr int CH = LT_GIANT_CH > 0 ? LT_GIANT_CH : (IB >= 4 ? 2 : 4);  // digits per load chunk
   const int b0 = blockIdx.x * IB;
   const int n = blockIdx.y * blockDim.x + threadIdx.x;
   const int l = blockIdx.z;
