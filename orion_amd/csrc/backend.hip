@@ -845,6 +845,7 @@ struct Context {
       mc.bar_mu = (u64)(((u128)1 << (2 * mc.bar_k)) / q);
       mc.bar_mu2 = (u64)(((u128)1 << (2 * mc.bar_k + 2)) / q);
       mc.bar_mu8 = mc.bar_k <= 52 ? (u64)(((u128)1 << (2 * mc.bar_k + 8)) / q) : 0;
+      mc.bar_mu3 = mc.bar_k <= 60 ? (u64)(((u128)1 << (2 * mc.bar_k + 3)) / q) : 0;
       // CI: the unfold's 1/2 rides on the inverse's final scaling, (2N)^-1
       mc.ninv = hm_invmod((u64)N << (ci ? 1 : 0), q);
       mc.ninv_s = hm_shoup(mc.ninv, q);

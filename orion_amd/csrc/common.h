@@ -30,6 +30,7 @@ struct ModConst {
   int f64;      // 1: NTT in float64 arithmetic (q < 2^ORION_F64_BITS)
   u64 bar_mu2;  // floor(2^(2k+2) / q)                    (Barrett for x < 4 q^2)
   u64 bar_mu8;  // floor(2^(2k+8) / q), k <= 52           (Barrett for x < 256 q^2)
+  u64 bar_mu3;  // floor(2^(2k+3) / q), k <= 60           (Barrett for x < 8 q^2)
   u64 ninv, ninv_s;  // N^-1 and its Shoup companion
   double qd, qinv_d, ninv_d;  // float64 path: q, 1/q, centered N^-1
   // ConjugateInvariant ring (scheme.go:49-52, NthRoot 4N): W = psi^N (a square
@@ -289,6 +290,25 @@ __device__ __forceinline__ u64 barrett_256q2(u64 hi, u64 lo, const ModConst& m) 
   u64 r = lo - t2 * m.q;
   r = r >= m.q ? r - m.q : r;
   return r >= m.q ? r - m.q : r;
+}
+// Barrett reduction of hi:lo = x < 8 q^2 for moduli of k <= 60 bits
+// (t1 = x >> (k-1) < 2^(k+4) <= 2^64, mu3 < 2^(k+4); q_est low by at most 2)
+__device__ __forceinline__ u64 barrett_8q2(u64 hi, u64 lo, const ModConst& m) {
+  const int k = m.bar_k;
+  const u64 t1 = (lo >> (k - 1)) | (hi << (65 - k));
+  const u64 ph = mulhi64(t1, m.bar_mu3), pl = t1 * m.bar_mu3;
+  const u64 t2 = (k < 60 ? pl >> (k + 4) : 0) | (ph << (60 - k));
+  u64 r = lo - t2 * m.q;
+  r = r >= m.q ? r - m.q : r;
+  return r >= m.q ? r - m.q : r;
+}
+// a MacAcc of up to 8 products of operands below 2^60 (x1, y1 < 2^28 keep
+// the 16 mid terms below 2^64), reduced once (x < 8 q^2)
+__device__ __forceinline__ u64 mac_reduce8(const MacAcc& a, const ModConst& m) {
+  const u64 ml = a.mid << 32;
+  const u64 L = a.lo + ml;
+  const u64 H = a.hi + (a.mid >> 32) + a.c + (L < ml);
+  return barrett_8q2(H, L, m);
 }
 // a MacAcc of up to 128 products of operands < 2^52, reduced once (x < 128 q^2;
 // x1, y1 < 2^20 keep mid and hi far below 2^64)

@@ -11,7 +11,9 @@
 #include "common.h"
 
 // timing-only ablation of lt_bsgs (0 in the product): bit 0 skips the giant
-// inner products, bit 1 skips the baby gadget products
+// inner products of moduli below 2^48, bit 1 skips the baby gadget products,
+// bit 2 the giant products of the integer-path (>= 2^48) moduli, bit 3 their
+// baby gadget products
 #ifndef LT_ABLATE
 #define LT_ABLATE 0
 #endif
@@ -31,6 +33,9 @@
 // 1: lt_giant accumulates all giants unreduced on moduli below 2^52
 #ifndef LT_GIANT_ACC
 #define LT_GIANT_ACC 1
+#endif
+#ifndef LT_INT_ACC8
+#define LT_INT_ACC8 1
 #endif
 // images per lt_giant thread
 #ifndef LT_GIANT_IB
@@ -443,7 +448,7 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
   for (int s = 0; s < MB; ++s) {
     x0[s] = x1[s] = 0;
     if (s < Bb.nb) {
-      if (Bb.key[s] && !(LT_ABLATE & 2)) {
+      if (Bb.key[s] && !(LT_ABLATE & 2) && !((LT_ABLATE & 8) && mc.bar_k > 48)) {
         const int j = jx[s];
         u64 r0, r1;
         gadget_at(dp, D.comp_stride, c1p, owndigit, Bb.key[s], Bb.beta, Bb.L, Bb.K, Bb.klvl[s], m, N, j, mc, r0, r1);
@@ -505,6 +510,8 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
     else giants(std::false_type{});
     return;
   }
+  // moduli of at most 60 bits: 8 products per reduction (mac_reduce8)
+  const bool acc8 = LT_INT_ACC8 && mc.bar_k <= 60;
   for (int g = g0; g < g1; ++g) {
     const unsigned long long mask = P->mask[g] >> Bb.s0;
     u64 r0 = 0, r1 = 0;
@@ -521,13 +528,13 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
     mac_zero(a0), mac_zero(a1);
 #pragma unroll
     for (int s = 0; s < MB; ++s) {
-      if ((mask >> s) & 1ull) {
+      if (((mask >> s) & 1ull) && !(LT_ABLATE & 4)) {
         mac_add(a0, pv[s], x0[s]);
         mac_add(a1, pv[s], x1[s]);
       }
-      if ((s & 3) == 3) {
-        r0 = add_mod(r0, mac_reduce(a0, mc), mc.q);
-        r1 = add_mod(r1, mac_reduce(a1, mc), mc.q);
+      if (acc8 ? (s & 7) == 7 : (s & 3) == 3) {  // (acc8 is block-uniform)
+        r0 = add_mod(r0, acc8 ? mac_reduce8(a0, mc) : mac_reduce(a0, mc), mc.q);
+        r1 = add_mod(r1, acc8 ? mac_reduce8(a1, mc) : mac_reduce(a1, mc), mc.q);
         mac_zero(a0), mac_zero(a1);
       }
     }
