@@ -425,10 +425,11 @@ __device__ __forceinline__ void mac_add1(MacAcc& a, u64 x) {
 template <int MB>
 __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb,
                                                       const LtPlan* __restrict__ P, int g0, int g1, int accumulate,
-                                                      LimbSet ptl, const DeviceTables* __restrict__ tb, int N) {
+                                                      LimbSet ptl, const DeviceTables* __restrict__ tb, int N,
+                                                      int z0) {
   const int bi = blockIdx.x;
   const int n = blockIdx.y * blockDim.x + threadIdx.x;
-  const int l = blockIdx.z;
+  const int l = z0 + blockIdx.z;
   if (n >= N) return;
   const int m = arg_byte(t0.mod, l);
   const ModConst mc = tb->mc[m];
@@ -766,13 +767,26 @@ int orion_launch_lt_bsgs(const LimbSet& t0, const LimbSet& t1, const LimbSet& D,
                          const LtBabies& Bb, const LtPlan* plan, int g0, int g1, int accumulate, const LimbSet& ptl,
                          const DeviceTables* tb, int N, hipStream_t st) {
   if (Bb.nb < 1 || Bb.nb > LT_MAXB || g1 <= g0) return -1;
-  dim3 g(t0.nbatch, (N + 255) / 256, t0.nlimb);
-  if (Bb.nb <= 8)
-    hipLaunchKernelGGL(lt_bsgs_kernel<8>, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate, ptl, tb,
-                       N);
-  else
-    hipLaunchKernelGGL(lt_bsgs_kernel<16>, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate, ptl, tb,
-                       N);
+  auto launch = [&](int z0, int nz) {
+    if (nz <= 0) return;
+    dim3 g(t0.nbatch, (N + 255) / 256, nz);
+    if (Bb.nb <= 8)
+      hipLaunchKernelGGL(lt_bsgs_kernel<8>, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate, ptl, tb,
+                         N, z0);
+    else
+      hipLaunchKernelGGL(lt_bsgs_kernel<16>, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate, ptl, tb,
+                         N, z0);
+  };
+  // ORION_LT_SPLIT=1 (timing diagnostics): three launches, limb 0, the middle
+  // Q limbs and the last Bb.K (P) limbs, so a kernel trace times each class
+  static const bool split = getenv("ORION_LT_SPLIT") && atoi(getenv("ORION_LT_SPLIT")) == 1;
+  if (split && t0.nlimb > Bb.K + 1) {
+    launch(0, 1);
+    launch(1, t0.nlimb - 1 - Bb.K);
+    launch(t0.nlimb - Bb.K, Bb.K);
+  } else {
+    launch(0, t0.nlimb);
+  }
   return 0;
 }
 
