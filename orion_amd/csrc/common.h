@@ -392,6 +392,31 @@ struct NttIO {
 // are folded by macs_reduce.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ u64 split24(u64 x) { return (x & 0xffffffull) | ((x >> 24) << 32); }
+// operands of 48..60-bit moduli split at bit 30, kept as (lo 30 bits | hi 30
+// bits << 32) (lt_bsgs's diagonal copies): the four 30 x 30-bit piece products
+// accumulate without carries -- 8 products keep lo and hi below 2^63 and the
+// 16 mid terms below 2^64 -- one v_mad_u64_u32 each
+__device__ __forceinline__ u64 split30(u64 x) { return (x & 0x3fffffffull) | ((x >> 30) << 32); }
+struct MacW {
+  u64 lo, mid, hi;
+};
+__device__ __forceinline__ void macw_zero(MacW& a) { a.lo = a.mid = a.hi = 0; }
+// x = xa 2^30 + xb, y = ya 2^30 + yb
+__device__ __forceinline__ void macw_add(MacW& a, u32 xb, u32 xa, u32 yb, u32 ya) {
+  a.lo += (u64)xb * yb;
+  a.mid += (u64)xb * ya;
+  a.mid += (u64)xa * yb;
+  a.hi += (u64)xa * ya;
+}
+// up to 8 products of operands below q <= 2^60: x = hi 2^60 + mid 2^30 + lo
+// < 8 q^2, folded into 128 bits and Barrett-reduced
+__device__ __forceinline__ u64 macw_reduce8(const MacW& a, const ModConst& m) {
+  const u64 ml = a.mid << 30, hl = a.hi << 60;
+  const u64 L1 = a.lo + ml;
+  const u64 L = L1 + hl;
+  const u64 H = (a.mid >> 34) + (a.hi >> 4) + (L1 < ml) + (L < hl);
+  return barrett_8q2(H, L, m);
+}
 struct MacS {
   u64 lo, mid, hi;
 };

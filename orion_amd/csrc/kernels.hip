@@ -37,6 +37,13 @@
 #ifndef LT_INT_ACC8
 #define LT_INT_ACC8 1
 #endif
+#ifndef LT_WAVES8
+#define LT_WAVES8 4  // lt_bsgs_kernel8: minimum waves per SIMD (VGPR budget 512 / this)
+#endif
+// 1: lt_bsgs's 48..60-bit limbs multiply 30-bit pieces (split30 diagonals)
+#ifndef LT_INT30
+#define LT_INT30 1
+#endif
 // images per lt_giant thread
 #ifndef LT_GIANT_IB
 #define LT_GIANT_IB 4
@@ -70,7 +77,8 @@ enum EwOp : int {
   EW_SUBSCALE = 7, // o = (a - b) * s_l
   EW_COPY = 8,     // o = a
   EW_ADDSCALE = 9, // o = o + a * s_l
-  EW_SPLIT24 = 10, // o = split24(a) on limbs below 2^48 (lt_bsgs's split-MAC operand form), else a
+  EW_SPLIT24 = 10, // o = split24(a) on limbs below 2^48, split30(a) on limbs up to 2^60 (LT_INT30), else a
+                   // (lt_bsgs's split-MAC operand forms)
 };
 
 struct Scalars {
@@ -113,7 +121,11 @@ __global__ void __launch_bounds__(256) ew_kernel(LimbSet o, LimbSet a, LimbSet b
       z.y = shoup_mul(sub_mod(x.y, y.y, q), sc.s[l], sc.ss[l], q);
       break;
     case EW_COPY: z = x; break;
-    case EW_SPLIT24: z = mc.bar_k <= 48 ? make_ulonglong2(split24(x.x), split24(x.y)) : x; break;
+    case EW_SPLIT24:
+      z = mc.bar_k <= 48                 ? make_ulonglong2(split24(x.x), split24(x.y))
+          : (LT_INT30 && mc.bar_k <= 60) ? make_ulonglong2(split30(x.x), split30(x.y))
+                                         : x;
+      break;
     case EW_ADDSCALE: {
       const ulonglong2 w = *po;
       z.x = add_mod(w.x, shoup_mul(x.x, sc.s[l], sc.ss[l], q), q);
@@ -423,10 +435,10 @@ __device__ __forceinline__ void mac_add1(MacAcc& a, u64 x) {
 // touch HBM, and every diagonal (shared by the batch; the image index is the
 // fastest grid dimension) is read from L2.
 template <int MB>
-__global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb,
-                                                      const LtPlan* __restrict__ P, int g0, int g1, int accumulate,
-                                                      LimbSet ptl, const DeviceTables* __restrict__ tb, int N,
-                                                      int z0) {
+__device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const LimbSet& D, const LimbSet& ct,
+                                             const LtBabies& Bb, const LtPlan* __restrict__ P, int g0, int g1,
+                                             int accumulate, const LimbSet& ptl, const DeviceTables* __restrict__ tb,
+                                             int N, int z0) {
   const int bi = blockIdx.x;
   const int n = blockIdx.y * blockDim.x + threadIdx.x;
   const int l = z0 + blockIdx.z;
@@ -511,6 +523,42 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
     else giants(std::false_type{});
     return;
   }
+  if (LT_INT30 && mc.bar_k <= 60) {
+    // 48..60-bit moduli: 30-bit piece products accumulated without carries
+    // (MacW, one v_mad_u64_u32 each), one reduction per 8 babies; the plan's
+    // diagonal copies are stored split30
+    // (the baby pieces are cut per giant: kept as whole words they cost no
+    // extra registers)
+    for (int g = g0; g < g1; ++g) {
+      const unsigned long long mask = P->mask[g] >> Bb.s0;
+      u64 r0 = 0, r1 = 0;
+      if (accumulate) {
+        r0 = t0.p[(long long)(g - g0) * t0.comp_stride + ro];
+        r1 = t1.p[(long long)(g - g0) * t1.comp_stride + ro];
+      }
+      u64 pv[MB];
+#pragma unroll
+      for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? gld(P->pt[g][Bb.s0 + s], po) : 0;
+      MacW a0, a1;
+      macw_zero(a0), macw_zero(a1);
+#pragma unroll
+      for (int s = 0; s < MB; ++s) {
+        if (((mask >> s) & 1ull) && !(LT_ABLATE & 4)) {
+          const u32 yb = (u32)pv[s], ya = (u32)(pv[s] >> 32);
+          macw_add(a0, (u32)x0[s] & 0x3fffffffu, (u32)(x0[s] >> 30), yb, ya);
+          macw_add(a1, (u32)x1[s] & 0x3fffffffu, (u32)(x1[s] >> 30), yb, ya);
+        }
+        if ((s & 7) == 7) {
+          r0 = add_mod(r0, macw_reduce8(a0, mc), mc.q);
+          r1 = add_mod(r1, macw_reduce8(a1, mc), mc.q);
+          macw_zero(a0), macw_zero(a1);
+        }
+      }
+      t0.p[(long long)(g - g0) * t0.comp_stride + ro] = r0;
+      t1.p[(long long)(g - g0) * t1.comp_stride + ro] = r1;
+    }
+    return;
+  }
   // moduli of at most 60 bits: 8 products per reduction (mac_reduce8)
   const bool acc8 = LT_INT_ACC8 && mc.bar_k <= 60;
   for (int g = g0; g < g1; ++g) {
@@ -542,6 +590,18 @@ __global__ void __launch_bounds__(256) lt_bsgs_kernel(LimbSet t0, LimbSet t1, Li
     t0.p[(long long)(g - g0) * t0.comp_stride + ro] = r0;
     t1.p[(long long)(g - g0) * t1.comp_stride + ro] = r1;
   }
+}
+
+// MB = 8 at 4 waves per SIMD (<= 128 VGPRs); MB = 16 holds twice the babies
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LT_WAVES8)))
+lt_bsgs_kernel8(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb, const LtPlan* __restrict__ P, int g0,
+                int g1, int accumulate, LimbSet ptl, const DeviceTables* __restrict__ tb, int N, int z0) {
+  lt_bsgs_body<8>(t0, t1, D, ct, Bb, P, g0, g1, accumulate, ptl, tb, N, z0);
+}
+__global__ void __launch_bounds__(256)
+lt_bsgs_kernel16(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb, const LtPlan* __restrict__ P, int g0,
+                 int g1, int accumulate, LimbSet ptl, const DeviceTables* __restrict__ tb, int N, int z0) {
+  lt_bsgs_body<16>(t0, t1, D, ct, Bb, P, g0, g1, accumulate, ptl, tb, N, z0);
 }
 
 // Giant steps of a hoisted BSGS transform, key switches and accumulation fused:
@@ -771,10 +831,10 @@ int orion_launch_lt_bsgs(const LimbSet& t0, const LimbSet& t1, const LimbSet& D,
     if (nz <= 0) return;
     dim3 g(t0.nbatch, (N + 255) / 256, nz);
     if (Bb.nb <= 8)
-      hipLaunchKernelGGL(lt_bsgs_kernel<8>, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate, ptl, tb,
+      hipLaunchKernelGGL(lt_bsgs_kernel8, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate, ptl, tb,
                          N, z0);
     else
-      hipLaunchKernelGGL(lt_bsgs_kernel<16>, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate, ptl, tb,
+      hipLaunchKernelGGL(lt_bsgs_kernel16, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate, ptl, tb,
                          N, z0);
   };
   // ORION_LT_SPLIT=1 (timing diagnostics): three launches, limb 0, the middle
