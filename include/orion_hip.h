@@ -179,7 +179,8 @@ unsigned long OrionHipBootstrapModulus(int slots, int idx);
  * the same inputs (tests only).  Returns the element count written, or needed
  * when out is NULL; -1 on error.  Items (element type):
  *   PARAMS (long double): F, gap, K, r, degree, slots, s_y, top, L, K_P,
- *          #trace rotations, #transforms, #cosine coefficients
+ *          #trace rotations, #transforms, #cosine coefficients, t0 (EvalMod
+ *          polynomial target scale)
  *   COS (long double): EvalMod's Chebyshev coefficients, lowest first
  *   TRACE (unsigned long): Galois elements of the trace
  *   RLK / GALOIS (arg = galEl) (unsigned long): key in the full-chain layout
@@ -189,9 +190,14 @@ unsigned long OrionHipBootstrapModulus(int slots, int idx);
  *          level, N1, #diagonals, diagonal indices
  *   LT_DIAG (arg = transform << 32 | k) (unsigned long): k-th diagonal,
  *          [level+1+K_P][N] NTT domain
- *   MONO_I (unsigned long): X^(N/2) over the Q limbs, NTT domain (full slots) */
+ *   MONO_I (unsigned long): X^(N/2) over the Q limbs, NTT domain (full slots)
+ *   D2S / S2D (unsigned long): the ephemeral-secret keys EvkDenseToSparse
+ *          (made for level 0) and EvkSparseToDense, full-chain layout
+ * The CPU oracle takes only the keys (RLK, GALOIS, D2S, S2D) and derives the
+ * constants, diagonals and prime chain itself; the other items let the tests
+ * compare the two derivations. */
 enum { ORION_BTX_PARAMS = 0, ORION_BTX_COS, ORION_BTX_TRACE, ORION_BTX_RLK, ORION_BTX_GALOIS_KEYS,
-       ORION_BTX_GALOIS, ORION_BTX_LT_INFO, ORION_BTX_LT_DIAG, ORION_BTX_MONO_I };
+       ORION_BTX_GALOIS, ORION_BTX_LT_INFO, ORION_BTX_LT_DIAG, ORION_BTX_MONO_I, ORION_BTX_D2S, ORION_BTX_S2D };
 long OrionHipBootstrapExport(int slots, int what, long arg, void *out, unsigned long n);
 
 /* batch ciphertexts: one handle holds B images; ops act on the whole batch */

@@ -1563,25 +1563,408 @@ int oracle_eval_poly_ld(const oracle_ctx *c, int level, const u64 *ct, long doub
 }
 
 /* ------------------------------------------------------------------ */
-/* bootstrapping circuit of the HIP backend (backend.hip                 */
-/* Context::bootstrap / run_circuit; bootstrapper.go:19-80 is the call   */
-/* site, the circuit itself is this backend's), restated   */
-/* on the shared inputs in P (keys, diagonals, constants exported by     */
-/* OrionHipBootstrapExport):                                             */
-/*   c0 = F * INTT(limb 0)  (scheme context, mod q0)                     */
-/*   t  = NTT(centered lift of c0 to every Q limb of the boot chain),    */
-/*        scale q0                                                       */
+/* bootstrapping (bootstrapper.go:19-80 is the call site; Orion sets    */
+/* LogN, LogP, Xs and LogSlots, bootstrapper.go:33-38, and every other  */
+/* parameter is Lattigo v6's default bootstrapping.ParametersLiteral    */
+/* [U], restated here from the parameters alone -- no constant, prime   */
+/* or diagonal comes from the library under test; the shared inputs    */
+/* are the keys and the input ciphertext):                               */
+/*   CoeffsToSlots 4 x 56-bit levels, SlotsToCoeffs 3 x 39-bit levels,   */
+/*   EvalMod 60-bit levels, K = 16, Mod1 degree 30, 3 double angles,     */
+/*   Mod1InvDegree 0, LogMessageRatio 8, LogBSGSRatio 1 for the DFT      */
+/*   matrices, an ephemeral secret of Hamming weight 32.                 */
+/* Circuit:                                                              */
+/*   x  = F * (level-0 residues), F = round(q0 / 2^(8 + logScale))       */
+/*   x  = (x0, 0) + KS_{s -> s_eph}(x1) at level 0                       */
+/*   t  = NTT(centred lift of INTT(x) to every Q limb), scale q0         */
+/*   t  = (t0, 0) + KS_{s_eph -> s}(t1) at the top level                 */
 /*   gap > 1: t = gap^-1 t, then t += sigma_g(t) for each trace element  */
-/*   z  = three CoeffsToSlots transforms, each followed by a rescale     */
-/*        (the scale stays q0)                                           */
-/*   zc = sigma_{2N-1}(z)                                                */
-/*   gap > 1: y = EvalMod(z + zc)                                        */
-/*   else:    y = i EvalMod(i (zc - z)) + EvalMod(z + zc), i = X^(N/2)   */
-/*   EvalMod(u) = cosine polynomial at target 2^60, then r double angles */
-/*        y <- 2 rescale(y^2) - 1                                        */
-/*   o  = three SlotsToCoeffs transforms with rescales                   */
+/*   z  = the 4 CoeffsToSlots transforms, each followed by a rescale     */
+/*   gap > 1: y = EvalMod(z + conj z)                                    */
+/*   else:    y = i EvalMod(i (conj z - z)) + EvalMod(z + conj z)        */
+/*   EvalMod(u) = cosine polynomial at target t0, then r double angles   */
+/*        y <- rescale(2 y^2 - a^(2^(k+1)))                              */
+/*   o  = the 3 SlotsToCoeffs transforms with rescales                   */
 /*   out = gap * o (residual top level, scheme primes)                   */
 /* ------------------------------------------------------------------ */
+#define BTP_CTS 4
+#define BTP_CTS_BITS 56
+#define BTP_STC 3
+#define BTP_STC_BITS 39
+#define BTP_MOD_BITS 60
+#define BTP_DEG 30
+#define BTP_DEPTH 5 /* bits.Len64(BTP_DEG) */
+#define BTP_R 3
+#define BTP_K 16
+#define BTP_LOGMSG 8
+#define BTP_LOGBSGS 1
+#define BTP_EPH_H 32
+static const long double BTP_PI = 3.14159265358979323846264338327950288L;
+
+/* the bootstrapping chain: the residual Q primes, then fresh primes of the
+ * circuit's sizes (SlotsToCoeffs, EvalMod, CoeffsToSlots, bottom to top) and
+ * of logP, each size from its own NTTFriendlyPrimesGenerator stream, skipping
+ * every prime of the residual parameters (scheme_qp: their Q and P) */
+int oracle_btp_chain(int logN, const u64 *scheme_qp, int n_scheme, int Lres, const int *logP, int lenP, u64 *out) {
+  int bits[MAXMOD], nb = 0;
+  for (int i = 0; i < BTP_STC; i++) bits[nb++] = BTP_STC_BITS;
+  for (int i = 0; i < BTP_DEPTH + BTP_R; i++) bits[nb++] = BTP_MOD_BITS;
+  for (int i = 0; i < BTP_CTS; i++) bits[nb++] = BTP_CTS_BITS;
+  for (int i = 0; i < lenP; i++) bits[nb++] = logP[i];
+  if (Lres + nb > MAXMOD) return -1;
+  u64 taken[2 * MAXMOD];
+  int nt = 0;
+  for (int i = 0; i < n_scheme; i++) taken[nt++] = scheme_qp[i];
+  primegen gens[MAXMOD];
+  int gsize[MAXMOD], ng = 0;
+  const u64 nthroot = (u64)2 << logN;
+  for (int i = 0; i < Lres; i++) out[i] = scheme_qp[i];
+  for (int i = 0; i < nb; i++) {
+    int k;
+    for (k = 0; k < ng; k++)
+      if (gsize[k] == bits[i]) break;
+    if (k == ng) {
+      pg_init(&gens[ng], bits[i], nthroot);
+      gsize[ng++] = bits[i];
+    }
+    u64 q;
+    int dup;
+    do {
+      q = bits[i] == 61 ? pg_next_downstream(&gens[k]) : pg_next_alternating(&gens[k]);
+      if (!q) return -1;
+      dup = 0;
+      for (int j = 0; j < nt; j++) dup |= taken[j] == q;
+    } while (dup);
+    taken[nt++] = q;
+    out[Lres + i] = q;
+  }
+  return Lres + nb;
+}
+
+/* EvalMod's polynomial: the Chebyshev interpolant (degree+1 Chebyshev nodes
+ * of [-1, 1]) of a cos(2 pi (K u - 1/4) / 2^r), a = (2 pi)^(-1/2^r) */
+void oracle_btp_cos(int K, int degree, int r, long double *c) {
+  const long double a = powl(2 * BTP_PI, -1.0L / (long double)(1 << r));
+  const int m = degree + 1;
+  long double *fx = (long double *)malloc(sizeof(long double) * m);
+  for (int k = 0; k < m; k++) {
+    const long double u = cosl(BTP_PI * (k + 0.5L) / m);
+    fx[k] = a * cosl(2 * BTP_PI * (K * u - 0.25L) / (long double)(1 << r));
+  }
+  for (int j = 0; j < m; j++) {
+    long double acc = 0;
+    for (int k = 0; k < m; k++) acc += fx[k] * cosl(BTP_PI * j * (k + 0.5L) / m);
+    c[j] = acc * (j == 0 ? 1.0L : 2.0L) / m;
+  }
+  free(fx);
+}
+
+/* a diagonal map: offset (mod n slots) -> n complex values, NULL if absent;
+ * walked in ascending offset order */
+typedef struct {
+  int n;
+  cplx **d;
+} dmap;
+static dmap dm_new(int n) {
+  dmap m = {n, (cplx **)calloc(n, sizeof(cplx *))};
+  return m;
+}
+static cplx *dm_at(dmap *m, int off) {
+  if (!m->d[off]) m->d[off] = (cplx *)calloc(m->n, sizeof(cplx));
+  return m->d[off];
+}
+static void dm_free(dmap *m) {
+  for (int i = 0; i < m->n; i++) free(m->d[i]);
+  free(m->d);
+  m->d = NULL;
+}
+/* the special FFT's twiddles for ns slots (SpecialFFT / SpecialiFFT):
+ * tw[h + j] = roots[(rot[j] mod 4 len) M / (4 len)] (forward) or
+ * roots[(4 len - rot[j] mod 4 len) M / (4 len)] (inverse), len = 2h, M = 4 ns */
+static cplx *btp_twiddles(int ns, int inverse) {
+  const int M = 4 * ns;
+  int *rot;
+  cplx *roots;
+  special_tables(ns, M, &rot, &roots);
+  cplx *tw = (cplx *)calloc(ns, sizeof(cplx));
+  for (int h = 1; h < ns; h <<= 1) {
+    const int lq = h << 3, gap = M / lq;
+    for (int j = 0; j < h; j++) tw[h + j] = roots[(inverse ? lq - rot[j] % lq : rot[j] % lq) * gap];
+  }
+  free(rot);
+  free(roots);
+  return tw;
+}
+/* one butterfly stage of length len as diagonals on n slots: forward
+ * (x_p + w x_{p+h}, x_{p-h} - w x_p), inverse (x_p + x_{p+h}, (x_{p-h} - x_p) w) */
+static dmap btp_stage(int n, int len, int inverse, const cplx *tw) {
+  const int h = len / 2;
+  dmap m = dm_new(n);
+  cplx *d0 = dm_at(&m, 0), *dp = dm_at(&m, h), *dn = dm_at(&m, n - h);
+  for (int p = 0; p < n; p++) {
+    const int j = p & (len - 1);
+    if (j < h) {
+      cplx w = tw[h + j];
+      if (inverse) w.re = 1, w.im = 0;
+      d0[p].re += 1.0;
+      dp[p].re += w.re;
+      dp[p].im += w.im;
+    } else {
+      const cplx w = tw[j];
+      if (inverse) {
+        dn[p].re += w.re;
+        dn[p].im += w.im;
+      } else {
+        dn[p].re += 1.0;
+      }
+      d0[p].re -= w.re;
+      d0[p].im -= w.im;
+    }
+  }
+  return m;
+}
+/* A o B (B applied first): C[a + b] += A[a][p] B[b][p + a], offsets ascending */
+static dmap btp_compose(const dmap *A, const dmap *B) {
+  const int n = A->n;
+  dmap C = dm_new(n);
+  for (int a = 0; a < n; a++) {
+    if (!A->d[a]) continue;
+    for (int b = 0; b < n; b++) {
+      if (!B->d[b]) continue;
+      cplx *c = dm_at(&C, (a + b) % n);
+      const cplx *x = A->d[a], *y = B->d[b];
+      for (int p = 0; p < n; p++) {
+        const cplx t = cmul(x[p], y[(p + a) % n]);
+        c[p].re += t.re;
+        c[p].im += t.im;
+      }
+    }
+  }
+  return C;
+}
+/* the stages of the ns-point transform in application order, over ng
+ * transforms, the extra stages to the first ones */
+static int btp_groups(int ns, int inverse, int ng, int lens[][16], int *cnt) {
+  int all[32], tot = 0;
+  if (inverse)
+    for (int len = ns; len >= 2; len /= 2) all[tot++] = len;
+  else
+    for (int len = 2; len <= ns; len *= 2) all[tot++] = len;
+  int at = 0;
+  for (int k = 0; k < ng; k++) {
+    cnt[k] = tot / ng + (k < tot % ng ? 1 : 0);
+    for (int i = 0; i < cnt[k]; i++) lens[k][i] = all[at++];
+  }
+  return tot;
+}
+
+typedef struct {
+  int level, n1, nd;
+  int *idx;
+  u64 **pts; /* [level+1+K][N] QP plaintexts, pre-rotated by the giant step */
+} btp_lt;
+
+struct oracle_btp_circuit {
+  int slots, gap, K, r, degree, top, log_scale;
+  u64 F;
+  long double cos[BTP_DEG + 1], dac[BTP_R], t0, s_y;
+  btp_lt lt[BTP_CTS + BTP_STC]; /* CoeffsToSlots, then SlotsToCoeffs */
+  int ntrace;
+  u64 trace[32];
+  u64 *mono_i; /* X^(N/2) over the Q limbs (NTT), full slots only */
+};
+
+/* complex values on the N/2 slots encoded at scale over the limbs mods
+ * (encoder.go Encode of a complex vector; oracle_encode's real-valued path
+ * with the imaginary parts kept) */
+static void encode_cplx(const oracle_ctx *c, const cplx *vals, double scale, const int *mods, int nm, u64 *out) {
+  const int N = c->N, n = N / 2, M = 4 * n;
+  int *rot;
+  cplx *roots;
+  special_tables(n, M, &rot, &roots);
+  cplx *v = (cplx *)malloc(sizeof(cplx) * n);
+  memcpy(v, vals, sizeof(cplx) * n);
+  special_ifft(v, n, M, rot, roots);
+  for (int i = 0; i < n; i++) {
+    to_crt(v[i].re, scale, c, mods, nm, out + i, (size_t)N);
+    to_crt(v[i].im, scale, c, mods, nm, out + i + n, (size_t)N);
+  }
+  for (int m = 0; m < nm; m++) oracle_ntt(c, mods[m], out + (size_t)m * N);
+  free(v);
+  free(rot);
+  free(roots);
+}
+
+/* a BSGS transform from a diagonal map: N1 (FindBestBSGSRatio, LogBSGSRatio
+ * 1), each diagonal rotated by minus its giant step and encoded at scale
+ * q_level over QP (lineartransform.go:61-68's Encode, restated) */
+static void btp_make_lt(const oracle_ctx *bc, const dmap *m, int level, btp_lt *T) {
+  const int N = bc->N, n = N / 2, K = bc->K;
+  T->level = level;
+  T->nd = 0;
+  T->idx = (int *)malloc(sizeof(int) * n);
+  for (int off = 0; off < n; off++)
+    if (m->d[off]) T->idx[T->nd++] = off;
+  T->n1 = oracle_find_best_bsgs_n1(T->idx, T->nd, n, BTP_LOGBSGS);
+  T->pts = (u64 **)malloc(sizeof(u64 *) * T->nd);
+  int mods[MAXMOD], nm = 0;
+  for (int j = 0; j <= level; j++) mods[nm++] = j;
+  for (int k = 0; k < K; k++) mods[nm++] = bc->L + k;
+  cplx *vec = (cplx *)malloc(sizeof(cplx) * n);
+  for (int d = 0; d < T->nd; d++) {
+    int gi, bi;
+    bsgs_split(T->idx[d], n, T->n1, &gi, &bi);
+    const cplx *src = m->d[T->idx[d]];
+    for (int s = 0; s < n; s++) vec[s] = src[((s - gi) % n + n) % n];
+    T->pts[d] = (u64 *)malloc(sizeof(u64) * (size_t)nm * N);
+    encode_cplx(bc, vec, (double)bc->mod[level], mods, nm, T->pts[d]);
+  }
+  free(vec);
+}
+
+oracle_btp_circuit *oracle_btp_new(const oracle_ctx *bc, int log_scale, int slots) {
+  const int N = bc->N, n = N / 2;
+  if (bc->ci || slots < 2 || slots > n || (slots & (slots - 1))) return NULL;
+  if (bc->L < BTP_CTS + BTP_DEPTH + BTP_R + BTP_STC + 1) return NULL;
+  oracle_btp_circuit *C = (oracle_btp_circuit *)calloc(1, sizeof(oracle_btp_circuit));
+  C->slots = slots;
+  C->gap = n / slots;
+  C->K = BTP_K;
+  C->r = BTP_R;
+  C->degree = BTP_DEG;
+  C->log_scale = log_scale;
+  C->top = bc->L - 1;
+  oracle_btp_cos(C->K, C->degree, C->r, C->cos);
+  {
+    long double v = powl(2 * BTP_PI, -1.0L / (long double)(1 << C->r));
+    for (int i = 0; i < C->r; i++) C->dac[i] = v = v * v;
+  }
+  {
+    const long double f = roundl((long double)bc->mod[0] / ldexpl(1.0L, BTP_LOGMSG + log_scale));
+    C->F = f < 1 ? 1 : (u64)f;
+  }
+  for (int s = slots; s < n; s *= 2) C->trace[C->ntrace++] = oracle_galois_element(bc, s);
+  const int packed = slots < n;
+  int lens[8][16], cnt[8];
+  /* CoeffsToSlots: 2^-s and the 4th root of 1 / (2K) per transform */
+  {
+    cplx *twi = btp_twiddles(slots, 1);
+    btp_groups(slots, 1, BTP_CTS, lens, cnt);
+    const double kf = sqrt(sqrt(1.0 / (2.0 * C->K)));
+    int level = C->top;
+    for (int k = 0; k < BTP_CTS; k++) {
+      dmap M = dm_new(n);
+      cplx *m0 = dm_at(&M, 0);
+      for (int p = 0; p < n; p++) m0[p].re = ldexp(kf, -cnt[k]), m0[p].im = 0;
+      for (int i = 0; i < cnt[k]; i++) {
+        dmap S = btp_stage(n, lens[k][i], 1, twi);
+        dmap X = btp_compose(&S, &M);
+        dm_free(&S);
+        dm_free(&M);
+        M = X;
+      }
+      if (packed && k == BTP_CTS - 1) { /* a = 1 on [0, n), -i on [n, 2n) of every 2n-period */
+        dmap A = dm_new(n);
+        cplx *a0 = dm_at(&A, 0);
+        for (int p = 0; p < n; p++) {
+          const int lo = (p % (2 * slots)) < slots;
+          a0[p].re = lo ? 1 : 0;
+          a0[p].im = lo ? 0 : -1;
+        }
+        dmap X = btp_compose(&A, &M);
+        dm_free(&A);
+        dm_free(&M);
+        M = X;
+      }
+      btp_make_lt(bc, &M, level--, &C->lt[k]);
+      dm_free(&M);
+    }
+    free(twi);
+  }
+  /* EvalMod scales: t0 such that the r double angles end on 2^60 */
+  const int lp = C->top - BTP_CTS - BTP_DEPTH;
+  {
+    long double T = ldexpl(1.0L, BTP_MOD_BITS);
+    for (int i = C->r - 1; i >= 0; i--) T = sqrtl(T * (long double)bc->mod[lp - i]);
+    C->t0 = T;
+    long double sc = T;
+    for (int i = 0; i < C->r; i++) sc = sc * sc / (long double)bc->mod[lp - i];
+    C->s_y = sc;
+  }
+  /* SlotsToCoeffs: forward stages times the cube root of q0 / (F s_y) each */
+  {
+    cplx *twf = btp_twiddles(slots, 0);
+    btp_groups(slots, 0, BTP_STC, lens, cnt);
+    const double cf = cbrt((double)((long double)bc->mod[0] / ((long double)C->F * C->s_y)));
+    int level = lp - C->r;
+    for (int k = 0; k < BTP_STC; k++) {
+      dmap M = dm_new(n);
+      if (packed && k == 0) { /* unpack real + i imag */
+        cplx *m0 = dm_at(&M, 0), *m1 = dm_at(&M, slots);
+        for (int p = 0; p < n; p++) {
+          const int lo = (p % (2 * slots)) < slots;
+          m0[p].re = lo ? cf : 0, m0[p].im = lo ? 0 : cf;
+          m1[p].re = lo ? 0 : cf, m1[p].im = lo ? cf : 0;
+        }
+      } else {
+        cplx *m0 = dm_at(&M, 0);
+        for (int p = 0; p < n; p++) m0[p].re = cf, m0[p].im = 0;
+      }
+      for (int i = 0; i < cnt[k]; i++) {
+        dmap S = btp_stage(n, lens[k][i], 0, twf);
+        dmap X = btp_compose(&S, &M);
+        dm_free(&S);
+        dm_free(&M);
+        M = X;
+      }
+      btp_make_lt(bc, &M, level--, &C->lt[BTP_CTS + k]);
+      dm_free(&M);
+    }
+    free(twf);
+  }
+  if (!packed) { /* X^(N/2) */
+    C->mono_i = (u64 *)calloc((size_t)bc->L * N, sizeof(u64));
+    for (int l = 0; l < bc->L; l++) {
+      C->mono_i[(size_t)l * N + N / 2] = 1;
+      oracle_ntt(bc, l, C->mono_i + (size_t)l * N);
+    }
+  }
+  return C;
+}
+
+void oracle_btp_free(oracle_btp_circuit *C) {
+  if (!C) return;
+  for (int k = 0; k < BTP_CTS + BTP_STC; k++) {
+    for (int d = 0; d < C->lt[k].nd; d++) free(C->lt[k].pts[d]);
+    free(C->lt[k].pts);
+    free(C->lt[k].idx);
+  }
+  free(C->mono_i);
+  free(C);
+}
+
+int oracle_btp_params(const oracle_btp_circuit *C, long double *out) {
+  const long double v[] = {(long double)C->F, (long double)C->gap, (long double)C->K, (long double)C->r,
+                           (long double)C->degree, (long double)C->slots, C->s_y, (long double)C->top,
+                           (long double)C->ntrace, (long double)(BTP_CTS + BTP_STC), (long double)(C->degree + 1),
+                           C->t0};
+  const int cnt = (int)(sizeof(v) / sizeof(v[0]));
+  if (out) memcpy(out, v, sizeof(v));
+  return cnt;
+}
+int oracle_btp_lt_info(const oracle_btp_circuit *C, int k, int *level, int *n1, int *idx) {
+  if (k < 0 || k >= BTP_CTS + BTP_STC) return -1;
+  *level = C->lt[k].level;
+  *n1 = C->lt[k].n1;
+  if (idx) memcpy(idx, C->lt[k].idx, sizeof(int) * C->lt[k].nd);
+  return C->lt[k].nd;
+}
+const u64 *oracle_btp_lt_diag(const oracle_btp_circuit *C, int k, int j) {
+  if (k < 0 || k >= BTP_CTS + BTP_STC || j < 0 || j >= C->lt[k].nd) return NULL;
+  return C->lt[k].pts[j];
+}
+const long double *oracle_btp_cos_of(const oracle_btp_circuit *C) { return C->cos; }
+
 static const u64 *btp_key(const oracle_btp *P, u64 g) {
   for (int i = 0; i < P->ngk; i++)
     if (P->galEls[i] == g) return P->gks[i];
@@ -1622,11 +2005,11 @@ static void pct_mul_pt(const oracle_ctx *c, pct *a, const u64 *pt) {
         *x = mulmod(*x, pt[(size_t)l * c->N + i], c->mod[l]);
       }
 }
-static int btp_lt_rescale(const oracle_ctx *bc, const oracle_btp *P, int k, pct *x) {
-  if (P->lt_level[k] != x->level) return -1;
+static int btp_lt_rescale(const oracle_ctx *bc, const oracle_btp *P, const btp_lt *T, pct *x) {
+  if (T->level != x->level) return -1;
   pct y = pct_alloc(bc, x->level, x->scale);
-  oracle_lt_bsgs(bc, x->level, x->v, P->lt_ndiag[k], P->lt_idx[k], P->lt_pts[k], P->lt_n1[k], P->ngk, P->galEls,
-                 P->gks, y.v);
+  oracle_lt_bsgs(bc, x->level, x->v, T->nd, T->idx, (const u64 *const *)T->pts, T->n1, P->ngk, P->galEls, P->gks,
+                 y.v);
   free(x->v);
   const long double s = x->scale;
   *x = y;
@@ -1634,11 +2017,10 @@ static int btp_lt_rescale(const oracle_ctx *bc, const oracle_btp *P, int k, pct 
   x->scale = s; /* diagonals at scale q_level: the rescale restores the input scale */
   return 0;
 }
-static int btp_eval_mod(const oracle_ctx *bc, const oracle_btp *P, const pct *u, pct *y) {
+static int btp_eval_mod(const oracle_ctx *bc, const oracle_btp_circuit *C, const oracle_btp *P, const pct *u, pct *y) {
   pct o = pct_alloc(bc, u->level, 0);
   long double sc = 0;
-  const int lv = oracle_eval_poly_ld(bc, u->level, u->v, u->scale, P->cos, P->ncos, 1, P->poly_scale, P->rlk, o.v,
-                                     &sc);
+  const int lv = oracle_eval_poly_ld(bc, u->level, u->v, u->scale, C->cos, C->degree + 1, 1, C->t0, P->rlk, o.v, &sc);
   if (lv < 0) {
     free(o.v);
     return -1;
@@ -1647,89 +2029,111 @@ static int btp_eval_mod(const oracle_ctx *bc, const oracle_btp *P, const pct *u,
   memcpy(t.v, o.v, sizeof(u64) * 2 * (size_t)(lv + 1) * bc->N);
   free(o.v);
   u64 k[MAXMOD];
-  for (int j = 0; j < P->r; j++) { /* cos(2a) = 2 cos(a)^2 - 1 */
+  for (int j = 0; j < C->r; j++) { /* y <- 2 y^2 - a^(2^(j+1)), then the rescale */
     pct s2 = pct_mul_relin(bc, &t, &t, P->rlk);
     free(t.v);
-    pct_rescale(bc, &s2);
     const size_t L = (size_t)(s2.level + 1) * bc->N;
     for (size_t i = 0; i < 2 * L; i++) {
       const int l = (int)((i % L) / bc->N);
       s2.v[i] = addmod(s2.v[i], s2.v[i], bc->mod[l]);
     }
-    big_const_res(bc, -s2.scale, s2.level, k);
+    big_const_res(bc, -C->dac[j] * s2.scale, s2.level, k);
     for (int l = 0; l <= s2.level; l++)
       for (int i = 0; i < bc->N; i++) s2.v[(size_t)l * bc->N + i] = addmod(s2.v[(size_t)l * bc->N + i], k[l], bc->mod[l]);
+    pct_rescale(bc, &s2);
     t = s2;
   }
   *y = t;
   return 0;
 }
 
-int oracle_bootstrap(const oracle_ctx *sc, const oracle_ctx *bc, const oracle_btp *P, int level, const u64 *ct,
-                     u64 *out) {
+int oracle_bootstrap(const oracle_ctx *sc, const oracle_ctx *bc, const oracle_btp_circuit *C, const oracle_btp *P,
+                     int level, const u64 *ct, u64 *out) {
   const int N = bc->N, Ls = sc->L, top = bc->L - 1;
-  if (sc->N != N || sc->mod[0] != bc->mod[0]) return -1;
+  if (sc->N != N || sc->mod[0] != bc->mod[0] || C->top != top) return -1;
+  if (!P->d2s || !P->s2d || !P->rlk) return -1;
   const u64 q0 = bc->mod[0];
-  /* c0: level-0 residues of both components, coefficient domain, times F */
-  u64 *c0 = (u64 *)malloc(sizeof(u64) * 2 * N);
-  for (int comp = 0; comp < 2; comp++) {
-    memcpy(c0 + (size_t)comp * N, ct + (size_t)comp * (level + 1) * N, sizeof(u64) * N);
-    oracle_intt(sc, 0, c0 + (size_t)comp * N);
-    if (P->F > 1)
-      for (int i = 0; i < N; i++) c0[(size_t)comp * N + i] = mulmod(c0[(size_t)comp * N + i], P->F % q0, q0);
-  }
-  /* ModRaise: the centered lift (x > q0 / 2 is x - q0) to every Q limb */
-  pct t = pct_alloc(bc, top, (long double)q0);
+  /* ScaleDown: F times the level-0 residues (NTT domain) */
+  u64 *x = (u64 *)malloc(sizeof(u64) * 2 * N);
   for (int comp = 0; comp < 2; comp++)
+    for (int i = 0; i < N; i++) x[(size_t)comp * N + i] = mulmod(ct[(size_t)comp * (level + 1) * N + i], C->F % q0, q0);
+  /* EvkDenseToSparse at level 0 */
+  {
+    u64 *k0 = (u64 *)malloc(sizeof(u64) * N), *k1 = (u64 *)malloc(sizeof(u64) * N);
+    oracle_keyswitch(bc, 0, x + N, P->d2s, k0, k1);
+    for (int i = 0; i < N; i++) {
+      x[i] = addmod(x[i], k0[i], q0);
+      x[N + i] = k1[i];
+    }
+    free(k0);
+    free(k1);
+  }
+  /* ModRaise: the centred lift (x > q0 / 2 is x - q0) to every Q limb */
+  pct m = pct_alloc(bc, top, (long double)q0);
+  for (int comp = 0; comp < 2; comp++) {
+    oracle_intt(bc, 0, x + (size_t)comp * N);
     for (int l = 0; l <= top; l++) {
       const u64 q = bc->mod[l];
-      u64 *o = t.v + ((size_t)comp * (top + 1) + l) * N;
+      u64 *o = m.v + ((size_t)comp * (top + 1) + l) * N;
       for (int i = 0; i < N; i++) {
-        const u64 x = c0[(size_t)comp * N + i];
-        const int neg = x > (q0 >> 1);
-        const u64 r = (neg ? q0 - x : x) % q;
+        const u64 v = x[(size_t)comp * N + i];
+        const int neg = v > (q0 >> 1);
+        const u64 r = (neg ? q0 - v : v) % q;
         o[i] = neg ? (r ? q - r : 0) : r;
       }
       oracle_ntt(bc, l, o);
     }
-  free(c0);
+  }
+  free(x);
+  /* EvkSparseToDense at the top level */
+  pct t = pct_alloc(bc, top, m.scale);
+  {
+    const size_t PQ = (size_t)(top + 1) * N;
+    oracle_keyswitch(bc, top, m.v + PQ, P->s2d, t.v, t.v + PQ);
+    for (int l = 0; l <= top; l++)
+      for (int i = 0; i < N; i++) {
+        const size_t j = (size_t)l * N + i;
+        t.v[j] = addmod(t.v[j], m.v[j], bc->mod[l]);
+      }
+  }
+  free(m.v);
   int rc = 0;
-  if (P->gap > 1) { /* trace: gap^-1 t + its rotations by slots * 2^i */
+  if (C->gap > 1) { /* trace: gap^-1 t + its rotations by slots * 2^i */
     for (int l = 0; l <= top; l++) {
-      const u64 q = bc->mod[l], gi = invmod((u64)P->gap % q, q);
+      const u64 q = bc->mod[l], gi = invmod((u64)C->gap % q, q);
       for (int comp = 0; comp < 2; comp++)
         for (int i = 0; i < N; i++) {
-          u64 *x = t.v + ((size_t)comp * (top + 1) + l) * N + i;
-          *x = mulmod(*x, gi, q);
+          u64 *v = t.v + ((size_t)comp * (top + 1) + l) * N + i;
+          *v = mulmod(*v, gi, q);
         }
     }
-    for (int j = 0; j < P->ntrace && !rc; j++) {
+    for (int j = 0; j < C->ntrace && !rc; j++) {
       pct r = pct_clone(bc, &t);
-      rc = btp_galois(bc, P, &r, P->trace_gal[j]);
+      rc = btp_galois(bc, P, &r, C->trace[j]);
       if (!rc) pct_addsub(bc, &t, &r, 0);
       free(r.v);
     }
   }
-  for (int k = 0; k < 3 && !rc; k++) rc = btp_lt_rescale(bc, P, k, &t); /* CoeffsToSlots */
+  for (int k = 0; k < BTP_CTS && !rc; k++) rc = btp_lt_rescale(bc, P, &C->lt[k], &t); /* CoeffsToSlots */
   pct y = {0, 0, NULL};
   if (!rc) {
     pct zc = pct_clone(bc, &t);
     rc = btp_galois(bc, P, &zc, 2 * (u64)N - 1);
-    if (!rc && P->gap > 1) {
+    if (!rc && C->gap > 1) {
       pct u = pct_clone(bc, &t);
       pct_addsub(bc, &u, &zc, 0);
-      rc = btp_eval_mod(bc, P, &u, &y);
+      rc = btp_eval_mod(bc, C, P, &u, &y);
       free(u.v);
     } else if (!rc) {
       pct re = pct_clone(bc, &t), im = pct_clone(bc, &zc);
       pct_addsub(bc, &re, &zc, 0);
       pct_addsub(bc, &im, &t, 1);
-      pct_mul_pt(bc, &im, P->mono_i);
+      pct_mul_pt(bc, &im, C->mono_i);
       pct yr, yi;
-      rc = btp_eval_mod(bc, P, &re, &yr);
-      if (!rc) rc = btp_eval_mod(bc, P, &im, &yi);
+      rc = btp_eval_mod(bc, C, P, &re, &yr);
+      if (!rc) rc = btp_eval_mod(bc, C, P, &im, &yi);
       if (!rc) {
-        pct_mul_pt(bc, &yi, P->mono_i);
+        pct_mul_pt(bc, &yi, C->mono_i);
         if (yr.level != yi.level) rc = -1;
         else pct_addsub(bc, &yi, &yr, 0);
         y = yi;
@@ -1741,12 +2145,12 @@ int oracle_bootstrap(const oracle_ctx *sc, const oracle_ctx *bc, const oracle_bt
     free(zc.v);
   }
   free(t.v);
-  for (int k = 3; k < 6 && !rc; k++) rc = btp_lt_rescale(bc, P, k, &y); /* SlotsToCoeffs */
+  for (int k = 0; k < BTP_STC && !rc; k++) rc = btp_lt_rescale(bc, P, &C->lt[BTP_CTS + k], &y); /* SlotsToCoeffs */
   if (!rc && y.level != Ls - 1) rc = -1;
   if (!rc) { /* post-scale gap (Orion bootstrapper.go:73-74), on the scheme's primes */
     for (int comp = 0; comp < 2; comp++)
       for (int l = 0; l < Ls; l++) {
-        const u64 q = bc->mod[l], g = (u64)P->gap % q;
+        const u64 q = bc->mod[l], g = (u64)C->gap % q;
         for (int i = 0; i < N; i++)
           out[((size_t)comp * Ls + l) * N + i] = mulmod(y.v[((size_t)comp * (y.level + 1) + l) * N + i], g, q);
       }

@@ -178,30 +178,40 @@ int oracle_eval_poly_ld(const oracle_ctx *ctx, int level, const uint64_t *ct,
                         long double target, const uint64_t *rlk, uint64_t *out,
                         long double *out_scale);
 
-/* ---- bootstrapping: the HIP backend's circuit (backend.hip run_circuit,
- * reached from bootstrapper.go:61-80), restated on shared inputs exported
- * by OrionHipBootstrapExport.  sc: the scheme's context (its Q primes are the
- * first L primes of bc); bc: the bootstrapping chain.  ct: [2][level+1][N]
- * (scheme); out: [2][L_scheme][N] at the residual top level.  Returns 0, or
- * -1 when an input is missing or a level does not match. ---- */
+/* ---- bootstrapping (bootstrapper.go:19-80 call site): Lattigo v6's default
+ * bootstrapping.ParametersLiteral [U] restated, every constant, diagonal and
+ * prime derived here from the parameters (nothing from the library under
+ * test); the shared inputs are the keys and the input ciphertext.
+ * sc: the scheme's context; bc: the bootstrapping chain (its first L_sc Q
+ * primes are the scheme's). ---- */
+/* the bootstrapping chain: scheme Q (Lres), circuit primes, then P of logP;
+ * returns the prime count (Q count = Lres + 15), -1 when a stream runs out */
+int oracle_btp_chain(int logN, const uint64_t *scheme_qp, int n_scheme, int Lres, const int *logP, int lenP,
+                     uint64_t *out);
+/* EvalMod's Chebyshev coefficients (degree+1, lowest first) */
+void oracle_btp_cos(int K, int degree, int r, long double *c);
+typedef struct oracle_btp_circuit oracle_btp_circuit;
+/* the circuit for `slots` slots under bc, scheme default scale 2^log_scale */
+oracle_btp_circuit *oracle_btp_new(const oracle_ctx *bc, int log_scale, int slots);
+void oracle_btp_free(oracle_btp_circuit *C);
+/* F, gap, K, r, degree, slots, s_y, top, #trace, #transforms, degree+1, t0 */
+int oracle_btp_params(const oracle_btp_circuit *C, long double *out);
+const long double *oracle_btp_cos_of(const oracle_btp_circuit *C);
+/* transform k (0..3 CoeffsToSlots, 4..6 SlotsToCoeffs): level, N1, indices;
+ * returns the diagonal count; diag j: [level+1+K][N] NTT, pre-rotated */
+int oracle_btp_lt_info(const oracle_btp_circuit *C, int k, int *level, int *n1, int *idx);
+const uint64_t *oracle_btp_lt_diag(const oracle_btp_circuit *C, int k, int j);
+/* the keys of bc (full-chain layout [dnum][2][L+K][N]) */
 typedef struct oracle_btp {
-  int gap, K, r;                    /* gap = N / (2 slots) */
-  uint64_t F;                       /* message pre-scale before ModRaise */
-  int ncos;
-  const long double *cos;           /* EvalMod Chebyshev coefficients */
-  long double poly_scale;           /* EvalMod polynomial target scale (2^60) */
-  int ntrace;
-  const uint64_t *trace_gal;
-  int lt_level[6], lt_n1[6], lt_ndiag[6]; /* 0..2 CoeffsToSlots, 3..5 SlotsToCoeffs */
-  const int *lt_idx[6];
-  const uint64_t *const *lt_pts[6];
-  const uint64_t *mono_i;           /* X^(N/2) over the Q limbs (NTT), full slots */
+  const uint64_t *rlk;
   int ngk;
   const uint64_t *galEls;
-  const uint64_t *const *gks;       /* Galois keys of bc, layout as evk */
-  const uint64_t *rlk;              /* relinearisation key of bc */
+  const uint64_t *const *gks;
+  const uint64_t *d2s, *s2d; /* EvkDenseToSparse (level 0), EvkSparseToDense */
 } oracle_btp;
-int oracle_bootstrap(const oracle_ctx *sc, const oracle_ctx *bc, const oracle_btp *P,
+/* ct: [2][level+1][N] (scheme); out: [2][L_scheme][N] at the residual top
+ * level.  Returns 0, or -1 when a key is missing or a level does not match. */
+int oracle_bootstrap(const oracle_ctx *sc, const oracle_ctx *bc, const oracle_btp_circuit *C, const oracle_btp *P,
                      int level, const uint64_t *ct, uint64_t *out);
 
 /* coefficient-wise helpers used by tests */

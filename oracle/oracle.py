@@ -23,13 +23,10 @@ _u32p = ctypes.POINTER(ctypes.c_uint32)
 
 
 class OracleBtp(ctypes.Structure):
-    """oracle_btp (ckks_oracle.h): the bootstrapping circuit's shared inputs."""
-    _fields_ = [("gap", ctypes.c_int), ("K", ctypes.c_int), ("r", ctypes.c_int), ("F", ctypes.c_uint64),
-                ("ncos", ctypes.c_int), ("cos", ctypes.POINTER(ctypes.c_longdouble)),
-                ("poly_scale", ctypes.c_longdouble), ("ntrace", ctypes.c_int), ("trace_gal", _u64p),
-                ("lt_level", ctypes.c_int * 6), ("lt_n1", ctypes.c_int * 6), ("lt_ndiag", ctypes.c_int * 6),
-                ("lt_idx", _intp * 6), ("lt_pts", ctypes.POINTER(_u64p) * 6), ("mono_i", _u64p),
-                ("ngk", ctypes.c_int), ("galEls", _u64p), ("gks", ctypes.POINTER(_u64p)), ("rlk", _u64p)]
+    """oracle_btp (ckks_oracle.h): the bootstrapping keys, the circuit's only
+    shared inputs besides the input ciphertext."""
+    _fields_ = [("rlk", _u64p), ("ngk", ctypes.c_int), ("galEls", _u64p), ("gks", ctypes.POINTER(_u64p)),
+                ("d2s", _u64p), ("s2d", _u64p)]
 
 
 def build():
@@ -77,7 +74,16 @@ def _load():
         "oracle_eval_poly_ldp": (ctypes.c_int, [vp, ctypes.c_int, _u64p, ctypes.POINTER(ctypes.c_longdouble), _dblp,
                                                 ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_longdouble), _u64p,
                                                 _u64p, ctypes.POINTER(ctypes.c_longdouble)]),
-        "oracle_bootstrap": (ctypes.c_int, [vp, vp, ctypes.POINTER(OracleBtp), ctypes.c_int, _u64p, _u64p]),
+        "oracle_bootstrap": (ctypes.c_int, [vp, vp, vp, ctypes.POINTER(OracleBtp), ctypes.c_int, _u64p, _u64p]),
+        "oracle_btp_chain": (ctypes.c_int, [ctypes.c_int, _u64p, ctypes.c_int, ctypes.c_int, _intp, ctypes.c_int,
+                                            _u64p]),
+        "oracle_btp_cos": (None, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_longdouble)]),
+        "oracle_btp_new": (vp, [vp, ctypes.c_int, ctypes.c_int]),
+        "oracle_btp_free": (None, [vp]),
+        "oracle_btp_params": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_longdouble)]),
+        "oracle_btp_cos_of": (ctypes.POINTER(ctypes.c_longdouble), [vp]),
+        "oracle_btp_lt_info": (ctypes.c_int, [vp, ctypes.c_int, _intp, _intp, _intp]),
+        "oracle_btp_lt_diag": (_u64p, [vp, ctypes.c_int, ctypes.c_int]),
         "oracle_chacha20_block": (None, [_u32p, ctypes.c_uint32, _u32p, _u32p]),
         "oracle_enc_key": (None, [ctypes.c_uint64, _u32p]),
         "oracle_gauss_cdt": (None, [ctypes.c_double, ctypes.c_int, _u64p]),
@@ -299,11 +305,12 @@ class Oracle:
             raise ValueError("level < depth")
         return out[:2 * (lv + 1) * self.N].reshape(2, lv + 1, self.N).copy(), lv, osc.value
 
-    def bootstrap(self, boot, inputs, ct, level):
-        """The HIP backend's bootstrapping circuit restated (oracle_bootstrap):
-        self = the scheme's oracle, boot = the bootstrapping chain's oracle,
-        inputs = the circuit's shared inputs (tests: HipLibrary.bootstrap_export),
-        ct [2][level+1][N].  Returns [2][L][N] at the residual top level."""
+    def bootstrap(self, boot, circuit, keys, ct, level):
+        """Bootstrap restated (oracle_bootstrap): self = the scheme's oracle,
+        boot = the bootstrapping chain's oracle, circuit = BtpCircuit (the
+        oracle's own constants and diagonals), keys = dict(rlk, gks {galEl:
+        key}, d2s, s2d) of the bootstrapping chain, ct [2][level+1][N].
+        Returns [2][L][N] at the residual top level."""
         keep = []
 
         def u64arr(a):
@@ -312,29 +319,17 @@ class Oracle:
             return _p(a)
 
         P = OracleBtp()
-        P.gap, P.K, P.r, P.F = inputs["gap"], inputs["K"], inputs["r"], inputs["F"]
-        cos = np.ascontiguousarray(inputs["cos"], dtype=np.longdouble)  # the 80-bit values, not via double
-        keep.append(cos)
-        P.ncos, P.cos = len(cos), cos.ctypes.data_as(ctypes.POINTER(ctypes.c_longdouble))
-        P.poly_scale = inputs["poly_scale"]
-        P.ntrace, P.trace_gal = len(inputs["trace"]), u64arr(inputs["trace"] if len(inputs["trace"]) else [0])
-        for k, lt in enumerate(inputs["lts"]):
-            P.lt_level[k], P.lt_n1[k], P.lt_ndiag[k] = lt["level"], lt["N1"], len(lt["idx"])
-            ia = _ip(lt["idx"])
-            pa = (_u64p * len(lt["pts"]))(*[u64arr(x) for x in lt["pts"]])
-            keep += [ia, pa]
-            P.lt_idx[k], P.lt_pts[k] = ia, pa
-        P.mono_i = u64arr(inputs["mono_i"]) if inputs.get("mono_i") is not None else None
-        gels = list(inputs["gks"].keys())
-        P.ngk, P.galEls = len(gels), u64arr(gels)
-        ka = (_u64p * len(gels))(*[u64arr(inputs["gks"][g]) for g in gels])
+        gels = list(keys["gks"].keys())
+        P.ngk, P.galEls = len(gels), u64arr(gels if gels else [0])
+        ka = (_u64p * max(1, len(gels)))(*[u64arr(keys["gks"][g]) for g in gels])
         keep.append(ka)
-        P.gks, P.rlk = ka, u64arr(inputs["rlk"])
+        P.gks, P.rlk = ka, u64arr(keys["rlk"])
+        P.d2s, P.s2d = u64arr(keys["d2s"]), u64arr(keys["s2d"])
         ct = np.ascontiguousarray(ct, dtype=np.uint64)
         out = np.zeros((2, self.L, self.N), dtype=np.uint64)
-        rc = lib().oracle_bootstrap(self._h, boot._h, ctypes.byref(P), level, _p(ct), _p(out))
+        rc = lib().oracle_bootstrap(self._h, boot._h, circuit._h, ctypes.byref(P), level, _p(ct), _p(out))
         if rc != 0:
-            raise ValueError("oracle_bootstrap: missing input or level mismatch")
+            raise ValueError("oracle_bootstrap: missing key or level mismatch")
         return out
 
     def eval_poly_ld(self, ct, level, scale, coeffs, cheb, target, rlk):
@@ -392,3 +387,65 @@ def enc_sample(N, seed, enc, image, comp):
     lib().oracle_enc_sample(N, _u32(enc_key(seed)), enc, image, comp,
                             out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
     return out
+
+
+def btp_chain(logN, scheme_moduli, Lres, logP):
+    """The bootstrapping chain (Q primes, P primes) derived by the oracle from
+    the scheme's moduli and the bootstrapper's logPs (oracle_btp_chain)."""
+    sm = np.array(scheme_moduli, dtype=np.uint64)
+    out = np.zeros(128, dtype=np.uint64)
+    n = lib().oracle_btp_chain(logN, _p(sm), len(sm), Lres, _ip(list(logP)), len(logP), _p(out))
+    if n < 0:
+        raise ValueError("prime stream exhausted")
+    m = [int(x) for x in out[:n]]
+    return m[:n - len(logP)], m[n - len(logP):]
+
+
+def btp_cos(K, degree, r):
+    """EvalMod's Chebyshev coefficients (oracle_btp_cos), as numpy longdouble."""
+    out = np.zeros(degree + 1, dtype=np.longdouble)
+    lib().oracle_btp_cos(K, degree, r, out.ctypes.data_as(ctypes.POINTER(ctypes.c_longdouble)))
+    return out
+
+
+class BtpCircuit:
+    """The oracle's own bootstrapping circuit for `slots` slots under the
+    bootstrapping chain `boot` (an Oracle), scheme default scale 2^log_scale:
+    constants, diagonals and trace elements derived from the parameters."""
+
+    def __init__(self, boot, log_scale, slots):
+        self.boot = boot  # keeps the chain's context alive
+        self._h = lib().oracle_btp_new(boot._h, log_scale, slots)
+        if not self._h:
+            raise ValueError("oracle_btp_new: unsupported slot count or chain")
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.oracle_btp_free(self._h)
+            self._h = None
+
+    def params(self):
+        """dict: F, gap, K, r, degree, slots, s_y, top, ntrace, nlt, ncos, t0 (longdouble)."""
+        out = np.zeros(16, dtype=np.longdouble)
+        n = lib().oracle_btp_params(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_longdouble)))
+        names = ["F", "gap", "K", "r", "degree", "slots", "s_y", "top", "ntrace", "nlt", "ncos", "t0"]
+        return dict(zip(names, out[:n]))
+
+    def cos(self):
+        n = int(self.params()["ncos"])
+        p = lib().oracle_btp_cos_of(self._h)
+        return np.array([p[i] for i in range(n)], dtype=np.longdouble)
+
+    def lt(self, k):
+        """(level, N1, diagonal indices, diagonals [level+1+K][N]) of transform k."""
+        lv, n1 = ctypes.c_int(0), ctypes.c_int(0)
+        nd = lib().oracle_btp_lt_info(self._h, k, ctypes.byref(lv), ctypes.byref(n1), None)
+        idx = (ctypes.c_int * max(1, nd))()
+        lib().oracle_btp_lt_info(self._h, k, ctypes.byref(lv), ctypes.byref(n1), idx)
+        nl = lv.value + 1 + self.boot.K
+        diags = []
+        for j in range(nd):
+            p = lib().oracle_btp_lt_diag(self._h, k, j)
+            diags.append(np.ctypeslib.as_array(p, shape=(nl * self.boot.N,)).reshape(nl, self.boot.N).copy())
+        return lv.value, n1.value, [idx[i] for i in range(nd)], diags
+

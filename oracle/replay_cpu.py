@@ -47,7 +47,7 @@ class CpuStream:
         self.pts = {}
         self.lts = {}
         self.polys = {}  # handle -> (coefficients, chebyshev)
-        self.bootstrappers = {}  # slots -> (bootstrapping-chain Oracle, shared circuit inputs)
+        self.bootstrappers = {}  # slots -> (bootstrapping-chain Oracle, oracle.BtpCircuit, keys)
 
     # ---- keys ----
     def keygen(self):
@@ -289,8 +289,8 @@ class CpuStream:
                 cts[ret] = (y, lv, sc)
             elif op == "Bootstrap":
                 x, l, s = cts[a[0]]
-                boot, inputs = self.bootstrappers[a[1]]
-                y = o.bootstrap(boot, inputs, np.ascontiguousarray(x[:, :l + 1]), l)
+                boot, circ, keys = self.bootstrappers[a[1]]
+                y = o.bootstrap(boot, circ, keys, np.ascontiguousarray(x[:, :l + 1]), l)
                 cts[ret] = (y, self.L - 1, s)
             else:
                 raise RuntimeError(f"cpu replay: unsupported op {op}")

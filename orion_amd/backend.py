@@ -192,13 +192,32 @@ LATTIGO_SYMBOLS = [n for n in SIGNATURES if not n.startswith("OrionHip") and n n
     "KeyBundleBytes", "ExportKeyBundle", "ImportKeyBundle", "ModDropCiphertext", "GetPolyDepth")]
 
 
+def _hip_runtimes():
+    """Paths of the HIP runtime libraries mapped into this process."""
+    with open("/proc/self/maps") as f:
+        return sorted({ln.split()[-1] for ln in f if "libamdhip64" in ln})
+
+
 def load_library(path=LIB_PATH):
-    """Load liborion_hip.so and declare every symbol; raises if missing."""
+    """Load liborion_hip.so and declare every symbol; raises if missing.
+
+    torch is imported first, so that the process holds ONE HIP runtime: the
+    torch wheel bundles its own libamdhip64 / libhsa-runtime64 and links them
+    by the unversioned name (NEEDED libamdhip64.so), which does not match the
+    versioned soname this library links (libamdhip64.so.7 from /opt/rocm).
+    Loaded after this library, torch would map a second HIP and HSA runtime
+    beside ours; under rocprofv3's HIP API interception a torch kernel launch
+    was then routed into the other runtime and crashed (the r03p
+    SIGSEGV).  Loaded after torch, this library binds to torch's runtime."""
     if not os.path.exists(path):
         raise RuntimeError(
             f"HIP backend library not found at {path}: build it with "
             "`python orion_amd/build.py` (no CPU fallback exists)")
+    import torch  # noqa: F401  (one HIP runtime per process; see above)
     lib = ctypes.CDLL(path)
+    rt = _hip_runtimes()
+    if len(rt) > 1:
+        raise RuntimeError(f"two HIP runtimes are mapped ({rt}): load torch before liborion_hip.so")
     for name, (args, res) in SIGNATURES.items():
         f = getattr(lib, name)
         f.argtypes = args
@@ -349,10 +368,13 @@ class HipLibrary:
         m = [int(self.OrionHipBootstrapModulus(slots, i)) for i in range(nq + npr)]
         return m[:nq], m[nq:]
 
-    BTX = dict(params=0, cos=1, trace=2, rlk=3, galois_keys=4, galois=5, lt_info=6, lt_diag=7, mono_i=8)
+    BTX = dict(params=0, cos=1, trace=2, rlk=3, galois_keys=4, galois=5, lt_info=6, lt_diag=7, mono_i=8,
+               d2s=9, s2d=10)
 
     def bootstrap_export(self, slots, what, arg=0):
-        """A bootstrapper's shared inputs for the CPU oracle (OrionHipBootstrapExport)."""
+        """A bootstrapper's keys (the CPU oracle's only shared inputs) and, for
+        comparison with the oracle's own derivation, its constants and diagonals
+        (OrionHipBootstrapExport)."""
         w = self.BTX[what]
         n = self._chk(self.lib.OrionHipBootstrapExport(slots, w, arg, None, 0), "OrionHipBootstrapExport")
         dt = {0: np.longdouble, 1: np.longdouble, 6: np.int64}.get(w, np.uint64)

@@ -1,4 +1,5 @@
 """Build liborion_hip.so in-tree for gfx950 (hipcc, no JIT cache)."""
+import fcntl
 import hashlib
 import json
 import os
@@ -32,15 +33,25 @@ def _stamp(build_dir, recipe):
     digest = hashlib.sha256(json.dumps(recipe, sort_keys=True).encode()).hexdigest()
     old = None
     if os.path.exists(path):
-        with open(path) as f:
-            old = json.load(f).get("digest")
+        try:
+            with open(path) as f:
+                old = json.load(f).get("digest")
+        except ValueError:  # a stamp cut short: rebuild
+            old = None
     return path, digest, old != digest
 
 
 def build(verbose=False, extra_flags=(), lib=LIB, build_dir=BUILD):
-    """Compile liborion_hip.so (extra_flags/lib/build_dir: timing-only variants)."""
+    """Compile liborion_hip.so (extra_flags/lib/build_dir: timing-only variants).
+    Concurrent callers (pytest -n workers) serialise on a lock in build_dir."""
+    os.makedirs(build_dir, exist_ok=True)
+    with open(os.path.join(build_dir, ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        return _build(verbose, extra_flags, lib, build_dir)
+
+
+def _build(verbose, extra_flags, lib, build_dir):
     BUILD_, LIB_ = build_dir, lib
-    os.makedirs(BUILD_, exist_ok=True)
     recipe = {"hipcc": HIPCC, "arch": ARCH, "flags": FLAGS + list(extra_flags), "sources": SOURCES}
     stamp, digest, changed = _stamp(BUILD_, recipe)
     headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
@@ -68,8 +79,9 @@ def build(verbose=False, extra_flags=(), lib=LIB, build_dir=BUILD):
         list(ex.map(run, jobs))
     if jobs or changed or not os.path.exists(LIB_):
         run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_] + objs)
-    with open(stamp, "w") as f:
+    with open(stamp + ".tmp", "w") as f:
         json.dump({"digest": digest, "recipe": recipe}, f, indent=1)
+    os.replace(stamp + ".tmp", stamp)
     return LIB_
 
 

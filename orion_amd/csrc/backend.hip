@@ -99,7 +99,9 @@ class DevicePool {
       }
     }
     if (tracking_) touched_[p] = bytes;
-    if (poison_) {  // debugging: every buffer handed out holds garbage, not stale or zero pages
+    // debugging: every buffer handed out holds garbage, not stale or zero pages
+    // (skipped inside a graph capture: a device sync there would invalidate it)
+    if (poison_ && !tracking_) {
       (void)hipDeviceSynchronize();
       (void)hipMemset(p, 0xA5, bytes);
     }
@@ -806,6 +808,11 @@ struct Context {
     logScale = logScale_;
     h = h_;
     if (L + K > ORION_MAXMOD || L + K > ORION_MAXLIMB) throw std::runtime_error("too many moduli");
+    // the lazy NTT ranges (NTT_INT_CUT keeps forward values in [0, 8q)) and
+    // lt_bsgs's 8-product Barrett (barrett_8q2, bar_k <= 60 for x < 8 q^2)
+    // hold only for moduli below 2^61 (ntt_arith.h)
+    for (u64 q : m)
+      if (q >= (1ull << 61) || q < 3 || !(q & 1)) throw std::runtime_error("moduli must be odd and below 2^61");
     mods = m;
     logQ_bits = logQ;
     logP_bits = logP;
@@ -1110,13 +1117,17 @@ struct Context {
   // keys
   // ---------------------------------------------------------------------------
   void gen_secret() { import_secret(sample_ternary_h(h)); }
-  // the secret with these (ternary) coefficients, expanded over QP
-  void import_secret(const std::vector<int64_t>& s) {
-    sk = alloc(1, L + K, 1);
+  // a secret with these (ternary) coefficients, expanded over QP (NTT domain)
+  Poly secret_poly(const std::vector<int64_t>& s) {
+    Poly p = alloc(1, L + K, 1);
     std::vector<u64> host((size_t)(L + K) * N);
     small_residues(s, iota(0, L + K), host.data());
-    upload(sk, host);
-    ntt(ls(sk, 0, 1, iota(0, L + K), iota(0, L + K)), false);
+    upload(p, host);
+    ntt(ls(p, 0, 1, iota(0, L + K), iota(0, L + K)), false);
+    return p;
+  }
+  void import_secret(const std::vector<int64_t>& s) {
+    sk = secret_poly(s);
     have_sk = true;
   }
   LimbSet full(const Poly& P, int c0, int nc) const { return ls(P, c0, nc, iota(0, L + K), iota(0, L + K)); }
@@ -1200,7 +1211,11 @@ struct Context {
       throw std::runtime_error(have == gks.end() ? "secret key not generated"
                                                  : "galois key " + std::to_string(g) + " covers level " +
                                                        std::to_string(have->second.level) + " < " +
-                                                       std::to_string(level) + " and there is no secret key");
+                                                       std::to_string(level) +
+                                                       " and there is no secret key (LoadRotationKey keeps a key "
+                                                       "over the highest level of the linear transforms that exist "
+                                                       "when it is loaded: load keys after creating the transforms "
+                                                       "and before any higher-level rotation)");
     const u64 M = nthroot;
     u64 ginv = hm_powmod(g, M / 2 - 1, M);  // g^-1 mod NthRoot (the group order divides M/2)
     if ((g * ginv) % M != 1) {
@@ -1283,7 +1298,8 @@ struct Context {
       // and the NTT is VALU-bound, so that was measured slower)
       {
         Scope sc(this, P_BEXT, 8.0 * N * B * nc * (in.nlimb + out.nlimb));
-        orion_launch_basis_ext(out, in, T, d_tb, N, stream);
+        if (orion_launch_basis_ext(out, in, T, d_tb, N, stream))
+          throw std::runtime_error("basis_ext: unsupported source count");
       }
       ntt(out, false);
     }
@@ -1340,7 +1356,8 @@ struct Context {
     LimbSet le = lsq(ext, 0, nc, level);
     {
       Scope sc(this, P_BEXT, 8.0 * N * B * nc * (K + level + 1));
-      orion_launch_basis_ext(le, xp, moddown_tab(level), d_tb, N, stream);
+      if (orion_launch_basis_ext(le, xp, moddown_tab(level), d_tb, N, stream))
+        throw std::runtime_error("basis_ext: unsupported source count");
     }
     NttIO io = nio(out, le);  // NTT of the extension and (x_Q - .) * P^-1, fused
     io.epi = NTT_EPI_SUBSCALE;
@@ -1428,7 +1445,10 @@ struct Context {
     Poly d = alloc(3, level + 1, B);
     {
       LimbSet ld = lsq(d, 0, 3, level);
-      Scope sc(this, P_TENSOR, 8.0 * N * (level + 1) * B * 7);
+      // distinct bytes: both operands' 2 components and the 3 outputs; a
+      // square (Quad's x * x, activation.py:55) reads one ciphertext
+      const bool square = a.poly.ptr() == b.poly.ptr();
+      Scope sc(this, P_TENSOR, 8.0 * N * (level + 1) * B * (square ? 5 : 7));
       orion_launch_tensor(ld, lsq(a.poly, 0, 2, level, B), lsq(b.poly, 0, 2, level, B), d_tb, N, stream);
     }
     Ciphertext out = new_ct(level, B, a.scale * b.scale);
@@ -1994,31 +2014,50 @@ struct Context {
   // ---------------------------------------------------------------------------
   // bootstrapping (bootstrapper.go:15-87).  As in Lattigo, a
   // bootstrapper is made per slot count (NewBootstrapper(logPs, slots)), and
-  // its circuit runs under bootstrapping parameters of its own: the residual Q
-  // chain extended by the 15 levels the circuit consumes, with key-switching P
-  // primes of the bit sizes logPs (bootstrapping.ParametersLiteral{LogP}).
-  // Those parameters live in a second Context -- the bootstrapping context,
-  // one per distinct logPs, shared by the slot counts -- that holds the same
-  // secret and its own relinearisation and Galois keys.  The scheme's context,
-  // its chain and its keys are not touched.  The circuit, for n slots
-  // (gap = N / 2n):
-  //   ModRaise (level 0 -> top of the bootstrapping chain, t = m + q0 I)
+  // its circuit runs under bootstrapping parameters of its own.  Orion sets
+  // only LogN, LogP, Xs and LogSlots (bootstrapper.go:33-38); every other
+  // field is Lattigo v6's default bootstrapping.ParametersLiteral [U]
+  // (DESIGN.md §6 lists each default beside what is done here):
+  //   CoeffsToSlots 4 levels of 56-bit primes, SlotsToCoeffs 3 levels of
+  //   39-bit primes, EvalMod 60-bit primes, K = 16, Mod1 degree 30, 3 double
+  //   angles, no arcsine (Mod1InvDegree 0), LogMessageRatio 8, an ephemeral
+  //   secret of Hamming weight 32.
+  // The chain is the residual Q chain + 3 x 39 + (bitlen(30) + 3) x 60 + 4 x
+  // 56 bits, with key-switching P primes of the bit sizes logPs.  Those
+  // parameters live in a second Context -- the bootstrapping context, one per
+  // distinct logPs, shared by the slot counts -- that holds the same secret
+  // and its own relinearisation and Galois keys; the scheme's context, chain
+  // and keys are not touched.  The circuit, for n slots (gap = N / 2n), with
+  // every constant derived from the parameters (oracle_bootstrap derives
+  // them again, independently):
+  //   ScaleDown: the level-0 residues times F = round(q0 / (2^8 Delta)), so
+  //      the message sits 2^LogMessageRatio below q0
+  //   -> EvkDenseToSparse at level 0 (key switch s -> s_eph, h(s_eph) = 32)
+  //   -> ModRaise (level 0 -> top of the bootstrapping chain, t = m + q0 I
+  //      with |I| small because s_eph is sparse)
+  //   -> EvkSparseToDense at the top level (s_eph -> s)
   //   -> Trace, n < N/2 only: multiply by gap^-1 mod Q, then add the
-  //      log2(gap) rotations by n 2^i (ModUp's SubSum): the exact projection
-  //      on Z[X^gap], whose slots are the n-periodic average of the input's
+  //      log2(gap) rotations by n 2^i (SubSum): the exact projection on
+  //      Z[X^gap], whose slots are the n-periodic average of the input's
   //   -> CoeffsToSlots: the n-point special inverse FFT's butterfly stages
-  //      merged into 3 BSGS transforms with complex diagonals (n-periodic);
-  //      the final bit reversal is skipped because EvalMod is slot-wise and
-  //      SlotsToCoeffs starts with the matching one.  For n < N/2 the last
-  //      transform also packs: real parts into slots [0, n) and imaginary
-  //      parts into [n, 2n) of every 2n-period, so that one EvalMod serves both
-  //   -> EvalMod: Chebyshev approximation of cos(2 pi (x - 1/4) / 2^r) on
-  //      [-(K+1), K+1], then r double angles, giving sin(2 pi x) =
-  //      2 pi m / q0 + O(m^3); once (n < N/2) or on the real and the
-  //      imaginary part (n = N/2, recombined with x i = X^(N/2))
-  //   -> SlotsToCoeffs: the forward stages, 3 transforms (for n < N/2 the
-  //      first one also unpacks real + i imag) -> the residual top level,
-  //      copied back into the scheme's context at the input's scale.
+  //      merged into 4 BSGS transforms with complex diagonals (n-periodic; the
+  //      extra stages go to the first transforms); the final bit reversal is
+  //      skipped because EvalMod is slot-wise and SlotsToCoeffs starts with
+  //      the matching one.  The 1/n and EvalMod's 1/(2K) are spread over the
+  //      transforms.  For n < N/2 the last transform also packs: real parts
+  //      into slots [0, n) and imaginary parts into [n, 2n) of every
+  //      2n-period, so that one EvalMod serves both
+  //   -> EvalMod: the degree-30 Chebyshev interpolant of
+  //      a cos(2 pi (K u - 1/4) / 2^r) on [-1, 1], a = (2 pi)^(-1/2^r), at a
+  //      target scale chosen so that after the r double angles
+  //      y <- 2 y^2 - a^(2^(i+1)) (constant added before the rescale, as
+  //      Lattigo's mod1 evaluator does) the scale is 2^60; the result is
+  //      sin(2 pi x) / (2 pi) = F m / q0 + O(m^3); once (n < N/2) or on the
+  //      real and the imaginary part (n = N/2, recombined with x i = X^(N/2))
+  //   -> SlotsToCoeffs: the forward stages, 3 transforms carrying
+  //      q0 / (F s_y) (for n < N/2 the first one also unpacks real + i imag)
+  //      -> the residual top level, copied back into the scheme's context at
+  //      the input's scale.
   // Bootstrap then applies Orion's post-scale 2^(LogMaxSlots - LogSlots)
   // (bootstrapper.go:73-74): an input whose slots >= n are zero comes back with
   // its n slots replicated over all N/2 (Lattigo's sparse packing).
@@ -2048,14 +2087,15 @@ struct Context {
     ntt(out, false);
     return pt;
   }
-  // BSGS transform y = sum_d diag_d * rot(x, d) with complex diagonals encoded at scale q_level
+  // BSGS transform y = sum_d diag_d * rot(x, d) with complex diagonals encoded
+  // at scale q_level; the bootstrapping DFT matrices' LogBSGSRatio is 1 [U]
   LinTrans make_lt_complex(const DiagMap& dm, int level) {
     const int slots = N / 2;
     LinTrans T;
     T.level = level;
     T.ratio = 2;
     for (auto& kv : dm) T.idx.push_back(kv.first);
-    T.N1 = find_best_n1(T.idx, slots, 0);
+    T.N1 = find_best_n1(T.idx, slots, 1);
     std::set<int> seenb;
     for (int d : T.idx) {
       int gi, bi;
@@ -2122,39 +2162,66 @@ struct Context {
     return C;
   }
   struct Bootstrapper {
-    static constexpr int kDegree = 63, kR = 3, kDepthPoly = 6;  // EvalMod: cos degree, double angles, depth(63)
+    // Lattigo v6 bootstrapping.ParametersLiteral defaults [U]:
+    // CoeffsToSlots / SlotsToCoeffs factorisation depths and prime sizes,
+    // EvalMod prime size, Mod1 degree, double angles, K, LogMessageRatio and
+    // the ephemeral secret's Hamming weight
+    static constexpr int kCtS = 4, kCtSBits = 56, kStC = 3, kStCBits = 39, kModBits = 60;
+    static constexpr int kDegree = 30, kR = 3, kK = 16, kLogMsgRatio = 8, kEphH = 32;
+    static constexpr int kDepthPoly = 5;  // bits.Len64(kDegree)
+    static constexpr int kLogBSGSRatio = 1;  // dft.MatrixLiteral LogBSGSRatio
+    static_assert(kCtS == 4 && kStC == 3, "the constant spreading below takes 4th and cube roots");
     Context* bc = nullptr;  // the bootstrapping context (owned by the scheme's btp_ctx)
-    int slots = 0, gap = 1, K = 0, r = kR, degree = kDegree;
+    int slots = 0, gap = 1, K = kK, r = kR, degree = kDegree;
     PolyFn cosp;
+    long double t0 = 0;              // EvalMod polynomial target scale
+    std::vector<long double> dac;    // double-angle constants a^(2^(i+1)), i < r
     std::vector<LinTrans> cts, stc;  // in application order
     std::vector<u64> trace_gal;      // Galois elements of the trace (rotations by slots * 2^i)
     int top = 0;
     Poly mono_i;          // n = N/2: NTT of X^(N/2) (x i on every slot), all Q limbs
-    long double s_y = 0;  // scale of the EvalMod output
-    u64 F = 1;            // message pre-scaling before ModRaise: F m <= q0 / 2^9 at the default scale
+    long double s_y = 0;  // scale of the EvalMod output (2^60 up to rounding)
+    u64 F = 1;            // ScaleDown: message times F = round(q0 / (2^8 Delta)) before ModRaise
+    EvKey d2s, s2d;       // EvkDenseToSparse (level 0), EvkSparseToDense (full chain)
   };
   // declared in this order so that the circuits (whose buffers belong to a
   // bootstrapping context's pool) are destroyed before the contexts
   std::map<std::vector<int>, std::unique_ptr<Context>> btp_ctx;  // logPs -> bootstrapping context
   std::map<int, std::unique_ptr<Bootstrapper>> btps;             // slot count -> circuit
 
+  // the butterfly stages of the n-point special FFT (lengths in application
+  // order) split over ng transforms, the extra stages to the first ones
+  static std::vector<std::vector<int>> fft_groups(int ns, bool inverse, int ng) {
+    std::vector<int> lens;
+    for (int len = inverse ? ns : 2; inverse ? len >= 2 : len <= ns; len = inverse ? len / 2 : len * 2)
+      lens.push_back(len);
+    std::vector<std::vector<int>> g(ng);
+    const int tot = (int)lens.size();
+    int at = 0;
+    for (int k = 0; k < ng; ++k)
+      for (int i = 0; i < tot / ng + (k < tot % ng ? 1 : 0); ++i) g[k].push_back(lens[at++]);
+    return g;
+  }
+
   // (on the bootstrapping context) the circuit for `ns` slots
   std::unique_ptr<Bootstrapper> make_circuit(int ns) {
+    typedef Bootstrapper BT;
     const int n = N / 2;
     auto B = std::unique_ptr<Bootstrapper>(new Bootstrapper());
     B->bc = this;
     B->slots = ns;
     B->gap = n / ns;
-    // EvalMod range from the secret's Hamming weight: I ~ N(0, (h+1)/12) per coefficient
-    B->K = (int)ceil(6.0 * sqrt((h + 1) / 12.0)) + 2;
-    // Chebyshev interpolation of cos(2 pi ((K+1) u - 1/4) / 2^r) at degree+1 nodes on [-1, 1]
+    const long double PI = 3.14159265358979323846264338327950288L;
+    // EvalMod: the Chebyshev interpolant of a cos(2 pi (K u - 1/4) / 2^r) at
+    // the degree+1 Chebyshev nodes of [-1, 1], a = (2 pi)^(-1/2^r); after the r
+    // double angles y <- 2 y^2 - a^(2^(i+1)) it is sin(2 pi x) / (2 pi)
+    const long double a = powl(2 * PI, -1.0L / (long double)(1 << B->r));
     {
       const int d = B->degree, m = d + 1;
-      const long double PI = 3.14159265358979323846264338327950288L;
       std::vector<long double> fx(m), c(m, 0);
       for (int k = 0; k < m; ++k) {
         const long double u = cosl(PI * (k + 0.5L) / m);
-        fx[k] = cosl(2 * PI * ((B->K + 1) * u - 0.25L) / (long double)(1 << B->r));
+        fx[k] = a * cosl(2 * PI * (B->K * u - 0.25L) / (long double)(1 << B->r));
       }
       for (int j = 0; j < m; ++j) {
         long double acc = 0;
@@ -2164,10 +2231,14 @@ struct Context {
       B->cosp.cheb = true;
       B->cosp.c = c;
     }
+    {
+      long double v = a;
+      for (int i = 0; i < B->r; ++i) B->dac.push_back(v = v * v);
+    }
     B->top = L - 1;
-    {  // EvalMod sees x = F m / q0 + I: raise the message to <= 2^-9 of q0 (sin 2 pi x ~ 2 pi x to 3e-5)
-      const int lg = (63 - __builtin_clzll(mods[0])) - logScale - 9;
-      B->F = lg > 0 ? (1ull << lg) : 1;
+    {  // ScaleDown (LogMessageRatio): round(q0 / (2^8 Delta)), Delta the default scale
+      const long double f = roundl((long double)mods[0] / ldexpl(1.0L, BT::kLogMsgRatio + logScale));
+      B->F = f < 1 ? 1 : (u64)f;
     }
     for (int s = ns; s < n; s *= 2) B->trace_gal.push_back(galois_element(s));
     int logns = 0;
@@ -2175,31 +2246,20 @@ struct Context {
     // the n-point special FFT (slots of Z[Y]/(Y^2n + 1), Y = X^gap); its
     // diagonals act n-periodically on the N/2 slots
     const std::vector<Cplx> twi = special_fft_twiddles(logns + 1, true), twf = special_fft_twiddles(logns + 1, false);
-    auto groups = [&](bool inverse) {  // 3 groups of stages, split as evenly as possible
-      std::vector<std::vector<int>> g(3);
-      std::vector<int> lens;
-      for (int len = inverse ? ns : 2; inverse ? len >= 2 : len <= ns; len = inverse ? len / 2 : len * 2) lens.push_back(len);
-      int at = 0;
-      for (int k = 0; k < 3; ++k) {
-        const int cnt = (int)(lens.size() - at) / (3 - k);
-        for (int i = 0; i < cnt; ++i) g[k].push_back(lens[at++]);
-      }
-      return g;
-    };
     const bool packed = ns < n;
-    // CoeffsToSlots: slots of t / q0 -> bitrev((t_j + i t_{j+n}) / q0) / (2 (K+1)).  The 1/n of
-    // the inverse transform and EvalMod's 1 / (2 (K+1)) are spread over the groups (2^-r per
-    // group of r stages, the cube root of 1 / (2 (K+1)) each), so no diagonal is small against
+    // CoeffsToSlots: slots of t / q0 -> bitrev((t_j + i t_{j+n}) / q0) / (2K).  The 1/n of the
+    // inverse transform and EvalMod's 1 / (2K) are spread over the transforms (2^-s per
+    // transform of s stages, the 4th root of 1 / (2K) each), so no diagonal is small against
     // the fixed-point grid of its encoding
     {
-      auto g = groups(true);
+      const auto g = fft_groups(ns, true, BT::kCtS);
       int level = B->top;
-      const double kf = cbrt(1.0 / (2.0 * (B->K + 1)));
-      for (int k = 0; k < 3; ++k) {
+      const double kf = sqrt(sqrt(1.0 / (2.0 * B->K)));
+      for (int k = 0; k < BT::kCtS; ++k) {
         DiagMap M;
         M[0] = std::vector<cplx>(n, cplx(ldexp(kf, -(int)g[k].size()), 0));
         for (int len : g[k]) M = diag_compose(fft_stage(len, true, twi), M);
-        if (packed && k == 2) {
+        if (packed && k == BT::kCtS - 1) {
           // w -> a w, a = 1 on [0, n) and -i on [n, 2n) of every 2n-period: then
           // a w + conj(a w) = 2 Re w on the first half, 2 Im w on the second
           DiagMap A;
@@ -2210,21 +2270,24 @@ struct Context {
         B->cts.push_back(make_lt_complex(M, level--));
       }
     }
-    // scale of the EvalMod output (simulated: CtS keeps scale q0, poly lands on 2^60 exactly)
+    // EvalMod scales: the polynomial's target t0 is chosen so that the r
+    // double angles (rescaled by the primes below its output level) end on
+    // 2^60; s_y is the scale they actually reach (the same long double steps
+    // as mul_relin and rescale_inplace)
     {
-      const int lvl_poly = B->top - 3 - Bootstrapper::kDepthPoly;
-      long double sc = ldexpl(1.0L, 60);
-      int lv = lvl_poly;
-      for (int k = 0; k < B->r; ++k) sc = sc * sc / (long double)mods[lv--];
+      const int lp = B->top - BT::kCtS - BT::kDepthPoly;  // level of the polynomial's output
+      long double T = ldexpl(1.0L, BT::kModBits);
+      for (int i = B->r - 1; i >= 0; --i) T = sqrtl(T * (long double)mods[lp - i]);
+      B->t0 = T;
+      long double sc = T;
+      for (int i = 0; i < B->r; ++i) sc = sc * sc / (long double)mods[lp - i];
       B->s_y = sc;
-      // SlotsToCoeffs: forward stages times c = q0 / (2 pi F s_y), so the output decodes at
-      // the input scale
-      auto g = groups(false);
-      int level = lv;
-      const long double PI = 3.14159265358979323846264338327950288L;
-      const double cst = (double)((long double)mods[0] / (2 * PI * (long double)B->F * sc));
-      const double cf = cbrt(cst);  // spread like CoeffsToSlots' constant
-      for (int k = 0; k < 3; ++k) {
+      // SlotsToCoeffs: forward stages times c = q0 / (F s_y), so the output decodes at the
+      // input scale
+      const auto g = fft_groups(ns, false, BT::kStC);
+      int level = lp - B->r;
+      const double cf = cbrt((double)((long double)mods[0] / ((long double)B->F * sc)));
+      for (int k = 0; k < BT::kStC; ++k) {
         DiagMap M;
         if (packed && k == 0) {
           // unpack: y_p + i y_{p+n} on the first half of a 2n-period, i y_p + y_{p-n}
@@ -2250,6 +2313,11 @@ struct Context {
       upload(B->mono_i, host);
       ntt(lsq(B->mono_i, 0, 1, L - 1), false);
     }
+    {  // the ephemeral secret and its keys (genEncapsulationEvaluationKeysNew)
+      const Poly se = secret_poly(sample_ternary_h(BT::kEphH));
+      B->d2s = EvKey{gen_evk(sk, se, 0), 0};
+      B->s2d = EvKey{gen_evk(se, sk, L - 1), L - 1};
+    }
     return B;
   }
 
@@ -2267,27 +2335,39 @@ struct Context {
     y.scale = x.scale;  // diagonals at scale q_level
     return y;
   }
+  // mod1 evaluator: the cosine polynomial, then the double angles
+  // y <- 2 y^2 - a^(2^(k+1)), the constant added at the product's scale
+  // before its rescale
   Ciphertext eval_mod(const Bootstrapper& bt, const Ciphertext& u) {
-    Ciphertext y = eval_poly(u, bt.cosp, ldexpl(1.0L, 60));
-    for (int k = 0; k < bt.r; ++k) {  // cos(2a) = 2 cos(a)^2 - 1
+    Ciphertext y = eval_poly(u, bt.cosp, bt.t0);
+    for (int k = 0; k < bt.r; ++k) {
       Ciphertext t = mul_relin(y, y);
-      rescale_inplace(t);
       const LimbSet lt = lsq(t.poly, 0, 2, t.level);
       ew(EW_ADD, lt, lt, lt);
-      std::vector<u64> one = big_const_residues(-t.scale, t.level);
-      ew1(EW_ADDC, lsq(t.poly, 0, 1, t.level), lsq(t.poly, 0, 1, t.level), &one);
+      std::vector<u64> c = big_const_residues(-bt.dac[k] * t.scale, t.level);
+      ew1(EW_ADDC, lsq(t.poly, 0, 1, t.level), lsq(t.poly, 0, 1, t.level), &c);
+      rescale_inplace(t);
       y = std::move(t);
     }
     return y;
   }
-  // (on the bootstrapping context) c0: the level-0 residues mod q0 of a batch
-  // of B ciphertexts, coefficient domain, already pre-scaled by F
-  Ciphertext run_circuit(Bootstrapper& bt, const Poly& c0, int B) {
-    // ModRaise: level-0 residues (coefficient domain) lifted to every Q limb
-    Ciphertext t = new_ct(L - 1, B, (long double)mods[0]);
+  // (on the bootstrapping context) x: the level-0 residues (NTT domain) of a
+  // batch of B ciphertexts, already scaled down by F
+  Ciphertext run_circuit(Bootstrapper& bt, const Poly& x, int B) {
+    // EvkDenseToSparse at level 0: (x0, 0) + KS(x1), now under the ephemeral secret
+    Poly e = alloc(2, 1, B);
+    keyswitch(lsq(x, 1, 1, 0), 0, B, bt.d2s.k, bt.d2s.level, e, x.ptr());
+    // ModRaise: the centred level-0 residues (coefficient domain) lifted to every Q limb
+    Poly c0 = alloc(2, 1, B);
+    ntt_io(nio(lsq(c0, 0, 2, 0), lsq(e, 0, 2, 0)), true);
+    Ciphertext m = new_ct(L - 1, B, (long double)mods[0]);
+    const LimbSet ml = lsq(m.poly, 0, 2, L - 1);
+    if (orion_launch_modraise(ml, lsq(c0, 0, 2, 0), d_tb, N, stream)) throw std::runtime_error("modraise failed");
+    ntt(ml, false);
+    // EvkSparseToDense at the top level: (m0, 0) + KS(m1), back under the secret
+    Ciphertext t = new_ct(L - 1, B, m.scale);
+    keyswitch(lsq(m.poly, 1, 1, L - 1), L - 1, B, bt.s2d.k, bt.s2d.level, t.poly, m.poly.ptr());
     const LimbSet tl = lsq(t.poly, 0, 2, L - 1);
-    if (orion_launch_modraise(tl, lsq(c0, 0, 2, 0), d_tb, N, stream)) throw std::runtime_error("modraise failed");
-    ntt(tl, false);
     if (bt.gap > 1) {  // Trace: (gap^-1 t) summed over the rotations by slots * 2^i
       std::vector<u64> gi(L);
       for (int l = 0; l < L; ++l) gi[l] = hm_invmod((u64)bt.gap % mods[l], mods[l]);
@@ -2298,9 +2378,8 @@ struct Context {
       }
     }
     // CoeffsToSlots
-    Ciphertext z = lt_rescale(bt.cts[0], t);
-    z = lt_rescale(bt.cts[1], z);
-    z = lt_rescale(bt.cts[2], z);
+    Ciphertext z = std::move(t);
+    for (LinTrans& T : bt.cts) z = lt_rescale(T, z);
     Ciphertext zc = apply_galois(z, 2 * (u64)N - 1);
     Ciphertext y;
     if (bt.gap > 1) {
@@ -2319,15 +2398,14 @@ struct Context {
       ew(EW_ADD, lsq(y.poly, 0, 2, y.level), lsq(y.poly, 0, 2, y.level), lsq(yr.poly, 0, 2, y.level));
     }
     // SlotsToCoeffs
-    Ciphertext o = lt_rescale(bt.stc[0], y);
-    o = lt_rescale(bt.stc[1], o);
-    o = lt_rescale(bt.stc[2], o);
-    return o;
+    for (LinTrans& T : bt.stc) y = lt_rescale(T, y);
+    return y;
   }
 
   // bootstrapper.go:19-58: one circuit per slot count (made once); logPs
   // empty = the scheme's own P bit sizes
   void new_bootstrapper(std::vector<int> logPs, int ns) {
+    typedef Bootstrapper BT;
     if (ci) throw std::runtime_error("bootstrapping needs the Standard ring (Lattigo has no ConjugateInvariant bootstrapper)");
     if (ns < 2 || ns > N / 2 || (ns & (ns - 1)))
       throw std::runtime_error("slots must be a power of two in [2, " + std::to_string(N / 2) + "]");
@@ -2338,13 +2416,13 @@ struct Context {
       if (b < 20 || b > 61) throw std::runtime_error("bootstrapping P primes must be 20..61 bits");
     auto it = btp_ctx.find(logPs);
     if (it == btp_ctx.end()) {
-      // Lattigo's bootstrapping chain: the residual Q, then SlotsToCoeffs 3 x 40-bit,
-      // EvalMod depth(poly) + r x 60-bit, CoeffsToSlots 3 x 55-bit (bottom to top), so the
-      // refreshed ciphertext comes out at the residual chain's top level; P from logPs.
-      // New primes skip every prime of the scheme.
-      std::vector<int> ext(3, 40);
-      ext.insert(ext.end(), Bootstrapper::kDepthPoly + Bootstrapper::kR, 60);
-      ext.insert(ext.end(), 3, 55);
+      // the bootstrapping chain: the residual Q, then SlotsToCoeffs 3 x 39-bit, EvalMod
+      // depth(poly) + r x 60-bit, CoeffsToSlots 4 x 56-bit (bottom to top), so the refreshed
+      // ciphertext comes out at the residual chain's top level; P from logPs.  New primes skip
+      // every prime of the scheme.
+      std::vector<int> ext(BT::kStC, BT::kStCBits);
+      ext.insert(ext.end(), BT::kDepthPoly + BT::kR, BT::kModBits);
+      ext.insert(ext.end(), BT::kCtS, BT::kCtSBits);
       std::vector<int> bits = ext;
       bits.insert(bits.end(), logPs.begin(), logPs.end());
       const std::vector<u64> fresh = gen_moduli_excluding(logN, bits, mods);
@@ -2372,13 +2450,11 @@ struct Context {
     if (it == btps.end()) throw std::runtime_error("no bootstrapper found for slot count: " + std::to_string(ns));
     Bootstrapper& bt = *it->second;
     const int B = in.poly.B;
-    Poly c0 = alloc(2, 1, B);
-    ntt_io(nio(lsq(c0, 0, 2, 0), lsq(in.poly, 0, 2, 0)), true);
-    if (bt.F > 1) {
-      std::vector<u64> f{bt.F % mods[0]};
-      ew1(EW_SCALE, lsq(c0, 0, 2, 0), lsq(c0, 0, 2, 0), &f);
-    }
-    Ciphertext o = bt.bc->run_circuit(bt, c0, B);
+    // ScaleDown: F times the level-0 residues (an integer: no level)
+    Poly x = alloc(2, 1, B);
+    std::vector<u64> f{bt.F % mods[0]};
+    ew1(EW_SCALE, lsq(x, 0, 2, 0), lsq(in.poly, 0, 2, 0), &f);
+    Ciphertext o = bt.bc->run_circuit(bt, x, B);
     if (o.level != L - 1) throw std::logic_error("bootstrapping circuit did not end at the residual top level");
     Ciphertext out = new_ct(L - 1, B, in.scale);
     // the residual limbs hold the same primes in both contexts
@@ -3495,11 +3571,11 @@ long OrionHipBootstrapExport(int slots, int what, long arg, void* out, unsigned 
     return i < (long)bt.cts.size() ? bt.cts[i] : bt.stc[i - bt.cts.size()];
   };
   switch (what) {
-    case ORION_BTX_PARAMS: {  // long double: F, gap, K, r, degree, slots, s_y, top, L, K_P, ntrace, nlt, degree+1
+    case ORION_BTX_PARAMS: {  // long double: F, gap, K, r, degree, slots, s_y, top, L, K_P, ntrace, nlt, degree+1, t0
       const long double v[] = {(long double)bt.F, (long double)bt.gap, (long double)bt.K, (long double)bt.r,
                                (long double)bt.degree, (long double)bt.slots, bt.s_y, (long double)bt.top,
                                (long double)b.L, (long double)b.K, (long double)bt.trace_gal.size(),
-                               (long double)(bt.cts.size() + bt.stc.size()), (long double)bt.cosp.c.size()};
+                               (long double)(bt.cts.size() + bt.stc.size()), (long double)bt.cosp.c.size(), bt.t0};
       const long cnt = (long)(sizeof(v) / sizeof(v[0]));
       if (out) {
         if (n < (unsigned long)cnt) throw std::runtime_error("export buffer too small");
@@ -3567,6 +3643,12 @@ long OrionHipBootstrapExport(int slots, int what, long arg, void* out, unsigned 
         b.download(p, host);
         memcpy(out, host.data(), (size_t)cnt * 8);
       }
+      return cnt;
+    }
+    case ORION_BTX_D2S:  // the ephemeral-secret keys (full-chain layout; EvkDenseToSparse fills level 0)
+    case ORION_BTX_S2D: {
+      const long cnt = 2L * b.dnum * (b.L + b.K) * b.N;
+      if (out) export_evk_full(b, what == ORION_BTX_D2S ? bt.d2s : bt.s2d, (unsigned long*)out, n);
       return cnt;
     }
     case ORION_BTX_MONO_I: {

@@ -34,17 +34,24 @@ class SchemeCache:
         return self.val
 
 
-def bootstrap_inputs(lib, ns):
-    """The circuit's shared inputs (keys, diagonals, constants) for the oracle."""
-    F, gap, K, r, _deg, _slots, _sy, _top, _lb, _kb, _nt, nlt, _nc = lib.bootstrap_export(ns, "params")
-    inp = dict(F=int(F), gap=int(gap), K=int(K), r=int(r), cos=lib.bootstrap_export(ns, "cos"),
-               poly_scale=2.0 ** 60, trace=lib.bootstrap_export(ns, "trace"), rlk=lib.bootstrap_export(ns, "rlk"))
-    inp["lts"] = []
-    for k in range(int(nlt)):
-        info = lib.bootstrap_export(ns, "lt_info", k)
-        level, n1, nd = (int(v) for v in info[:3])
-        inp["lts"].append(dict(level=level, N1=n1, idx=[int(v) for v in info[3:]],
-                               pts=[lib.bootstrap_export(ns, "lt_diag", (k << 32) | j) for j in range(nd)]))
-    inp["gks"] = {int(g): lib.bootstrap_export(ns, "galois", int(g)) for g in lib.bootstrap_export(ns, "galois_keys")}
-    inp["mono_i"] = lib.bootstrap_export(ns, "mono_i") if int(gap) == 1 else None
-    return inp
+def bootstrap_keys(lib, ns):
+    """The keys of the bootstrapper for `ns` slots (relinearisation, Galois,
+    EvkDenseToSparse, EvkSparseToDense): with the input ciphertext, the only
+    inputs the CPU oracle shares with the library.  Everything else in the
+    circuit -- the prime chain, F, K, the cosine coefficients, the
+    CoeffsToSlots / SlotsToCoeffs diagonals and their encoding, the trace
+    elements -- the oracle derives itself (oracle.BtpCircuit)."""
+    return dict(rlk=lib.bootstrap_export(ns, "rlk"), d2s=lib.bootstrap_export(ns, "d2s"),
+                s2d=lib.bootstrap_export(ns, "s2d"),
+                gks={int(g): lib.bootstrap_export(ns, "galois", int(g)) for g in lib.bootstrap_export(ns, "galois_keys")})
+
+
+def bootstrap_oracle(oracle_mod, lib, logn, log_scale, ns, logp):
+    """(bootstrapping-chain Oracle, BtpCircuit) derived by the oracle from the
+    scheme's moduli and logPs; checks the library's chain is the same."""
+    sm = lib.moduli()
+    bq, bp = oracle_mod.btp_chain(logn, sm, lib.L, logp)
+    lq, lp = lib.bootstrap_moduli(ns)
+    assert (lq, lp) == (bq, bp), "the library's bootstrapping chain differs from the oracle's"
+    boot = oracle_mod.Oracle(logn, bq + bp, len(bq), len(bp))
+    return boot, oracle_mod.BtpCircuit(boot, log_scale, ns)

@@ -3,7 +3,7 @@ the same inputs.  Integer ring arithmetic must match bit for bit."""
 import numpy as np
 import pytest
 
-from tests.helpers import SMALL, rand_ct, SchemeCache, bootstrap_inputs
+from tests.helpers import SMALL, rand_ct, SchemeCache, bootstrap_keys, bootstrap_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -467,15 +467,15 @@ def test_bootstrap_functional(torch_cuda, h):
     """Bootstrap (bootstrapper.go:19-80) of a level-0 batch.  As in Lattigo,
     each slot count gets its own bootstrapper, made once, under bootstrapping
     parameters of its own: the residual Q chain plus the circuit's 15 levels
-    (3 CoeffsToSlots + 6 polynomial + 3 double-angle + 3 SlotsToCoeffs), and
-    P primes of the bit sizes logPs.  The scheme's chain and keys are not
+    (Lattigo's defaults [U]: 4 CoeffsToSlots + 5 polynomial + 3 double-angle
+    + 3 SlotsToCoeffs), and P primes of the bit sizes logPs.  The scheme's chain and keys are not
     touched.  The refreshed ciphertext sits on the residual top level at the
     input scale.  A sparse slot count n runs the n-point circuit (trace, one
     packed EvalMod) and Orion's post-scale 2^(LogMaxSlots - LogSlots)
     (bootstrapper.go:73-74): an input whose slots >= n are zero comes back with
     its n slots replicated over all N/2, as Lattigo's sparse packing leaves it.
-    Parity with Lattigo's bootstrapper is unpinned (different circuit
-    parameters); the bar is the functional one."""
+    Bit parity with Lattigo's own bootstrapper is unpinned (Lattigo is not
+    in this image); the bar here is the functional one."""
     from orion_amd.backend import HipLibrary
     lib = HipLibrary().new_scheme(13, BTP_LOGQ, [60, 60], 40, h=h, seed=5)
     lib.GenerateSecretKey()
@@ -511,7 +511,9 @@ def test_bootstrap_functional(torch_cuda, h):
     assert lib.GetCiphertextScaleF(out) == 2.0 ** 40
     dec = lib.decode_f64(lib.Decrypt(out))
     err = np.abs(dec - vals.astype(np.float64))
-    assert err.max() < 1e-5 and err.mean() < 1e-6, (err.max(), err.mean())  # measured ~6e-8 / 1.4e-8
+    # Lattigo's default message ratio (2^8) and degree-30 cosine: the oracle's own
+    # run of this circuit measures 1.0e-5 / 1.8e-6 (tests/test_oracle.py)
+    assert err.max() < 1e-4 and err.mean() < 1e-5, (err.max(), err.mean())
     # the refreshed ciphertext computes: square and rescale
     sq = lib.MulRelinCiphertextNew(out, out)
     lib.Rescale(sq)
@@ -542,14 +544,20 @@ def test_bootstrap_functional(torch_cuda, h):
 
 @pytest.mark.parametrize("sparse", [False, True])
 def test_bootstrap_parity(torch_cuda, oracle_mod, sparse):
-    """Bootstrap bit for bit against the oracle's restatement of
-    the same circuit (oracle_bootstrap: F pre-scale, centered ModRaise, trace,
-    3 CoeffsToSlots transforms, conjugation, EvalMod = Chebyshev cosine +
-    double angles, 3 SlotsToCoeffs transforms, Orion's post-scale) on shared
-    inputs: the bootstrapping chain's keys, the transforms' diagonals and the
-    cosine coefficients, exported through OrionHipBootstrapExport.  Full slots
-    (real and imaginary EvalMod) and a sparse slot count (trace, one packed
-    EvalMod); a batch of two images."""
+    """Bootstrap bit for bit against the oracle's own
+    restatement of Lattigo v6's default bootstrapping circuit
+    (oracle_bootstrap: ScaleDown by F, EvkDenseToSparse, centred ModRaise,
+    EvkSparseToDense, trace, 4 CoeffsToSlots transforms, conjugation, EvalMod
+    = degree-30 Chebyshev cosine + 3 double angles, 3 SlotsToCoeffs
+    transforms, Orion's post-scale).  The oracle derives the prime chain, F,
+    K, the cosine coefficients, the trace elements and every CoeffsToSlots /
+    SlotsToCoeffs diagonal (special-FFT factorisation, constant spreading,
+    packing, BSGS split, encoding at scale q_level over QP) from the
+    parameters; only the keys and the input ciphertext are shared.  The two
+    derivations are compared item by item first (so a mismatch names its
+    constant), then the outputs bit for bit.  Full slots (real and imaginary
+    EvalMod) and a sparse slot count (trace, one packed EvalMod); a batch of
+    two images."""
     from orion_amd.backend import HipLibrary
     logp = [60, 60]
     lib = HipLibrary().new_scheme(13, BTP_LOGQ, logp, 40, h=192, seed=21)
@@ -566,12 +574,26 @@ def test_bootstrap_parity(torch_cuda, oracle_mod, sparse):
     lib.DeleteCiphertext(lib.Bootstrap(ct, ns))  # every key made at the level it ends at
     out = lib.Bootstrap(ct, ns)
     got, x = lib.export_ciphertext(out), lib.export_ciphertext(ct)
-    inputs = bootstrap_inputs(lib, ns)
+    boot, circ = bootstrap_oracle(oracle_mod, lib, 13, 40, ns, [61, 61])
+    # the library's constants against the oracle's own derivation
+    lp, op = lib.bootstrap_export(ns, "params"), circ.params()
+    for i, name in ((0, "F"), (1, "gap"), (2, "K"), (3, "r"), (4, "degree"), (7, "top")):
+        assert int(lp[i]) == int(op[name]), name
+    assert lp[6] == op["s_y"] and lp[13] == op["t0"]
+    assert np.array_equal(lib.bootstrap_export(ns, "cos"), circ.cos())
+    assert sorted(int(g) for g in lib.bootstrap_export(ns, "trace")) == sorted(
+        boot.galois_element(ns << i) for i in range(int(op["ntrace"])))
+    for k in range(int(op["nlt"])):
+        level, n1, idx, diags = circ.lt(k)
+        info = lib.bootstrap_export(ns, "lt_info", k)
+        assert (int(info[0]), int(info[1]), [int(v) for v in info[3:]]) == (level, n1, idx), k
+        for j in range(len(idx)):
+            assert np.array_equal(lib.bootstrap_export(ns, "lt_diag", (k << 32) | j).reshape(diags[j].shape),
+                                  diags[j]), (k, j)
+    keys = bootstrap_keys(lib, ns)
     orc = oracle_mod.Oracle(13, lib.moduli(), len(BTP_LOGQ), len(logp))
-    bq, bp = lib.bootstrap_moduli(ns)
-    borc = oracle_mod.Oracle(13, bq + bp, len(bq), len(bp))
     for b in range(2):
-        ref = orc.bootstrap(borc, inputs, x[b], 0)
+        ref = orc.bootstrap(boot, circ, keys, x[b], 0)
         assert np.array_equal(got[b], ref), b
     exp = np.tile(vals[:, :ns], (1, n // ns)).astype(np.float64)
     assert np.abs(lib.decode_f64(lib.Decrypt(out)) - exp).max() < 1e-4

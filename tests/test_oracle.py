@@ -414,3 +414,95 @@ def test_cpu_replay_mlp_n13_c1():
     v = s.decrypt(out)[:10]
     exp = s.arrays["expected_output"].reshape(-1)
     assert np.abs(v - exp).mean() < 0.005
+
+
+# ---- bootstrapping: the oracle's own circuit (Lattigo v6 defaults [U]) ----
+
+def test_btp_cos_matches_mpmath(oracle_mod):
+    """EvalMod's cosine polynomial (oracle_btp_cos, 80-bit arithmetic): the
+    Chebyshev interpolant of (2 pi)^(-1/8) cos(2 pi (16 u - 1/4) / 8), degree
+    30, equals the 60-digit mpmath computation (tools/gen_btp_cos.py ->
+    tests/golden/btp_cos.json) to 1e-17 per coefficient (measured 6e-19)."""
+    with open(os.path.join(GOLD, "btp_cos.json")) as f:
+        g = json.load(f)
+    c = oracle_mod.btp_cos(g["K"], g["degree"], g["r"])
+    ref = np.array([np.longdouble(v) for v in g["coeffs"]], dtype=np.longdouble)  # parsed at 80 bits
+    assert np.abs(c - ref).max() < 1e-17
+    assert float(g["max_abs_error_on_grid"]) < 1e-9  # the interpolant's own error on [-1, 1]
+
+
+def test_btp_chain_and_constants(oracle_mod):
+    """The bootstrapping chain and constants the oracle derives from the
+    parameters alone: residual Q kept, 3 x 39 + 8 x 60 + 4 x 56-bit circuit
+    primes (Lattigo's default StC / EvalMod / CtS log-scales [U]) plus P of
+    logP, none reused from the residual parameters; F = round(q0 / 2^(8 +
+    logScale)); the EvalMod scale reaches 2^60 after the double angles; 4 +
+    3 transforms at the right levels."""
+    logq, logp = [60] + [40] * 5, [60, 60]
+    sm = oracle_mod.gen_moduli(13, logq, logp)
+    bq, bp = oracle_mod.btp_chain(13, sm, len(logq), [61, 61])
+    assert bq[:len(logq)] == sm[:len(logq)] and len(bq) == len(logq) + 15
+    sizes = [39] * 3 + [60] * 8 + [56] * 4 + [61, 61]  # primes within half a bit of 2^size
+    assert all(abs(np.log2(float(q)) - b) < 0.5 for q, b in zip(bq[len(logq):] + bp, sizes))
+    assert len(set(bq + bp + sm)) == len(bq) + len(bp) + len(sm) - len(logq)
+    assert all(q % (2 << 13) == 1 for q in bq + bp)
+    boot = oracle_mod.Oracle(13, bq + bp, len(bq), len(bp))
+    for ns in (4096, 512, 2):
+        c = oracle_mod.BtpCircuit(boot, 40, ns)
+        p = c.params()
+        assert int(p["F"]) == round(bq[0] / 2 ** 48) and int(p["K"]) == 16 and int(p["degree"]) == 30
+        assert int(p["gap"]) == 4096 // ns and int(p["ntrace"]) == (4096 // ns).bit_length() - 1
+        assert abs(float(p["s_y"]) / 2 ** 60 - 1) < 1e-15
+        levels = [c.lt(k)[0] for k in range(7)]
+        top = len(bq) - 1
+        assert levels == [top, top - 1, top - 2, top - 3, top - 12, top - 13, top - 14]
+
+
+def _btp_keys(o, sk, circ, seed):
+    """Test keys for the oracle's circuit: relinearisation, every Galois key the
+    circuit uses (BSGS babies / giants, trace, conjugation), and the ephemeral
+    secret's two switching keys."""
+    N, n = o.N, o.N // 2
+    gels = {2 * N - 1}
+    p = circ.params()
+    gels |= {o.galois_element(int(p["slots"]) << i) for i in range(int(p["ntrace"]))}
+    for k in range(int(p["nlt"])):
+        _, n1, idx, _ = circ.lt(k)
+        for d in idx:
+            giant, baby = ((d // n1) * n1) % n, d % n1
+            gels |= {o.galois_element(r) for r in (giant, baby) if r}
+    keys = dict(rlk=o.gen_evk(seed, o.mul_coeffs(sk, sk, list(range(o.L + o.K))), sk), gks={})
+    for i, g in enumerate(sorted(gels)):
+        keys["gks"][g] = o.gen_evk(seed + 1 + i, sk, o.automorphism_ntt(sk, pow(g, -1, 2 * N)))
+    se = o.gen_secret(seed + 999, 32)
+    keys["d2s"] = o.gen_evk(seed + 1000, sk, se)
+    keys["s2d"] = o.gen_evk(seed + 1001, se, sk)
+    return keys
+
+
+@pytest.mark.parametrize("sparse", [True, False])
+def test_oracle_bootstrap_functional(oracle_mod, sparse):
+    """The oracle's bootstrapping circuit works on its own, with keys the
+    oracle made (no GPU, nothing from the library): a level-0 encryption
+    under a dense h = 192 secret comes back on the residual top level at its
+    scale, decrypting to the input (sparse slots: replicated) within 1e-4."""
+    logq, logp = [60] + [40] * 5, [60, 60]
+    sm = oracle_mod.gen_moduli(13, logq, logp)
+    bq, bp = oracle_mod.btp_chain(13, sm, len(logq), [61, 61])
+    boot = oracle_mod.Oracle(13, bq + bp, len(bq), len(bp))
+    sc = oracle_mod.Oracle(13, sm, len(logq), len(logp))
+    n = boot.N // 2
+    ns = n // 8 if sparse else n
+    circ = oracle_mod.BtpCircuit(boot, 40, ns)
+    sk = boot.gen_secret(7, 192)
+    keys = _btp_keys(boot, sk, circ, 50)
+    rng = np.random.default_rng(5)
+    v = rng.uniform(-1, 1, n)
+    v[ns:] = 0
+    ct = boot.encrypt_sk(3, sk, boot.encode(v, 2.0 ** 40, [0]), 0)
+    out = sc.bootstrap(boot, circ, keys, ct, 0)
+    top = len(logq) - 1
+    dec = boot.decode(boot.decrypt(out, sk, top), top, 2.0 ** 40)
+    exp = np.tile(v[:ns], n // ns)
+    err = np.abs(dec - exp)
+    assert err.max() < 1e-4 and err.mean() < 1e-5, (err.max(), err.mean())
