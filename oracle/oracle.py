@@ -432,9 +432,12 @@ class BtpCircuit:
         return dict(zip(names, out[:n]))
 
     def cos(self):
+        """The circuit's cosine coefficients as 80-bit values (read as bytes:
+        indexing a ctypes c_longdouble pointer would round them to double)."""
         n = int(self.params()["ncos"])
         p = lib().oracle_btp_cos_of(self._h)
-        return np.array([p[i] for i in range(n)], dtype=np.longdouble)
+        ld = np.dtype(np.longdouble).itemsize
+        return np.frombuffer(ctypes.string_at(p, n * ld), dtype=np.longdouble).copy()
 
     def lt(self, k):
         """(level, N1, diagonal indices, diagonals [level+1+K][N]) of transform k."""

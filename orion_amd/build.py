@@ -16,7 +16,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: the float64 quotient of the exact basis extension and the
 # encoder FFT must round exactly as written (bit parity with the CPU oracle).
 FLAGS = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result"]
-SOURCES = ["ntt.hip", "ntt2.hip", "kernels.hip", "encoder.hip", "backend.hip", "hostmath.cpp", "wire.cpp"]
+SOURCES = ["ntt.hip", "ntt2.hip", "ntt2s.hip", "kernels.hip", "encoder.hip", "backend.hip", "hostmath.cpp", "wire.cpp"]
 
 
 def _needs(obj, deps):

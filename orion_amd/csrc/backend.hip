@@ -27,6 +27,7 @@
 int orion_launch_ntt(int logN, const LimbSet& s, const DeviceTables* tb, bool inverse, hipStream_t st);
 int orion_launch_ntt_io(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st);
 int orion_launch_ntt2(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st);
+int orion_launch_ntt2s(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st);
 int orion_ntt_init();
 int orion_launch_ew(int op, const LimbSet& o, const LimbSet& a, const LimbSet& b, const u64* s, const u64* ss,
                     const DeviceTables* tb, int N, hipStream_t st);
@@ -60,7 +61,8 @@ static int find_best_n1(const std::vector<int>& idx, int slots, int logMaxRatio)
 
 namespace orion {
 
-enum { EW_ADD = 0, EW_SUB, EW_MUL, EW_MULADD, EW_NEG, EW_SCALE, EW_ADDC, EW_SUBSCALE, EW_COPY, EW_ADDSCALE, EW_SPLIT24 };
+enum { EW_ADD = 0, EW_SUB, EW_MUL, EW_MULADD, EW_NEG, EW_SCALE, EW_ADDC, EW_SUBSCALE, EW_COPY, EW_ADDSCALE, EW_SPLIT24,
+       EW_SPLIT30 };
 
 #define HIPCHK(x)                                                                                  \
   do {                                                                                             \
@@ -304,8 +306,10 @@ struct ProfRec {
   double bytes;
 };
 static const char* kProfNames[] = {"ntt_fwd", "ntt_inv", "elementwise", "basis_ext", "ks_mac", "automorph",
-                                   "tensor", "rescale_prep", "lt_bsgs", "lt_giant"};
-enum { P_NTT_FWD = 0, P_NTT_INV, P_EW, P_BEXT, P_MAC, P_AUT, P_TENSOR, P_RSPREP, P_LTMAC, P_LTGIANT, P_NCAT };
+                                   "tensor", "rescale_prep", "lt_bsgs", "lt_giant", "ntt_bext"};
+// ntt_bext: forward NTTs whose prologue forms the extended limb (NTT_PRO_BEXT),
+// priced (ns + 1) 8 N per limb-transform (+ 8 N for a subtract-and-scale epilogue)
+enum { P_NTT_FWD = 0, P_NTT_INV, P_EW, P_BEXT, P_MAC, P_AUT, P_TENSOR, P_RSPREP, P_LTMAC, P_LTGIANT, P_NTT_BEXT, P_NCAT };
 
 // ---------------------------------------------------------------------------
 // context
@@ -338,6 +342,29 @@ struct Context {
   // levels 1-4 under a 48-prime bootstrapping chain) keeps its ~120 keys in
   // a few GB instead of ~150 GB of full-chain keys.
   std::map<u64, EvKey> gks;
+  // split30 copies of the Galois keys lt_bsgs's baby steps read (made on
+  // first use; a copy remembers the key buffer it was made from, so a key
+  // made again for a higher level gets a fresh copy)
+  struct SplitKey {
+    std::shared_ptr<Buffer> src;
+    Poly k;
+  };
+  std::map<u64, SplitKey> gks_split;
+  int split_keys = getenv("ORION_LT_SPLIT_KEYS") ? atoi(getenv("ORION_LT_SPLIT_KEYS")) : 1;
+  const u64* split_key(u64 g, const EvKey& kk) {
+    auto it = gks_split.find(g);
+    if (it != gks_split.end() && it->second.src == kk.k.buf) return it->second.k.ptr();
+    no_capture("a split Galois key copy");
+    const Poly& src = kk.k;
+    Poly dst = alloc(src.ncomp, src.nlimb, 1);
+    std::vector<int> md;
+    for (int x = 0; x < src.nlimb; ++x) md.push_back(x <= kk.level ? x : L + (x - kk.level - 1));
+    for (int c0 = 0; c0 < src.ncomp; c0 += 1)
+      ew(EW_SPLIT30, ls(dst, c0, 1, iota(0, src.nlimb), md), ls(src, c0, 1, iota(0, src.nlimb), md),
+         ls(src, c0, 1, iota(0, src.nlimb), md));
+    gks_split[g] = SplitKey{src.buf, dst};
+    return dst.ptr();
+  }
   std::map<u64, int> key_hint;  // galEl -> highest level of a linear transform that uses it
   std::map<u64, u32*> autidx;
   std::map<std::pair<int, int>, BasisExtTable*> betab;
@@ -385,6 +412,7 @@ struct Context {
       hipGraphDestroy(kv.second.g);
     }
     graphs.clear();
+    gks_split.clear();
     gks.clear();
     sk = pk = rlk = Poly();
     pts.reset();
@@ -533,6 +561,7 @@ struct Context {
     };
     add(sk), add(pk), add(rlk);
     for (auto& kv : gks) add(kv.second.k);
+    for (auto& kv : gks_split) add(kv.second.k);
     for (int id : cts.live()) add(cts.get(id).poly);
     for (int id : pts.live()) add(pts.get(id).poly);
     for (int id : lts.live()) {
@@ -657,9 +686,19 @@ struct Context {
   // 15 vs 37 us; 64 jobs: 32 vs 40 us, float64 path).  Batched launches
   // (>= 128 jobs at 64 images) keep the one-pass kernel.
   int ntt2_below = getenv("ORION_NTT2_BELOW") ? atoi(getenv("ORION_NTT2_BELOW")) : 128;
+  // two-pass launches of at most this many limb-transforms use the
+  // latency-oriented kernels of ntt2s.hip (one butterfly per thread per
+  // stage, the tile in LDS) instead of ntt2.hip's 16-point threads
+  int ntt2s_below = getenv("ORION_NTT2S_BELOW") ? atoi(getenv("ORION_NTT2S_BELOW")) : 128;
   // decompositions with fewer limb-transforms per digit than this run every
   // digit's ModUp + NTT as one launch pair (0 = always per digit)
   int modup_merge = getenv("ORION_MODUP_MERGE") ? atoi(getenv("ORION_MODUP_MERGE")) : 256;
+  // 1: ModUp and ModDown form the extended limbs in the forward NTT's prologue
+  // (NTT_PRO_BEXT) instead of a basis_ext / modup_all launch whose output the
+  // NTT reads back (sources of at most 2 limbs, Standard ring), when the NTT
+  // runs on the two-pass kernels (fuse_bext); 2: on the one-pass kernel too
+  // (timing switch); 0: never
+  int bext_fuse = getenv("ORION_BEXT_FUSE") ? atoi(getenv("ORION_BEXT_FUSE")) : 1;
   // N = 2^15 inverse launches up to ntt2_tail_max limb-transforms whose last
   // round of one-limb workgroups would be partial (jobs / (rounds * CUs) below
   // ntt2_tail_eff) also take the two-pass kernels: a one-pass round costs one
@@ -714,28 +753,54 @@ struct Context {
     fprintf(ntt_log, "%d %d %d %d %d %d\n", impl, io.jobs, io.epi == NTT_EPI_SUBSCALE ? 1 : 0, inv ? 1 : 0, io.pro,
             io.jobs / std::max(1, io.dst.nlimb) * nint);
   }
-  void ntt_io(NttIO io, bool inv) {
+  // whether an NTT launch of `jobs` limb-transforms runs on the two-pass
+  // kernels (ntt2.hip): N = 2^16 always; N = 2^15 for small launches and for
+  // partial last rounds of inverse and plain forward launches (see above)
+  bool two_pass(int jobs, bool inv, int pro, int epi, bool inplace_sub) {
+    if (logN == 16) return true;
+    if (logN != 15 || ci) return false;
+    if (ntt_impl == 2 || jobs < ntt2_below) return true;
+    const bool plain = (pro == NTT_PRO_LOAD || pro == NTT_PRO_BEXT) && epi == NTT_EPI_STORE;
+    return (inv || (ntt2_tail_fwd == 1 && plain) || (ntt2_tail_fwd == 2 && !inplace_sub)) && ntt2_tail(jobs);
+  }
+  // the fused basis extension (NTT_PRO_BEXT) pays on the two-pass kernels
+  // only: in the one-pass kernel, one CU per limb, every target re-forms the
+  // shared y_i and float quotient and loads ns source limbs in its memory
+  // phase, and the LoLA step took 36.8 instead of 30.6 ms
+  // (profiles/r04c_bext_fuse_ab.txt); on the two-pass kernels batch 1 went
+  // from 3.0 to 2.84 ms per image
+  // and at B = 64 LoLA its partial-round two-pass launches were neutral to
+  // -0.5% (2089 / 2091 vs 2105 / 2097 img/s, profiles/r04d_bext_fuse_ab.txt),
+  // so it is kept to small launches (bext_fuse_below limb-transforms)
+  bool fuse_bext(int jobs, int ns, int epi) {
+    if (!bext_fuse || ns > 2 || ci) return false;
+    return bext_fuse == 2 || (jobs <= bext_fuse_below && two_pass(jobs, false, NTT_PRO_BEXT, epi, false));
+  }
+  int bext_fuse_below = getenv("ORION_BEXT_FUSE_BELOW") ? atoi(getenv("ORION_BEXT_FUSE_BELOW")) : 64;
+  // src_per_job: NTT_PRO_BEXT launches, the mean source limbs read per
+  // limb-transform (their algorithmic bytes are (src_per_job + 1) 8 N, + 8 N
+  // for a subtract-and-scale epilogue, in the ntt_bext category)
+  void ntt_io(NttIO io, bool inv, double src_per_job = 0) {
     io.order = ntt_order;
     io.ci = ci ? 1 : 0;
     io.jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
+    const bool bx = io.pro == NTT_PRO_BEXT;
+    const double per = (bx ? (src_per_job + 1) * 8.0 * N : 16.0 * N) + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
+    const int cat = bx ? P_NTT_BEXT : inv ? P_NTT_INV : P_NTT_FWD;
     if (io.order == 2) {  // integer-path (>= 2^46) limbs are ~1.4x slower per transform: dispatch them first
       int k = 0;
       for (int pass = 0; pass < 2; ++pass)
         for (int l = 0; l < io.dst.nlimb; ++l)
           if ((host_tb.mc[io.dst.mod[l]].f64 != 0) == (pass == 1)) io.lord[k++] = (unsigned char)l;
     }
-    if (logN == 16 || (logN == 15 && !ci && (ntt_impl == 2 || io.jobs < ntt2_below ||
-                          ((inv || (ntt2_tail_fwd == 1 && io.pro == NTT_PRO_LOAD && io.epi == NTT_EPI_STORE) ||
-                            (ntt2_tail_fwd == 2 && !(io.epi == NTT_EPI_SUBSCALE && io.ex.p == io.dst.p))) &&
-                           ntt2_tail(io.jobs))))) {  // N = 2^16: two-pass only
+    if (two_pass(io.jobs, inv, io.pro, io.epi, io.epi == NTT_EPI_SUBSCALE && io.ex.p == io.dst.p)) {
       Poly scratch;
       if (ntt2_chunk > 0 && io.jobs > 0) {  // chunks of jobs through one reused compact scratch
         const int chunk = std::min(ntt2_chunk, io.jobs);
         scratch = alloc(1, 1, chunk);
         io.mid = ls(scratch, 0, 1, {0}, {0});
         io.mid_compact = 1;
-        const double per = 16.0 * N + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
-        Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, per * io.jobs);
+        Scope sc(this, cat, per * io.jobs);
         for (int j0 = 0; j0 < io.jobs; j0 += chunk) {
           io.job0 = j0;
           io.njob = std::min(chunk, io.jobs - j0);
@@ -751,19 +816,19 @@ struct Context {
         scratch = alloc(io.dst.ncomp, io.dst.nlimb, io.dst.nbatch);
         io.mid = ls(scratch, 0, io.dst.ncomp, iota(0, io.dst.nlimb), std::vector<int>(io.dst.mod, io.dst.mod + io.dst.nlimb));
       }
-      const double per = 16.0 * N + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
-      Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, per * io.jobs);
-      if (orion_launch_ntt2(logN, io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
-      log_ntt(2, io, inv);
+      Scope sc(this, cat, per * io.jobs);
+      const bool small = io.jobs <= ntt2s_below;
+      if ((small ? orion_launch_ntt2s : orion_launch_ntt2)(logN, io, d_tb, inv, stream))
+        throw std::runtime_error("NTT launch failed");
+      log_ntt(small ? 3 : 2, io, inv);
       return;
     }
     if (ntt_stagger > 0) {
       io.stagger = io.jobs >= ntt_stagger_min * cus() ? ntt_stagger : 0;
     }
     // algorithmic bytes per limb-transform: read + write the limb (16 N), + 8 N
-    // for the epilogue's second operand
-    const double per = 16.0 * N + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
-    Scope sc(this, inv ? P_NTT_INV : P_NTT_FWD, per * io.dst.ncomp * io.dst.nlimb * io.dst.nbatch);
+    // for the epilogue's second operand (per, above)
+    Scope sc(this, cat, per * io.dst.ncomp * io.dst.nlimb * io.dst.nbatch);
     if (orion_launch_ntt_io(logN, io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
     log_ntt(1, io, inv);
   }
@@ -774,7 +839,9 @@ struct Context {
       s = *sc;
       for (int l = 0; l < o.nlimb; ++l) ss.push_back(hm_shoup(s[l], mods[o.mod[l]]));
     }
-    int nin = (op == EW_NEG || op == EW_SCALE || op == EW_ADDC || op == EW_COPY || op == EW_SPLIT24) ? 1 : 2;
+    int nin = (op == EW_NEG || op == EW_SCALE || op == EW_ADDC || op == EW_COPY || op == EW_SPLIT24 || op == EW_SPLIT30)
+                  ? 1
+                  : 2;
     if (op == EW_MULADD || op == EW_ADDSCALE) nin += 1;
     Scope scp(this, P_EW, 8.0 * N * o.ncomp * o.nlimb * o.nbatch * (nin + 1));
     orion_launch_ew(op, o, a, b, sc ? s.data() : nullptr, sc ? ss.data() : nullptr, d_tb, N, stream);
@@ -1265,16 +1332,36 @@ struct Context {
       for (int j = 0; j < nqp; ++j) md.push_back(qp_mod(level, j));
       LimbSet Dl = ls(D, 0, nc * beta, iota(0, nqp), md);
       LimbSet in = ls(cinv, 0, nc, iota(0, level + 1), iota(0, level + 1));
+      std::vector<int> tpos, tmod;
+      for (int i = 0; i < beta; ++i)
+        for (int j = 0; j < nqp; ++j)
+          if (!(j >= i * K && j < std::min((i + 1) * K, level + 1))) tpos.push_back(i * nqp + j), tmod.push_back(md[j]);
+      const bool tset = beta * nqp <= 256 && (int)tpos.size() <= ORION_MAXLIMB;
+      if (tset && fuse_bext(nc * B * (int)tpos.size(), K, NTT_EPI_STORE)) {
+        // every digit's extension formed in the prologue of one NTT over the
+        // target limbs (no modup_all launch, no round trip through HBM)
+        LimbSet T = ls(D, 0, nc, tpos, tmod);
+        T.comp_stride = (long long)beta * D.comp_stride();
+        NttIO io = nio(T, in);
+        io.pro = NTT_PRO_BEXT;
+        io.bx = modup_tabs(level);
+        for (int i = 0; i < beta; ++i) io.bx_s0[i] = (unsigned char)(i * K);
+        double srcs = 0;
+        for (size_t l = 0; l < tpos.size(); ++l) {
+          const int i = tpos[l] / nqp, j = tpos[l] % nqp, lo = i * K, ns = std::min(K, level + 1 - lo);
+          io.bx_tab[l] = (unsigned char)i;
+          io.bx_t[l] = (unsigned char)(j < lo ? j : j - ns);
+          srcs += ns;
+        }
+        ntt_io(io, false, srcs / (double)tpos.size());
+        return D;
+      }
       {
         Scope sc(this, P_BEXT, 8.0 * N * B * nc * (level + 1 + beta * nqp - (level + 1)));
         if (orion_launch_modup_all(Dl, in, modup_tabs(level), beta, K, nqp, d_tb, N, stream))
           throw std::runtime_error("modup_all: bad launch shape");
       }
-      std::vector<int> tpos, tmod;
-      for (int i = 0; i < beta; ++i)
-        for (int j = 0; j < nqp; ++j)
-          if (!(j >= i * K && j < std::min((i + 1) * K, level + 1))) tpos.push_back(i * nqp + j), tmod.push_back(md[j]);
-      if (beta * nqp <= 256 && (int)tpos.size() <= ORION_MAXLIMB) {
+      if (tset) {
         LimbSet T = ls(D, 0, nc, tpos, tmod);
         T.comp_stride = (long long)beta * D.comp_stride();
         ntt(T, false);
@@ -1293,9 +1380,17 @@ struct Context {
       LimbSet in = ls(cinv, 0, nc, iota(lo, hi), iota(lo, hi));
       LimbSet out = ls(D, i, nc, tpos, tmod);
       out.comp_stride = dstride;
-      // ModUp as its own kernel: y_i and the float64 quotient are shared by every
-      // target (fusing it into the NTT prologue recomputes them per target limb,
-      // and the NTT is VALU-bound, so that was measured slower)
+      if (fuse_bext(nc * B * out.nlimb, hi - lo, NTT_EPI_STORE)) {  // the extension formed in the NTT's prologue
+        NttIO io = nio(out, in);
+        io.pro = NTT_PRO_BEXT;
+        io.bx = T;
+        for (int t = 0; t < out.nlimb; ++t) io.bx_tab[t] = 0, io.bx_t[t] = (unsigned char)t;
+        io.bx_s0[0] = 0;
+        ntt_io(io, false, hi - lo);
+        continue;
+      }
+      // ModUp as its own kernel (the ORION_BEXT_FUSE=0 path, and digits of more
+      // than 2 limbs): y_i and the float64 quotient are shared by every target
       {
         Scope sc(this, P_BEXT, 8.0 * N * B * nc * (in.nlimb + out.nlimb));
         if (orion_launch_basis_ext(out, in, T, d_tb, N, stream))
@@ -1352,6 +1447,24 @@ struct Context {
     const int nc = x.ncomp, B = x.nbatch;
     LimbSet xp = limbs(x, level + 1, K);
     ntt(xp, true);
+    if (fuse_bext(nc * B * (level + 1), K, NTT_EPI_SUBSCALE)) {
+      // the extension of the P limbs formed in the prologue of the NTT whose
+      // epilogue is (x_Q - .) * P^-1: no basis_ext launch, no extended limbs in HBM
+      NttIO io = nio(out, xp);
+      io.pro = NTT_PRO_BEXT;
+      io.bx = moddown_tab(level);
+      for (int j = 0; j <= level; ++j) io.bx_tab[j] = 0, io.bx_t[j] = (unsigned char)j;
+      io.bx_s0[0] = 0;
+      io.epi = NTT_EPI_SUBSCALE;
+      io.ex = limbs(x, 0, level + 1);
+      const std::vector<u64> pq = p_mod_q(level);
+      for (int j = 0; j <= level; ++j) {
+        io.s[j] = hm_invmod(pq[j], mods[j]);
+        io.ss[j] = hm_shoup(io.s[j], mods[j]);
+      }
+      ntt_io(io, false, K);
+      return;
+    }
     Poly ext = alloc(nc, level + 1, B);
     LimbSet le = lsq(ext, 0, nc, level);
     {
@@ -1609,6 +1722,7 @@ struct Context {
           const u64 g = galois_element(b);
           const EvKey& kk = galois_key(g, level);
           Bb.key[s] = kk.k.ptr();
+          Bb.keyw[s] = split_keys ? split_key(g, kk) : nullptr;
           Bb.klvl[s] = kk.level;
           Bb.idx[s] = aut_index(g);
           ++nrot;
@@ -3428,6 +3542,7 @@ void RemovePlaintextDiagonals(int tid) {
 }
 void RemoveRotationKeys(void) {
   API_BEGIN
+  ctx().gks_split.clear();
   ctx().gks.clear();
   API_END_VOID
 }

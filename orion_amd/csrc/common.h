@@ -231,6 +231,7 @@ struct LtPlan {
 };
 struct LtBabies {  // the baby steps of register slots [s0, s0 + nb) of one lt_bsgs launch
   const u64* key[LT_MAXB];  // Galois key of the slot (null: the zero baby)
+  const u64* keyw[LT_MAXB]; // its split30 copy (limbs up to 2^60; null: use key)
   const u32* idx[LT_MAXB];  // its NTT-domain automorphism index
   int klvl[LT_MAXB];        // level the key was made for
   int nb, s0, beta, K, level, L;
@@ -357,16 +358,60 @@ __device__ __forceinline__ u64 bext_prep(const BasisExtTable* __restrict__ T, co
   }
   return (u64)vf;
 }
+// the target side of the exact basis extension: sum_i y_i (S/s_i mod t) -
+// v S mod t (basis_ext_kernel, modup_all_kernel and the NTT prologue
+// NTT_PRO_BEXT); the per-target constants are wave-uniform (SGPR) and v*S mod
+// t is selected from the ns+1 precomputed values with v_cndmask instead of a
+// per-lane table lookup
+template <int MS>
+__device__ __forceinline__ u64 bext_target_sel(const BasisExtTable* __restrict__ T, int t, int ns, u64 q,
+                                               const u64* y, u64 v) {
+  u64 acc = T->vS_t[t][0];
+#pragma unroll
+  for (int j = 1; j <= MS; ++j) {
+    if (j > ns) break;
+    acc = v == (u64)j ? T->vS_t[t][j] : acc;
+  }
+  if (T->narrow[t]) {  // wave-uniform: sources and target < 2^32 (ResNet's 30-bit chains)
+    // the whole sum in one u64: one 32x32 -> 64 multiply-add per source,
+    // then a single reduction with a float64 quotient (off by at most one)
+#pragma unroll
+    for (int i = 0; i < MS; ++i) {
+      if (i >= ns) break;
+      acc += (u64)(u32)y[i] * (u32)T->qhat_t[t][i];
+    }
+    const u64 k = (u64)((double)acc * T->tinv[t]);
+    long long r = (long long)(acc - k * q);
+    r = r < 0 ? r + (long long)q : r;
+    r = r >= (long long)q ? r - (long long)q : r;
+    return (u64)r;
+  }
+  // lazy: each Shoup product is in [0, 2q) and the running sum is kept in
+  // [0, 2q) by one conditional subtraction (4q < 2^63 for q < 2^61)
+  const u64 q2 = q << 1, nq = 0 - q;
+#pragma unroll
+  for (int i = 0; i < MS; ++i) {
+    if (i >= ns) break;
+    acc += shoup_lazy_nq(y[i], T->qhat_t[t][i], T->qhat_ts[t][i], nq);
+    acc = acc >= q2 ? acc - q2 : acc;
+  }
+  return acc >= q ? acc - q : acc;
+}
 // ---------------------------------------------------------------------------
 // NTT launch descriptor: transform + fused producer (prologue) / consumer
 // (epilogue).  Job j = (c, l, b) over dst's (ncomp, nlimb, nbatch); the limb's
 // modulus is dst.mod[l].
 //   prologue NTT_PRO_LOAD:    load row (c, l, b) of src (src == dst: in place)
 //            NTT_PRO_RESCALE: ((x + h) mod q_L) mod q_l - (h mod q_l), x = row (c, 0, b) of src
+//            NTT_PRO_BEXT:    the exact basis extension of the sources to dst limb l,
+//                             formed in registers (ModUp of a gadget digit, or
+//                             ModDown's extension of the P limbs): table bx + bx_tab[l],
+//                             target bx_t[l], sources = src rows (c, bx_s0[table] + i, b),
+//                             coefficient domain -- bit-identical to basis_ext_kernel
 //   epilogue NTT_EPI_STORE:   store to row (c, l, b) of dst
 //            NTT_EPI_SUBSCALE (forward only): dst = (ex - y) * s_l, ex row (c, l, b)
 // ---------------------------------------------------------------------------
-enum { NTT_PRO_LOAD = 0, NTT_PRO_RESCALE = 2 };
+enum { NTT_PRO_LOAD = 0, NTT_PRO_RESCALE = 2, NTT_PRO_BEXT = 3 };
 enum { NTT_EPI_STORE = 0, NTT_EPI_SUBSCALE = 1 };
 struct NttIO {
   LimbSet dst, src, ex;
@@ -384,6 +429,10 @@ struct NttIO {
   int job0, njob, mid_compact;
   u64 s[ORION_MAXLIMB], ss[ORION_MAXLIMB];
   unsigned char lord[ORION_MAXLIMB];  // order 2: dispatch order of dst's limbs
+  // NTT_PRO_BEXT: the basis-extension tables, and per dst limb its table and
+  // target index, per table its first source limb in src
+  const BasisExtTable* bx;
+  unsigned char bx_tab[ORION_MAXLIMB], bx_t[ORION_MAXLIMB], bx_s0[ORION_MAXLIMB];
 };
 
 // ---------------------------------------------------------------------------

@@ -78,6 +78,7 @@ enum EwOp : int {
   EW_COPY = 8,     // o = a
   EW_ADDSCALE = 9, // o = o + a * s_l
   EW_SPLIT24 = 10, // o = split24(a) on limbs below 2^48, split30(a) on limbs up to 2^60 (LT_INT30), else a
+  EW_SPLIT30 = 11, // o = split30(a) on limbs up to 2^60, else a (lt_bsgs's baby key copies)
                    // (lt_bsgs's split-MAC operand forms)
 };
 
@@ -126,6 +127,7 @@ __global__ void __launch_bounds__(256) ew_kernel(LimbSet o, LimbSet a, LimbSet b
           : (LT_INT30 && mc.bar_k <= 60) ? make_ulonglong2(split30(x.x), split30(x.y))
                                          : x;
       break;
+    case EW_SPLIT30: z = mc.bar_k <= 60 ? make_ulonglong2(split30(x.x), split30(x.y)) : x; break;
     case EW_ADDSCALE: {
       const ulonglong2 w = *po;
       z.x = add_mod(w.x, shoup_mul(x.x, sc.s[l], sc.ss[l], q), q);
@@ -163,43 +165,7 @@ __global__ void __launch_bounds__(256) tensor_kernel(LimbSet d, LimbSet a, LimbS
 // Exact basis extension (Lattigo ModUpExact restated; the
 // source-side math is bext_prep in common.h, the target side bext_target_sel).
 // in: ns source limbs (coefficient domain), out: nt target limbs.  Two
-// coefficients per thread (16-B accesses); the per-target constants are
-// wave-uniform (SGPR) and v*S mod t is selected from the ns+1 precomputed
-// values with v_cndmask instead of a per-lane table lookup.
-template <int MS>
-__device__ __forceinline__ u64 bext_target_sel(const BasisExtTable* __restrict__ T, int t, int ns, u64 q,
-                                               const u64* y, u64 v) {
-  u64 acc = T->vS_t[t][0];
-#pragma unroll
-  for (int j = 1; j <= MS; ++j) {
-    if (j > ns) break;
-    acc = v == (u64)j ? T->vS_t[t][j] : acc;
-  }
-  if (T->narrow[t]) {  // wave-uniform: sources and target < 2^32 (ResNet's 30-bit chains)
-    // the whole sum in one u64: one 32x32 -> 64 multiply-add per source,
-    // then a single reduction with a float64 quotient (off by at most one)
-#pragma unroll
-    for (int i = 0; i < MS; ++i) {
-      if (i >= ns) break;
-      acc += (u64)(u32)y[i] * (u32)T->qhat_t[t][i];
-    }
-    const u64 k = (u64)((double)acc * T->tinv[t]);
-    long long r = (long long)(acc - k * q);
-    r = r < 0 ? r + (long long)q : r;
-    r = r >= (long long)q ? r - (long long)q : r;
-    return (u64)r;
-  }
-  // lazy: each Shoup product is in [0, 2q) and the running sum is kept in
-  // [0, 2q) by one conditional subtraction (4q < 2^63 for q < 2^61)
-  const u64 q2 = q << 1, nq = 0 - q;
-#pragma unroll
-  for (int i = 0; i < MS; ++i) {
-    if (i >= ns) break;
-    acc += shoup_lazy_nq(y[i], T->qhat_t[t][i], T->qhat_ts[t][i], nq);
-    acc = acc >= q2 ? acc - q2 : acc;
-  }
-  return acc >= q ? acc - q : acc;
-}
+// coefficients per thread (16-B accesses).
 template <int MS>
 __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in, const BasisExtTable* __restrict__ T,
                                                         const DeviceTables* __restrict__ tb, int N, int tchunk) {
@@ -418,6 +384,45 @@ __device__ __forceinline__ void gadget_at(const u64* __restrict__ dp, long long 
   }
 }
 
+// the same gadget product from a split30 copy of the key (moduli up to 2^60):
+// 30-bit piece products accumulated without carries (MacW, one
+// v_mad_u64_u32 each; the digit is cut once for both components), one
+// reduction per 8 digits
+__device__ __forceinline__ void gadget_at_w(const u64* __restrict__ dp, long long dstride, const u64* ownp,
+                                            int owndigit, const u64* __restrict__ keyw, int beta, int L, int K,
+                                            int klvl, int m, int N, int j, const ModConst& mc, u64& r0, u64& r1) {
+  r0 = r1 = 0;
+  const long long kstride = (long long)(klvl + 1 + K) * N;
+  const u64* kp = keyw + (long long)key_pos(m, L, klvl) * N + j;
+  MacW a0, a1;
+  macw_zero(a0), macw_zero(a1);
+  for (int i0 = 0; i0 < beta; i0 += 4) {
+    u64 d[4], k0[4], k1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u;
+      if (i < beta) {
+        d[u] = i == owndigit ? ownp[j] : dp[i * dstride + j];
+        k0[u] = kp[(2 * i + 0) * kstride];
+        k1[u] = kp[(2 * i + 1) * kstride];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i0 + u < beta) {
+        const u64 ds = split30(d[u]);
+        macw_add(a0, (u32)ds, (u32)(ds >> 32), (u32)k0[u], (u32)(k0[u] >> 32));
+        macw_add(a1, (u32)ds, (u32)(ds >> 32), (u32)k1[u], (u32)(k1[u] >> 32));
+      }
+    }
+    if ((i0 & 4) || i0 + 4 >= beta) {  // 8 products accumulated, or the last chunk
+      r0 = add_mod(r0, macw_reduce8(a0, mc), mc.q);
+      r1 = add_mod(r1, macw_reduce8(a1, mc), mc.q);
+      macw_zero(a0), macw_zero(a1);
+    }
+  }
+}
+
 __device__ __forceinline__ void mac_add1(MacAcc& a, u64 x) {
   a.lo += x;
   a.c += (a.lo < x);
@@ -464,7 +469,11 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
       if (Bb.key[s] && !(LT_ABLATE & 2) && !((LT_ABLATE & 8) && mc.bar_k > 48)) {
         const int j = jx[s];
         u64 r0, r1;
-        gadget_at(dp, D.comp_stride, c1p, owndigit, Bb.key[s], Bb.beta, Bb.L, Bb.K, Bb.klvl[s], m, N, j, mc, r0, r1);
+        if (Bb.keyw[s] && mc.bar_k <= 60)  // (block-uniform)
+          gadget_at_w(dp, D.comp_stride, c1p, owndigit, Bb.keyw[s], Bb.beta, Bb.L, Bb.K, Bb.klvl[s], m, N, j, mc, r0,
+                      r1);
+        else
+          gadget_at(dp, D.comp_stride, c1p, owndigit, Bb.key[s], Bb.beta, Bb.L, Bb.K, Bb.klvl[s], m, N, j, mc, r0, r1);
         if (isq) r0 = add_mod(r0, shoup_mul(c0p[j], pq, pqs, mc.q), mc.q);
         x0[s] = r0;
         x1[s] = r1;
@@ -526,9 +535,11 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
   if (LT_INT30 && mc.bar_k <= 60) {
     // 48..60-bit moduli: 30-bit piece products accumulated without carries
     // (MacW, one v_mad_u64_u32 each), one reduction per 8 babies; the plan's
-    // diagonal copies are stored split30
-    // (the baby pieces are cut per giant: kept as whole words they cost no
-    // extra registers)
+    // diagonal copies are stored split30, and the baby rotations are cut into
+    // their pieces once here (the split30 word takes the same two VGPRs), not
+    // per giant
+#pragma unroll
+    for (int s = 0; s < MB; ++s) x0[s] = split30(x0[s]), x1[s] = split30(x1[s]);
     for (int g = g0; g < g1; ++g) {
       const unsigned long long mask = P->mask[g] >> Bb.s0;
       u64 r0 = 0, r1 = 0;
@@ -545,8 +556,8 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
       for (int s = 0; s < MB; ++s) {
         if (((mask >> s) & 1ull) && !(LT_ABLATE & 4)) {
           const u32 yb = (u32)pv[s], ya = (u32)(pv[s] >> 32);
-          macw_add(a0, (u32)x0[s] & 0x3fffffffu, (u32)(x0[s] >> 30), yb, ya);
-          macw_add(a1, (u32)x1[s] & 0x3fffffffu, (u32)(x1[s] >> 30), yb, ya);
+          macw_add(a0, (u32)x0[s], (u32)(x0[s] >> 32), yb, ya);
+          macw_add(a1, (u32)x1[s], (u32)(x1[s] >> 32), yb, ya);
         }
         if ((s & 7) == 7) {
           r0 = add_mod(r0, macw_reduce8(a0, mc), mc.q);
@@ -762,7 +773,7 @@ int orion_launch_ew(int op, const LimbSet& o, const LimbSet& a, const LimbSet& b
 #define CASE(OPC) \
   case OPC: hipLaunchKernelGGL(ew_kernel<OPC>, g, blk, 0, st, o, a, b, sc, tb, N); break;
     CASE(EW_ADD) CASE(EW_SUB) CASE(EW_MUL) CASE(EW_MULADD) CASE(EW_NEG) CASE(EW_SCALE) CASE(EW_ADDC)
-    CASE(EW_SUBSCALE) CASE(EW_COPY) CASE(EW_ADDSCALE) CASE(EW_SPLIT24)
+    CASE(EW_SUBSCALE) CASE(EW_COPY) CASE(EW_ADDSCALE) CASE(EW_SPLIT24) CASE(EW_SPLIT30)
 #undef CASE
     default: return -1;
   }

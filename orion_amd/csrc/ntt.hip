@@ -51,6 +51,37 @@ __device__ __forceinline__ u64 ci_fold(u64 x, u64 y, const ModConst& mc) {
   return sub_mod(x, shoup_mul(y, mc.ciw, mc.ciw_s, mc.q), mc.q);
 }
 
+// NTT_PRO_BEXT, one-pass kernel: rows 4G .. 4G+3 of the thread's 32 formed
+// by the exact basis extension, the next group's source loads in flight.  The
+// groups recurse on a template index so that every a[] index is a constant
+// (a loop over groups that is not unrolled would index a[] dynamically and put
+// the whole limb in scratch); fenced so that no group's loads are hoisted
+// ahead (the limb's 64 VGPRs leave no room for them)
+template <int G, class A, int B0>
+__device__ __forceinline__ void bext_rows(typename A::T (&a)[32], const u64 (&xa)[4], const u64 (&xb)[4], const A& ar,
+                                          const BasisExtTable* __restrict__ T, const DeviceTables* __restrict__ tb,
+                                          int ti, int ns, u64 q, __amdgpu_buffer_rsrc_t r0, __amdgpu_buffer_rsrc_t r1,
+                                          int t) {
+  if constexpr (G < 8) {
+    u64 na[4], nb[4];
+    if constexpr (G < 7) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        na[k] = buf_ld(r0, t * 8, ((4 * (G + 1) + k) << B0) * 8);
+        nb[k] = ns > 1 ? buf_ld(r1, t * 8, ((4 * (G + 1) + k) << B0) * 8) : 0;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      u64 x[2] = {xa[k], xb[k]}, y[2];
+      const u64 v = bext_prep<2>(T, tb, x, y);
+      a[4 * G + k] = ar.from_u64(bext_target_sel<2>(T, ti, ns, q, y, v));
+    }
+    NTT_FENCE();
+    if constexpr (G < 7) bext_rows<G + 1, A, B0>(a, na, nb, ar, T, tb, ti, ns, q, r0, r1, t);
+  }
+}
+
 template <class A, int LOGN, int PRO, int EPI, bool CI>
 __device__ __forceinline__ void ntt_fwd_body(const NttIO& io, int c, int l, int b, const ModConst& mc, const A& ar,
                                              __amdgpu_buffer_rsrc_t w, u32* lds, const DeviceTables* __restrict__ tb) {
@@ -75,6 +106,23 @@ __device__ __forceinline__ void ntt_fwd_body(const NttIO& io, int c, int l, int 
 #pragma unroll
       for (int k = 0; k < 32; ++k) a[k] = ar.from_u64(buf_ld(rs, t * 8, (k << B0) * 8));
     }
+  } else if constexpr (PRO == NTT_PRO_BEXT) {
+    // the exact basis extension of (at most 2) source limbs to this limb, in
+    // registers (the value basis_ext_kernel would have stored)
+    static_assert(!CI, "no fused basis extension on the ConjugateInvariant ring");
+    const int tk = arg_byte(io.bx_tab, l), ti = arg_byte(io.bx_t, l), s0 = arg_byte(io.bx_s0, tk);
+    const BasisExtTable* __restrict__ T = io.bx + tk;
+    const int ns = T->ns;
+    const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.src, c, s0, b), 0, N * 8, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r1 =
+        __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.src, c, s0 + (ns > 1 ? 1 : 0), b), 0, N * 8, 0x00020000);
+    u64 xa[4], xb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      xa[k] = buf_ld(r0, t * 8, (k << B0) * 8);
+      xb[k] = ns > 1 ? buf_ld(r1, t * 8, (k << B0) * 8) : 0;
+    }
+    bext_rows<0, A, B0>(a, xa, xb, ar, T, tb, ti, ns, mc.q, r0, r1, t);
   } else {  // NTT_PRO_RESCALE (DivRoundByLastModulusNTT), fused with the NTT of every other limb
     const u64* sp = row_ptr(io.src, c, 0, b);
     const u64 qL = tb->mc[io.modL].q, h = qL >> 1;
@@ -355,6 +403,10 @@ int launch_ntt_ring(const NttIO& io, const DeviceTables* tb, bool inverse, hipSt
   FWD(NTT_PRO_LOAD, NTT_EPI_STORE)
   FWD(NTT_PRO_LOAD, NTT_EPI_SUBSCALE)
   FWD(NTT_PRO_RESCALE, NTT_EPI_SUBSCALE)
+  if constexpr (!CI) {
+    FWD(NTT_PRO_BEXT, NTT_EPI_STORE)
+    FWD(NTT_PRO_BEXT, NTT_EPI_SUBSCALE)
+  }
 #undef FWD
   return -1;
 }
@@ -369,6 +421,10 @@ void init_lds_ring() {
   set_lds_attr<LOGN, NTT_PRO_LOAD, NTT_EPI_STORE, CI>();
   set_lds_attr<LOGN, NTT_PRO_LOAD, NTT_EPI_SUBSCALE, CI>();
   set_lds_attr<LOGN, NTT_PRO_RESCALE, NTT_EPI_SUBSCALE, CI>();
+  if constexpr (!CI) {
+    set_lds_attr<LOGN, NTT_PRO_BEXT, NTT_EPI_STORE, CI>();
+    set_lds_attr<LOGN, NTT_PRO_BEXT, NTT_EPI_SUBSCALE, CI>();
+  }
   hipFuncSetAttribute((const void*)ntt_inv_kernel<LOGN, CI>, hipFuncAttributeMaxDynamicSharedMemorySize,
                       ((1 << LOGN) + (1 << LOGN) / 32) * 4);
 }

@@ -66,11 +66,32 @@ __device__ __forceinline__ void fwd_cols(const NttIO& io, int job, int c, int l,
   const int t = threadIdx.x, cl = t & 15, rg = t >> 4;
   const int col = tile * 16 + cl;
   typename A::T a[16];
-  const u64* src = row_ptr(io.src, c, PRO == NTT_PRO_LOAD ? l : 0, b);
   if constexpr (PRO == NTT_PRO_LOAD) {
+    const u64* src = row_ptr(io.src, c, l, b);
 #pragma unroll
     for (int i = 0; i < 16; ++i) a[i] = ar.from_u64(src[col + ((rg + RG * i) << 8)]);
+  } else if constexpr (PRO == NTT_PRO_BEXT) {
+    // the exact basis extension of (at most 2) source limbs to this limb, in
+    // registers: the value basis_ext_kernel would have stored
+    const int k = arg_byte(io.bx_tab, l), ti = arg_byte(io.bx_t, l), s0 = arg_byte(io.bx_s0, k);
+    const BasisExtTable* __restrict__ T = io.bx + k;
+    const int ns = T->ns;
+    const u64* sp0 = row_ptr(io.src, c, s0, b);
+    const u64* sp1 = row_ptr(io.src, c, s0 + (ns > 1 ? 1 : 0), b);
+    u64 x0[16], x1[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      x0[i] = sp0[col + ((rg + RG * i) << 8)];
+      x1[i] = ns > 1 ? sp1[col + ((rg + RG * i) << 8)] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      u64 x[2] = {x0[i], x1[i]}, y[2];
+      const u64 v = bext_prep<2>(T, tb, x, y);
+      a[i] = ar.from_u64(bext_target_sel<2>(T, ti, ns, mc.q, y, v));
+    }
   } else {  // NTT_PRO_RESCALE (DivRoundByLastModulusNTT prep of every other limb)
+    const u64* src = row_ptr(io.src, c, 0, b);
     const u64 qL = tb->mc[io.modL].q, h = qL >> 1;
     const u64 hm = barrett128(0, h, mc);
 #pragma unroll
@@ -345,6 +366,8 @@ int launch2(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t s
   }
   if (io.pro == NTT_PRO_LOAD)
     hipLaunchKernelGGL((ntt2_fwd_cols<LOGN, NTT_PRO_LOAD>), ga, ba, 0, st, io, tb);
+  else if (io.pro == NTT_PRO_BEXT && !io.ci)
+    hipLaunchKernelGGL((ntt2_fwd_cols<LOGN, NTT_PRO_BEXT>), ga, ba, 0, st, io, tb);
   else if (io.pro == NTT_PRO_RESCALE)
     hipLaunchKernelGGL((ntt2_fwd_cols<LOGN, NTT_PRO_RESCALE>), ga, ba, 0, st, io, tb);
   else
