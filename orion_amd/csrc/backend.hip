@@ -61,8 +61,7 @@ static int find_best_n1(const std::vector<int>& idx, int slots, int logMaxRatio)
 
 namespace orion {
 
-enum { EW_ADD = 0, EW_SUB, EW_MUL, EW_MULADD, EW_NEG, EW_SCALE, EW_ADDC, EW_SUBSCALE, EW_COPY, EW_ADDSCALE, EW_SPLIT24,
-       EW_SPLIT30 };
+enum { EW_ADD = 0, EW_SUB, EW_MUL, EW_MULADD, EW_NEG, EW_SCALE, EW_ADDC, EW_SUBSCALE, EW_COPY, EW_ADDSCALE, EW_SPLIT24 };
 
 #define HIPCHK(x)                                                                                  \
   do {                                                                                             \
@@ -342,29 +341,6 @@ struct Context {
   // levels 1-4 under a 48-prime bootstrapping chain) keeps its ~120 keys in
   // a few GB instead of ~150 GB of full-chain keys.
   std::map<u64, EvKey> gks;
-  // split30 copies of the Galois keys lt_bsgs's baby steps read (made on
-  // first use; a copy remembers the key buffer it was made from, so a key
-  // made again for a higher level gets a fresh copy)
-  struct SplitKey {
-    std::shared_ptr<Buffer> src;
-    Poly k;
-  };
-  std::map<u64, SplitKey> gks_split;
-  int split_keys = getenv("ORION_LT_SPLIT_KEYS") ? atoi(getenv("ORION_LT_SPLIT_KEYS")) : 1;
-  const u64* split_key(u64 g, const EvKey& kk) {
-    auto it = gks_split.find(g);
-    if (it != gks_split.end() && it->second.src == kk.k.buf) return it->second.k.ptr();
-    no_capture("a split Galois key copy");
-    const Poly& src = kk.k;
-    Poly dst = alloc(src.ncomp, src.nlimb, 1);
-    std::vector<int> md;
-    for (int x = 0; x < src.nlimb; ++x) md.push_back(x <= kk.level ? x : L + (x - kk.level - 1));
-    for (int c0 = 0; c0 < src.ncomp; c0 += 1)
-      ew(EW_SPLIT30, ls(dst, c0, 1, iota(0, src.nlimb), md), ls(src, c0, 1, iota(0, src.nlimb), md),
-         ls(src, c0, 1, iota(0, src.nlimb), md));
-    gks_split[g] = SplitKey{src.buf, dst};
-    return dst.ptr();
-  }
   std::map<u64, int> key_hint;  // galEl -> highest level of a linear transform that uses it
   std::map<u64, u32*> autidx;
   std::map<std::pair<int, int>, BasisExtTable*> betab;
@@ -412,7 +388,6 @@ struct Context {
       hipGraphDestroy(kv.second.g);
     }
     graphs.clear();
-    gks_split.clear();
     gks.clear();
     sk = pk = rlk = Poly();
     pts.reset();
@@ -561,7 +536,6 @@ struct Context {
     };
     add(sk), add(pk), add(rlk);
     for (auto& kv : gks) add(kv.second.k);
-    for (auto& kv : gks_split) add(kv.second.k);
     for (int id : cts.live()) add(cts.get(id).poly);
     for (int id : pts.live()) add(pts.get(id).poly);
     for (int id : lts.live()) {
@@ -839,7 +813,7 @@ struct Context {
       s = *sc;
       for (int l = 0; l < o.nlimb; ++l) ss.push_back(hm_shoup(s[l], mods[o.mod[l]]));
     }
-    int nin = (op == EW_NEG || op == EW_SCALE || op == EW_ADDC || op == EW_COPY || op == EW_SPLIT24 || op == EW_SPLIT30)
+    int nin = (op == EW_NEG || op == EW_SCALE || op == EW_ADDC || op == EW_COPY || op == EW_SPLIT24)
                   ? 1
                   : 2;
     if (op == EW_MULADD || op == EW_ADDSCALE) nin += 1;
@@ -1722,7 +1696,6 @@ struct Context {
           const u64 g = galois_element(b);
           const EvKey& kk = galois_key(g, level);
           Bb.key[s] = kk.k.ptr();
-          Bb.keyw[s] = split_keys ? split_key(g, kk) : nullptr;
           Bb.klvl[s] = kk.level;
           Bb.idx[s] = aut_index(g);
           ++nrot;
@@ -3542,7 +3515,6 @@ void RemovePlaintextDiagonals(int tid) {
 }
 void RemoveRotationKeys(void) {
   API_BEGIN
-  ctx().gks_split.clear();
   ctx().gks.clear();
   API_END_VOID
 }

@@ -231,7 +231,6 @@ struct LtPlan {
 };
 struct LtBabies {  // the baby steps of register slots [s0, s0 + nb) of one lt_bsgs launch
   const u64* key[LT_MAXB];  // Galois key of the slot (null: the zero baby)
-  const u64* keyw[LT_MAXB]; // its split30 copy (limbs up to 2^60; null: use key)
   const u32* idx[LT_MAXB];  // its NTT-domain automorphism index
   int klvl[LT_MAXB];        // level the key was made for
   int nb, s0, beta, K, level, L;

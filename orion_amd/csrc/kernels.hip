@@ -51,6 +51,11 @@
 #ifndef LT_GIANT_CH
 #define LT_GIANT_CH 0  // lt_giant digits per load chunk (0: 2 at IB >= 4, else 4)
 #endif
+// 1: lt_bsgs cuts the baby rotations into 30-bit pieces once, before the
+// integer giant loop (0: per giant)
+#ifndef LT_PRESPLIT
+#define LT_PRESPLIT 1
+#endif
 
 namespace {
 
@@ -78,7 +83,6 @@ enum EwOp : int {
   EW_COPY = 8,     // o = a
   EW_ADDSCALE = 9, // o = o + a * s_l
   EW_SPLIT24 = 10, // o = split24(a) on limbs below 2^48, split30(a) on limbs up to 2^60 (LT_INT30), else a
-  EW_SPLIT30 = 11, // o = split30(a) on limbs up to 2^60, else a (lt_bsgs's baby key copies)
                    // (lt_bsgs's split-MAC operand forms)
 };
 
@@ -127,7 +131,6 @@ __global__ void __launch_bounds__(256) ew_kernel(LimbSet o, LimbSet a, LimbSet b
           : (LT_INT30 && mc.bar_k <= 60) ? make_ulonglong2(split30(x.x), split30(x.y))
                                          : x;
       break;
-    case EW_SPLIT30: z = mc.bar_k <= 60 ? make_ulonglong2(split30(x.x), split30(x.y)) : x; break;
     case EW_ADDSCALE: {
       const ulonglong2 w = *po;
       z.x = add_mod(w.x, shoup_mul(x.x, sc.s[l], sc.ss[l], q), q);
@@ -384,45 +387,6 @@ __device__ __forceinline__ void gadget_at(const u64* __restrict__ dp, long long 
   }
 }
 
-// the same gadget product from a split30 copy of the key (moduli up to 2^60):
-// 30-bit piece products accumulated without carries (MacW, one
-// v_mad_u64_u32 each; the digit is cut once for both components), one
-// reduction per 8 digits
-__device__ __forceinline__ void gadget_at_w(const u64* __restrict__ dp, long long dstride, const u64* ownp,
-                                            int owndigit, const u64* __restrict__ keyw, int beta, int L, int K,
-                                            int klvl, int m, int N, int j, const ModConst& mc, u64& r0, u64& r1) {
-  r0 = r1 = 0;
-  const long long kstride = (long long)(klvl + 1 + K) * N;
-  const u64* kp = keyw + (long long)key_pos(m, L, klvl) * N + j;
-  MacW a0, a1;
-  macw_zero(a0), macw_zero(a1);
-  for (int i0 = 0; i0 < beta; i0 += 4) {
-    u64 d[4], k0[4], k1[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = i0 + u;
-      if (i < beta) {
-        d[u] = i == owndigit ? ownp[j] : dp[i * dstride + j];
-        k0[u] = kp[(2 * i + 0) * kstride];
-        k1[u] = kp[(2 * i + 1) * kstride];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (i0 + u < beta) {
-        const u64 ds = split30(d[u]);
-        macw_add(a0, (u32)ds, (u32)(ds >> 32), (u32)k0[u], (u32)(k0[u] >> 32));
-        macw_add(a1, (u32)ds, (u32)(ds >> 32), (u32)k1[u], (u32)(k1[u] >> 32));
-      }
-    }
-    if ((i0 & 4) || i0 + 4 >= beta) {  // 8 products accumulated, or the last chunk
-      r0 = add_mod(r0, macw_reduce8(a0, mc), mc.q);
-      r1 = add_mod(r1, macw_reduce8(a1, mc), mc.q);
-      macw_zero(a0), macw_zero(a1);
-    }
-  }
-}
-
 __device__ __forceinline__ void mac_add1(MacAcc& a, u64 x) {
   a.lo += x;
   a.c += (a.lo < x);
@@ -469,11 +433,10 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
       if (Bb.key[s] && !(LT_ABLATE & 2) && !((LT_ABLATE & 8) && mc.bar_k > 48)) {
         const int j = jx[s];
         u64 r0, r1;
-        if (Bb.keyw[s] && mc.bar_k <= 60)  // (block-uniform)
-          gadget_at_w(dp, D.comp_stride, c1p, owndigit, Bb.keyw[s], Bb.beta, Bb.L, Bb.K, Bb.klvl[s], m, N, j, mc, r0,
-                      r1);
-        else
-          gadget_at(dp, D.comp_stride, c1p, owndigit, Bb.key[s], Bb.beta, Bb.L, Bb.K, Bb.klvl[s], m, N, j, mc, r0, r1);
+        // (a split30 copy of the keys with carry-free MacW products measured
+        // 1848 -> 1947 us per lt_bsgs_kernel8 launch just for being compiled in,
+        // and no faster when used: profiles/r04h_lt_gadget_w_ab.txt)
+        gadget_at(dp, D.comp_stride, c1p, owndigit, Bb.key[s], Bb.beta, Bb.L, Bb.K, Bb.klvl[s], m, N, j, mc, r0, r1);
         if (isq) r0 = add_mod(r0, shoup_mul(c0p[j], pq, pqs, mc.q), mc.q);
         x0[s] = r0;
         x1[s] = r1;
@@ -538,8 +501,10 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
     // diagonal copies are stored split30, and the baby rotations are cut into
     // their pieces once here (the split30 word takes the same two VGPRs), not
     // per giant
+    if (LT_PRESPLIT) {
 #pragma unroll
-    for (int s = 0; s < MB; ++s) x0[s] = split30(x0[s]), x1[s] = split30(x1[s]);
+      for (int s = 0; s < MB; ++s) x0[s] = split30(x0[s]), x1[s] = split30(x1[s]);
+    }
     for (int g = g0; g < g1; ++g) {
       const unsigned long long mask = P->mask[g] >> Bb.s0;
       u64 r0 = 0, r1 = 0;
@@ -556,8 +521,13 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
       for (int s = 0; s < MB; ++s) {
         if (((mask >> s) & 1ull) && !(LT_ABLATE & 4)) {
           const u32 yb = (u32)pv[s], ya = (u32)(pv[s] >> 32);
-          macw_add(a0, (u32)x0[s], (u32)(x0[s] >> 32), yb, ya);
-          macw_add(a1, (u32)x1[s], (u32)(x1[s] >> 32), yb, ya);
+          if (LT_PRESPLIT) {
+            macw_add(a0, (u32)x0[s], (u32)(x0[s] >> 32), yb, ya);
+            macw_add(a1, (u32)x1[s], (u32)(x1[s] >> 32), yb, ya);
+          } else {
+            macw_add(a0, (u32)x0[s] & 0x3fffffffu, (u32)(x0[s] >> 30), yb, ya);
+            macw_add(a1, (u32)x1[s] & 0x3fffffffu, (u32)(x1[s] >> 30), yb, ya);
+          }
         }
         if ((s & 7) == 7) {
           r0 = add_mod(r0, macw_reduce8(a0, mc), mc.q);
@@ -773,7 +743,7 @@ int orion_launch_ew(int op, const LimbSet& o, const LimbSet& a, const LimbSet& b
 #define CASE(OPC) \
   case OPC: hipLaunchKernelGGL(ew_kernel<OPC>, g, blk, 0, st, o, a, b, sc, tb, N); break;
     CASE(EW_ADD) CASE(EW_SUB) CASE(EW_MUL) CASE(EW_MULADD) CASE(EW_NEG) CASE(EW_SCALE) CASE(EW_ADDC)
-    CASE(EW_SUBSCALE) CASE(EW_COPY) CASE(EW_ADDSCALE) CASE(EW_SPLIT24) CASE(EW_SPLIT30)
+    CASE(EW_SUBSCALE) CASE(EW_COPY) CASE(EW_ADDSCALE) CASE(EW_SPLIT24)
 #undef CASE
     default: return -1;
   }
