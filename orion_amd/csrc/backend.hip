@@ -27,7 +27,8 @@
 int orion_launch_ntt(int logN, const LimbSet& s, const DeviceTables* tb, bool inverse, hipStream_t st);
 int orion_launch_ntt_io(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st);
 int orion_launch_ntt2(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st);
-int orion_launch_ntt2s(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st);
+int orion_launch_ntt2s(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st,
+                       bool rows_only = false);
 int orion_ntt_init();
 int orion_launch_ew(int op, const LimbSet& o, const LimbSet& a, const LimbSet& b, const u64* s, const u64* ss,
                     const DeviceTables* tb, int N, hipStream_t st);
@@ -754,19 +755,62 @@ struct Context {
   // src_per_job: NTT_PRO_BEXT launches, the mean source limbs read per
   // limb-transform (their algorithmic bytes are (src_per_job + 1) 8 N, + 8 N
   // for a subtract-and-scale epilogue, in the ntt_bext category)
-  void ntt_io(NttIO io, bool inv, double src_per_job = 0) {
+  void prep_io(NttIO& io) {
     io.order = ntt_order;
     io.ci = ci ? 1 : 0;
     io.jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
-    const bool bx = io.pro == NTT_PRO_BEXT;
-    const double per = (bx ? (src_per_job + 1) * 8.0 * N : 16.0 * N) + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
-    const int cat = bx ? P_NTT_BEXT : inv ? P_NTT_INV : P_NTT_FWD;
     if (io.order == 2) {  // integer-path (>= 2^46) limbs are ~1.4x slower per transform: dispatch them first
       int k = 0;
       for (int pass = 0; pass < 2; ++pass)
         for (int l = 0; l < io.dst.nlimb; ++l)
           if ((host_tb.mc[io.dst.mod[l]].f64 != 0) == (pass == 1)) io.lord[k++] = (unsigned char)l;
     }
+  }
+  // 1: an INTT whose output feeds only the prologue of the forward NTT that
+  // follows (ModUp and ModDown sources, the rescale's last limb) runs its rows
+  // pass alone when both launches take the latency kernels (ntt2s.hip); the
+  // forward launch finishes the INTT's columns pass on its own column tile
+  // (ntt2s_ifwd_cols), so the INTT output never goes to HBM and its second
+  // launch disappears
+  int ntt_ifuse = getenv("ORION_NTT_IFUSE") ? atoi(getenv("ORION_NTT_IFUSE")) : 1;
+  bool on_ntt2s(int jobs, bool inv, int pro, int epi, bool inplace_sub) {
+    return (logN == 15 || logN == 16) && !ci && ntt2_chunk <= 0 && jobs <= ntt2s_below &&
+           two_pass(jobs, inv, pro, epi, inplace_sub);
+  }
+  // the INTT iio (load prologue, store epilogue) and then the forward fio whose
+  // BEXT / RESCALE prologue reads the INTT's output (fio.src = iio.dst)
+  void intt_then_fwd(NttIO iio, NttIO fio, double src_per_job = 0) {
+    const int ij = iio.dst.ncomp * iio.dst.nlimb * iio.dst.nbatch;
+    const int fj = fio.dst.ncomp * fio.dst.nlimb * fio.dst.nbatch;
+    bool same = iio.dst.p == fio.src.p && iio.dst.nlimb == fio.src.nlimb && iio.dst.ncomp == fio.src.ncomp &&
+                iio.dst.nbatch == fio.src.nbatch && iio.dst.comp_stride == fio.src.comp_stride &&
+                iio.dst.limb_stride == fio.src.limb_stride && iio.dst.batch_stride == fio.src.batch_stride;
+    for (int l = 0; same && l < iio.dst.nlimb; ++l)
+      same = iio.dst.pos[l] == fio.src.pos[l] && iio.dst.mod[l] == fio.src.mod[l];
+    const bool inplace_sub = fio.epi == NTT_EPI_SUBSCALE && fio.ex.p == fio.dst.p;
+    if (!ntt_ifuse || !same || iio.pro != NTT_PRO_LOAD || iio.epi != NTT_EPI_STORE ||
+        (fio.pro != NTT_PRO_BEXT && fio.pro != NTT_PRO_RESCALE) ||
+        !on_ntt2s(ij, true, NTT_PRO_LOAD, NTT_EPI_STORE, false) || !on_ntt2s(fj, false, fio.pro, fio.epi, inplace_sub)) {
+      ntt_io(iio, true);
+      ntt_io(fio, false, src_per_job);
+      return;
+    }
+    prep_io(iio);
+    iio.mid = iio.dst;  // the rows pass leaves its intermediate in the INTT's own output rows
+    {
+      Scope sc(this, P_NTT_INV, 16.0 * N * ij);
+      if (orion_launch_ntt2s(logN, iio, d_tb, true, stream, true)) throw std::runtime_error("NTT launch failed");
+      log_ntt(3, iio, true);
+    }
+    fio.ifuse = 1;
+    fio.imid = iio.dst;
+    ntt_io(fio, false, src_per_job);
+  }
+  void ntt_io(NttIO io, bool inv, double src_per_job = 0) {
+    prep_io(io);
+    const bool bx = io.pro == NTT_PRO_BEXT;
+    const double per = (bx ? (src_per_job + 1) * 8.0 * N : 16.0 * N) + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
+    const int cat = bx ? P_NTT_BEXT : inv ? P_NTT_INV : P_NTT_FWD;
     if (two_pass(io.jobs, inv, io.pro, io.epi, io.epi == NTT_EPI_SUBSCALE && io.ex.p == io.dst.p)) {
       Poly scratch;
       if (ntt2_chunk > 0 && io.jobs > 0) {  // chunks of jobs through one reused compact scratch
@@ -792,11 +836,13 @@ struct Context {
       }
       Scope sc(this, cat, per * io.jobs);
       const bool small = io.jobs <= ntt2s_below;
-      if ((small ? orion_launch_ntt2s : orion_launch_ntt2)(logN, io, d_tb, inv, stream))
+      if (io.ifuse && !small) throw std::runtime_error("NTT: a fused INTT columns pass needs the latency kernels");
+      if (small ? orion_launch_ntt2s(logN, io, d_tb, inv, stream) : orion_launch_ntt2(logN, io, d_tb, inv, stream))
         throw std::runtime_error("NTT launch failed");
       log_ntt(small ? 3 : 2, io, inv);
       return;
     }
+    if (io.ifuse) throw std::runtime_error("NTT: a fused INTT columns pass needs the latency kernels");
     if (ntt_stagger > 0) {
       io.stagger = io.jobs >= ntt_stagger_min * cus() ? ntt_stagger : 0;
     }
@@ -984,6 +1030,34 @@ struct Context {
     return r;
   }
 
+  // how a target's sum is formed (common.h BextTarget): every bound is checked
+  // with the actual moduli, so each column and the final value fit their words
+  // (the terms: y_i < s_i times qh_i < t, and v <= ns times nS < t)
+  // 0: BEXT_WT / BEXT_NT off (timing switch)
+  int bext_modes = getenv("ORION_BEXT_MODES") ? atoi(getenv("ORION_BEXT_MODES")) : 1;
+  int bext_mode(const std::vector<int>& src, int ns, u64 t) const {
+    const u128 M30 = (1u << 30) - 1, T1 = t - 1;
+    u128 ssum = ns;  // sum (s_i - 1) + ns
+    bool src32 = true, src62 = true;
+    for (int i = 0; i < ns; ++i) {
+      const u64 si = mods[src[i]];
+      ssum += si - 1;
+      src32 = src32 && si < (1ull << 32);
+      src62 = src62 && si < (1ull << 62);
+    }
+    const u128 two64 = (u128)1 << 64;
+    if (src32 && t < (1ull << 32) && (ssum + 1) * t < ((u128)1 << 63)) return BEXT_NARROW;
+    if (!bext_modes) return BEXT_LAZY;
+    if (ns >= 3 && src32 && t >= (1ull << 32) && t < (1ull << 61) && ssum * M30 < two64 &&
+        ssum * T1 < (u128)4 * t * t)
+      return BEXT_WT;
+    // (columns: ns + 1 terms of a 30-bit piece times t - 1; the whole sum below
+    // 2^96, so the folded high word is below 2^32)
+    if (ns >= 4 && src62 && t < (1ull << 31) && (u128)(ns + 1) * M30 * T1 < two64 && ssum * T1 < ((u128)1 << 96))
+      return BEXT_NT;
+    return BEXT_LAZY;
+  }
+
   // centered: a gadget digit (Lattigo DecomposeAndSplit extends a one-prime
   // digit from its centered representative; ModDown's ModUpExact does not)
   BasisExtTable* make_betab(const std::vector<int>& src, const std::vector<int>& dst, bool centered = false) {
@@ -998,6 +1072,7 @@ struct Context {
     for (int i = 0; i < T.ns; ++i) {
       const u64 si = mods[src[i]];
       T.src_mod[i] = src[i];
+      T.sq[i] = si;
       T.qhatinv[i] = hm_invmod(prod_mod(src, i, si), si);
       T.qhatinv_s[i] = hm_shoup(T.qhatinv[i], si);
       T.qf[i] = (double)si;
@@ -1005,24 +1080,29 @@ struct Context {
     }
     for (int t = 0; t < T.nt; ++t) {
       const u64 tm = mods[dst[t]];
+      BextTarget& R = T.tgt[t];
       T.dst_mod[t] = dst[t];
-      T.S_t[t] = prod_mod(src, -1, tm);
+      R.q = tm;
+      const u64 S = prod_mod(src, -1, tm);
       for (int i = 0; i < T.ns; ++i) {
-        T.qhat_t[t][i] = prod_mod(src, i, tm);
-        T.qhat_ts[t][i] = hm_shoup(T.qhat_t[t][i], tm);
+        R.qh[i] = prod_mod(src, i, tm);
+        R.qhs[i] = hm_shoup(R.qh[i], tm);
       }
-      for (int v = 0; v <= T.ns; ++v) {
-        const u64 vs = hm_mulmod((u64)v, T.S_t[t], tm);
-        T.vS_t[t][v] = vs ? tm - vs : 0;
-      }
-      u128 bound = 1;  // (sum s_i + 1) t
-      bool narrow = tm < (1ull << 32);
-      for (int i = 0; i < T.ns; ++i) {
-        narrow = narrow && mods[src[i]] < (1ull << 32);
-        bound += mods[src[i]];
-      }
-      T.narrow[t] = narrow && bound * tm < ((u128)1 << 63) ? 1 : 0;
-      T.tinv[t] = 1.0 / (double)tm;
+      R.nS = S ? tm - S : 0;
+      R.nSs = hm_shoup(R.nS, tm);
+      for (int v = 0; v < 3; ++v) R.vS[v] = hm_mulmod((u64)v, R.nS, tm);
+      R.qd = (double)tm;
+      R.tinv = 1.0 / (double)tm;
+      R.tinv32 = std::ldexp(R.tinv, 32);
+      R.k = 64 - __builtin_clzll(tm);
+      R.mu2 = R.k <= 61 ? (u64)(((u128)1 << (2 * R.k + 2)) / tm) : 0;
+      R.c64 = (u64)(((u128)1 << 64) % tm);
+      auto pieces = [](u64 x, u32& a, u32& b, u32& c) {
+        a = (u32)(x & 0x3fffffffu), b = (u32)((x >> 30) & 0x3fffffffu), c = (u32)(x >> 60);
+      };
+      for (int i = 0; i < T.ns; ++i) pieces(R.qh[i], R.h0[i], R.h1[i], R.h2[i]);
+      pieces(R.nS, R.n0, R.n1, R.n2);
+      R.mode = T.centered ? BEXT_LAZY : bext_mode(src, T.ns, tm);
     }
     BasisExtTable* d;
     HIPCHK(hipMalloc(&d, sizeof(T)));
@@ -1295,7 +1375,7 @@ struct Context {
     const int beta = (level + 1 + K - 1) / K;
     const int nqp = level + 1 + K;
     Poly cinv = alloc(nc, level + 1, B);
-    ntt_io(nio(lsq(cinv, 0, nc, level), c), true);  // out-of-place INTT
+    const NttIO iio = nio(lsq(cinv, 0, nc, level), c);  // out-of-place INTT
     Poly D = alloc(nc * beta, nqp, B);
     if (nc * B * (nqp - K) < modup_merge && nqp <= ORION_MAXLIMB) {
       // small decomposition: every digit's ModUp in one launch (own limbs not
@@ -1327,9 +1407,10 @@ struct Context {
           io.bx_t[l] = (unsigned char)(j < lo ? j : j - ns);
           srcs += ns;
         }
-        ntt_io(io, false, srcs / (double)tpos.size());
+        intt_then_fwd(iio, io, srcs / (double)tpos.size());
         return D;
       }
+      ntt_io(iio, true);
       {
         Scope sc(this, P_BEXT, 8.0 * N * B * nc * (level + 1 + beta * nqp - (level + 1)));
         if (orion_launch_modup_all(Dl, in, modup_tabs(level), beta, K, nqp, d_tb, N, stream))
@@ -1344,6 +1425,7 @@ struct Context {
       }
       return D;
     }
+    ntt_io(iio, true);
     const long long dstride = (long long)beta * D.comp_stride();
     for (int i = 0; i < beta; ++i) {
       const int lo = i * K, hi = std::min((i + 1) * K, level + 1);
@@ -1420,7 +1502,6 @@ struct Context {
   void moddown(const LimbSet& x, int level, const LimbSet& out) {
     const int nc = x.ncomp, B = x.nbatch;
     LimbSet xp = limbs(x, level + 1, K);
-    ntt(xp, true);
     if (fuse_bext(nc * B * (level + 1), K, NTT_EPI_SUBSCALE)) {
       // the extension of the P limbs formed in the prologue of the NTT whose
       // epilogue is (x_Q - .) * P^-1: no basis_ext launch, no extended limbs in HBM
@@ -1436,9 +1517,10 @@ struct Context {
         io.s[j] = hm_invmod(pq[j], mods[j]);
         io.ss[j] = hm_shoup(io.s[j], mods[j]);
       }
-      ntt_io(io, false, K);
+      intt_then_fwd(nio(xp, xp), io, K);
       return;
     }
+    ntt(xp, true);
     Poly ext = alloc(nc, level + 1, B);
     LimbSet le = lsq(ext, 0, nc, level);
     {
@@ -1501,7 +1583,6 @@ struct Context {
     if (l < 1) throw std::runtime_error("cannot rescale a level-0 ciphertext");
     const int B = ct.poly.B;
     LimbSet last = ls(ct.poly, 0, 2, {l}, {l});
-    ntt(last, true);
     // (DivRoundByLastModulusNTT) prep of every other limb, NTT and (c - .) * q_l^-1, fused
     LimbSet cq = lsq(ct.poly, 0, 2, l - 1);
     NttIO io = nio(cq, last);
@@ -1514,7 +1595,7 @@ struct Context {
       io.ss[j] = hm_shoup(io.s[j], mods[j]);
     }
     (void)B;
-    ntt_io(io, false);
+    intt_then_fwd(nio(last, last), io);  // INTT of the last limb, then the prep + NTT + tail
     ct.level = l - 1;
     ct.scale /= (long double)mods[l];
   }

@@ -176,6 +176,35 @@ __host__ __device__ static inline void mac128(Acc128& a, u64 x, u64 y) {
 // ---------------------------------------------------------------------------
 #define ORION_MAXSRC 8
 #define ORION_MAXBABY 64  // baby steps fused into one BSGS giant-step MAC launch
+// the constants of one target t, in one record so that a kernel reads them
+// from a single wave-uniform base (s_load_dwordx* at fixed offsets).  The
+// target sum sum_i y_i qh_i + v nS (then mod t) is formed in one of four ways,
+// chosen per target on the host from the moduli's sizes (BasisExtTable.ns >=
+// 3 for the last two):
+//   BEXT_LAZY:   Shoup products, the running sum kept in [0, 2t)
+//   BEXT_NARROW: sources and t below 2^32 and (sum s_i + ns) t < 2^63: the whole
+//                sum in one u64 of 32x32-bit products, one float64 reduction
+//   BEXT_WT:     sources below 2^32, t wide: qh cut into 30-bit pieces on the
+//                host, three carry-free u64 columns of 32x32-bit products, one
+//                Barrett reduction of the 128-bit sum (x < 4 t^2)
+//   BEXT_NT:     t below 2^31, sources wide: y cut into 30-bit pieces, three
+//                carry-free columns, folded to 128 bits and reduced in float64
+enum { BEXT_LAZY = 0, BEXT_NARROW = 1, BEXT_WT = 2, BEXT_NT = 3 };
+struct BextTarget {
+  u64 q;                // t
+  double tinv, tinv32;  // RN(1 / t) and 2^32 times it (BEXT_NARROW, BEXT_NT)
+  double qd;            // (double)t
+  int mode, k;          // k = bitlen(t) (BEXT_WT's Barrett)
+  u64 mu2;              // floor(2^(2k+2) / t) (BEXT_WT)
+  u64 c64;              // 2^64 mod t (BEXT_NT)
+  u64 nS, nSs;          // (t - S mod t) mod t (v * nS = Lattigo's vtimesqmodp[v]) and its Shoup companion
+  u64 vS[3];            // v nS mod t for v = 0, 1, 2 (BEXT_LAZY with at most 2 sources: selected, not multiplied)
+  u32 n0, n1, n2;       // nS in 30-bit pieces (BEXT_WT)
+  u32 pad;
+  u64 qh[ORION_MAXSRC];  // (S/s_i) mod t
+  u64 qhs[ORION_MAXSRC]; // its Shoup companion
+  u32 h0[ORION_MAXSRC], h1[ORION_MAXSRC], h2[ORION_MAXSRC];  // qh in 30-bit pieces (BEXT_WT)
+};
 struct BasisExtTable {
   int ns, nt;
   int centered;
@@ -183,17 +212,11 @@ struct BasisExtTable {
   u64 chalf;  // s_0 >> 1 (centered tables)
   int src_mod[ORION_MAXSRC];
   int dst_mod[ORION_MAXLIMB];
+  u64 sq[ORION_MAXSRC];  // s_i
   u64 qhatinv[ORION_MAXSRC], qhatinv_s[ORION_MAXSRC];
   double qinv_f[ORION_MAXSRC];  // RN(1 / (double)s_i)
   double qf[ORION_MAXSRC];      // (double)s_i (rounded, as Lattigo's float64(Q[i]))
-  u64 qhat_t[ORION_MAXLIMB][ORION_MAXSRC];    // (S/s_i) mod t
-  u64 qhat_ts[ORION_MAXLIMB][ORION_MAXSRC];   // its Shoup companion
-  u64 S_t[ORION_MAXLIMB];
-  u64 vS_t[ORION_MAXLIMB][ORION_MAXSRC + 1];  // (t - v*S mod t) mod t, v = 0..ns (Lattigo vtimesqmodp)
-  // narrow targets: sources and t below 2^32 and (sum s_i + 1) t < 2^63, so the
-  // target sum is exact in one u64 of 32x32-bit products (bext_target_sel)
-  int narrow[ORION_MAXLIMB];
-  double tinv[ORION_MAXLIMB];  // 1 / t
+  BextTarget tgt[ORION_MAXLIMB];
 };
 
 // ---------------------------------------------------------------------------
@@ -337,8 +360,7 @@ __device__ __forceinline__ u64 mac_reduce(const MacAcc& a, const ModConst& m) {
 // y[] and v are shared by every target.
 // ---------------------------------------------------------------------------
 template <int MS = ORION_MAXSRC>  // MS >= ns: the register arrays' size
-__device__ __forceinline__ u64 bext_prep(const BasisExtTable* __restrict__ T, const DeviceTables* __restrict__ tb,
-                                         const u64* x, u64* y) {
+__device__ __forceinline__ u64 bext_prep(const BasisExtTable* __restrict__ T, const u64* x, u64* y) {
   if (T->centered) {  // one source, qhatinv = 1 (wave-uniform)
     y[0] = x[0];
     return x[0] >= T->chalf ? 1 : 0;
@@ -348,8 +370,7 @@ __device__ __forceinline__ u64 bext_prep(const BasisExtTable* __restrict__ T, co
 #pragma unroll
   for (int i = 0; i < MS; ++i) {
     if (i >= ns) break;
-    const u64 si = tb->mc[T->src_mod[i]].q;
-    y[i] = shoup_mul(x[i], T->qhatinv[i], T->qhatinv_s[i], si);
+    y[i] = shoup_mul(x[i], T->qhatinv[i], T->qhatinv_s[i], T->sq[i]);
     const double yd = (double)y[i], rc = T->qinv_f[i];
     const double q0 = __dmul_rn(yd, rc);
     const double r = __builtin_fma(-q0, T->qf[i], yd);
@@ -359,42 +380,163 @@ __device__ __forceinline__ u64 bext_prep(const BasisExtTable* __restrict__ T, co
 }
 // the target side of the exact basis extension: sum_i y_i (S/s_i mod t) -
 // v S mod t (basis_ext_kernel, modup_all_kernel and the NTT prologue
-// NTT_PRO_BEXT); the per-target constants are wave-uniform (SGPR) and v*S mod
-// t is selected from the ns+1 precomputed values with v_cndmask instead of a
-// per-lane table lookup
+// NTT_PRO_BEXT).  The per-target constants are wave-uniform (SGPR); the
+// correction -v S is one more term of the sum, v times nS = -S mod t (v <= ns
+// is small), except on the lazy path with at most 2 sources, where it is one
+// of 3 precomputed values
+__device__ __forceinline__ u64 bext_narrow_red(u64 acc, const BextTarget* __restrict__ R) {
+  // acc mod t for t < 2^32, any acc < 2^64, in float64: k = rint(acc / t)
+  // from the two words (|acc/t - k| <= 1/2 + 2^-18), then acc - k t exactly as
+  // fma(-k, t, hi 2^32) + lo (every intermediate an integer below 2^53), in
+  // [-t/2 - 1, t/2 + 1], and one correction into [0, t).  (The high word goes
+  // through an opaque register: converting (u32)(acc >> 32) directly left an
+  // add of 0.0 * 2^32 behind.)
+  u32 hw = (u32)(acc >> 32);
+  asm volatile("" : "+v"(hw));
+  const double ah = (double)hw, al = (double)(u32)acc;
+  const double k = __builtin_rint(__builtin_fma(ah, R->tinv32, al * R->tinv));
+  double r = __builtin_fma(-k, R->qd, ah * 0x1p32) + al;
+  r = r < 0.0 ? r + R->qd : r;
+  return (u64)(u32)r;
+}
+// hi 2^60 + mid 2^30 + lo as a 128-bit H:L
+__device__ __forceinline__ void bext_fold(u64 lo, u64 mid, u64 hi, u64& H, u64& L) {
+  const u64 ml = mid << 30, hl = hi << 60;
+  const u64 L1 = lo + ml;
+  L = L1 + hl;
+  H = (mid >> 34) + (hi >> 4) + (L1 < ml) + (L < hl);
+}
+// BEXT_WT: y_i < 2^32, qh_i = h2 2^60 + h1 2^30 + h0 (host pieces)
 template <int MS>
-__device__ __forceinline__ u64 bext_target_sel(const BasisExtTable* __restrict__ T, int t, int ns, u64 q,
-                                               const u64* y, u64 v) {
-  u64 acc = T->vS_t[t][0];
-#pragma unroll
-  for (int j = 1; j <= MS; ++j) {
-    if (j > ns) break;
-    acc = v == (u64)j ? T->vS_t[t][j] : acc;
-  }
-  if (T->narrow[t]) {  // wave-uniform: sources and target < 2^32 (ResNet's 30-bit chains)
-    // the whole sum in one u64: one 32x32 -> 64 multiply-add per source,
-    // then a single reduction with a float64 quotient (off by at most one)
-#pragma unroll
-    for (int i = 0; i < MS; ++i) {
-      if (i >= ns) break;
-      acc += (u64)(u32)y[i] * (u32)T->qhat_t[t][i];
-    }
-    const u64 k = (u64)((double)acc * T->tinv[t]);
-    long long r = (long long)(acc - k * q);
-    r = r < 0 ? r + (long long)q : r;
-    r = r >= (long long)q ? r - (long long)q : r;
-    return (u64)r;
-  }
-  // lazy: each Shoup product is in [0, 2q) and the running sum is kept in
-  // [0, 2q) by one conditional subtraction (4q < 2^63 for q < 2^61)
-  const u64 q2 = q << 1, nq = 0 - q;
+__device__ __forceinline__ u64 bext_wt(const BextTarget* __restrict__ R, int ns, const u64* y, u64 v) {
+  const u32 vv = (u32)v;
+  u64 lo = (u64)vv * R->n0, mid = (u64)vv * R->n1, hi = (u64)vv * R->n2;
 #pragma unroll
   for (int i = 0; i < MS; ++i) {
     if (i >= ns) break;
-    acc += shoup_lazy_nq(y[i], T->qhat_t[t][i], T->qhat_ts[t][i], nq);
+    const u32 yy = (u32)y[i];
+    lo += (u64)yy * R->h0[i];
+    mid += (u64)yy * R->h1[i];
+    hi += (u64)yy * R->h2[i];
+  }
+  u64 H, L;
+  bext_fold(lo, mid, hi, H, L);
+  // Barrett of x < 4 t^2 (barrett_4q2 with the record's constants)
+  const int k = R->k;
+  const u64 q = R->q;
+  const u64 t1 = (L >> (k - 1)) | (H << (65 - k));
+  const u64 ph = mulhi64(t1, R->mu2), pl = t1 * R->mu2;
+  const u64 t2 = (k < 61 ? pl >> (k + 3) : 0) | (ph << (61 - k));
+  u64 r = L - t2 * q;
+  r = r >= q ? r - q : r;
+  return r >= q ? r - q : r;
+}
+// BEXT_NT: t < 2^31, y_i = y2 2^60 + y1 2^30 + y0 cut here
+template <int MS>
+__device__ __forceinline__ u64 bext_nt(const BextTarget* __restrict__ R, int ns, const u64* y, u64 v) {
+  u64 lo = (u64)(u32)v * (u32)R->nS, mid = 0, hi = 0;
+#pragma unroll
+  for (int i = 0; i < MS; ++i) {
+    if (i >= ns) break;
+    const u32 h = (u32)R->qh[i];
+    lo += (u64)((u32)y[i] & 0x3fffffffu) * h;
+    mid += (u64)((u32)(y[i] >> 30) & 0x3fffffffu) * h;
+    hi += (u64)(u32)(y[i] >> 60) * h;
+  }
+  u64 H, L;
+  bext_fold(lo, mid, hi, H, L);
+  // x = H 2^64 + L, H < 2^32: (H (2^64 mod t) + (L mod t)) < 2^63, reduced again
+  return bext_narrow_red(H * R->c64 + bext_narrow_red(L, R), R);
+}
+template <int MS>
+__device__ __forceinline__ u64 bext_target_sel(const BextTarget* __restrict__ R, int ns, const u64* y, u64 v) {
+  const int mode = R->mode;  // wave-uniform
+  if (mode == BEXT_NARROW) {  // sources and target < 2^32 (ResNet's 30-bit chains)
+    // the whole sum in one u64: one 32x32 -> 64 multiply-add per term
+    u64 acc = (u64)(u32)v * (u32)R->nS;
+#pragma unroll
+    for (int i = 0; i < MS; ++i) {
+      if (i >= ns) break;
+      acc += (u64)(u32)y[i] * (u32)R->qh[i];
+    }
+    return bext_narrow_red(acc, R);
+  }
+  if constexpr (MS > 2) {
+    if (mode == BEXT_WT) return bext_wt<MS>(R, ns, y, v);
+    if (mode == BEXT_NT) return bext_nt<MS>(R, ns, y, v);
+  }
+  // lazy: each Shoup product is in [0, 2q) and the running sum is kept in
+  // [0, 2q) by one conditional subtraction (4q < 2^63 for q < 2^61)
+  const u64 q = R->q, q2 = q << 1, nq = 0 - q;
+  u64 acc;
+  if constexpr (MS <= 2) {
+    acc = R->vS[0];
+    acc = v == 1 ? R->vS[1] : acc;
+    acc = v == 2 ? R->vS[2] : acc;
+  } else {
+    acc = shoup_lazy_nq((u32)v, R->nS, R->nSs, nq);  // (v <= ns: the high words fold away)
+  }
+#pragma unroll
+  for (int i = 0; i < MS; ++i) {
+    if (i >= ns) break;
+    acc += shoup_lazy_nq(y[i], R->qh[i], R->qhs[i], nq);
     acc = acc >= q2 ? acc - q2 : acc;
   }
   return acc >= q ? acc - q : acc;
+}
+// the same for two coefficients at once (basis_ext_kernel, modup_all_kernel):
+// one pass over the target's constants and one branch for both
+template <int MS>
+__device__ __forceinline__ void bext_target2(const BextTarget* __restrict__ R, int ns, const u64* y0, u64 v0,
+                                             const u64* y1, u64 v1, u64& o0, u64& o1) {
+  const int mode = R->mode;
+  if (mode == BEXT_NARROW) {
+    const u32 s = (u32)R->nS;
+    u64 a0 = (u64)(u32)v0 * s, a1 = (u64)(u32)v1 * s;
+#pragma unroll
+    for (int i = 0; i < MS; ++i) {
+      if (i >= ns) break;
+      const u32 h = (u32)R->qh[i];
+      a0 += (u64)(u32)y0[i] * h;
+      a1 += (u64)(u32)y1[i] * h;
+    }
+    o0 = bext_narrow_red(a0, R);
+    o1 = bext_narrow_red(a1, R);
+    return;
+  }
+  if constexpr (MS > 2) {
+    if (mode == BEXT_WT) {
+      o0 = bext_wt<MS>(R, ns, y0, v0);
+      o1 = bext_wt<MS>(R, ns, y1, v1);
+      return;
+    }
+    if (mode == BEXT_NT) {
+      o0 = bext_nt<MS>(R, ns, y0, v0);
+      o1 = bext_nt<MS>(R, ns, y1, v1);
+      return;
+    }
+  }
+  const u64 q = R->q, q2 = q << 1, nq = 0 - q;
+  u64 a0, a1;
+  if constexpr (MS <= 2) {
+    const u64 s1 = R->vS[1], s2 = R->vS[2];
+    a0 = v0 == 1 ? s1 : v0 == 2 ? s2 : R->vS[0];
+    a1 = v1 == 1 ? s1 : v1 == 2 ? s2 : R->vS[0];
+  } else {
+    a0 = shoup_lazy_nq((u32)v0, R->nS, R->nSs, nq);
+    a1 = shoup_lazy_nq((u32)v1, R->nS, R->nSs, nq);
+  }
+#pragma unroll
+  for (int i = 0; i < MS; ++i) {
+    if (i >= ns) break;
+    const u64 h = R->qh[i], hs = R->qhs[i];
+    a0 += shoup_lazy_nq(y0[i], h, hs, nq);
+    a1 += shoup_lazy_nq(y1[i], h, hs, nq);
+    a0 = a0 >= q2 ? a0 - q2 : a0;
+    a1 = a1 >= q2 ? a1 - q2 : a1;
+  }
+  o0 = a0 >= q ? a0 - q : a0;
+  o1 = a1 >= q ? a1 - q : a1;
 }
 // ---------------------------------------------------------------------------
 // NTT launch descriptor: transform + fused producer (prologue) / consumer
@@ -432,6 +574,12 @@ struct NttIO {
   // target index, per table its first source limb in src
   const BasisExtTable* bx;
   unsigned char bx_tab[ORION_MAXLIMB], bx_t[ORION_MAXLIMB], bx_s0[ORION_MAXLIMB];
+  // ifuse (ntt2s.hip, forward launches with the BEXT / RESCALE prologue): the
+  // source limbs of src have been through the inverse's rows pass only, whose
+  // intermediate sits in imid (src's geometry); the forward columns pass runs
+  // their inverse columns pass itself, in registers and LDS
+  int ifuse;
+  LimbSet imid;
 };
 
 // ---------------------------------------------------------------------------

@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(256) tensor_kernel(LimbSet d, LimbSet a, LimbS
 // coefficients per thread (16-B accesses).
 template <int MS>
 __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in, const BasisExtTable* __restrict__ T,
-                                                        const DeviceTables* __restrict__ tb, int N, int tchunk) {
+                                                        int N, int tchunk) {
   const int row = blockIdx.y;  // (comp, image)
   const int bi = row % out.nbatch;
   const int c = row / out.nbatch;
@@ -186,14 +186,12 @@ __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in,
     x0[i] = v.x;
     x1[i] = v.y;
   }
-  const u64 v0 = bext_prep<MS>(T, tb, x0, y0), v1 = bext_prep<MS>(T, tb, x1, y1);
+  const u64 v0 = bext_prep<MS>(T, x0, y0), v1 = bext_prep<MS>(T, x1, y1);
   const int tend = min(nt, (int)(blockIdx.z + 1) * tchunk);
   for (int t = blockIdx.z * tchunk; t < tend; ++t) {
-    const u64 q = tb->mc[T->dst_mod[t]].q;
-    ulonglong2 o;
-    o.x = bext_target_sel<MS>(T, t, ns, q, y0, v0);
-    o.y = bext_target_sel<MS>(T, t, ns, q, y1, v1);
-    *(ulonglong2*)(out.p + row_off(out, c, t, bi) + n) = o;
+    u64 o0, o1;
+    bext_target2<MS>(T->tgt + t, ns, y0, v0, y1, v1, o0, o1);
+    *(ulonglong2*)(out.p + row_off(out, c, t, bi) + n) = make_ulonglong2(o0, o1);
   }
 }
 
@@ -203,11 +201,10 @@ __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in,
 // nqp QP positions.  Digit i's own positions [iK, iK + ns) are not written
 // (consumers read the own limbs from the NTT-domain input, and the NTT that
 // follows covers only the target positions).
-// D: comps c*beta + i, limb pos j at D.pos[j]; Ts[i] = digit i's table.
+// D: comps c*beta + i, limb j at position j; Ts[i] = digit i's table.
 template <int MS>
 __global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, const BasisExtTable* __restrict__ Ts,
-                                                        int beta, int K, int nqp, const DeviceTables* __restrict__ tb,
-                                                        int N, int tchunk) {
+                                                        int beta, int K, int nqp, int N, int tchunk) {
   const int row = blockIdx.y;
   const int bi = row % D.nbatch;
   const int r = row / D.nbatch;
@@ -225,19 +222,26 @@ __global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, c
     x0[s] = v.x;
     x1[s] = v.y;
   }
-  const u64 v0 = bext_prep<MS>(T, tb, x0, y0), v1 = bext_prep<MS>(T, tb, x1, y1);
-  const int jend = min(nqp, (int)(blockIdx.z + 1) * tchunk);
-  for (int j = blockIdx.z * tchunk; j < jend; ++j) {
-    // own limbs are not written: every consumer reads them from the NTT-domain
-    // input of the decomposition (j is uniform: no divergence)
-    if (j >= lo && j < lo + ns) continue;
-    const int t = j < lo ? j : j - ns;
-    const u64 q = tb->mc[T->dst_mod[t]].q;
-    ulonglong2 o;
-    o.x = bext_target_sel<MS>(T, t, ns, q, y0, v0);
-    o.y = bext_target_sel<MS>(T, t, ns, q, y1, v1);
-    *(ulonglong2*)(D.p + row_off(D, c * beta + i, j, bi) + n) = o;
-  }
+  const u64 v0 = bext_prep<MS>(T, x0, y0), v1 = bext_prep<MS>(T, x1, y1);
+  // D's positions are the identity (checked at launch): limb j of the row is
+  // limb_stride past limb j - 1, so the loop carries one pointer and one
+  // target record instead of re-deriving both from (j, pos[j], dst_mod[t])
+  // own limbs [lo, lo + ns) are not written: every consumer reads them from
+  // the NTT-domain input of the decomposition; positions below them are
+  // targets 0.., positions above them targets lo..
+  const int j0 = blockIdx.z * tchunk, jend = min(nqp, j0 + tchunk);
+  u64* const dst = D.p + row_off(D, c * beta + i, 0, bi) + n;
+  auto targets = [&](int ja, int jb, int toff) {
+    u64* op = dst + (long long)ja * D.limb_stride;
+    const BextTarget* __restrict__ R = T->tgt + (ja - toff);
+    for (int j = ja; j < jb; ++j, ++R, op += D.limb_stride) {
+      u64 o0, o1;
+      bext_target2<MS>(R, ns, y0, v0, y1, v1, o0, o1);
+      *(ulonglong2*)op = make_ulonglong2(o0, o1);
+    }
+  };
+  targets(j0, min(jend, lo), 0);
+  targets(max(j0, lo + ns), jend, ns);
 }
 
 // Gadget-product MAC over G groups (one evaluation key per group):
@@ -767,11 +771,11 @@ int orion_launch_basis_ext(const LimbSet& out, const LimbSet& in, const BasisExt
   const int tc = (nt + g.z - 1) / g.z;
   // the kernel's source arrays sized for in.nlimb (= the table's ns)
   if (in.nlimb <= 2)
-    hipLaunchKernelGGL(basis_ext_kernel<2>, g, dim3(256), 0, st, out, in, T, tb, N, tc);
+    hipLaunchKernelGGL(basis_ext_kernel<2>, g, dim3(256), 0, st, out, in, T, N, tc);
   else if (in.nlimb <= 4)
-    hipLaunchKernelGGL(basis_ext_kernel<4>, g, dim3(256), 0, st, out, in, T, tb, N, tc);
+    hipLaunchKernelGGL(basis_ext_kernel<4>, g, dim3(256), 0, st, out, in, T, N, tc);
   else if (in.nlimb <= ORION_MAXSRC)
-    hipLaunchKernelGGL(basis_ext_kernel<ORION_MAXSRC>, g, dim3(256), 0, st, out, in, T, tb, N, tc);
+    hipLaunchKernelGGL(basis_ext_kernel<ORION_MAXSRC>, g, dim3(256), 0, st, out, in, T, N, tc);
   else
     return -1;
   return 0;
@@ -780,16 +784,18 @@ int orion_launch_basis_ext(const LimbSet& out, const LimbSet& in, const BasisExt
 int orion_launch_modup_all(const LimbSet& D, const LimbSet& in, const BasisExtTable* Ts, int beta, int K,
                            int nqp, const DeviceTables* tb, int N, hipStream_t st) {
   if (beta < 1 || nqp > ORION_MAXLIMB || D.ncomp != in.ncomp * beta) return -1;
+  for (int j = 0; j < nqp; ++j)
+    if (D.pos[j] != j) return -1;  // the kernel walks the limbs with one pointer
   const int rows = D.ncomp * D.nbatch;
   dim3 g = ew_grid(N, rows);
   g.z = target_chunks(g, nqp);
   const int tc = (nqp + g.z - 1) / g.z;
   if (K <= 2)  // every digit has at most K sources
-    hipLaunchKernelGGL(modup_all_kernel<2>, g, dim3(256), 0, st, D, in, Ts, beta, K, nqp, tb, N, tc);
+    hipLaunchKernelGGL(modup_all_kernel<2>, g, dim3(256), 0, st, D, in, Ts, beta, K, nqp, N, tc);
   else if (K <= 4)
-    hipLaunchKernelGGL(modup_all_kernel<4>, g, dim3(256), 0, st, D, in, Ts, beta, K, nqp, tb, N, tc);
+    hipLaunchKernelGGL(modup_all_kernel<4>, g, dim3(256), 0, st, D, in, Ts, beta, K, nqp, N, tc);
   else if (K <= ORION_MAXSRC)
-    hipLaunchKernelGGL(modup_all_kernel<ORION_MAXSRC>, g, dim3(256), 0, st, D, in, Ts, beta, K, nqp, tb, N, tc);
+    hipLaunchKernelGGL(modup_all_kernel<ORION_MAXSRC>, g, dim3(256), 0, st, D, in, Ts, beta, K, nqp, N, tc);
   else
     return -1;
   return 0;

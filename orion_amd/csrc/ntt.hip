@@ -59,8 +59,8 @@ __device__ __forceinline__ u64 ci_fold(u64 x, u64 y, const ModConst& mc) {
 // ahead (the limb's 64 VGPRs leave no room for them)
 template <int G, class A, int B0>
 __device__ __forceinline__ void bext_rows(typename A::T (&a)[32], const u64 (&xa)[4], const u64 (&xb)[4], const A& ar,
-                                          const BasisExtTable* __restrict__ T, const DeviceTables* __restrict__ tb,
-                                          int ti, int ns, u64 q, __amdgpu_buffer_rsrc_t r0, __amdgpu_buffer_rsrc_t r1,
+                                          const BasisExtTable* __restrict__ T, int ti, int ns,
+                                          __amdgpu_buffer_rsrc_t r0, __amdgpu_buffer_rsrc_t r1,
                                           int t) {
   if constexpr (G < 8) {
     u64 na[4], nb[4];
@@ -74,11 +74,11 @@ __device__ __forceinline__ void bext_rows(typename A::T (&a)[32], const u64 (&xa
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       u64 x[2] = {xa[k], xb[k]}, y[2];
-      const u64 v = bext_prep<2>(T, tb, x, y);
-      a[4 * G + k] = ar.from_u64(bext_target_sel<2>(T, ti, ns, q, y, v));
+      const u64 v = bext_prep<2>(T, x, y);
+      a[4 * G + k] = ar.from_u64(bext_target_sel<2>(T->tgt + ti, ns, y, v));
     }
     NTT_FENCE();
-    if constexpr (G < 7) bext_rows<G + 1, A, B0>(a, na, nb, ar, T, tb, ti, ns, q, r0, r1, t);
+    if constexpr (G < 7) bext_rows<G + 1, A, B0>(a, na, nb, ar, T, ti, ns, r0, r1, t);
   }
 }
 
@@ -122,7 +122,7 @@ __device__ __forceinline__ void ntt_fwd_body(const NttIO& io, int c, int l, int 
       xa[k] = buf_ld(r0, t * 8, (k << B0) * 8);
       xb[k] = ns > 1 ? buf_ld(r1, t * 8, (k << B0) * 8) : 0;
     }
-    bext_rows<0, A, B0>(a, xa, xb, ar, T, tb, ti, ns, mc.q, r0, r1, t);
+    bext_rows<0, A, B0>(a, xa, xb, ar, T, ti, ns, r0, r1, t);
   } else {  // NTT_PRO_RESCALE (DivRoundByLastModulusNTT), fused with the NTT of every other limb
     const u64* sp = row_ptr(io.src, c, 0, b);
     const u64 qL = tb->mc[io.modL].q, h = qL >> 1;

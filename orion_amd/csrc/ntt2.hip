@@ -87,8 +87,8 @@ __device__ __forceinline__ void fwd_cols(const NttIO& io, int job, int c, int l,
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       u64 x[2] = {x0[i], x1[i]}, y[2];
-      const u64 v = bext_prep<2>(T, tb, x, y);
-      a[i] = ar.from_u64(bext_target_sel<2>(T, ti, ns, mc.q, y, v));
+      const u64 v = bext_prep<2>(T, x, y);
+      a[i] = ar.from_u64(bext_target_sel<2>(T->tgt + ti, ns, y, v));
     }
   } else {  // NTT_PRO_RESCALE (DivRoundByLastModulusNTT prep of every other limb)
     const u64* src = row_ptr(io.src, c, 0, b);

@@ -56,8 +56,8 @@ __device__ __forceinline__ typename A::T fwd_load(const NttIO& io, int c, int l,
     const BasisExtTable* __restrict__ T = io.bx + k;
     const int ns = T->ns;
     u64 x[2] = {row_ptr(io.src, c, s0, b)[e], ns > 1 ? row_ptr(io.src, c, s0 + 1, b)[e] : 0}, y[2];
-    const u64 v = bext_prep<2>(T, tb, x, y);
-    return ar.from_u64(bext_target_sel<2>(T, ti, ns, mc.q, y, v));
+    const u64 v = bext_prep<2>(T, x, y);
+    return ar.from_u64(bext_target_sel<2>(T->tgt + ti, ns, y, v));
   } else {  // NTT_PRO_RESCALE
     const u64 qL = tb->mc[io.modL].q, h = qL >> 1;
     const u64 hm = barrett128(0, h, mc);
@@ -71,11 +71,11 @@ __device__ __forceinline__ typename A::T fwd_load(const NttIO& io, int c, int l,
 // the R stages d = LOGN-1 .. 8 (row bit rb = d - 8); twiddle of row group
 // i = lo >> (rb + 1) = k >> rb is w[(N >> (d+1)) + i]
 // ---------------------------------------------------------------------------
-template <class A, int LOGN, int PRO>
-__device__ __forceinline__ void s_fwd_cols(const NttIO& io, int job, int c, int l, int b, int tile, const ModConst& mc,
-                                           const A& ar, __amdgpu_buffer_rsrc_t tw, u64* lds,
-                                           const DeviceTables* __restrict__ tb) {
-  constexpr int N = 1 << LOGN, R = S2<LOGN>::R, CW = S2<LOGN>::CW, H = S2<LOGN>::H;
+template <class A, int LOGN>
+__device__ __forceinline__ void s_fwd_cols_core(const NttIO& io, int job, int c, int l, int b, int tile,
+                                                typename A::T x, typename A::T y, const A& ar,
+                                                __amdgpu_buffer_rsrc_t tw, u64* lds) {
+  constexpr int N = 1 << LOGN, R = S2<LOGN>::R, CW = S2<LOGN>::CW;
   const int t = threadIdx.x, cl = t % CW, k = t / CW, col = tile * CW + cl;
   typename A::W w[R];
 #pragma unroll
@@ -83,8 +83,6 @@ __device__ __forceinline__ void s_fwd_cols(const NttIO& io, int job, int c, int 
     const int rb = R - 1 - s;
     w[s] = ar.tw(tw, k >> rb, N >> (rb + 9));
   }
-  typename A::T x = fwd_load<A, PRO>(io, c, l, b, col + (k << 8), mc, ar, tb);
-  typename A::T y = fwd_load<A, PRO>(io, c, l, b, col + ((k + H) << 8), mc, ar, tb);
 #pragma unroll
   for (int s = 0; s < R; ++s) {
     const int rb = R - 1 - s, lo = lo_of(k, rb);
@@ -105,6 +103,16 @@ __device__ __forceinline__ void s_fwd_cols(const NttIO& io, int job, int c, int 
   const int lo = 2 * k;  // the last stage's pair: rows 2k, 2k + 1
   mid[col + (lo << 8)] = to_bits(x);
   mid[col + ((lo + 1) << 8)] = to_bits(y);
+}
+template <class A, int LOGN, int PRO>
+__device__ __forceinline__ void s_fwd_cols(const NttIO& io, int job, int c, int l, int b, int tile, const ModConst& mc,
+                                           const A& ar, __amdgpu_buffer_rsrc_t tw, u64* lds,
+                                           const DeviceTables* __restrict__ tb) {
+  constexpr int CW = S2<LOGN>::CW, H = S2<LOGN>::H;
+  const int t = threadIdx.x, cl = t % CW, k = t / CW, col = tile * CW + cl;
+  const typename A::T x = fwd_load<A, PRO>(io, c, l, b, col + (k << 8), mc, ar, tb);
+  const typename A::T y = fwd_load<A, PRO>(io, c, l, b, col + ((k + H) << 8), mc, ar, tb);
+  s_fwd_cols_core<A, LOGN>(io, job, c, l, b, tile, x, y, ar, tw, lds);
 }
 
 // forward rows pass: thread (rr, kk) owns butterfly kk of row rr in each of
@@ -215,6 +223,135 @@ __device__ __forceinline__ void s_inv_cols(const NttIO& io, int job, int c, int 
   dst[col + ((k + H) << 8)] = ar.final_inv(y);
 }
 
+// the inverse's columns pass over one column tile of up to two source limbs
+// (interleaved, one LDS region each), kept in registers: thread (cl, k) ends
+// with rows k and k + H of column col of every source -- exactly the pair its
+// forward columns pass starts from, so the two passes meet without an exchange
+template <class A0, class A1, int LOGN, bool TWO>
+__device__ __forceinline__ void s_inv_cols_src(const u64* m0, const u64* m1, const A0& a0, const A1& a1,
+                                               __amdgpu_buffer_rsrc_t tw0, __amdgpu_buffer_rsrc_t tw1, u64* lds,
+                                               u64 (&xa)[2], u64 (&xb)[2]) {
+  constexpr int N = 1 << LOGN, R = S2<LOGN>::R, CW = S2<LOGN>::CW;
+  const int t = threadIdx.x, cl = t % CW, k = t / CW, col = blockIdx.x % S2<LOGN>::CTILES * CW + cl;
+  typename A0::W w0[R];
+  typename A1::W w1[R];
+#pragma unroll
+  for (int rb = 0; rb < R; ++rb) {
+    w0[rb] = a0.tw(tw0, k >> rb, N >> (rb + 9));
+    if (TWO) w1[rb] = a1.tw(tw1, k >> rb, N >> (rb + 9));
+  }
+  typename A0::T x0 = from_bits<typename A0::T>(m0[col + ((2 * k) << 8)]);
+  typename A0::T y0 = from_bits<typename A0::T>(m0[col + ((2 * k + 1) << 8)]);
+  typename A1::T x1{}, y1{};
+  if (TWO) {
+    x1 = from_bits<typename A1::T>(m1[col + ((2 * k) << 8)]);
+    y1 = from_bits<typename A1::T>(m1[col + ((2 * k + 1) << 8)]);
+  }
+  u64* const l0 = lds;
+  u64* const l1 = lds + (CW << R);
+#pragma unroll
+  for (int rb = 0; rb < R; ++rb) {
+    const int lo = lo_of(k, rb), hi = lo + (1 << rb);
+    if (rb > 0) {
+      x0 = from_bits<typename A0::T>(l0[lo * CW + cl]);
+      y0 = from_bits<typename A0::T>(l0[hi * CW + cl]);
+      if (TWO) {
+        x1 = from_bits<typename A1::T>(l1[lo * CW + cl]);
+        y1 = from_bits<typename A1::T>(l1[hi * CW + cl]);
+      }
+    }
+    a0.gs(x0, y0, w0[rb], (rb & 1) == 1);
+    if (TWO) a1.gs(x1, y1, w1[rb], (rb & 1) == 1);
+    if (rb < R - 1) {
+      l0[lo * CW + cl] = to_bits(x0);
+      l0[hi * CW + cl] = to_bits(y0);
+      if (TWO) {
+        l1[lo * CW + cl] = to_bits(x1);
+        l1[hi * CW + cl] = to_bits(y1);
+      }
+      __syncthreads();
+    }
+  }
+  xa[0] = a0.final_inv(x0), xb[0] = a0.final_inv(y0);
+  if (TWO) xa[1] = a1.final_inv(x1), xb[1] = a1.final_inv(y1);
+}
+
+template <class A0, int LOGN>
+__device__ __forceinline__ void s_inv_cols_src2(const u64* m0, const u64* m1, const A0& a0, int mod1, bool two,
+                                                const DeviceTables* __restrict__ tb, __amdgpu_buffer_rsrc_t tw0,
+                                                u64* lds, u64 (&xa)[2], u64 (&xb)[2]) {
+  if (!two) {
+    s_inv_cols_src<A0, A0, LOGN, false>(m0, m0, a0, a0, tw0, tw0, lds, xa, xb);
+    return;
+  }
+  const ModConst& mc1 = tb->mc[mod1];
+  if (mc1.f64)
+    s_inv_cols_src<A0, F64Arith, LOGN, true>(m0, m1, a0, F64Arith(mc1), tw0, twr_s(tb->inv_d[mod1], 8 << LOGN), lds,
+                                             xa, xb);
+  else
+    s_inv_cols_src<A0, IntArith, LOGN, true>(m0, m1, a0, IntArith(mc1), tw0, twr_s(tb->inv[mod1], 16 << LOGN), lds,
+                                             xa, xb);
+}
+
+// forward columns pass of a launch whose sources skipped the inverse's columns
+// pass (NttIO.ifuse): each workgroup (target job, column tile) finishes the
+// sources' INTT on its tile, forms the prologue (the basis extension, or the
+// rescale prep) from registers, and runs the forward columns stages -- the
+// INTT output never goes to HBM and its second launch disappears
+template <int LOGN, int PRO>
+__global__ void __launch_bounds__(S2<LOGN>::CT) ntt2s_ifwd_cols(NttIO io, const DeviceTables* __restrict__ tb) {
+  __shared__ u64 lds[2 * (S2<LOGN>::CW << S2<LOGN>::R)];
+  const int job = io.job0 + blockIdx.x / S2<LOGN>::CTILES, tile = blockIdx.x % S2<LOGN>::CTILES;
+  int c, l, b;
+  job_of(io, job, c, l, b);
+  // the sources: limbs sl0 (, sl0 + 1) of src, inverse intermediate in imid
+  int sl0 = 0, ns = 1, ti = 0;
+  const BasisExtTable* __restrict__ T = nullptr;
+  if constexpr (PRO == NTT_PRO_BEXT) {
+    const int kt = arg_byte(io.bx_tab, l);
+    ti = arg_byte(io.bx_t, l);
+    sl0 = arg_byte(io.bx_s0, kt);
+    T = io.bx + kt;
+    ns = T->ns;
+  }
+  const int m0 = arg_byte(io.src.mod, sl0), m1 = ns > 1 ? arg_byte(io.src.mod, sl0 + 1) : m0;
+  const u64* p0 = row_ptr(io.imid, c, sl0, b);
+  const u64* p1 = ns > 1 ? row_ptr(io.imid, c, sl0 + 1, b) : p0;
+  u64 xa[2] = {0, 0}, xb[2] = {0, 0};
+  const ModConst& mc0 = tb->mc[m0];
+  if (mc0.f64)
+    s_inv_cols_src2<F64Arith, LOGN>(p0, p1, F64Arith(mc0), m1, ns > 1, tb, twr_s(tb->inv_d[m0], 8 << LOGN), lds, xa,
+                                    xb);
+  else
+    s_inv_cols_src2<IntArith, LOGN>(p0, p1, IntArith(mc0), m1, ns > 1, tb, twr_s(tb->inv[m0], 16 << LOGN), lds, xa,
+                                    xb);
+  __syncthreads();  // the forward stages reuse the LDS
+  const int mod = arg_byte(io.dst.mod, l);
+  const ModConst mc = tb->mc[mod];
+  u64 va, vb;
+  if constexpr (PRO == NTT_PRO_BEXT) {
+    u64 y[2];
+    const u64 v0 = bext_prep<2>(T, xa, y);
+    va = bext_target_sel<2>(T->tgt + ti, ns, y, v0);
+    const u64 v1 = bext_prep<2>(T, xb, y);
+    vb = bext_target_sel<2>(T->tgt + ti, ns, y, v1);
+  } else {  // NTT_PRO_RESCALE: ((x + h) mod q_L) mod q_l - (h mod q_l)
+    const u64 qL = tb->mc[io.modL].q, h = qL >> 1;
+    const u64 hm = barrett128(0, h, mc);
+    va = sub_mod(barrett128(0, add_mod(xa[0], h, qL), mc), hm, mc.q);
+    vb = sub_mod(barrett128(0, add_mod(xb[0], h, qL), mc), hm, mc.q);
+  }
+  if (mc.f64) {
+    const F64Arith ar(mc);
+    s_fwd_cols_core<F64Arith, LOGN>(io, job, c, l, b, tile, ar.from_u64(va), ar.from_u64(vb), ar,
+                                    twr_s(tb->fwd_d[mod], 8 << LOGN), lds);
+  } else {
+    const IntArith ar(mc);
+    s_fwd_cols_core<IntArith, LOGN>(io, job, c, l, b, tile, ar.from_u64(va), ar.from_u64(vb), ar,
+                                    twr_s(tb->fwd[mod], 16 << LOGN), lds);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // kernels: blockIdx.x = job * tiles + tile
 // ---------------------------------------------------------------------------
@@ -275,7 +412,7 @@ __global__ void __launch_bounds__(S2<LOGN>::CT) ntt2s_inv_cols(NttIO io, const D
 }
 
 template <int LOGN>
-int launch2s(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
+int launch2s(const NttIO& io, const DeviceTables* tb, bool inverse, bool rows_only, hipStream_t st) {
   const int total = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
   if (total == 0) return 0;
   if (io.jobs != total || io.ci) return -1;
@@ -286,10 +423,20 @@ int launch2s(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t 
   if (inverse) {
     if (io.pro != NTT_PRO_LOAD || io.epi != NTT_EPI_STORE) return -1;
     hipLaunchKernelGGL(ntt2s_inv_rows<LOGN>, gb, bb, 0, st, io, tb);
-    hipLaunchKernelGGL(ntt2s_inv_cols<LOGN>, ga, ba, 0, st, io, tb);
+    // rows_only: the columns pass is left to the forward launch that consumes
+    // this INTT (NttIO.ifuse; the intermediate stays in io.mid)
+    if (!rows_only) hipLaunchKernelGGL(ntt2s_inv_cols<LOGN>, ga, ba, 0, st, io, tb);
     return 0;
   }
-  if (io.pro == NTT_PRO_LOAD)
+  if (io.ifuse) {
+    if (io.mid_compact || !io.imid.p) return -1;
+    if (io.pro == NTT_PRO_BEXT)
+      hipLaunchKernelGGL((ntt2s_ifwd_cols<LOGN, NTT_PRO_BEXT>), ga, ba, 0, st, io, tb);
+    else if (io.pro == NTT_PRO_RESCALE)
+      hipLaunchKernelGGL((ntt2s_ifwd_cols<LOGN, NTT_PRO_RESCALE>), ga, ba, 0, st, io, tb);
+    else
+      return -1;
+  } else if (io.pro == NTT_PRO_LOAD)
     hipLaunchKernelGGL((ntt2s_fwd_cols<LOGN, NTT_PRO_LOAD>), ga, ba, 0, st, io, tb);
   else if (io.pro == NTT_PRO_BEXT)
     hipLaunchKernelGGL((ntt2s_fwd_cols<LOGN, NTT_PRO_BEXT>), ga, ba, 0, st, io, tb);
@@ -308,11 +455,15 @@ int launch2s(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t 
 
 }  // namespace
 
-// host entry: two launches on stream st (same contract as orion_launch_ntt2)
-int orion_launch_ntt2s(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
+// host entry: two launches on stream st (same contract as orion_launch_ntt2);
+// inverse with rows_only: the rows pass alone (its columns pass then runs
+// inside the forward launch that reads this INTT, NttIO.ifuse)
+int orion_launch_ntt2s(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st,
+                       bool rows_only) {
+  if (rows_only && (!inverse || io.mid_compact)) return -1;
   switch (logN) {
-    case 15: return launch2s<15>(io, tb, inverse, st);
-    case 16: return launch2s<16>(io, tb, inverse, st);
+    case 15: return launch2s<15>(io, tb, inverse, rows_only, st);
+    case 16: return launch2s<16>(io, tb, inverse, rows_only, st);
     default: return -1;
   }
 }

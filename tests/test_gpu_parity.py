@@ -776,3 +776,50 @@ def test_deep_chain_n16(torch_cuda, oracle_mod):
     for b in range(B):
         assert np.array_equal(out[b], orc.lt_bsgs(ref[b], level, idx, pts, N1, gkeys)), b
     lib.DeleteScheme()
+
+
+def test_basis_extension_modes(torch_cuda, oracle_mod):
+    """The four ways a basis-extension target sum is formed (common.h
+    BextTarget): ResNet's bootstrapping chain shape ([60] + [30] x 16 Q primes,
+    eight 61-bit P primes, so 8-limb gadget digits) puts narrow 30-bit digits
+    onto 61-bit P targets (BEXT_WT), the eight P limbs onto 30-bit Q targets in
+    every ModDown (BEXT_NT), 30-bit onto 30-bit (BEXT_NARROW), and digit 0
+    (with the 60-bit q0) and the q0 target on the lazy path; digits of 8, 3 and
+    1 limbs as the level drops.  mul_relin -> rescale steps and rotations,
+    bit-exact vs the oracle, with top residues (q - 1) in the inputs."""
+    from orion_amd.backend import HipLibrary
+    logq, logp = [60] + [30] * 16, [61] * 8
+    lib = HipLibrary().new_scheme(13, logq, logp, 30, h=192, seed=77)
+    mods = lib.moduli()
+    assert [q.bit_length() for q in mods[len(logq):]] == [61] * 8
+    orc = oracle_mod.Oracle(13, mods, len(logq), len(logp))
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    rlk = lib.export_relin_key()
+    rng = np.random.default_rng(8080)
+    level, B = len(logq) - 1, 2
+    x = rand_ct(rng, mods, level, orc.N, B=B)
+    for m in range(level + 1):
+        x[:, :, m, :16] = mods[m] - 1  # top residues in the NTT domain
+    ct = lib.import_ciphertext(x, 2.0 ** 30)
+    ref = [x[b] for b in range(B)]
+    g = int(lib.GaloisElement(3))
+    for step in range(8):  # levels 16 -> 8: digits of 8 + 8 + 1, then 8 + 3 limbs
+        nxt = lib.MulRelinCiphertextNew(ct, ct)
+        lib.Rescale(nxt)
+        lib.DeleteCiphertext(ct)
+        ct = nxt
+        got = lib.export_ciphertext(ct)
+        for b in range(B):
+            ref[b] = orc.rescale(orc.mul_relin(ref[b], ref[b], rlk, level), level)
+            assert np.array_equal(got[b], ref[b]), (step, b)
+        level -= 1
+        if step in (0, 5):
+            cr = lib.RotateNew(ct, 3)
+            gk = lib.export_galois_key(g)
+            got = lib.export_ciphertext(cr)
+            for b in range(B):
+                assert np.array_equal(got[b], orc.rotate(ref[b], g, gk, level)), (step, b)
+            lib.DeleteCiphertext(cr)
+    lib.DeleteScheme()

@@ -1,0 +1,47 @@
+"""Per-pass view of a batch-1 kernel trace (tools/gpu_b1_prof.sh): the timed
+forward passes are the last STEPS repetitions of the same dispatch sequence;
+report launches per pass, kernel-busy time per pass, the gaps between
+dispatches, and the top kernels per pass.
+usage: python tools/b1_trace_summ.py TRACE.csv [STEPS]"""
+import csv
+import collections
+import sys
+
+
+def main():
+    rows = list(csv.DictReader(open(sys.argv[1])))
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    names = [r["Kernel_Name"] for r in rows]
+    # the pass length: the smallest period P under which the middle half of
+    # the trace repeats; the timed passes are the run of STEPS periods ending
+    # where the repetition stops
+    n = len(names)
+    per = None
+    for P in range(20, n // 4):
+        lo, hi = n // 4, 3 * n // 4 - P
+        if hi > lo and sum(names[i] == names[i + P] for i in range(lo, hi)) >= 0.995 * (hi - lo):
+            per = P
+            break
+    if per is None:
+        raise SystemExit("no period found")
+    end = 3 * n // 4
+    while end + per < n and names[end] == names[end - per]:
+        end += 1
+    last = rows[end - per * steps:end]
+    t0, t1 = int(last[0]["Start_Timestamp"]), int(last[-1]["End_Timestamp"])
+    busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in last)
+    gaps = [int(b["Start_Timestamp"]) - int(a["End_Timestamp"]) for a, b in zip(last, last[1:])]
+    print(f"launches per pass {per}; wall per pass {(t1 - t0) / steps / 1e3:.1f} us; "
+          f"kernel busy per pass {busy / steps / 1e3:.1f} us; mean gap {sum(gaps) / len(gaps) / 1e3:.2f} us")
+    agg = collections.defaultdict(lambda: [0, 0])
+    for r in last:
+        short = r["Kernel_Name"].split("(")[0].replace("(anonymous namespace)::", "").replace("void ", "")
+        agg[short][0] += 1
+        agg[short][1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    for k, (n, ns) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:25]:
+        print(f"{n / steps:6.1f} x {ns / n / 1e3:6.2f} us = {ns / steps / 1e3:7.1f} us/pass  {k}")
+
+
+if __name__ == "__main__":
+    main()
