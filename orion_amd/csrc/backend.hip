@@ -773,13 +773,19 @@ struct Context {
   // (ntt2s_ifwd_cols), so the INTT output never goes to HBM and its second
   // launch disappears
   int ntt_ifuse = getenv("ORION_NTT_IFUSE") ? atoi(getenv("ORION_NTT_IFUSE")) : 1;
+  // ... as long as the sources' columns pass is not redone too often: every
+  // target workgroup redoes it for its own sources, (targets x sources per
+  // target) / source limbs times the INTT's own columns work (ResNet's
+  // N = 2^16 ModDowns onto 20-30 Q limbs measured slower fused)
+  double ntt_ifuse_maxr = getenv("ORION_NTT_IFUSE_MAXR") ? atof(getenv("ORION_NTT_IFUSE_MAXR")) : 8.0;
   bool on_ntt2s(int jobs, bool inv, int pro, int epi, bool inplace_sub) {
     return (logN == 15 || logN == 16) && !ci && ntt2_chunk <= 0 && jobs <= ntt2s_below &&
            two_pass(jobs, inv, pro, epi, inplace_sub);
   }
   // the INTT iio (load prologue, store epilogue) and then the forward fio whose
-  // BEXT / RESCALE prologue reads the INTT's output (fio.src = iio.dst)
-  void intt_then_fwd(NttIO iio, NttIO fio, double src_per_job = 0) {
+  // BEXT / RESCALE prologue reads the INTT's output (fio.src = iio.dst); ns_max:
+  // the most source limbs one target reads
+  void intt_then_fwd(NttIO iio, NttIO fio, int ns_max, double src_per_job = 0) {
     const int ij = iio.dst.ncomp * iio.dst.nlimb * iio.dst.nbatch;
     const int fj = fio.dst.ncomp * fio.dst.nlimb * fio.dst.nbatch;
     bool same = iio.dst.p == fio.src.p && iio.dst.nlimb == fio.src.nlimb && iio.dst.ncomp == fio.src.ncomp &&
@@ -788,7 +794,8 @@ struct Context {
     for (int l = 0; same && l < iio.dst.nlimb; ++l)
       same = iio.dst.pos[l] == fio.src.pos[l] && iio.dst.mod[l] == fio.src.mod[l];
     const bool inplace_sub = fio.epi == NTT_EPI_SUBSCALE && fio.ex.p == fio.dst.p;
-    if (!ntt_ifuse || !same || iio.pro != NTT_PRO_LOAD || iio.epi != NTT_EPI_STORE ||
+    const double redo = (double)fio.dst.nlimb * ns_max / std::max(1, iio.dst.nlimb);
+    if (!ntt_ifuse || redo > ntt_ifuse_maxr || !same || iio.pro != NTT_PRO_LOAD || iio.epi != NTT_EPI_STORE ||
         (fio.pro != NTT_PRO_BEXT && fio.pro != NTT_PRO_RESCALE) ||
         !on_ntt2s(ij, true, NTT_PRO_LOAD, NTT_EPI_STORE, false) || !on_ntt2s(fj, false, fio.pro, fio.epi, inplace_sub)) {
       ntt_io(iio, true);
@@ -1407,7 +1414,7 @@ struct Context {
           io.bx_t[l] = (unsigned char)(j < lo ? j : j - ns);
           srcs += ns;
         }
-        intt_then_fwd(iio, io, srcs / (double)tpos.size());
+        intt_then_fwd(iio, io, K, srcs / (double)tpos.size());
         return D;
       }
       ntt_io(iio, true);
@@ -1517,7 +1524,7 @@ struct Context {
         io.s[j] = hm_invmod(pq[j], mods[j]);
         io.ss[j] = hm_shoup(io.s[j], mods[j]);
       }
-      intt_then_fwd(nio(xp, xp), io, K);
+      intt_then_fwd(nio(xp, xp), io, K, K);
       return;
     }
     ntt(xp, true);
@@ -1595,7 +1602,7 @@ struct Context {
       io.ss[j] = hm_shoup(io.s[j], mods[j]);
     }
     (void)B;
-    intt_then_fwd(nio(last, last), io);  // INTT of the last limb, then the prep + NTT + tail
+    intt_then_fwd(nio(last, last), io, 1);  // INTT of the last limb, then the prep + NTT + tail
     ct.level = l - 1;
     ct.scale /= (long double)mods[l];
   }
@@ -1700,6 +1707,18 @@ struct Context {
          ls(src, 0, 1, iota(0, src.nlimb), md));
       T.sdiags.emplace(kv.first, dst);
     }
+    // a zero diagonal in every plan slot a giant does not use, so lt_bsgs can
+    // run its slots without per-slot branches (LT_DENSE; the products with it
+    // add zero)
+    {
+      const Poly& any = T.sdiags.begin()->second;
+      Poly z = alloc(any.ncomp, any.nlimb, any.B);
+      HIPCHK(hipMemsetAsync(z.ptr(), 0, (size_t)any.ncomp * any.nlimb * any.B * N * sizeof(u64), stream));
+      T.sdiags.emplace(-1, z);
+    }
+    for (auto& P : plans)
+      for (int gg = 0; gg < LT_MAXG; ++gg)
+        for (int sl = 0; sl < LT_MAXSLOT; ++sl) P.pt[gg][sl] = T.sdiags.at(-1).ptr();
     for (int gi = 0; gi < ng; ++gi) {
       LtPlan& P = plans[gi / LT_MAXG];
       const int j = T.gorder[gi], gg = gi % LT_MAXG;

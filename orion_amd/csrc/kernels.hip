@@ -51,6 +51,12 @@
 #ifndef LT_GIANT_CH
 #define LT_GIANT_CH 0  // lt_giant digits per load chunk (0: 2 at IB >= 4, else 4)
 #endif
+// 1: lt_bsgs runs every register slot of every giant without branches: the
+// plan points the slots a giant does not use at a zero diagonal, so their
+// products add zero (0: one uniform branch per slot)
+#ifndef LT_DENSE
+#define LT_DENSE 1
+#endif
 // 1: lt_bsgs cuts the baby rotations into 30-bit pieces once, before the
 // integer giant loop (0: per giant)
 #ifndef LT_PRESPLIT
@@ -472,12 +478,12 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
         }
         u64 pv[MB];
 #pragma unroll
-        for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? gld(P->pt[g][Bb.s0 + s], po) : 0;
+        for (int s = 0; s < MB; ++s) pv[s] = (LT_DENSE || ((mask >> s) & 1ull)) ? gld(P->pt[g][Bb.s0 + s], po) : 0;
         MacD a0, a1;
         macd_zero(a0), macd_zero(a1);
 #pragma unroll
         for (int s = 0; s < MB; ++s) {
-          if (((mask >> s) & 1ull) && !(LT_ABLATE & 1)) {
+          if ((LT_DENSE || ((mask >> s) & 1ull)) && !(LT_ABLATE & 1)) {
             // the plan's diagonal copies are stored split (EW_SPLIT24): pieces in the two dwords
             // (signed conversions of the dwords: converting (u32)(pv >> 32) went
             // through the u64 conversion and left an add of 0.0 * 2^32 behind)
@@ -518,12 +524,12 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
       }
       u64 pv[MB];
 #pragma unroll
-      for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? gld(P->pt[g][Bb.s0 + s], po) : 0;
+      for (int s = 0; s < MB; ++s) pv[s] = (LT_DENSE || ((mask >> s) & 1ull)) ? gld(P->pt[g][Bb.s0 + s], po) : 0;
       MacW a0, a1;
       macw_zero(a0), macw_zero(a1);
 #pragma unroll
       for (int s = 0; s < MB; ++s) {
-        if (((mask >> s) & 1ull) && !(LT_ABLATE & 4)) {
+        if ((LT_DENSE || ((mask >> s) & 1ull)) && !(LT_ABLATE & 4)) {
           const u32 yb = (u32)pv[s], ya = (u32)(pv[s] >> 32);
           if (LT_PRESPLIT) {
             macw_add(a0, (u32)x0[s], (u32)(x0[s] >> 32), yb, ya);
@@ -557,12 +563,12 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
     // their latencies overlap (the branches are wave-uniform)
     u64 pv[MB];
 #pragma unroll
-    for (int s = 0; s < MB; ++s) pv[s] = ((mask >> s) & 1ull) ? gld(P->pt[g][Bb.s0 + s], po) : 0;
+    for (int s = 0; s < MB; ++s) pv[s] = (LT_DENSE || ((mask >> s) & 1ull)) ? gld(P->pt[g][Bb.s0 + s], po) : 0;
     MacAcc a0, a1;
     mac_zero(a0), mac_zero(a1);
 #pragma unroll
     for (int s = 0; s < MB; ++s) {
-      if (((mask >> s) & 1ull) && !(LT_ABLATE & 4)) {
+      if ((LT_DENSE || ((mask >> s) & 1ull)) && !(LT_ABLATE & 4)) {
         mac_add(a0, pv[s], x0[s]);
         mac_add(a1, pv[s], x1[s]);
       }

@@ -46,11 +46,6 @@ __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, u64 v, int voff
 #ifndef NTT_INT_CUT
 #define NTT_INT_CUT 1
 #endif
-// 1: the inverse (GS) butterfly keeps values in [0, 4q) and uses the cut
-// quotient (timing switch; 0: [0, 2q) with the full Shoup quotient)
-#ifndef NTT_INV_CUT
-#define NTT_INV_CUT 0
-#endif
 struct IntArith {
   typedef u64 T;
   typedef ulonglong2 W;
@@ -81,33 +76,21 @@ struct IntArith {
       Y = x - t + q2;
     }
   }
-  // Harvey GS butterfly, values in [0, 2q); with NTT_INV_CUT in [0, 4q) and
-  // the cut Shoup quotient (as the forward butterfly)
+  // Harvey GS butterfly, values in [0, 2q).  (The cut quotient of the forward
+  // butterfly, with values in [0, 4q), spills the inverse kernel: 128 VGPRs +
+  // 172-196 B of scratch per lane at N = 2^15 in every formulation tried --
+  // cut, the nq form, fenced after every butterfly -- against 120 VGPRs here.)
   __device__ __forceinline__ void gs(T& X, T& Y, const W& w, bool) const {
     const u64 x = X, y = Y;
     const u64 s = x + y;
-    if constexpr (NTT_INV_CUT == 1) {
-      X = s >= q4 ? s - q4 : s;
-      Y = shoup_cut_nq(x - y + q4, w.x, w.y, nq);
-    } else if constexpr (NTT_INV_CUT == 2) {
-      const u64 d = x - y + q4;
-      PIN(X, Y);
-      Y = shoup_cut_nq(d, w.x, w.y, nq);
-      X = s >= q4 ? s - q4 : s;
-    } else if constexpr (NTT_INV_CUT == 3) {
-      X = s >= q4 ? s - q4 : s;
-      Y = shoup_lazy_nq(x - y + q4, w.x, w.y, nq);
-    } else {
-      X = s >= q2 ? s - q2 : s;
-      Y = shoup_lazy(x - y + q2, w.x, w.y, q);
-    }
+    X = s >= q2 ? s - q2 : s;
+    Y = shoup_lazy(x - y + q2, w.x, w.y, q);
   }
-  // the last GS stage with N^-1 folded in (inputs in [0, 2q) -- [0, 4q) with
-  // NTT_INV_CUT -- outputs in [0, 2q))
+  // the last GS stage with N^-1 folded in (inputs in [0, 2q), outputs in [0, 2q))
   __device__ __forceinline__ void gs_last(T& X, T& Y) const {
     const u64 x = X, y = Y;
     X = shoup_lazy(x + y, ninv, ninv_s, q);
-    Y = shoup_lazy(x - y + (NTT_INV_CUT ? q4 : q2), wl, wl_s, q);
+    Y = shoup_lazy(x - y + q2, wl, wl_s, q);
   }
   __device__ __forceinline__ u64 final_inv_folded(T x) const { return x >= q ? x - q : x; }
   __device__ __forceinline__ T reduce_round(T x) const { return x; }  // lazy range is invariant
