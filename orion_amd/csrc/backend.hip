@@ -707,16 +707,17 @@ struct Context {
   // job of every other CU in persistent launches of >= ntt_stagger_min rounds
   int ntt_stagger = getenv("ORION_NTT_STAGGER") ? atoi(getenv("ORION_NTT_STAGGER")) : 0;
   int ntt_stagger_min = getenv("ORION_NTT_STAGGER_MIN") ? atoi(getenv("ORION_NTT_STAGGER_MIN")) : 2;
-  // ORION_NTT_LOG=path: one line per NTT call ("<impl> <jobs> <sub> <inv>
-  // <pro> <intjobs>": impl 1 = one dispatch of ntt.hip, 2 = a two-pass pair of
-  // ntt2.hip; sub = the subtract-and-scale epilogue; pro = the prologue;
-  // intjobs = limb-transforms on integer-path (>= 2^46) moduli), so
+  // ORION_NTT_LOG=path: one line per NTT call ("<dispatches> <jobs> <sub> <inv>
+  // <pro> <intjobs> <family>": dispatches = kernel launches of the call (1 or
+  // 2); sub = the subtract-and-scale epilogue; pro = the prologue; intjobs =
+  // limb-transforms on integer-path (>= 2^46) moduli; family 1 = ntt.hip, 2 =
+  // ntt2.hip, 3 = ntt2s.hip, 4 = an ntt2s.hip INTT's rows pass alone), so
   // tools/pmc_summary.py can price each dispatch of a rocprofv3 pass with its
   // limb-transform count (persistent launches have fewer workgroups than
   // jobs) and break the NTT time down by launch class
   FILE* ntt_log = nullptr;
   bool ntt_log_init = false;
-  void log_ntt(int impl, const NttIO& io, bool inv) {
+  void log_ntt(int family, const NttIO& io, bool inv) {
     if (!ntt_log_init) {
       ntt_log_init = true;
       const char* p = getenv("ORION_NTT_LOG");
@@ -725,8 +726,9 @@ struct Context {
     if (!ntt_log) return;
     int nint = 0;
     for (int l = 0; l < io.dst.nlimb; ++l) nint += host_tb.mc[io.dst.mod[l]].f64 ? 0 : 1;
-    fprintf(ntt_log, "%d %d %d %d %d %d\n", impl, io.jobs, io.epi == NTT_EPI_SUBSCALE ? 1 : 0, inv ? 1 : 0, io.pro,
-            io.jobs / std::max(1, io.dst.nlimb) * nint);
+    const int dispatches = family == 2 || family == 3 ? 2 : 1;
+    fprintf(ntt_log, "%d %d %d %d %d %d %d\n", dispatches, io.jobs, io.epi == NTT_EPI_SUBSCALE ? 1 : 0, inv ? 1 : 0,
+            io.pro, io.jobs / std::max(1, io.dst.nlimb) * nint, family);
   }
   // whether an NTT launch of `jobs` limb-transforms runs on the two-pass
   // kernels (ntt2.hip): N = 2^16 always; N = 2^15 for small launches and for
@@ -807,7 +809,7 @@ struct Context {
     {
       Scope sc(this, P_NTT_INV, 16.0 * N * ij);
       if (orion_launch_ntt2s(logN, iio, d_tb, true, stream, true)) throw std::runtime_error("NTT launch failed");
-      log_ntt(3, iio, true);
+      log_ntt(4, iio, true);
     }
     fio.ifuse = 1;
     fio.imid = iio.dst;

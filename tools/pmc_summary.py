@@ -92,7 +92,7 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
             return [tuple(int(v) for v in ln.split()[:3]) for ln in f if ln.strip()]
 
     def ntt_log_full(name):
-        """(impl, jobs, sub, inv, pro, intjobs) per call (older logs: 3 fields)."""
+        """(dispatches, jobs, sub, inv, pro, intjobs[, family]) per call (older logs: 3 fields)."""
         p = os.path.join(d, f"ntt_log_{name}.txt")
         if not os.path.exists(p):
             return None
@@ -176,7 +176,9 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
             f = full[call]
             if jobs < 64:
                 continue
-            key = (f"{'inv' if f[3] else 'fwd'} {'1pass' if f[0] == 1 else '2pass'} "
+            fam = {1: "1pass", 2: "2pass", 3: "2pass-s", 4: "rows-only"}.get(f[6]) if len(f) >= 7 else None
+            fam = fam or ("1pass" if f[0] == 1 else "2pass")
+            key = (f"{'inv' if f[3] else 'fwd'} {fam} "
                    f"{'sub' if f[2] else 'store'} pro{f[4]} int{round(f[5] / f[1], 2)} jobs{f[1]}")
             c = classes.setdefault(key, {"calls": 0, "us": 0.0, "bytes": 0.0})
             c["us"] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
