@@ -414,7 +414,8 @@ __device__ __forceinline__ u64 bext_wt(const BextTarget* __restrict__ R, int ns,
 #pragma unroll
   for (int i = 0; i < MS; ++i) {
     if (i >= ns) break;
-    const u32 yy = (u32)y[i];
+    u32 yy = (u32)y[i];
+    asm volatile("" : "+v"(yy));  // (kept in the target loop, as in bext_nt)
     lo += (u64)yy * R->h0[i];
     mid += (u64)yy * R->h1[i];
     hi += (u64)yy * R->h2[i];
@@ -439,9 +440,13 @@ __device__ __forceinline__ u64 bext_nt(const BextTarget* __restrict__ R, int ns,
   for (int i = 0; i < MS; ++i) {
     if (i >= ns) break;
     const u32 h = (u32)R->qh[i];
-    lo += (u64)((u32)y[i] & 0x3fffffffu) * h;
-    mid += (u64)((u32)(y[i] >> 30) & 0x3fffffffu) * h;
-    hi += (u64)(u32)(y[i] >> 60) * h;
+    // the pieces are cut per target: hoisted out of the target loop they hold
+    // 3 x ns VGPRs per coefficient, and the kernels dropped to 2 waves per SIMD
+    u64 yy = y[i];
+    asm volatile("" : "+v"(yy));
+    lo += (u64)((u32)yy & 0x3fffffffu) * h;
+    mid += (u64)((u32)(yy >> 30) & 0x3fffffffu) * h;
+    hi += (u64)(u32)(yy >> 60) * h;
   }
   u64 H, L;
   bext_fold(lo, mid, hi, H, L);
