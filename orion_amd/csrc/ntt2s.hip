@@ -13,6 +13,8 @@
 // launches keep ntt2.hip / ntt.hip (more LDS traffic and barriers per
 // butterfly here).  Outputs are fully reduced, so they are bit-identical to
 // the other kernels'.
+#include <type_traits>
+
 #include "common.h"
 #include "ntt_arith.h"
 
@@ -28,6 +30,8 @@ struct S2 {
   static constexpr int RW = 4;                   // rows per rows-pass workgroup
   static constexpr int RT = RW * 128;            // rows-pass threads (512)
   static constexpr int RTILES = (1 << R) / RW;   // rows-pass workgroups per limb
+  static constexpr int CT4 = CW << (R - 2);      // radix-4 cols-pass threads (256)
+  static constexpr int RT4 = RW * 64;            // radix-4 rows-pass threads (256)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t twr_s(const void* t, int bytes) {
@@ -35,7 +39,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t twr_s(const void* t, int bytes
 }
 
 // lower index of butterfly k of a stage on bit `bit` (pairs lo, lo + 2^bit)
-__device__ __forceinline__ int lo_of(int k, int bit) { return ((k >> bit) << (bit + 1)) | (k & ((1 << bit) - 1)); }
+[[maybe_unused]] __device__ __forceinline__ int lo_of(int k, int bit) { return ((k >> bit) << (bit + 1)) | (k & ((1 << bit) - 1)); }
 
 __device__ __forceinline__ u64* mid_row_s(const NttIO& io, int job, int c, int l, int b) {
   if (io.mid_compact) {
@@ -293,13 +297,308 @@ __device__ __forceinline__ void s_inv_cols_src2(const u64* m0, const u64* m1, co
                                              xa, xb);
 }
 
+// ---------------------------------------------------------------------------
+// radix-4 form (NTT2S_R4): a thread owns 4 elements and runs two stages per
+// LDS exchange (two butterflies per stage), so a pass has half the barriers
+// and exchanges of the one-butterfly form with half the threads.  Step on
+// bits (b, b - 1) (forward) or (b, b + 1) (inverse) over elements
+//   e0 = j with two zero bits inserted at those positions, e1 = e0 + 2^lo_bit,
+//   e2 = e0 + 2^hi_bit, e3 = e2 + 2^lo_bit.
+// An odd stage count ends (forward) or ends (inverse) with one radix-2 stage.
+// A forward columns pass starts on, and an inverse columns pass ends on, the
+// set {j, j + 2^(R-2), j + 2^(R-1), j + 3 2^(R-2)} -- so ntt2s_ifwd_cols needs
+// no exchange between its inverse and forward halves.
+// ---------------------------------------------------------------------------
+#ifndef NTT2S_R4
+#define NTT2S_R4 1
+#endif
+__device__ __forceinline__ int ins2(int j, int lo) {  // j with zero bits inserted at lo, lo + 1
+  return ((j >> lo) << (lo + 2)) | (j & ((1 << lo) - 1));
+}
+template <class A>
+__device__ __forceinline__ void ct4(const A& ar, typename A::T (&x)[4], const typename A::W& wa,
+                                    const typename A::W& wb, const typename A::W& wc) {
+  ar.ct(x[0], x[2], wa);  // upper stage: (e0, e2), (e1, e3)
+  ar.ct(x[1], x[3], wa);
+  ar.ct(x[0], x[1], wb);  // lower stage: (e0, e1), (e2, e3)
+  ar.ct(x[2], x[3], wc);
+}
+template <class A>
+__device__ __forceinline__ void gs4(const A& ar, typename A::T (&x)[4], const typename A::W& wa,
+                                    const typename A::W& wb, const typename A::W& wc, bool red_lo, bool red_hi) {
+  ar.gs(x[0], x[1], wa, red_lo);  // lower stage: (e0, e1), (e2, e3)
+  ar.gs(x[2], x[3], wb, red_lo);
+  ar.gs(x[0], x[2], wc, red_hi);  // upper stage: (e0, e2), (e1, e3)
+  ar.gs(x[1], x[3], wc, red_hi);
+}
+
+// forward columns pass, radix 4: thread (cl, j), j < 2^(R-2)
+template <class A, int LOGN>
+__device__ __forceinline__ void s_fwd_cols4_core(const NttIO& io, int job, int c, int l, int b, int tile,
+                                                 typename A::T (&x)[4], const A& ar, __amdgpu_buffer_rsrc_t tw,
+                                                 u64* lds) {
+  constexpr int N = 1 << LOGN, R = S2<LOGN>::R, CW = S2<LOGN>::CW, NS = R / 2;
+  const int t = threadIdx.x, cl = t % CW, j = t / CW, col = tile * CW + cl;
+  typename A::W wa[NS], wb[NS], wc[NS], wl[2];
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    const int hb = R - 1 - 2 * st, g = j >> (hb - 1);
+    wa[st] = ar.tw(tw, g, N >> (hb + 9));
+    wb[st] = ar.tw(tw, 2 * g, N >> (hb + 8));
+    wc[st] = ar.tw(tw, 2 * g + 1, N >> (hb + 8));
+  }
+  if (R & 1) wl[0] = ar.tw(tw, 2 * j, N >> 9), wl[1] = ar.tw(tw, 2 * j + 1, N >> 9);
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    const int hb = R - 1 - 2 * st, lb = hb - 1;
+    const int e0 = ins2(j, lb), e1 = e0 + (1 << lb), e2 = e0 + (1 << hb), e3 = e2 + (1 << lb);
+    if (st > 0) {
+      x[0] = from_bits<typename A::T>(lds[e0 * CW + cl]);
+      x[1] = from_bits<typename A::T>(lds[e1 * CW + cl]);
+      x[2] = from_bits<typename A::T>(lds[e2 * CW + cl]);
+      x[3] = from_bits<typename A::T>(lds[e3 * CW + cl]);
+    }
+    ct4(ar, x, wa[st], wb[st], wc[st]);
+    if (st == 1)  // after 4 stages (float64: |x| stays below 16q)
+      for (int i = 0; i < 4; ++i) x[i] = ar.reduce_round(x[i]);
+    if (st < NS - 1 || (R & 1)) {
+      lds[e0 * CW + cl] = to_bits(x[0]);
+      lds[e1 * CW + cl] = to_bits(x[1]);
+      lds[e2 * CW + cl] = to_bits(x[2]);
+      lds[e3 * CW + cl] = to_bits(x[3]);
+      __syncthreads();
+    }
+  }
+  if (R & 1) {  // the last stage (bit 0): pairs (4j, 4j + 1), (4j + 2, 4j + 3)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = from_bits<typename A::T>(lds[(4 * j + i) * CW + cl]);
+    ar.ct(x[0], x[1], wl[0]);
+    ar.ct(x[2], x[3], wl[1]);
+  }
+  u64* mid = mid_row_s(io, job, c, l, b);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) mid[col + ((4 * j + i) << 8)] = to_bits(ar.reduce_round(x[i]));
+}
+template <class A, int LOGN, int PRO>
+__device__ __forceinline__ void s_fwd_cols4(const NttIO& io, int job, int c, int l, int b, int tile,
+                                            const ModConst& mc, const A& ar, __amdgpu_buffer_rsrc_t tw, u64* lds,
+                                            const DeviceTables* __restrict__ tb) {
+  constexpr int R = S2<LOGN>::R, CW = S2<LOGN>::CW, Q = 1 << (R - 2);
+  const int t = threadIdx.x, cl = t % CW, j = t / CW, col = tile * CW + cl;
+  typename A::T x[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x[i] = fwd_load<A, PRO>(io, c, l, b, col + ((j + i * Q) << 8), mc, ar, tb);
+  s_fwd_cols4_core<A, LOGN>(io, job, c, l, b, tile, x, ar, tw, lds);
+}
+
+// forward rows pass, radix 4: thread (rr, kk), kk < 64
+template <class A, int LOGN, int EPI>
+__device__ __forceinline__ void s_fwd_rows4(const NttIO& io, int job, int c, int l, int b, int tile, const ModConst& mc,
+                                            const A& ar, __amdgpu_buffer_rsrc_t tw, u64* lds) {
+  constexpr int N = 1 << LOGN;
+  const int t = threadIdx.x, rr = t >> 6, kk = t & 63, row = tile * S2<LOGN>::RW + rr;
+  typename A::W wa[4], wb[4], wc[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int hb = 7 - 2 * st, g = kk >> (hb - 1);
+    wa[st] = ar.tw(tw, (row << (7 - hb)) | g, N >> (hb + 1));
+    wb[st] = ar.tw(tw, (row << (8 - hb)) | (2 * g), N >> hb);
+    wc[st] = ar.tw(tw, (row << (8 - hb)) | (2 * g + 1), N >> hb);
+  }
+  const u64* mid = mid_row_s(io, job, c, l, b) + (row << 8);
+  typename A::T x[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x[i] = from_bits<typename A::T>(mid[kk + 64 * i]);
+  u64* lr = lds + rr * 256;
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int hb = 7 - 2 * st, lb = hb - 1;
+    const int e0 = ins2(kk, lb), e1 = e0 + (1 << lb), e2 = e0 + (1 << hb), e3 = e2 + (1 << lb);
+    if (st > 0) {
+      x[0] = from_bits<typename A::T>(lr[e0]);
+      x[1] = from_bits<typename A::T>(lr[e1]);
+      x[2] = from_bits<typename A::T>(lr[e2]);
+      x[3] = from_bits<typename A::T>(lr[e3]);
+    }
+    ct4(ar, x, wa[st], wb[st], wc[st]);
+    if (st == 1)
+      for (int i = 0; i < 4; ++i) x[i] = ar.reduce_round(x[i]);
+    if (st < 3) {  // (a thread writes back only the words it read: one barrier per step)
+      lr[e0] = to_bits(x[0]);
+      lr[e1] = to_bits(x[1]);
+      lr[e2] = to_bits(x[2]);
+      lr[e3] = to_bits(x[3]);
+      __syncthreads();
+    }
+  }
+  // the last step's elements: columns 4kk .. 4kk + 3
+  u64* dst = row_ptr(io.dst, c, l, b) + (row << 8) + 4 * kk;
+  u64 o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = ar.final_fwd(x[i]);
+  if constexpr (EPI == NTT_EPI_SUBSCALE) {  // dst = (ex - y) * s_l
+    const u64* ex = row_ptr(io.ex, c, l, b) + (row << 8) + 4 * kk;
+    const ulonglong2 e01 = *(const ulonglong2*)ex, e23 = *(const ulonglong2*)(ex + 2);
+    const u64 ev[4] = {e01.x, e01.y, e23.x, e23.y};
+    const u64 s = io.s[l], ss = io.ss[l];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = shoup_mul(sub_mod(ev[i], o[i], mc.q), s, ss, mc.q);
+  }
+  *(ulonglong2*)dst = make_ulonglong2(o[0], o[1]);
+  *(ulonglong2*)(dst + 2) = make_ulonglong2(o[2], o[3]);
+}
+
+// inverse rows pass, radix 4 (first): steps on bits (0, 1) .. (6, 7)
+template <class A, int LOGN>
+__device__ __forceinline__ void s_inv_rows4(const NttIO& io, int job, int c, int l, int b, int tile, const A& ar,
+                                            __amdgpu_buffer_rsrc_t tw, u64* lds) {
+  constexpr int N = 1 << LOGN;
+  const int t = threadIdx.x, rr = t >> 6, kk = t & 63, row = tile * S2<LOGN>::RW + rr;
+  typename A::W wa[4], wb[4], wc[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int lb = 2 * st, g = kk >> lb;
+    wa[st] = ar.tw(tw, (row << (7 - lb)) | (2 * g), N >> (lb + 1));
+    wb[st] = ar.tw(tw, (row << (7 - lb)) | (2 * g + 1), N >> (lb + 1));
+    wc[st] = ar.tw(tw, (row << (6 - lb)) | g, N >> (lb + 2));
+  }
+  const u64* src = row_ptr(io.src, c, l, b) + (row << 8) + 4 * kk;
+  const ulonglong2 v01 = *(const ulonglong2*)src, v23 = *(const ulonglong2*)(src + 2);
+  typename A::T x[4] = {ar.from_u64(v01.x), ar.from_u64(v01.y), ar.from_u64(v23.x), ar.from_u64(v23.y)};
+  u64* lr = lds + rr * 256;
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int lb = 2 * st, hb = lb + 1;
+    const int e0 = ins2(kk, lb), e1 = e0 + (1 << lb), e2 = e0 + (1 << hb), e3 = e2 + (1 << lb);
+    if (st > 0) {
+      x[0] = from_bits<typename A::T>(lr[e0]);
+      x[1] = from_bits<typename A::T>(lr[e1]);
+      x[2] = from_bits<typename A::T>(lr[e2]);
+      x[3] = from_bits<typename A::T>(lr[e3]);
+    }
+    gs4(ar, x, wa[st], wb[st], wc[st], false, true);
+    if (st < 3) {  // (a thread writes back only the words it read: one barrier per step)
+      lr[e0] = to_bits(x[0]);
+      lr[e1] = to_bits(x[1]);
+      lr[e2] = to_bits(x[2]);
+      lr[e3] = to_bits(x[3]);
+      __syncthreads();
+    }
+  }
+  u64* mid = mid_row_s(io, job, c, l, b) + (row << 8);  // the last step's elements: kk + 64 i
+#pragma unroll
+  for (int i = 0; i < 4; ++i) mid[kk + 64 * i] = to_bits(ar.reduce_round(x[i]));
+}
+
+// inverse columns pass, radix 4 (second), up to two source limbs interleaved
+// (ntt2s_ifwd_cols) or one (ntt2s_inv_cols); ends on the forward's first set
+template <class A0, class A1, int LOGN, bool TWO>
+__device__ __forceinline__ void s_inv_cols4_src(const u64* m0, const u64* m1, const A0& a0, const A1& a1,
+                                                __amdgpu_buffer_rsrc_t tw0, __amdgpu_buffer_rsrc_t tw1, u64* lds,
+                                                typename A0::T (&x)[4], typename A1::T (&y)[4]) {
+  constexpr int N = 1 << LOGN, R = S2<LOGN>::R, CW = S2<LOGN>::CW, NS = R / 2, Q = 1 << (R - 2);
+  const int t = threadIdx.x, cl = t % CW, j = t / CW, col = blockIdx.x % S2<LOGN>::CTILES * CW + cl;
+  typename A0::W wa0[NS], wb0[NS], wc0[NS], wl0;
+  typename A1::W wa1[NS], wb1[NS], wc1[NS], wl1;
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    const int lb = 2 * st, g = j >> lb;
+    wa0[st] = a0.tw(tw0, 2 * g, N >> (lb + 9));
+    wb0[st] = a0.tw(tw0, 2 * g + 1, N >> (lb + 9));
+    wc0[st] = a0.tw(tw0, g, N >> (lb + 10));
+    if (TWO) {
+      wa1[st] = a1.tw(tw1, 2 * g, N >> (lb + 9));
+      wb1[st] = a1.tw(tw1, 2 * g + 1, N >> (lb + 9));
+      wc1[st] = a1.tw(tw1, g, N >> (lb + 10));
+    }
+  }
+  if (R & 1) {  // the last stage (bit R - 1): one twiddle
+    wl0 = a0.tw(tw0, 0, N >> (R + 8));
+    if (TWO) wl1 = a1.tw(tw1, 0, N >> (R + 8));
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    x[i] = from_bits<typename A0::T>(m0[col + ((4 * j + i) << 8)]);
+    if (TWO) y[i] = from_bits<typename A1::T>(m1[col + ((4 * j + i) << 8)]);
+  }
+  u64* const l0 = lds;
+  u64* const l1 = lds + (CW << R);
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    const int lb = 2 * st, hb = lb + 1;
+    const int e0 = ins2(j, lb), e1 = e0 + (1 << lb), e2 = e0 + (1 << hb), e3 = e2 + (1 << lb);
+    const int e[4] = {e0, e1, e2, e3};
+    if (st > 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        x[i] = from_bits<typename A0::T>(l0[e[i] * CW + cl]);
+        if (TWO) y[i] = from_bits<typename A1::T>(l1[e[i] * CW + cl]);
+      }
+    }
+    gs4(a0, x, wa0[st], wb0[st], wc0[st], false, true);
+    if (TWO) gs4(a1, y, wa1[st], wb1[st], wc1[st], false, true);
+    if (st < NS - 1 || (R & 1)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        l0[e[i] * CW + cl] = to_bits(x[i]);
+        if (TWO) l1[e[i] * CW + cl] = to_bits(y[i]);
+      }
+      __syncthreads();
+    }
+  }
+  if (R & 1) {  // bit R - 1: pairs (j, j + 2Q), (j + Q, j + 3Q); the sum is not reduced (stage R - 1 even)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      x[i] = from_bits<typename A0::T>(l0[(j + i * Q) * CW + cl]);
+      if (TWO) y[i] = from_bits<typename A1::T>(l1[(j + i * Q) * CW + cl]);
+    }
+    a0.gs(x[0], x[2], wl0, ((R - 1) & 1) == 1);
+    a0.gs(x[1], x[3], wl0, ((R - 1) & 1) == 1);
+    if (TWO) {
+      a1.gs(y[0], y[2], wl1, ((R - 1) & 1) == 1);
+      a1.gs(y[1], y[3], wl1, ((R - 1) & 1) == 1);
+    }
+  }
+}
+
+// the radix-4 inverse columns pass of the sources, to canonical residues:
+// v[s][i] = element i of the thread's set, source s
+template <class A0, int LOGN>
+__device__ __forceinline__ void s_inv_cols4_src2(const u64* m0, const u64* m1, const A0& a0, int mod1, bool two,
+                                                 const DeviceTables* __restrict__ tb, __amdgpu_buffer_rsrc_t tw0,
+                                                 u64* lds, u64 (&v)[2][4]) {
+  typename A0::T x[4];
+  if (!two) {
+    typename A0::T y[4];
+    s_inv_cols4_src<A0, A0, LOGN, false>(m0, m0, a0, a0, tw0, tw0, lds, x, y);
+  } else {
+    const ModConst& mc1 = tb->mc[mod1];
+    if (mc1.f64) {
+      const F64Arith a1(mc1);
+      double y[4];
+      s_inv_cols4_src<A0, F64Arith, LOGN, true>(m0, m1, a0, a1, tw0, twr_s(tb->inv_d[mod1], 8 << LOGN), lds, x, y);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[1][i] = a1.final_inv(y[i]);
+    } else {
+      const IntArith a1(mc1);
+      u64 y[4];
+      s_inv_cols4_src<A0, IntArith, LOGN, true>(m0, m1, a0, a1, tw0, twr_s(tb->inv[mod1], 16 << LOGN), lds, x, y);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[1][i] = a1.final_inv(y[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[0][i] = a0.final_inv(x[i]);
+}
+
 // forward columns pass of a launch whose sources skipped the inverse's columns
 // pass (NttIO.ifuse): each workgroup (target job, column tile) finishes the
 // sources' INTT on its tile, forms the prologue (the basis extension, or the
 // rescale prep) from registers, and runs the forward columns stages -- the
 // INTT output never goes to HBM and its second launch disappears
 template <int LOGN, int PRO>
-__global__ void __launch_bounds__(S2<LOGN>::CT) ntt2s_ifwd_cols(NttIO io, const DeviceTables* __restrict__ tb) {
+__global__ void __launch_bounds__(NTT2S_R4 ? S2<LOGN>::CT4 : S2<LOGN>::CT)
+    ntt2s_ifwd_cols(NttIO io, const DeviceTables* __restrict__ tb) {
   __shared__ u64 lds[2 * (S2<LOGN>::CW << S2<LOGN>::R)];
   const int job = io.job0 + blockIdx.x / S2<LOGN>::CTILES, tile = blockIdx.x % S2<LOGN>::CTILES;
   int c, l, b;
@@ -317,95 +616,148 @@ __global__ void __launch_bounds__(S2<LOGN>::CT) ntt2s_ifwd_cols(NttIO io, const 
   const int m0 = arg_byte(io.src.mod, sl0), m1 = ns > 1 ? arg_byte(io.src.mod, sl0 + 1) : m0;
   const u64* p0 = row_ptr(io.imid, c, sl0, b);
   const u64* p1 = ns > 1 ? row_ptr(io.imid, c, sl0 + 1, b) : p0;
-  u64 xa[2] = {0, 0}, xb[2] = {0, 0};
   const ModConst& mc0 = tb->mc[m0];
-  if (mc0.f64)
-    s_inv_cols_src2<F64Arith, LOGN>(p0, p1, F64Arith(mc0), m1, ns > 1, tb, twr_s(tb->inv_d[m0], 8 << LOGN), lds, xa,
-                                    xb);
-  else
-    s_inv_cols_src2<IntArith, LOGN>(p0, p1, IntArith(mc0), m1, ns > 1, tb, twr_s(tb->inv[m0], 16 << LOGN), lds, xa,
-                                    xb);
+  constexpr int NE = NTT2S_R4 ? 4 : 2;  // elements per thread
+  u64 v[2][NE];
+  if constexpr (NTT2S_R4) {
+    if (mc0.f64)
+      s_inv_cols4_src2<F64Arith, LOGN>(p0, p1, F64Arith(mc0), m1, ns > 1, tb, twr_s(tb->inv_d[m0], 8 << LOGN), lds, v);
+    else
+      s_inv_cols4_src2<IntArith, LOGN>(p0, p1, IntArith(mc0), m1, ns > 1, tb, twr_s(tb->inv[m0], 16 << LOGN), lds, v);
+  } else {
+    u64 xa[2] = {0, 0}, xb[2] = {0, 0};
+    if (mc0.f64)
+      s_inv_cols_src2<F64Arith, LOGN>(p0, p1, F64Arith(mc0), m1, ns > 1, tb, twr_s(tb->inv_d[m0], 8 << LOGN), lds, xa,
+                                      xb);
+    else
+      s_inv_cols_src2<IntArith, LOGN>(p0, p1, IntArith(mc0), m1, ns > 1, tb, twr_s(tb->inv[m0], 16 << LOGN), lds, xa,
+                                      xb);
+    v[0][0] = xa[0], v[1][0] = xa[1], v[0][1] = xb[0], v[1][1] = xb[1];
+  }
   __syncthreads();  // the forward stages reuse the LDS
   const int mod = arg_byte(io.dst.mod, l);
   const ModConst mc = tb->mc[mod];
-  u64 va, vb;
-  if constexpr (PRO == NTT_PRO_BEXT) {
-    u64 y[2];
-    const u64 v0 = bext_prep<2>(T, xa, y);
-    va = bext_target_sel<2>(T->tgt + ti, ns, y, v0);
-    const u64 v1 = bext_prep<2>(T, xb, y);
-    vb = bext_target_sel<2>(T->tgt + ti, ns, y, v1);
-  } else {  // NTT_PRO_RESCALE: ((x + h) mod q_L) mod q_l - (h mod q_l)
-    const u64 qL = tb->mc[io.modL].q, h = qL >> 1;
-    const u64 hm = barrett128(0, h, mc);
-    va = sub_mod(barrett128(0, add_mod(xa[0], h, qL), mc), hm, mc.q);
-    vb = sub_mod(barrett128(0, add_mod(xb[0], h, qL), mc), hm, mc.q);
+  u64 o[NE];
+#pragma unroll
+  for (int i = 0; i < NE; ++i) {
+    if constexpr (PRO == NTT_PRO_BEXT) {
+      u64 x[2] = {v[0][i], ns > 1 ? v[1][i] : 0}, y[2];
+      const u64 vv = bext_prep<2>(T, x, y);
+      o[i] = bext_target_sel<2>(T->tgt + ti, ns, y, vv);
+    } else {  // NTT_PRO_RESCALE: ((x + h) mod q_L) mod q_l - (h mod q_l)
+      const u64 qL = tb->mc[io.modL].q, h = qL >> 1;
+      const u64 hm = barrett128(0, h, mc);
+      o[i] = sub_mod(barrett128(0, add_mod(v[0][i], h, qL), mc), hm, mc.q);
+    }
   }
-  if (mc.f64) {
-    const F64Arith ar(mc);
-    s_fwd_cols_core<F64Arith, LOGN>(io, job, c, l, b, tile, ar.from_u64(va), ar.from_u64(vb), ar,
-                                    twr_s(tb->fwd_d[mod], 8 << LOGN), lds);
-  } else {
-    const IntArith ar(mc);
-    s_fwd_cols_core<IntArith, LOGN>(io, job, c, l, b, tile, ar.from_u64(va), ar.from_u64(vb), ar,
-                                    twr_s(tb->fwd[mod], 16 << LOGN), lds);
-  }
+  auto fwd = [&](const auto& ar, __amdgpu_buffer_rsrc_t tw) {
+    using A = std::decay_t<decltype(ar)>;
+    if constexpr (NTT2S_R4) {
+      typename A::T x[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[i] = ar.from_u64(o[i]);
+      s_fwd_cols4_core<A, LOGN>(io, job, c, l, b, tile, x, ar, tw, lds);
+    } else {
+      s_fwd_cols_core<A, LOGN>(io, job, c, l, b, tile, ar.from_u64(o[0]), ar.from_u64(o[1]), ar, tw, lds);
+    }
+  };
+  if (mc.f64)
+    fwd(F64Arith(mc), twr_s(tb->fwd_d[mod], 8 << LOGN));
+  else
+    fwd(IntArith(mc), twr_s(tb->fwd[mod], 16 << LOGN));
 }
 
 // ---------------------------------------------------------------------------
 // kernels: blockIdx.x = job * tiles + tile
 // ---------------------------------------------------------------------------
 template <int LOGN, int PRO>
-__global__ void __launch_bounds__(S2<LOGN>::CT) ntt2s_fwd_cols(NttIO io, const DeviceTables* __restrict__ tb) {
+__global__ void __launch_bounds__(NTT2S_R4 ? S2<LOGN>::CT4 : S2<LOGN>::CT)
+    ntt2s_fwd_cols(NttIO io, const DeviceTables* __restrict__ tb) {
   __shared__ u64 lds[S2<LOGN>::CW << S2<LOGN>::R];
   const int job = io.job0 + blockIdx.x / S2<LOGN>::CTILES, tile = blockIdx.x % S2<LOGN>::CTILES;
   int c, l, b;
   job_of(io, job, c, l, b);
   const int mod = arg_byte(io.dst.mod, l);
   const ModConst mc = tb->mc[mod];
-  if (mc.f64)
+  if constexpr (NTT2S_R4) {
+    if (mc.f64)
+      s_fwd_cols4<F64Arith, LOGN, PRO>(io, job, c, l, b, tile, mc, F64Arith(mc), twr_s(tb->fwd_d[mod], 8 << LOGN), lds,
+                                       tb);
+    else
+      s_fwd_cols4<IntArith, LOGN, PRO>(io, job, c, l, b, tile, mc, IntArith(mc), twr_s(tb->fwd[mod], 16 << LOGN), lds,
+                                       tb);
+  } else if (mc.f64)
     s_fwd_cols<F64Arith, LOGN, PRO>(io, job, c, l, b, tile, mc, F64Arith(mc), twr_s(tb->fwd_d[mod], 8 << LOGN), lds, tb);
   else
     s_fwd_cols<IntArith, LOGN, PRO>(io, job, c, l, b, tile, mc, IntArith(mc), twr_s(tb->fwd[mod], 16 << LOGN), lds, tb);
 }
 
 template <int LOGN, int EPI>
-__global__ void __launch_bounds__(S2<LOGN>::RT) ntt2s_fwd_rows(NttIO io, const DeviceTables* __restrict__ tb) {
+__global__ void __launch_bounds__(NTT2S_R4 ? S2<LOGN>::RT4 : S2<LOGN>::RT)
+    ntt2s_fwd_rows(NttIO io, const DeviceTables* __restrict__ tb) {
   __shared__ u64 lds[S2<LOGN>::RW * 256];
   const int job = io.job0 + blockIdx.x / S2<LOGN>::RTILES, tile = blockIdx.x % S2<LOGN>::RTILES;
   int c, l, b;
   job_of(io, job, c, l, b);
   const int mod = arg_byte(io.dst.mod, l);
   const ModConst mc = tb->mc[mod];
-  if (mc.f64)
+  if constexpr (NTT2S_R4) {
+    if (mc.f64)
+      s_fwd_rows4<F64Arith, LOGN, EPI>(io, job, c, l, b, tile, mc, F64Arith(mc), twr_s(tb->fwd_d[mod], 8 << LOGN), lds);
+    else
+      s_fwd_rows4<IntArith, LOGN, EPI>(io, job, c, l, b, tile, mc, IntArith(mc), twr_s(tb->fwd[mod], 16 << LOGN), lds);
+  } else if (mc.f64)
     s_fwd_rows<F64Arith, LOGN, EPI>(io, job, c, l, b, tile, mc, F64Arith(mc), twr_s(tb->fwd_d[mod], 8 << LOGN), lds);
   else
     s_fwd_rows<IntArith, LOGN, EPI>(io, job, c, l, b, tile, mc, IntArith(mc), twr_s(tb->fwd[mod], 16 << LOGN), lds);
 }
 
 template <int LOGN>
-__global__ void __launch_bounds__(S2<LOGN>::RT) ntt2s_inv_rows(NttIO io, const DeviceTables* __restrict__ tb) {
+__global__ void __launch_bounds__(NTT2S_R4 ? S2<LOGN>::RT4 : S2<LOGN>::RT)
+    ntt2s_inv_rows(NttIO io, const DeviceTables* __restrict__ tb) {
   __shared__ u64 lds[S2<LOGN>::RW * 256];
   const int job = io.job0 + blockIdx.x / S2<LOGN>::RTILES, tile = blockIdx.x % S2<LOGN>::RTILES;
   int c, l, b;
   job_of(io, job, c, l, b);
   const int mod = arg_byte(io.dst.mod, l);
   const ModConst mc = tb->mc[mod];
-  if (mc.f64)
+  if constexpr (NTT2S_R4) {
+    if (mc.f64)
+      s_inv_rows4<F64Arith, LOGN>(io, job, c, l, b, tile, F64Arith(mc), twr_s(tb->inv_d[mod], 8 << LOGN), lds);
+    else
+      s_inv_rows4<IntArith, LOGN>(io, job, c, l, b, tile, IntArith(mc), twr_s(tb->inv[mod], 16 << LOGN), lds);
+  } else if (mc.f64)
     s_inv_rows<F64Arith, LOGN>(io, job, c, l, b, tile, F64Arith(mc), twr_s(tb->inv_d[mod], 8 << LOGN), lds);
   else
     s_inv_rows<IntArith, LOGN>(io, job, c, l, b, tile, IntArith(mc), twr_s(tb->inv[mod], 16 << LOGN), lds);
 }
 
 template <int LOGN>
-__global__ void __launch_bounds__(S2<LOGN>::CT) ntt2s_inv_cols(NttIO io, const DeviceTables* __restrict__ tb) {
+__global__ void __launch_bounds__(NTT2S_R4 ? S2<LOGN>::CT4 : S2<LOGN>::CT)
+    ntt2s_inv_cols(NttIO io, const DeviceTables* __restrict__ tb) {
   __shared__ u64 lds[S2<LOGN>::CW << S2<LOGN>::R];
   const int job = io.job0 + blockIdx.x / S2<LOGN>::CTILES, tile = blockIdx.x % S2<LOGN>::CTILES;
   int c, l, b;
   job_of(io, job, c, l, b);
   const int mod = arg_byte(io.dst.mod, l);
   const ModConst mc = tb->mc[mod];
-  if (mc.f64)
+  if constexpr (NTT2S_R4) {
+    auto inv = [&](const auto& ar, __amdgpu_buffer_rsrc_t tw) {
+      using A = std::decay_t<decltype(ar)>;
+      constexpr int CW = S2<LOGN>::CW, Q = 1 << (S2<LOGN>::R - 2);
+      const int t = threadIdx.x, cl = t % CW, j = t / CW, col = tile * CW + cl;
+      typename A::T x[4], y[4];
+      const u64* m = mid_row_s(io, job, c, l, b);
+      s_inv_cols4_src<A, A, LOGN, false>(m, m, ar, ar, tw, tw, lds, x, y);
+      u64* dst = row_ptr(io.dst, c, l, b);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dst[col + ((j + i * Q) << 8)] = ar.final_inv(x[i]);
+    };
+    if (mc.f64)
+      inv(F64Arith(mc), twr_s(tb->inv_d[mod], 8 << LOGN));
+    else
+      inv(IntArith(mc), twr_s(tb->inv[mod], 16 << LOGN));
+  } else if (mc.f64)
     s_inv_cols<F64Arith, LOGN>(io, job, c, l, b, tile, F64Arith(mc), twr_s(tb->inv_d[mod], 8 << LOGN), lds);
   else
     s_inv_cols<IntArith, LOGN>(io, job, c, l, b, tile, IntArith(mc), twr_s(tb->inv[mod], 16 << LOGN), lds);
@@ -419,7 +771,8 @@ int launch2s(const NttIO& io, const DeviceTables* tb, bool inverse, bool rows_on
   const int jobs = io.njob ? io.njob : total;
   if (io.job0 < 0 || io.job0 + jobs > total) return -1;
   if (io.mid_compact && io.mid.batch_stride < (1 << LOGN)) return -1;
-  const dim3 ga(jobs * S2<LOGN>::CTILES), ba(S2<LOGN>::CT), gb(jobs * S2<LOGN>::RTILES), bb(S2<LOGN>::RT);
+  const dim3 ga(jobs * S2<LOGN>::CTILES), ba(NTT2S_R4 ? S2<LOGN>::CT4 : S2<LOGN>::CT), gb(jobs * S2<LOGN>::RTILES),
+      bb(NTT2S_R4 ? S2<LOGN>::RT4 : S2<LOGN>::RT);
   if (inverse) {
     if (io.pro != NTT_PRO_LOAD || io.epi != NTT_EPI_STORE) return -1;
     hipLaunchKernelGGL(ntt2s_inv_rows<LOGN>, gb, bb, 0, st, io, tb);
