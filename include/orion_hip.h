@@ -121,6 +121,12 @@ ArrayResultInt GetLinearTransformRotationKeys(int transformId);            /* li
 void GenerateLinearTransformRotationKey(int galEl);                        /* lineartransform.go:125 */
 void GenerateConsolidatedRotationKeys(int *galEls, int n);                 /* fork: lt_evaluator.py:77 */
 ArrayResultByte GenerateAndSerializeRotationKey(int galEl);                /* lineartransform.go:131 */
+/* LoadRotationKey keeps a key only over the limbs and digits of the highest
+ * level at which the linear transforms existing at load time use it (a key
+ * with no such transform is kept whole).  A later use above that level needs
+ * the secret key (the key is regenerated) or fails with a message: load keys
+ * after creating the transforms that use them (Lattigo keeps the whole key;
+ * the cut keeps ResNet-20's ~120 keys in a few GB of HBM instead of ~150 GB). */
 void LoadRotationKey(char *data, unsigned long len, unsigned long galEl);  /* lineartransform.go:143 */
 ArrayResultByte SerializeDiagonal(int transformId, int diagIdx);           /* lineartransform.go:162 */
 void LoadPlaintextDiagonal(char *data, unsigned long len, int transformId,

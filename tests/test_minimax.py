@@ -1,9 +1,11 @@
 """GenerateMinimaxSignCoeffs (polyeval.go:91-167): composite minimax
 approximation of sign on [-1, -2^-logalpha] U [2^-logalpha, 1], host-side
-compile-time work, so it runs on the CPU.  Lattigo v6's
-GenMinimaxCompositePolynomial is restated [U] and pinned by the same
-construction computed at `prec` bits in mpmath (tools/gen_minimax.py ->
-tests/golden/minimax_sign.json): the doubles must be equal.  The other checks
+compile-time work, so it runs on the CPU.  Parity with Lattigo v6's
+GenMinimaxCompositePolynomial [U] is UNPINNED (not in this image; logerr is
+ignored here): the fixture (tools/gen_minimax.py ->
+tests/golden/minimax_sign.json) is this backend's own construction computed
+again in mpmath at `prec` bits, so the first test pins the arithmetic (the
+doubles must be equal), not Lattigo-equality.  The other checks
 are the contract the caller (orion/nn/activation.py:201-260, _Sign / ReLU)
 relies on -- one Chebyshev coefficient vector per degree, intermediate stages
 inside [-1, 1], the last stage mapped to [0, 1] -- and the approximation
