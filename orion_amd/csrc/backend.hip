@@ -775,6 +775,11 @@ struct Context {
   // (ntt2s_ifwd_cols), so the INTT output never goes to HBM and its second
   // launch disappears
   int ntt_ifuse = getenv("ORION_NTT_IFUSE") ? atoi(getenv("ORION_NTT_IFUSE")) : 1;
+  // 1: a one-pass launch whose last round of one-limb workgroups is partial
+  // (at most ntt_tailsplit_max jobs) runs its whole rounds on the one-pass
+  // kernel and the partial round on the two-pass kernels
+  int ntt_tailsplit = getenv("ORION_NTT_TAILSPLIT") ? atoi(getenv("ORION_NTT_TAILSPLIT")) : 0;
+  int ntt_tailsplit_max = getenv("ORION_NTT_TAILSPLIT_MAX") ? atoi(getenv("ORION_NTT_TAILSPLIT_MAX")) : 160;
   // ... as long as the sources' columns pass is not redone too often: every
   // target workgroup redoes it for its own sources, (targets x sources per
   // target) / source limbs times the INTT's own columns work (ResNet's
@@ -852,6 +857,31 @@ struct Context {
       return;
     }
     if (io.ifuse) throw std::runtime_error("NTT: a fused INTT columns pass needs the latency kernels");
+    cus();
+    const int tail = io.jobs % n_cu;
+    if (ntt_tailsplit && logN == 15 && !ci && io.jobs > n_cu && tail > 0 && tail <= ntt_tailsplit_max) {
+      // the whole rounds on the one-pass kernel, the partial last round (the
+      // fast float64 limbs: job order 2) on the two-pass kernels, which scale
+      // with the job count instead of costing a whole limb's latency on every CU
+      Scope sc(this, cat, per * io.jobs);
+      NttIO a = io;
+      a.njob = io.jobs - tail;
+      if (orion_launch_ntt_io(logN, a, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
+      NttIO b = io;
+      Poly scratch = alloc(1, 1, tail);
+      b.mid = ls(scratch, 0, 1, {0}, {0});
+      b.mid_compact = 1;
+      b.job0 = io.jobs - tail;
+      b.njob = tail;
+      const bool small = tail <= ntt2s_below;
+      if (small ? orion_launch_ntt2s(logN, b, d_tb, inv, stream) : orion_launch_ntt2(logN, b, d_tb, inv, stream))
+        throw std::runtime_error("NTT launch failed");
+      a.jobs = a.njob;
+      b.jobs = tail;
+      log_ntt(1, a, inv);
+      log_ntt(small ? 3 : 2, b, inv);
+      return;
+    }
     if (ntt_stagger > 0) {
       io.stagger = io.jobs >= ntt_stagger_min * cus() ? ntt_stagger : 0;
     }

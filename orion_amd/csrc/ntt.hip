@@ -346,7 +346,8 @@ __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_fwd_kernel(NttIO io, con
   if constexpr (FwdPersist<EPI>::value) {
     ntt_stagger(io);
 #pragma nounroll
-    for (int job = blockIdx.x; job < io.jobs; job += gridDim.x) ntt_fwd_job<LOGN, PRO, EPI, CI>(io, job, tb, lds);
+    for (int job = blockIdx.x; job < (io.njob > 0 ? io.njob : io.jobs); job += gridDim.x)
+      ntt_fwd_job<LOGN, PRO, EPI, CI>(io, job, tb, lds);
   } else {
     ntt_fwd_job<LOGN, PRO, EPI, CI>(io, blockIdx.x, tb, lds);
   }
@@ -358,7 +359,7 @@ __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_inv_kernel(NttIO io, con
   extern __shared__ u32 lds[];
   ntt_stagger(io);
 #pragma nounroll
-  for (int job = blockIdx.x; job < io.jobs; job += gridDim.x) {
+  for (int job = blockIdx.x; job < (io.njob > 0 ? io.njob : io.jobs); job += gridDim.x) {
     int c, l, b;
     job_of(io, job, c, l, b);
     const int mod = arg_byte(io.dst.mod, l);
@@ -385,9 +386,10 @@ int g_ntt_grid = 0;
 template <int LOGN, bool CI>
 int launch_ntt_ring(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
   constexpr int N = 1 << LOGN;
-  const int jobs = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
-  if (jobs == 0) return 0;
-  if (io.jobs != jobs) return -1;
+  const int total = io.dst.ncomp * io.dst.nlimb * io.dst.nbatch;
+  if (total == 0) return 0;
+  if (io.jobs != total || io.njob < 0 || io.njob > total || io.job0 != 0) return -1;
+  const int jobs = io.njob > 0 ? io.njob : total;  // njob: the first njob jobs only (a split launch)
   const size_t lds = (size_t)(N + N / 32) * sizeof(u32);
   const dim3 g(g_ntt_grid > 0 && jobs > g_ntt_grid ? g_ntt_grid : jobs), blk(NttGeom<LOGN>::T);
   if (inverse) {
