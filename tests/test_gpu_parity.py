@@ -823,3 +823,41 @@ def test_basis_extension_modes(torch_cuda, oracle_mod):
                 assert np.array_equal(got[b], orc.rotate(ref[b], g, gk, level)), (step, b)
             lib.DeleteCiphertext(cr)
     lib.DeleteScheme()
+
+
+@pytest.mark.parametrize("env", [{"ORION_NTT_TAILSPLIT": "1"}, {"ORION_NTT_IFUSE": "0"},
+                                 {"ORION_BEXT_MODES": "0", "ORION_NTT_IFUSE_MAXR": "1000"}])
+@pytest.mark.parametrize("B", [2, 40])
+def test_runtime_switch_parity(torch_cuda, oracle_mod, env, B, monkeypatch):
+    """The non-default NTT / basis-extension paths behind the runtime switches
+     stay bit-exact: the partial-round split (B=40 at
+    N=2^15 leaves 144- and 80-job tails), the unfused INTT + prologue NTT,
+    the lazy-only basis extension, and the INTT fusion with no redundancy
+    limit.  mul_relin -> rescale -> rotate on a LoLA-shaped chain; two of the
+    images are checked against the oracle."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    from orion_amd.backend import HipLibrary
+    logq, logp = [60, 40, 40, 40, 40, 40], [60, 60]
+    lib = HipLibrary().new_scheme(15, logq, logp, 40, h=192, seed=515)
+    mods = lib.moduli()
+    orc = oracle_mod.Oracle(15, mods, len(logq), len(logp))
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    rng = np.random.default_rng(5150 + B)
+    level = len(logq) - 1
+    x = rand_ct(rng, mods, level, orc.N, B=B)
+    ct = lib.import_ciphertext(x, 2.0 ** 40)
+    cc = lib.MulRelinCiphertextNew(ct, ct)
+    lib.Rescale(cc)
+    g = int(lib.GaloisElement(3))
+    cr = lib.RotateNew(cc, 3)
+    got_m = lib.export_ciphertext(cc)
+    got_r = lib.export_ciphertext(cr)
+    rlk, gk = lib.export_relin_key(), lib.export_galois_key(g)
+    for b in (0, B - 1):
+        ref = orc.rescale(orc.mul_relin(x[b], x[b], rlk, level), level)
+        assert np.array_equal(got_m[b], ref), b
+        assert np.array_equal(got_r[b], orc.rotate(ref, g, gk, level - 1)), b
+    lib.DeleteScheme()
