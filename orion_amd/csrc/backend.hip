@@ -727,7 +727,7 @@ struct Context {
     int nint = 0;
     for (int l = 0; l < io.dst.nlimb; ++l) nint += host_tb.mc[io.dst.mod[l]].f64 ? 0 : 1;
     const int dispatches = family == 2 || family == 3 ? 2 : 1;
-    fprintf(ntt_log, "%d %d %d %d %d %d %d\n", dispatches, io.jobs, io.epi == NTT_EPI_SUBSCALE ? 1 : 0, inv ? 1 : 0,
+    fprintf(ntt_log, "%d %d %d %d %d %d %d\n", dispatches, io.jobs, io.epi != NTT_EPI_STORE ? 1 : 0, inv ? 1 : 0,
             io.pro, io.jobs / std::max(1, io.dst.nlimb) * nint, family);
   }
   // whether an NTT launch of `jobs` limb-transforms runs on the two-pass
@@ -775,6 +775,9 @@ struct Context {
   // (ntt2s_ifwd_cols), so the INTT output never goes to HBM and its second
   // launch disappears
   int ntt_ifuse = getenv("ORION_NTT_IFUSE") ? atoi(getenv("ORION_NTT_IFUSE")) : 1;
+  // 1: a rotation's NTT-domain automorphism is applied in the ModDown's final
+  // NTT store (NTT_EPI_SUBSCALE_AUT) where the kernel supports it
+  int ntt_aut_fuse = getenv("ORION_NTT_AUT_FUSE") ? atoi(getenv("ORION_NTT_AUT_FUSE")) : 1;
   // 1: a one-pass launch whose last round of one-limb workgroups is partial
   // (at most ntt_tailsplit_max jobs) runs its whole rounds on the one-pass
   // kernel and the partial round on the two-pass kernels
@@ -800,7 +803,7 @@ struct Context {
                 iio.dst.limb_stride == fio.src.limb_stride && iio.dst.batch_stride == fio.src.batch_stride;
     for (int l = 0; same && l < iio.dst.nlimb; ++l)
       same = iio.dst.pos[l] == fio.src.pos[l] && iio.dst.mod[l] == fio.src.mod[l];
-    const bool inplace_sub = fio.epi == NTT_EPI_SUBSCALE && fio.ex.p == fio.dst.p;
+    const bool inplace_sub = fio.epi != NTT_EPI_STORE && fio.ex.p == fio.dst.p;
     const double redo = (double)fio.dst.nlimb * ns_max / std::max(1, iio.dst.nlimb);
     if (!ntt_ifuse || redo > ntt_ifuse_maxr || !same || iio.pro != NTT_PRO_LOAD || iio.epi != NTT_EPI_STORE ||
         (fio.pro != NTT_PRO_BEXT && fio.pro != NTT_PRO_RESCALE) ||
@@ -823,9 +826,11 @@ struct Context {
   void ntt_io(NttIO io, bool inv, double src_per_job = 0) {
     prep_io(io);
     const bool bx = io.pro == NTT_PRO_BEXT;
-    const double per = (bx ? (src_per_job + 1) * 8.0 * N : 16.0 * N) + (io.epi == NTT_EPI_SUBSCALE ? 8.0 * N : 0.0);
+    // (+ 8 N for the subtract-and-scale operand, + 4 N for an automorphism's scatter index)
+    const double per = (bx ? (src_per_job + 1) * 8.0 * N : 16.0 * N) + (io.epi != NTT_EPI_STORE ? 8.0 * N : 0.0) +
+                       (io.epi == NTT_EPI_SUBSCALE_AUT ? 4.0 * N : 0.0);
     const int cat = bx ? P_NTT_BEXT : inv ? P_NTT_INV : P_NTT_FWD;
-    if (two_pass(io.jobs, inv, io.pro, io.epi, io.epi == NTT_EPI_SUBSCALE && io.ex.p == io.dst.p)) {
+    if (two_pass(io.jobs, inv, io.pro, io.epi, io.epi != NTT_EPI_STORE && io.ex.p == io.dst.p)) {
       Poly scratch;
       if (ntt2_chunk > 0 && io.jobs > 0) {  // chunks of jobs through one reused compact scratch
         const int chunk = std::min(ntt2_chunk, io.jobs);
@@ -844,7 +849,7 @@ struct Context {
         return;
       }
       io.mid = io.dst;
-      if (io.epi == NTT_EPI_SUBSCALE && io.ex.p == io.dst.p) {  // in-place tail: keep ex intact for pass 2
+      if (io.epi != NTT_EPI_STORE && io.ex.p == io.dst.p) {  // in-place tail: keep ex intact for pass 2
         scratch = alloc(io.dst.ncomp, io.dst.nlimb, io.dst.nbatch);
         io.mid = ls(scratch, 0, io.dst.ncomp, iota(0, io.dst.nlimb), std::vector<int>(io.dst.mod, io.dst.mod + io.dst.nlimb));
       }
@@ -1376,12 +1381,7 @@ struct Context {
                                                        "over the highest level of the linear transforms that exist "
                                                        "when it is loaded: load keys after creating the transforms "
                                                        "and before any higher-level rotation)");
-    const u64 M = nthroot;
-    u64 ginv = hm_powmod(g, M / 2 - 1, M);  // g^-1 mod NthRoot (the group order divides M/2)
-    if ((g * ginv) % M != 1) {
-      for (ginv = 1; ginv < M; ginv += 2)
-        if ((g * ginv) % M == 1) break;
-    }
+    const u64 ginv = galois_inverse(g);
     Poly s_out = alloc(1, L + K, 1);
     automorph(full(s_out, 0, 1), full(sk, 0, 1), ginv, false);
     gks[g] = EvKey{gen_evk(sk, s_out, level), level};
@@ -1536,60 +1536,89 @@ struct Context {
         throw std::runtime_error("ks_mac launch failed");
     }
   }
+  // whether the forward NTT of jobs limb-transforms with prologue pro runs on
+  // a kernel with the automorphism-scatter epilogue (NTT_EPI_SUBSCALE_AUT):
+  // the one-pass kernel with the load prologue, or the radix-4 latency kernels
+  bool aut_epi_ok(int jobs, int pro) {
+    if (ci || ntt2_chunk > 0 || ntt_tailsplit) return false;
+    if (!two_pass(jobs, false, pro, NTT_EPI_SUBSCALE, false)) return logN <= 15 && pro == NTT_PRO_LOAD;
+    return jobs <= ntt2s_below && NTT2S_R4;
+  }
+  u64 galois_inverse(u64 g) const {
+    const u64 M = nthroot;
+    u64 ginv = hm_powmod(g, M / 2 - 1, M);  // g^-1 mod NthRoot (the group order divides M/2)
+    if ((g * ginv) % M != 1) {
+      for (ginv = 1; ginv < M; ginv += 2)
+        if ((g * ginv) % M == 1) break;
+    }
+    return ginv;
+  }
   // x: x.ncomp polys, QP limbs in the order [Q 0..level][P 0..K-1] (any strides);
-  // out = (x_Q - ModUp(INTT(x_P))) * P^-1.  Clobbers x's P limbs.
-  void moddown(const LimbSet& x, int level, const LimbSet& out) {
-    const int nc = x.ncomp, B = x.nbatch;
+  // out = (x_Q - ModUp(INTT(x_P))) * P^-1.  Clobbers x's P limbs.  aut_g != 0:
+  // out = sigma_g of that (a rotation's NTT-domain automorphism), applied in
+  // the final NTT's store when its kernel can scatter, else by automorph()
+  void moddown(const LimbSet& x, int level, const LimbSet& out, u64 aut_g = 0) {
+    const int nc = x.ncomp, B = x.nbatch, jobs = nc * B * (level + 1);
     LimbSet xp = limbs(x, level + 1, K);
-    if (fuse_bext(nc * B * (level + 1), K, NTT_EPI_SUBSCALE)) {
-      // the extension of the P limbs formed in the prologue of the NTT whose
-      // epilogue is (x_Q - .) * P^-1: no basis_ext launch, no extended limbs in HBM
-      NttIO io = nio(out, xp);
-      io.pro = NTT_PRO_BEXT;
-      io.bx = moddown_tab(level);
-      for (int j = 0; j <= level; ++j) io.bx_tab[j] = 0, io.bx_t[j] = (unsigned char)j;
-      io.bx_s0[0] = 0;
-      io.epi = NTT_EPI_SUBSCALE;
+    const bool fused = fuse_bext(jobs, K, NTT_EPI_SUBSCALE);
+    const bool scatter = aut_g && ntt_aut_fuse && aut_epi_ok(jobs, fused ? NTT_PRO_BEXT : NTT_PRO_LOAD);
+    Poly tmp;
+    LimbSet dst = out;
+    if (aut_g && !scatter) {  // the automorphism as its own launch, from a temporary
+      tmp = alloc(nc, level + 1, B);
+      dst = lsq(tmp, 0, nc, level);
+    }
+    auto epilogue = [&](NttIO& io) {
+      io.epi = scatter ? NTT_EPI_SUBSCALE_AUT : NTT_EPI_SUBSCALE;
+      if (scatter) {  // a scatter in place would overwrite ex words other rows still read
+        if (dst.p == x.p) throw std::runtime_error("moddown: the automorphism epilogue cannot run in place");
+        io.aut = aut_index(galois_inverse(aut_g));
+      }
       io.ex = limbs(x, 0, level + 1);
       const std::vector<u64> pq = p_mod_q(level);
       for (int j = 0; j <= level; ++j) {
         io.s[j] = hm_invmod(pq[j], mods[j]);
         io.ss[j] = hm_shoup(io.s[j], mods[j]);
       }
+    };
+    if (fused) {
+      // the extension of the P limbs formed in the prologue of the NTT whose
+      // epilogue is (x_Q - .) * P^-1: no basis_ext launch, no extended limbs in HBM
+      NttIO io = nio(dst, xp);
+      io.pro = NTT_PRO_BEXT;
+      io.bx = moddown_tab(level);
+      for (int j = 0; j <= level; ++j) io.bx_tab[j] = 0, io.bx_t[j] = (unsigned char)j;
+      io.bx_s0[0] = 0;
+      epilogue(io);
       intt_then_fwd(nio(xp, xp), io, K, K);
-      return;
+    } else {
+      ntt(xp, true);
+      Poly ext = alloc(nc, level + 1, B);
+      LimbSet le = lsq(ext, 0, nc, level);
+      {
+        Scope sc(this, P_BEXT, 8.0 * N * B * nc * (K + level + 1));
+        if (orion_launch_basis_ext(le, xp, moddown_tab(level), d_tb, N, stream))
+          throw std::runtime_error("basis_ext: unsupported source count");
+      }
+      NttIO io = nio(dst, le);  // NTT of the extension and (x_Q - .) * P^-1, fused
+      epilogue(io);
+      ntt_io(io, false);
     }
-    ntt(xp, true);
-    Poly ext = alloc(nc, level + 1, B);
-    LimbSet le = lsq(ext, 0, nc, level);
-    {
-      Scope sc(this, P_BEXT, 8.0 * N * B * nc * (K + level + 1));
-      if (orion_launch_basis_ext(le, xp, moddown_tab(level), d_tb, N, stream))
-        throw std::runtime_error("basis_ext: unsupported source count");
-    }
-    NttIO io = nio(out, le);  // NTT of the extension and (x_Q - .) * P^-1, fused
-    io.epi = NTT_EPI_SUBSCALE;
-    io.ex = limbs(x, 0, level + 1);
-    for (int j = 0; j <= level; ++j) {
-      u64 P = 1;
-      for (int k = 0; k < K; ++k) P = hm_mulmod(P, mods[L + k] % mods[j], mods[j]);
-      io.s[j] = hm_invmod(P, mods[j]);
-      io.ss[j] = hm_shoup(io.s[j], mods[j]);
-    }
-    ntt_io(io, false);
+    if (aut_g && !scatter) automorph(out, dst, aut_g, false);
   }
   // full key switch of c (Q, level) -> (k0, k1) written to out comps 0/1 (Q, level);
   // add0/add1 (optional, Q limbs 0..level with out's batch geometry): added to
-  // comps 0/1 of the result, folded into the gadget product as P * add
+  // comps 0/1 of the result, folded into the gadget product as P * add; aut_g:
+  // the result permuted by that Galois element's automorphism (moddown)
   void keyswitch(const LimbSet& c, int level, int B, const Poly& key, int klvl, const Poly& out,
-                 const u64* add0 = nullptr, const u64* add1 = nullptr) {
+                 const u64* add0 = nullptr, const u64* add1 = nullptr, u64 aut_g = 0) {
     if (klvl < level) throw std::runtime_error("evaluation key made for a lower level");
     Poly D = decompose(c, level, B);
     Poly u = alloc(2, level + 1 + K, B);
     const int beta = (level + 1 + K - 1) / K;
     mac_groups(lsqp(u, 0, 2, level, level), 0, lsqp(D, 0, beta, level, level), 0, c, 0, {key.ptr()}, {klvl}, beta,
                add0, 0, add0 ? level + 1 : 0, add1);
-    moddown(lsqp(u, 0, 2, level, level), level, lsq(out, 0, 2, level));
+    moddown(lsqp(u, 0, 2, level, level), level, lsq(out, 0, 2, level), aut_g);
   }
   std::vector<u64> p_mod_q(int level) const {
     std::vector<u64> v;
@@ -1670,11 +1699,10 @@ struct Context {
   Ciphertext apply_galois(const Ciphertext& a, u64 g) {
     const int level = a.level, B = a.poly.B;
     const EvKey& key = galois_key(g, level);
-    Poly t = alloc(2, level + 1, B);
-    // (c0, 0) + keyswitch(c1), the c0 addition folded into the gadget product
-    keyswitch(lsq(a.poly, 1, 1, level), level, B, key.k, key.level, t, a.poly.ptr());
+    // sigma_g((c0, 0) + keyswitch(c1)): the c0 addition folded into the gadget
+    // product, the automorphism into the ModDown's store
     Ciphertext out = new_ct(level, B, a.scale);
-    automorph(lsq(out.poly, 0, 2, level), lsq(t, 0, 2, level), g, false);
+    keyswitch(lsq(a.poly, 1, 1, level), level, B, key.k, key.level, out.poly, a.poly.ptr(), nullptr, g);
     return out;
   }
 

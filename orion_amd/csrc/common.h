@@ -556,9 +556,18 @@ __device__ __forceinline__ void bext_target2(const BextTarget* __restrict__ R, i
 //                             coefficient domain -- bit-identical to basis_ext_kernel
 //   epilogue NTT_EPI_STORE:   store to row (c, l, b) of dst
 //            NTT_EPI_SUBSCALE (forward only): dst = (ex - y) * s_l, ex row (c, l, b)
+//            NTT_EPI_SUBSCALE_AUT: the same, element e stored at position aut[e]
 // ---------------------------------------------------------------------------
 enum { NTT_PRO_LOAD = 0, NTT_PRO_RESCALE = 2, NTT_PRO_BEXT = 3 };
-enum { NTT_EPI_STORE = 0, NTT_EPI_SUBSCALE = 1 };
+// NTT_EPI_SUBSCALE_AUT: the subtract-and-scale epilogue storing element e at
+// position aut[e] -- the NTT-domain automorphism of a rotation (its scatter
+// index, the gather index of the inverse Galois element) applied in the
+// ModDown's store instead of by a separate automorph launch
+enum { NTT_EPI_STORE = 0, NTT_EPI_SUBSCALE = 1, NTT_EPI_SUBSCALE_AUT = 2 };
+// 1: the latency kernels (ntt2s.hip) run in radix-4 form
+#ifndef NTT2S_R4
+#define NTT2S_R4 1
+#endif
 struct NttIO {
   LimbSet dst, src, ex;
   LimbSet mid;  // two-pass N = 2^15 kernels: intermediate between the passes (dst's geometry)
@@ -585,6 +594,7 @@ struct NttIO {
   // their inverse columns pass itself, in registers and LDS
   int ifuse;
   LimbSet imid;
+  const u32* aut;  // NTT_EPI_SUBSCALE_AUT: the scatter index (N entries)
 };
 
 // ---------------------------------------------------------------------------

@@ -309,9 +309,6 @@ __device__ __forceinline__ void s_inv_cols_src2(const u64* m0, const u64* m1, co
 // set {j, j + 2^(R-2), j + 2^(R-1), j + 3 2^(R-2)} -- so ntt2s_ifwd_cols needs
 // no exchange between its inverse and forward halves.
 // ---------------------------------------------------------------------------
-#ifndef NTT2S_R4
-#define NTT2S_R4 1
-#endif
 __device__ __forceinline__ int ins2(int j, int lo) {  // j with zero bits inserted at lo, lo + 1
   return ((j >> lo) << (lo + 2)) | (j & ((1 << lo) - 1));
 }
@@ -436,13 +433,22 @@ __device__ __forceinline__ void s_fwd_rows4(const NttIO& io, int job, int c, int
   u64 o[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) o[i] = ar.final_fwd(x[i]);
-  if constexpr (EPI == NTT_EPI_SUBSCALE) {  // dst = (ex - y) * s_l
+  if constexpr (EPI != NTT_EPI_STORE) {  // dst = (ex - y) * s_l
     const u64* ex = row_ptr(io.ex, c, l, b) + (row << 8) + 4 * kk;
     const ulonglong2 e01 = *(const ulonglong2*)ex, e23 = *(const ulonglong2*)(ex + 2);
     const u64 ev[4] = {e01.x, e01.y, e23.x, e23.y};
     const u64 s = io.s[l], ss = io.ss[l];
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = shoup_mul(sub_mod(ev[i], o[i], mc.q), s, ss, mc.q);
+  }
+  if constexpr (EPI == NTT_EPI_SUBSCALE_AUT) {  // element e to position aut[e]
+    const uint4 ix = *(const uint4*)(io.aut + (row << 8) + 4 * kk);
+    u64* d = row_ptr(io.dst, c, l, b);
+    d[ix.x] = o[0];
+    d[ix.y] = o[1];
+    d[ix.z] = o[2];
+    d[ix.w] = o[3];
+    return;
   }
   *(ulonglong2*)dst = make_ulonglong2(o[0], o[1]);
   *(ulonglong2*)(dst + 2) = make_ulonglong2(o[2], o[3]);
@@ -701,6 +707,7 @@ __global__ void __launch_bounds__(NTT2S_R4 ? S2<LOGN>::RT4 : S2<LOGN>::RT)
   job_of(io, job, c, l, b);
   const int mod = arg_byte(io.dst.mod, l);
   const ModConst mc = tb->mc[mod];
+  static_assert(NTT2S_R4 || EPI != NTT_EPI_SUBSCALE_AUT, "the automorphism epilogue is radix-4 only");
   if constexpr (NTT2S_R4) {
     if (mc.f64)
       s_fwd_rows4<F64Arith, LOGN, EPI>(io, job, c, l, b, tile, mc, F64Arith(mc), twr_s(tb->fwd_d[mod], 8 << LOGN), lds);
@@ -801,6 +808,8 @@ int launch2s(const NttIO& io, const DeviceTables* tb, bool inverse, bool rows_on
     hipLaunchKernelGGL((ntt2s_fwd_rows<LOGN, NTT_EPI_STORE>), gb, bb, 0, st, io, tb);
   else if (io.epi == NTT_EPI_SUBSCALE)
     hipLaunchKernelGGL((ntt2s_fwd_rows<LOGN, NTT_EPI_SUBSCALE>), gb, bb, 0, st, io, tb);
+  else if (io.epi == NTT_EPI_SUBSCALE_AUT && NTT2S_R4 && io.aut)
+    hipLaunchKernelGGL((ntt2s_fwd_rows<LOGN, NTT2S_R4 ? NTT_EPI_SUBSCALE_AUT : NTT_EPI_SUBSCALE>), gb, bb, 0, st, io, tb);
   else
     return -1;
   return 0;

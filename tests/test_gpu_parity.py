@@ -825,15 +825,15 @@ def test_basis_extension_modes(torch_cuda, oracle_mod):
     lib.DeleteScheme()
 
 
-@pytest.mark.parametrize("env", [{"ORION_NTT_TAILSPLIT": "1"}, {"ORION_NTT_IFUSE": "0"},
+@pytest.mark.parametrize("env", [{"ORION_NTT_TAILSPLIT": "1"}, {"ORION_NTT_IFUSE": "0"}, {"ORION_NTT_AUT_FUSE": "0"},
                                  {"ORION_BEXT_MODES": "0", "ORION_NTT_IFUSE_MAXR": "1000"}])
 @pytest.mark.parametrize("B", [2, 40])
 def test_runtime_switch_parity(torch_cuda, oracle_mod, env, B, monkeypatch):
     """The non-default NTT / basis-extension paths behind the runtime switches
      stay bit-exact: the partial-round split (B=40 at
     N=2^15 leaves 144- and 80-job tails), the unfused INTT + prologue NTT,
-    the lazy-only basis extension, and the INTT fusion with no redundancy
-    limit.  mul_relin -> rescale -> rotate on a LoLA-shaped chain; two of the
+    the lazy-only basis extension, the INTT fusion with no redundancy
+    limit, and the rotation's automorphism as its own launch.  mul_relin -> rescale -> rotate on a LoLA-shaped chain; two of the
     images are checked against the oracle."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
