@@ -167,6 +167,11 @@ int OrionHipSynchronize(void);
  * on the library stream with one launch, into the same buffers (the pool pins
  * them until Destroy).  The captured calls must not need a synchronisation:
  * run the stream once before capturing it (keys, tables, LT plans). */
+/* ct += Rotate(ct, amount), in place: the same result as RotateNew(ct, amount)
+ * followed by AddCiphertext(ct, <that rotation>) (evaluator.go:70 + :251), the
+ * addition done in the key switch's final store.  The replay uses it when a
+ * rotation's only consumer is that addition (LoLA's rotate-and-sum). */
+int OrionHipRotateAdd(int ct, int amount);
 int OrionHipGraphBegin(void);
 int OrionHipGraphEnd(void);                               /* graph id, or -1 */
 int OrionHipGraphLaunch(int graph);

@@ -86,6 +86,7 @@ SIGNATURES = {
     "Negate": ([c_int], c_int),
     "Rotate": ([c_int, c_int], c_int),
     "RotateNew": ([c_int, c_int], c_int),
+    "OrionHipRotateAdd": ([c_int, c_int], c_int),
     "Rescale": ([c_int], c_int),
     "RescaleNew": ([c_int], c_int),
     "AddScalar": ([c_int, c_float], c_int),

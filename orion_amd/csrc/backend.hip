@@ -826,9 +826,10 @@ struct Context {
   void ntt_io(NttIO io, bool inv, double src_per_job = 0) {
     prep_io(io);
     const bool bx = io.pro == NTT_PRO_BEXT;
-    // (+ 8 N for the subtract-and-scale operand, + 4 N for an automorphism's scatter index)
+    // (+ 8 N for the subtract-and-scale operand, + 4 N for an automorphism's
+    // scatter index, + 8 N for the word it is added to)
     const double per = (bx ? (src_per_job + 1) * 8.0 * N : 16.0 * N) + (io.epi != NTT_EPI_STORE ? 8.0 * N : 0.0) +
-                       (io.epi == NTT_EPI_SUBSCALE_AUT ? 4.0 * N : 0.0);
+                       (epi_aut(io.epi) ? 4.0 * N : 0.0) + (io.epi == NTT_EPI_SUBSCALE_AUT_ACC ? 8.0 * N : 0.0);
     const int cat = bx ? P_NTT_BEXT : inv ? P_NTT_INV : P_NTT_FWD;
     if (two_pass(io.jobs, inv, io.pro, io.epi, io.epi != NTT_EPI_STORE && io.ex.p == io.dst.p)) {
       Poly scratch;
@@ -849,7 +850,10 @@ struct Context {
         return;
       }
       io.mid = io.dst;
-      if (io.epi != NTT_EPI_STORE && io.ex.p == io.dst.p) {  // in-place tail: keep ex intact for pass 2
+      // in-place tail: keep ex intact for pass 2; automorphism epilogue: a rows
+      // workgroup stores into other rows of dst (and, accumulating, reads
+      // their old words), so the intermediate cannot live there
+      if ((io.epi != NTT_EPI_STORE && io.ex.p == io.dst.p) || epi_aut(io.epi)) {
         scratch = alloc(io.dst.ncomp, io.dst.nlimb, io.dst.nbatch);
         io.mid = ls(scratch, 0, io.dst.ncomp, iota(0, io.dst.nlimb), std::vector<int>(io.dst.mod, io.dst.mod + io.dst.nlimb));
       }
@@ -1556,8 +1560,9 @@ struct Context {
   // x: x.ncomp polys, QP limbs in the order [Q 0..level][P 0..K-1] (any strides);
   // out = (x_Q - ModUp(INTT(x_P))) * P^-1.  Clobbers x's P limbs.  aut_g != 0:
   // out = sigma_g of that (a rotation's NTT-domain automorphism), applied in
-  // the final NTT's store when its kernel can scatter, else by automorph()
-  void moddown(const LimbSet& x, int level, const LimbSet& out, u64 aut_g = 0) {
+  // the final NTT's store when its kernel can scatter, else by automorph();
+  // aut_acc: out += sigma_g(...) instead
+  void moddown(const LimbSet& x, int level, const LimbSet& out, u64 aut_g = 0, bool aut_acc = false) {
     const int nc = x.ncomp, B = x.nbatch, jobs = nc * B * (level + 1);
     LimbSet xp = limbs(x, level + 1, K);
     const bool fused = fuse_bext(jobs, K, NTT_EPI_SUBSCALE);
@@ -1569,7 +1574,7 @@ struct Context {
       dst = lsq(tmp, 0, nc, level);
     }
     auto epilogue = [&](NttIO& io) {
-      io.epi = scatter ? NTT_EPI_SUBSCALE_AUT : NTT_EPI_SUBSCALE;
+      io.epi = !scatter ? NTT_EPI_SUBSCALE : aut_acc ? NTT_EPI_SUBSCALE_AUT_ACC : NTT_EPI_SUBSCALE_AUT;
       if (scatter) {  // a scatter in place would overwrite ex words other rows still read
         if (dst.p == x.p) throw std::runtime_error("moddown: the automorphism epilogue cannot run in place");
         io.aut = aut_index(galois_inverse(aut_g));
@@ -1604,21 +1609,22 @@ struct Context {
       epilogue(io);
       ntt_io(io, false);
     }
-    if (aut_g && !scatter) automorph(out, dst, aut_g, false);
+    if (aut_g && !scatter) automorph(out, dst, aut_g, aut_acc);
   }
   // full key switch of c (Q, level) -> (k0, k1) written to out comps 0/1 (Q, level);
   // add0/add1 (optional, Q limbs 0..level with out's batch geometry): added to
   // comps 0/1 of the result, folded into the gadget product as P * add; aut_g:
-  // the result permuted by that Galois element's automorphism (moddown)
+  // the result permuted by that Galois element's automorphism (moddown), and
+  // added to out's comps 0/1 for aut_acc
   void keyswitch(const LimbSet& c, int level, int B, const Poly& key, int klvl, const Poly& out,
-                 const u64* add0 = nullptr, const u64* add1 = nullptr, u64 aut_g = 0) {
+                 const u64* add0 = nullptr, const u64* add1 = nullptr, u64 aut_g = 0, bool aut_acc = false) {
     if (klvl < level) throw std::runtime_error("evaluation key made for a lower level");
     Poly D = decompose(c, level, B);
     Poly u = alloc(2, level + 1 + K, B);
     const int beta = (level + 1 + K - 1) / K;
     mac_groups(lsqp(u, 0, 2, level, level), 0, lsqp(D, 0, beta, level, level), 0, c, 0, {key.ptr()}, {klvl}, beta,
                add0, 0, add0 ? level + 1 : 0, add1);
-    moddown(lsqp(u, 0, 2, level, level), level, lsq(out, 0, 2, level), aut_g);
+    moddown(lsqp(u, 0, 2, level, level), level, lsq(out, 0, 2, level), aut_g, aut_acc);
   }
   std::vector<u64> p_mod_q(int level) const {
     std::vector<u64> v;
@@ -1704,6 +1710,17 @@ struct Context {
     Ciphertext out = new_ct(level, B, a.scale);
     keyswitch(lsq(a.poly, 1, 1, level), level, B, key.k, key.level, out.poly, a.poly.ptr(), nullptr, g);
     return out;
+  }
+
+  // a += sigma_{5^k}(a), in place: RotateNew(a, k) followed by
+  // AddCiphertext(a, that rotation), with the addition in the ModDown's store
+  // (c1 is decomposed and c0 folded into the gadget product before the ModDown
+  // writes a)
+  void rotate_add_inplace(Ciphertext& a, int k) {
+    const u64 g = galois_element(k);
+    const int level = a.level, B = a.poly.B;
+    const EvKey& key = galois_key(g, level);
+    keyswitch(lsq(a.poly, 1, 1, level), level, B, key.k, key.level, a.poly, a.poly.ptr(), nullptr, g, true);
   }
 
   // scale matching for additions (Lattigo evaluateInPlace: the lower-scale
@@ -2741,7 +2758,7 @@ using namespace orion;
 // recorded into a graph; every other call is refused while a capture is open
 static bool capture_ok(const char* fn) {
   static const std::set<std::string> ok = {
-      "Negate", "Rotate", "RotateNew", "Rescale", "RescaleNew", "ModDropCiphertext", "AddScalar", "AddScalarNew",
+      "Negate", "Rotate", "RotateNew", "OrionHipRotateAdd", "Rescale", "RescaleNew", "ModDropCiphertext", "AddScalar", "AddScalarNew",
       "SubScalar", "SubScalarNew", "MulScalarInt", "MulScalarIntNew", "MulScalarFloat", "MulScalarFloatNew",
       "AddPlaintext", "AddPlaintextNew", "SubPlaintext", "SubPlaintextNew", "MulPlaintext", "MulPlaintextNew",
       "AddCiphertext", "AddCiphertextNew", "SubCiphertext", "SubCiphertextNew", "MulRelinCiphertext",
@@ -3201,6 +3218,13 @@ int RotateNew(int id, int k) {
   API_BEGIN
   Context& c = ctx();
   return c.cts.add(c.rotate(c.cts.get(id), k));
+  API_END(-1)
+}
+int OrionHipRotateAdd(int id, int k) {
+  API_BEGIN
+  Context& c = ctx();
+  c.rotate_add_inplace(c.inplace_ct(id), k);
+  return id;
   API_END(-1)
 }
 int Rescale(int id) {

@@ -557,13 +557,17 @@ __device__ __forceinline__ void bext_target2(const BextTarget* __restrict__ R, i
 //   epilogue NTT_EPI_STORE:   store to row (c, l, b) of dst
 //            NTT_EPI_SUBSCALE (forward only): dst = (ex - y) * s_l, ex row (c, l, b)
 //            NTT_EPI_SUBSCALE_AUT: the same, element e stored at position aut[e]
+//            NTT_EPI_SUBSCALE_AUT_ACC: ... added to the word at aut[e]
 // ---------------------------------------------------------------------------
 enum { NTT_PRO_LOAD = 0, NTT_PRO_RESCALE = 2, NTT_PRO_BEXT = 3 };
 // NTT_EPI_SUBSCALE_AUT: the subtract-and-scale epilogue storing element e at
 // position aut[e] -- the NTT-domain automorphism of a rotation (its scatter
 // index, the gather index of the inverse Galois element) applied in the
 // ModDown's store instead of by a separate automorph launch
-enum { NTT_EPI_STORE = 0, NTT_EPI_SUBSCALE = 1, NTT_EPI_SUBSCALE_AUT = 2 };
+// NTT_EPI_SUBSCALE_AUT_ACC: the same, added to the word already at aut[e] (a
+// rotation whose result is added to its own input, x += sigma_g(x))
+enum { NTT_EPI_STORE = 0, NTT_EPI_SUBSCALE = 1, NTT_EPI_SUBSCALE_AUT = 2, NTT_EPI_SUBSCALE_AUT_ACC = 3 };
+__host__ __device__ constexpr bool epi_aut(int epi) { return epi == NTT_EPI_SUBSCALE_AUT || epi == NTT_EPI_SUBSCALE_AUT_ACC; }
 // 1: the latency kernels (ntt2s.hip) run in radix-4 form
 #ifndef NTT2S_R4
 #define NTT2S_R4 1

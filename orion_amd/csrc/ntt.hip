@@ -154,7 +154,7 @@ __device__ __forceinline__ void ntt_fwd_body(const NttIO& io, int c, int l, int 
 #pragma unroll
   for (int k = 0; k < 32; ++k) r[k] = ar.final_fwd(a[k]);
   const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.dst, c, l, b), 0, N * 8, 0x00020000);
-  static_assert(!NTT_FWD_DIRECT || EPI != NTT_EPI_SUBSCALE_AUT, "no automorphism epilogue in the direct-store build");
+  static_assert(!NTT_FWD_DIRECT || !epi_aut(EPI), "no automorphism epilogue in the direct-store build");
   if constexpr (NTT_FWD_DIRECT) {  // thread t holds outputs 32 t .. 32 t + 31
     if constexpr (EPI == NTT_EPI_STORE) {
 #pragma unroll
@@ -184,10 +184,11 @@ __device__ __forceinline__ void ntt_fwd_body(const NttIO& io, int c, int l, int 
       buf_st(rd, r[k], t * 8, (k << B0) * 8);
       if ((k & 3) == 3) NTT_FENCE();
     }
-  } else if constexpr (EPI == NTT_EPI_SUBSCALE_AUT) {
-    // dst[aut[e]] = (ex[e] - y[e]) * s_l: the rotation's NTT-domain
-    // automorphism folded into the ModDown's store (groups of 8 rows: the ex
-    // words and the scatter indices of a group loaded before it is stored)
+  } else if constexpr (epi_aut(EPI)) {
+    // dst[aut[e]] = (ex[e] - y[e]) * s_l (+ dst[aut[e]] for _ACC): the
+    // rotation's NTT-domain automorphism folded into the ModDown's store (groups
+    // of 8 rows: the ex words and the scatter indices of a group loaded before
+    // it is stored)
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(row_ptr(io.ex, c, l, b), 0, N * 8, 0x00020000);
     const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc((void*)io.aut, 0, N * 4, 0x00020000);
     const u64 s = io.s[l], ss = io.ss[l];
@@ -201,8 +202,18 @@ __device__ __forceinline__ void ntt_fwd_body(const NttIO& io, int c, int l, int 
         ix[k] = __builtin_amdgcn_raw_buffer_load_b32(ri, t * 4, ((8 * g + k) << B0) * 4, 0);
       }
       NTT_FENCE();
+      if constexpr (EPI == NTT_EPI_SUBSCALE_AUT_ACC) {
+        u64 ov[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) buf_st(rd, shoup_mul(sub_mod(xv[k], r[8 * g + k], mc.q), s, ss, mc.q), (int)ix[k] * 8, 0);
+        for (int k = 0; k < 8; ++k) ov[k] = buf_ld(rd, (int)ix[k] * 8, 0);
+        NTT_FENCE();
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          buf_st(rd, add_mod(ov[k], shoup_mul(sub_mod(xv[k], r[8 * g + k], mc.q), s, ss, mc.q), mc.q), (int)ix[k] * 8, 0);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) buf_st(rd, shoup_mul(sub_mod(xv[k], r[8 * g + k], mc.q), s, ss, mc.q), (int)ix[k] * 8, 0);
+      }
       NTT_FENCE();
     }
   } else {  // NTT_EPI_SUBSCALE: dst = (ex - y) * s_l  (ModDown / rescale tail)
@@ -427,8 +438,9 @@ int launch_ntt_ring(const NttIO& io, const DeviceTables* tb, bool inverse, hipSt
   FWD(NTT_PRO_LOAD, NTT_EPI_STORE)
   FWD(NTT_PRO_LOAD, NTT_EPI_SUBSCALE)
   if constexpr (!CI) {
-    if (io.epi == NTT_EPI_SUBSCALE_AUT && !io.aut) return -1;
+    if (epi_aut(io.epi) && !io.aut) return -1;
     FWD(NTT_PRO_LOAD, NTT_EPI_SUBSCALE_AUT)
+    FWD(NTT_PRO_LOAD, NTT_EPI_SUBSCALE_AUT_ACC)
   }
   FWD(NTT_PRO_RESCALE, NTT_EPI_SUBSCALE)
   if constexpr (!CI) {
@@ -450,6 +462,7 @@ void init_lds_ring() {
   set_lds_attr<LOGN, NTT_PRO_LOAD, NTT_EPI_SUBSCALE, CI>();
   set_lds_attr<LOGN, NTT_PRO_RESCALE, NTT_EPI_SUBSCALE, CI>();
   if constexpr (!CI) set_lds_attr<LOGN, NTT_PRO_LOAD, NTT_EPI_SUBSCALE_AUT, CI>();
+  if constexpr (!CI) set_lds_attr<LOGN, NTT_PRO_LOAD, NTT_EPI_SUBSCALE_AUT_ACC, CI>();
   if constexpr (!CI) {
     set_lds_attr<LOGN, NTT_PRO_BEXT, NTT_EPI_STORE, CI>();
     set_lds_attr<LOGN, NTT_PRO_BEXT, NTT_EPI_SUBSCALE, CI>();

@@ -441,9 +441,15 @@ __device__ __forceinline__ void s_fwd_rows4(const NttIO& io, int job, int c, int
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = shoup_mul(sub_mod(ev[i], o[i], mc.q), s, ss, mc.q);
   }
-  if constexpr (EPI == NTT_EPI_SUBSCALE_AUT) {  // element e to position aut[e]
+  if constexpr (epi_aut(EPI)) {  // element e to position aut[e] (added to the word there for _ACC)
     const uint4 ix = *(const uint4*)(io.aut + (row << 8) + 4 * kk);
     u64* d = row_ptr(io.dst, c, l, b);
+    if constexpr (EPI == NTT_EPI_SUBSCALE_AUT_ACC) {
+      o[0] = add_mod(o[0], d[ix.x], mc.q);
+      o[1] = add_mod(o[1], d[ix.y], mc.q);
+      o[2] = add_mod(o[2], d[ix.z], mc.q);
+      o[3] = add_mod(o[3], d[ix.w], mc.q);
+    }
     d[ix.x] = o[0];
     d[ix.y] = o[1];
     d[ix.z] = o[2];
@@ -707,7 +713,7 @@ __global__ void __launch_bounds__(NTT2S_R4 ? S2<LOGN>::RT4 : S2<LOGN>::RT)
   job_of(io, job, c, l, b);
   const int mod = arg_byte(io.dst.mod, l);
   const ModConst mc = tb->mc[mod];
-  static_assert(NTT2S_R4 || EPI != NTT_EPI_SUBSCALE_AUT, "the automorphism epilogue is radix-4 only");
+  static_assert(NTT2S_R4 || !epi_aut(EPI), "the automorphism epilogue is radix-4 only");
   if constexpr (NTT2S_R4) {
     if (mc.f64)
       s_fwd_rows4<F64Arith, LOGN, EPI>(io, job, c, l, b, tile, mc, F64Arith(mc), twr_s(tb->fwd_d[mod], 8 << LOGN), lds);
@@ -810,6 +816,8 @@ int launch2s(const NttIO& io, const DeviceTables* tb, bool inverse, bool rows_on
     hipLaunchKernelGGL((ntt2s_fwd_rows<LOGN, NTT_EPI_SUBSCALE>), gb, bb, 0, st, io, tb);
   else if (io.epi == NTT_EPI_SUBSCALE_AUT && NTT2S_R4 && io.aut)
     hipLaunchKernelGGL((ntt2s_fwd_rows<LOGN, NTT2S_R4 ? NTT_EPI_SUBSCALE_AUT : NTT_EPI_SUBSCALE>), gb, bb, 0, st, io, tb);
+  else if (io.epi == NTT_EPI_SUBSCALE_AUT_ACC && NTT2S_R4 && io.aut)
+    hipLaunchKernelGGL((ntt2s_fwd_rows<LOGN, NTT2S_R4 ? NTT_EPI_SUBSCALE_AUT_ACC : NTT_EPI_SUBSCALE>), gb, bb, 0, st, io, tb);
   else
     return -1;
   return 0;

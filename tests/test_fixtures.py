@@ -56,3 +56,55 @@ def test_fixture_integrity(name):
     from orion_amd.replay import _CT_OPS
     assert ops <= set(_CT_OPS) | {"Decrypt", "Decode", "DeletePlaintext", "DeleteCiphertext",
                                   "SetCiphertextScale"}
+
+
+@pytest.mark.parametrize("name,pairs", [("lola_n15", 10), ("lola_n13", "all"), ("mlp_n13", None), ("mlp_n14", None),
+                                        ("resnet20_n13", None)])
+def test_rotate_add_pairs(name, pairs):
+    """The replay's RotateNew + AddCiphertext fusion (OrionHipRotateAdd) takes
+    exactly the pairs x += Rotate(x, k) whose rotation nothing else reads:
+    LoLA's rotate-and-sum steps (all of its RotateNew).  Every taken pair is adjacent, adds into
+    the rotation's own input, and the rotation's handle is not read again
+    before it is redefined or deleted."""
+    from orion_amd.replay import rotate_add_pairs, _CT_OPS
+    t, _ = load(name)
+    ev = t["events"]
+    got = rotate_add_pairs(ev, t["meta"].get("output_ids", []))
+    if pairs == "all":
+        pairs = sum(e["phase"] == "forward" and e["op"] == "RotateNew" for e in ev)
+    if pairs is not None:
+        assert len(got) == pairs
+    for a, b in got.items():
+        r, s = ev[a], ev[b]
+        assert r["op"] == "RotateNew" and s["op"] == "AddCiphertext"
+        assert s["args"] == [r["args"][0], r["ret"]] and s["ret"] == r["args"][0]
+        for e in ev[b + 1:]:
+            if e.get("ret") == r["ret"] or (e["op"] == "DeleteCiphertext" and e["args"][0] == r["ret"]):
+                break
+            kinds = _CT_OPS.get(e["op"], ())
+            assert not any(k == "ct" and v == r["ret"] for k, v in zip(kinds, e["args"]))
+    # a rotation read again later is never fused
+    x = [{"phase": "forward", "op": "RotateNew", "args": [2, 4], "ret": 1},
+         {"phase": "forward", "op": "AddCiphertext", "args": [2, 1], "ret": 2},
+         {"phase": "forward", "op": "AddCiphertext", "args": [3, 1], "ret": 3}]
+    assert rotate_add_pairs(x) == {}
+    assert rotate_add_pairs(x[:2]) == {0: 1}
+
+
+@pytest.mark.parametrize("name", ["lola_n15", "lola_n13", "mlp_n13", "mlp_n14", "resnet20_n13"])
+def test_rescale_aliases(name):
+    """The replay runs RescaleNew(x) -> y as an in-place Rescale(x) named y
+    only when nothing reads x afterwards (LoLA: all three)."""
+    from orion_amd.replay import rescale_aliases, _CT_OPS
+    t, _ = load(name)
+    ev = t["events"]
+    got = rescale_aliases(ev, t["meta"].get("output_ids", []))
+    if name.startswith("lola"):
+        assert len(got) == sum(e["phase"] == "forward" and e["op"] == "RescaleNew" for e in ev)
+    for i in got:
+        x = ev[i]["args"][0]
+        for e in ev[i + 1:]:
+            if e.get("ret") == x or (e["op"] == "DeleteCiphertext" and e["args"][0] == x):
+                break
+            kinds = _CT_OPS.get(e["op"], ())
+            assert not any(k == "ct" and v == x for k, v in zip(kinds, e["args"]))

@@ -827,14 +827,19 @@ def test_basis_extension_modes(torch_cuda, oracle_mod):
 
 @pytest.mark.parametrize("env", [{"ORION_NTT_TAILSPLIT": "1"}, {"ORION_NTT_IFUSE": "0"}, {"ORION_NTT_AUT_FUSE": "0"},
                                  {"ORION_BEXT_MODES": "0", "ORION_NTT_IFUSE_MAXR": "1000"}])
-@pytest.mark.parametrize("B", [2, 40])
+@pytest.mark.parametrize("B", [2, 12, 40])
 def test_runtime_switch_parity(torch_cuda, oracle_mod, env, B, monkeypatch):
     """The non-default NTT / basis-extension paths behind the runtime switches
      stay bit-exact: the partial-round split (B=40 at
     N=2^15 leaves 144- and 80-job tails), the unfused INTT + prologue NTT,
-    the lazy-only basis extension, the INTT fusion with no redundancy
-    limit, and the rotation's automorphism as its own launch.  mul_relin -> rescale -> rotate on a LoLA-shaped chain; two of the
-    images are checked against the oracle."""
+    the lazy-only basis extension, the INTT fusion with no redundancy limit,
+    and the rotation's automorphism as its own launch; and the fused
+    rotate-and-add (OrionHipRotateAdd) on each of those paths.  B=12 gives
+    120-job latency-kernel launches, with more rows-pass workgroups than the
+    chip holds at once: a scattering rows pass that stored into rows another
+    workgroup has yet to read would show there.  mul_relin -> rescale ->
+    rotate on a LoLA-shaped chain; two of the images are checked against the
+    oracle."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     from orion_amd.backend import HipLibrary
@@ -856,8 +861,15 @@ def test_runtime_switch_parity(torch_cuda, oracle_mod, env, B, monkeypatch):
     got_m = lib.export_ciphertext(cc)
     got_r = lib.export_ciphertext(cr)
     rlk, gk = lib.export_relin_key(), lib.export_galois_key(g)
+    # x += Rotate(x, 3) in one call (the addition in the ModDown's store, or
+    # the accumulating automorph launch with ORION_NTT_AUT_FUSE=0)
+    lib.OrionHipRotateAdd(cc, 3)
+    got_a = lib.export_ciphertext(cc)
+    qs = np.array(mods[:level], dtype=np.uint64)[:, None]
     for b in (0, B - 1):
         ref = orc.rescale(orc.mul_relin(x[b], x[b], rlk, level), level)
         assert np.array_equal(got_m[b], ref), b
-        assert np.array_equal(got_r[b], orc.rotate(ref, g, gk, level - 1)), b
+        rot = orc.rotate(ref, g, gk, level - 1)
+        assert np.array_equal(got_r[b], rot), b
+        assert np.array_equal(got_a[b], (ref + rot) % qs), b
     lib.DeleteScheme()
