@@ -707,9 +707,9 @@ struct Context {
   // job of every other CU in persistent launches of >= ntt_stagger_min rounds
   int ntt_stagger = getenv("ORION_NTT_STAGGER") ? atoi(getenv("ORION_NTT_STAGGER")) : 0;
   int ntt_stagger_min = getenv("ORION_NTT_STAGGER_MIN") ? atoi(getenv("ORION_NTT_STAGGER_MIN")) : 2;
-  // ORION_NTT_LOG=path: one line per NTT call ("<dispatches> <jobs> <sub> <inv>
+  // ORION_NTT_LOG=path: one line per NTT call ("<dispatches> <jobs> <epi> <inv>
   // <pro> <intjobs> <family>": dispatches = kernel launches of the call (1 or
-  // 2); sub = the subtract-and-scale epilogue; pro = the prologue; intjobs =
+  // 2); epi = the epilogue (NTT_EPI_*); pro = the prologue; intjobs =
   // limb-transforms on integer-path (>= 2^46) moduli; family 1 = ntt.hip, 2 =
   // ntt2.hip, 3 = ntt2s.hip, 4 = an ntt2s.hip INTT's rows pass alone), so
   // tools/pmc_summary.py can price each dispatch of a rocprofv3 pass with its
@@ -727,7 +727,7 @@ struct Context {
     int nint = 0;
     for (int l = 0; l < io.dst.nlimb; ++l) nint += host_tb.mc[io.dst.mod[l]].f64 ? 0 : 1;
     const int dispatches = family == 2 || family == 3 ? 2 : 1;
-    fprintf(ntt_log, "%d %d %d %d %d %d %d\n", dispatches, io.jobs, io.epi != NTT_EPI_STORE ? 1 : 0, inv ? 1 : 0,
+    fprintf(ntt_log, "%d %d %d %d %d %d %d\n", dispatches, io.jobs, io.epi, inv ? 1 : 0,
             io.pro, io.jobs / std::max(1, io.dst.nlimb) * nint, family);
   }
   // whether an NTT launch of `jobs` limb-transforms runs on the two-pass

@@ -91,6 +91,13 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
         with open(p) as f:
             return [tuple(int(v) for v in ln.split()[:3]) for ln in f if ln.strip()]
 
+    # the log's epilogue field (backend.hip log_ntt; 0/1 in logs before the
+    # automorphism epilogues): extra algorithmic bytes per coefficient over the
+    # 16 of a plain transform -- the subtract-and-scale operand (8), the
+    # scatter index (4) and the word the scatter adds to (8)
+    EPI_BYTES = {0: 0.0, 1: 8.0, 2: 12.0, 3: 20.0}
+    EPI_NAME = {0: "store", 1: "sub", 2: "sub-aut", 3: "sub-aut-acc"}
+
     def ntt_log_full(name):
         """(dispatches, jobs, sub, inv, pro, intjobs[, family]) per call (older logs: 3 fields)."""
         p = os.path.join(d, f"ntt_log_{name}.txt")
@@ -108,7 +115,7 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
             for k in range(nd):
                 if i >= len(dispatches):
                     raise RuntimeError("NTT log longer than the dispatch list")
-                alg = jobs * (24.0 if sub else 16.0) * N if k == 0 else None
+                alg = jobs * (16.0 + EPI_BYTES.get(sub, 8.0)) * N if k == 0 else None
                 yield call, dispatches[i], alg, jobs
                 i += 1
         if i != len(dispatches):
@@ -179,7 +186,7 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
             fam = {1: "1pass", 2: "2pass", 3: "2pass-s", 4: "rows-only"}.get(f[6]) if len(f) >= 7 else None
             fam = fam or ("1pass" if f[0] == 1 else "2pass")
             key = (f"{'inv' if f[3] else 'fwd'} {fam} "
-                   f"{'sub' if f[2] else 'store'} pro{f[4]} int{round(f[5] / f[1], 2)} jobs{f[1]}")
+                   f"{EPI_NAME.get(f[2], 'sub')} pro{f[4]} int{round(f[5] / f[1], 2)} jobs{f[1]}")
             c = classes.setdefault(key, {"calls": 0, "us": 0.0, "bytes": 0.0})
             c["us"] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
             if alg is not None:
