@@ -377,3 +377,29 @@ def test_resnet20_n16_end_to_end(torch_cuda):
     assert np.abs(res - exp).mean() < 0.005, (res, exp)
     assert np.argmax(res) == np.argmax(exp)
     st.lib.DeleteScheme()
+
+
+def test_replay_fusion_matches_op_by_op(torch_cuda):
+    """The replay's rewrites (rotate-and-add pairs as OrionHipRotateAdd,
+    dead-input RescaleNew as an in-place Rescale) give exactly the op-by-op
+    result, on LoLA N=2^13 at batch 5 (the latency kernels' scatter-add
+    store) and N=2^15 at batch 40 (the one-pass kernel's)."""
+    import numpy as np
+    from orion_amd.replay import OrionStream
+    for name, B in (("lola_n13", 5), ("lola_n15", 40)):
+        st = OrionStream(name, seed=37)
+        st.keygen()
+        st.compile()
+        lib = st.lib
+        assert st._rot_add and st._rescale_alias
+        rng = np.random.default_rng(41)
+        imgs = rng.standard_normal((B,) + np.asarray(st.reference_input()).shape[1:]).astype(np.float32)
+        ct = st.encrypt_batch(imgs)
+        st.fuse = False
+        x = lib.CloneCiphertext(ct)
+        ref = lib.export_ciphertext(st.forward(x))
+        st.fuse = True
+        y = lib.CloneCiphertext(ct)
+        got = lib.export_ciphertext(st.forward(y))
+        assert np.array_equal(got, ref), name
+        lib.DeleteScheme()
