@@ -331,7 +331,7 @@ __device__ __forceinline__ void ntt_inv_body(const NttIO& io, int c, int l, int 
 
 
 // Persistent: a grid of at most one workgroup per CU walks the launch's jobs
-// (job = blockIdx.x + k gridDim.x, in io.order), so a CU goes from one limb's
+// (job w + k G in round k, or G - 1 - w in odd rounds with NTT_SNAKE; in io.order), so a CU goes from one limb's
 // stores straight to the next limb's loads: no workgroup retire/dispatch
 // bubble between limbs, and the stores drain while the next limb loads and
 // computes.  LDS needs no extra barrier between jobs: every exchange ends
@@ -352,6 +352,19 @@ __device__ __forceinline__ void ntt_stagger(const NttIO& io) {
 #ifndef NTT_PERSIST_ALL
 #define NTT_PERSIST_ALL 1
 #endif
+// 1: a persistent workgroup's jobs run in snake order -- job w of every even
+// round, job G - 1 - w of every odd one (G workgroups).  With the integer-path
+// (slower) limbs dispatched first, the workgroups that took the fast float64
+// jobs of a round take the first jobs of the next: a 384-job launch (1.5
+// rounds, one third integer-path) ends after one float64 job more on the
+// float64 workgroups instead of one more after an integer job
+#ifndef NTT_SNAKE
+#define NTT_SNAKE 1
+#endif
+__device__ __forceinline__ int snake_job(int r, int w, int G) {
+  return r * G + ((NTT_SNAKE && (r & 1)) ? G - 1 - w : w);
+}
+
 template <int EPI>
 struct FwdPersist {
   static constexpr bool value = EPI == NTT_EPI_STORE || NTT_PERSIST_ALL;
@@ -378,9 +391,12 @@ __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_fwd_kernel(NttIO io, con
   extern __shared__ u32 lds[];
   if constexpr (FwdPersist<EPI>::value) {
     ntt_stagger(io);
+    const int nj = io.njob > 0 ? io.njob : io.jobs;
 #pragma nounroll
-    for (int job = blockIdx.x; job < (io.njob > 0 ? io.njob : io.jobs); job += gridDim.x)
-      ntt_fwd_job<LOGN, PRO, EPI, CI>(io, job, tb, lds);
+    for (int r = 0; r * (int)gridDim.x < nj; ++r) {
+      const int job = snake_job(r, blockIdx.x, gridDim.x);
+      if (job < nj) ntt_fwd_job<LOGN, PRO, EPI, CI>(io, job, tb, lds);
+    }
   } else {
     ntt_fwd_job<LOGN, PRO, EPI, CI>(io, blockIdx.x, tb, lds);
   }
@@ -391,8 +407,11 @@ __global__ void __launch_bounds__(NttGeom<LOGN>::T) ntt_inv_kernel(NttIO io, con
   constexpr int N = 1 << LOGN;
   extern __shared__ u32 lds[];
   ntt_stagger(io);
+  const int nj = io.njob > 0 ? io.njob : io.jobs;
 #pragma nounroll
-  for (int job = blockIdx.x; job < (io.njob > 0 ? io.njob : io.jobs); job += gridDim.x) {
+  for (int r = 0; r * (int)gridDim.x < nj; ++r) {
+    const int job = snake_job(r, blockIdx.x, gridDim.x);
+    if (job >= nj) continue;
     int c, l, b;
     job_of(io, job, c, l, b);
     const int mod = arg_byte(io.dst.mod, l);
