@@ -121,12 +121,12 @@ ArrayResultInt GetLinearTransformRotationKeys(int transformId);            /* li
 void GenerateLinearTransformRotationKey(int galEl);                        /* lineartransform.go:125 */
 void GenerateConsolidatedRotationKeys(int *galEls, int n);                 /* fork: lt_evaluator.py:77 */
 ArrayResultByte GenerateAndSerializeRotationKey(int galEl);                /* lineartransform.go:131 */
-/* LoadRotationKey keeps a key only over the limbs and digits of the highest
- * level at which the linear transforms existing at load time use it (a key
- * with no such transform is kept whole).  A later use above that level needs
- * the secret key (the key is regenerated) or fails with a message: load keys
- * after creating the transforms that use them (Lattigo keeps the whole key;
- * the cut keeps ResNet-20's ~120 keys in a few GB of HBM instead of ~150 GB). */
+/* LoadRotationKey keeps a key in HBM only over the limbs and digits of the
+ * highest level at which the linear transforms existing at load time use it
+ * (a key with no such transform is kept whole); the cut keeps ResNet-20's
+ * ~120 keys in a few GB of HBM instead of ~150 GB.  The whole key stays in
+ * host memory, as Lattigo keeps it (lineartransform.go:143-159): a later use
+ * above the cut level uploads it whole, the loaded key itself. */
 void LoadRotationKey(char *data, unsigned long len, unsigned long galEl);  /* lineartransform.go:143 */
 ArrayResultByte SerializeDiagonal(int transformId, int diagIdx);           /* lineartransform.go:162 */
 void LoadPlaintextDiagonal(char *data, unsigned long len, int transformId,
@@ -268,8 +268,14 @@ int ImportKeyBundle(const void *dptr, unsigned long bytes);
  * 1 ntt_inv, 2 elementwise, 3 basis_ext, 4 ks_mac, 5 automorph, 6 tensor,
  * 7 rescale_prep, 8 lt_bsgs, 9 lt_giant) */
 void OrionHipProfile(int enable);
-/* fills up to max entries: name (32 chars each), launches, total ms, algorithmic bytes */
+/* fills up to max entries: name (32 chars each), launches, total ms, algorithmic
+ * bytes (NTT: 16 N per limb-transform + 8 N per epilogue operand or addend read,
+ * the "fused" model; the automorphism scatter index is not counted) */
 int OrionHipProfileRead(char *names, long *launches, double *ms, double *bytes, int max);
+/* the same categories priced strictly as SURVEY §8d does: 16 N per NTT
+ * limb-transform, whatever the prologue and epilogue read (other categories:
+ * equal to their algorithmic bytes) */
+int OrionHipProfileReadStrict(double *strict, int max);
 void OrionHipProfileReset(void);
 
 /* raw kernel entry for the roofline microbenchmark and parity tests:

@@ -1641,22 +1641,86 @@ int oracle_btp_chain(int logN, const u64 *scheme_qp, int n_scheme, int Lres, con
   return Lres + nb;
 }
 
-/* EvalMod's polynomial: the Chebyshev interpolant (degree+1 Chebyshev nodes
- * of [-1, 1]) of a cos(2 pi (K u - 1/4) / 2^r), a = (2 pi)^(-1/2^r) */
+/* EvalMod's polynomial, Lattigo v6 mod1 CosDiscrete [U] (the default
+ * Mod1Type; bootstrapper.go:33-38 leaves it at its default): a cos(2 pi (x -
+ * 1/4) / 2^r), a = (2 pi)^(-1/2^r), interpolated at nodes on the integers
+ * i in [-(K-1), K-1] the ModRaise overflow takes -- d_i Chebyshev nodes of the
+ * first kind within dev = 2^-LogMessageRatio of i (i itself when d_i = 1), one
+ * per integer and the remaining degree + 1 - (2K - 1) handed out greedily to
+ * the largest bound dev^d_i / 2^(d_i - 1) prod_{j != i} |i - j|^d_j -- as
+ * Chebyshev coefficients of u = x / K on [-1, 1].  Computed here in binary128
+ * by Newton's divided differences and a change of basis (the library solves
+ * the interpolation system instead, hostmath.cpp cos_discrete_cheb). */
+typedef __float128 q128;
+static const q128 Q_PI = (q128)3.141592653589793 + (q128)1.2246467991473532e-16 + (q128)-2.9947698097183397e-33;
+static q128 q_cos(q128 x) { /* reduce into [-pi, pi], then Taylor */
+  const long double k = roundl((long double)(x / (2 * Q_PI)));
+  x -= (q128)k * 2 * Q_PI;
+  q128 x2 = x * x, t = 1, s = 1;
+  for (int i = 1; i < 60; i++) {
+    t = -t * x2 / (q128)((2 * i - 1) * (2 * i));
+    s += t;
+    if ((t < 0 ? -t : t) < (q128)ldexpl(1.0L, -124)) break;
+  }
+  return s;
+}
+static q128 q_sqrt(q128 v) {
+  q128 y = (q128)sqrtl((long double)v);
+  for (int i = 0; i < 3; i++) y = (y + v / y) / 2;
+  return y;
+}
 void oracle_btp_cos(int K, int degree, int r, long double *c) {
-  const long double a = powl(2 * BTP_PI, -1.0L / (long double)(1 << r));
-  const int m = degree + 1;
-  long double *fx = (long double *)malloc(sizeof(long double) * m);
-  for (int k = 0; k < m; k++) {
-    const long double u = cosl(BTP_PI * (k + 0.5L) / m);
-    fx[k] = a * cosl(2 * BTP_PI * (K * u - 0.25L) / (long double)(1 << r));
+  const int n = degree + 1;
+  const double dev = ldexp(1.0, -BTP_LOGMSG);
+  int *d = (int *)malloc(sizeof(int) * K);
+  for (int i = 0; i < K; i++) d[i] = 1;
+  int tot = 2 * K - 1;
+  while (tot < n) {
+    int best = -1;
+    long double bb = 0;
+    for (int i = 0; i < K; i++) {
+      if (i > 0 && tot + 2 > n) continue;
+      long double lb = d[i] * log2l((long double)dev) - (d[i] - 1);
+      for (int j = -(K - 1); j < K; j++)
+        if (j != i) lb += d[j < 0 ? -j : j] * log2l((long double)(i > j ? i - j : j - i));
+      if (best < 0 || lb > bb) best = i, bb = lb;
+    }
+    d[best] += 1;
+    tot += best == 0 ? 1 : 2;
   }
-  for (int j = 0; j < m; j++) {
-    long double acc = 0;
-    for (int k = 0; k < m; k++) acc += fx[k] * cosl(BTP_PI * j * (k + 0.5L) / m);
-    c[j] = acc * (j == 0 ? 1.0L : 2.0L) / m;
+  q128 *x = (q128 *)malloc(sizeof(q128) * n), *g = (q128 *)malloc(sizeof(q128) * n);
+  int m = 0;
+  for (int i = -(K - 1); i < K && m < n; i++) {
+    const int di = d[i < 0 ? -i : i];
+    for (int j = 0; j < di; j++)
+      x[m++] = di == 1 ? (q128)i : (q128)i + (q128)dev * q_cos(Q_PI * (q128)(2 * j + 1) / (q128)(2 * di));
   }
-  free(fx);
+  q128 a = 1 / (2 * Q_PI);
+  for (int i = 0; i < r; i++) a = q_sqrt(a);
+  for (int k = 0; k < n; k++) g[k] = a * q_cos(2 * Q_PI * (x[k] - (q128)0.25) / (q128)(1 << r));
+  /* divided differences: g[k] = f[x_0 .. x_k] */
+  for (int lvl = 1; lvl < n; lvl++)
+    for (int k = n - 1; k >= lvl; k--) g[k] = (g[k] - g[k - 1]) / (x[k] - x[k - lvl]);
+  /* Horner in the Chebyshev basis of u = x / K: P <- P (K u - x_k) + g_k,
+   * u T_0 = T_1, u T_j = (T_{j+1} + T_{j-1}) / 2 */
+  q128 *P = (q128 *)calloc(n + 1, sizeof(q128)), *T = (q128 *)calloc(n + 1, sizeof(q128));
+  P[0] = g[n - 1];
+  for (int k = n - 2; k >= 0; k--) {
+    for (int j = 0; j <= n; j++) T[j] = 0;
+    for (int j = 0; j < n - 1 - k; j++) { /* K u P */
+      if (j == 0) {
+        T[1] += (q128)K * P[0];
+      } else {
+        T[j + 1] += (q128)K * P[j] / 2;
+        T[j - 1] += (q128)K * P[j] / 2;
+      }
+    }
+    for (int j = 0; j < n - 1 - k; j++) T[j] -= x[k] * P[j];
+    T[0] += g[k];
+    for (int j = 0; j <= n; j++) P[j] = T[j];
+  }
+  for (int j = 0; j < n; j++) c[j] = (long double)P[j];
+  free(d), free(x), free(g), free(P), free(T);
 }
 
 /* a diagonal map: offset (mod n slots) -> n complex values, NULL if absent;
@@ -2048,15 +2112,22 @@ static int btp_eval_mod(const oracle_ctx *bc, const oracle_btp_circuit *C, const
 }
 
 int oracle_bootstrap(const oracle_ctx *sc, const oracle_ctx *bc, const oracle_btp_circuit *C, const oracle_btp *P,
-                     int level, const u64 *ct, u64 *out) {
+                     int level, long double scale, const u64 *ct, u64 *out, long double *out_scale) {
   const int N = bc->N, Ls = sc->L, top = bc->L - 1;
   if (sc->N != N || sc->mod[0] != bc->mod[0] || C->top != top) return -1;
   if (!P->d2s || !P->s2d || !P->rlk) return -1;
   const u64 q0 = bc->mod[0];
-  /* ScaleDown: F times the level-0 residues (NTT domain) */
+  /* ScaleDown (Lattigo ScaleDown [U]): F = round(q0 / (2^LogMessageRatio
+   * scale)) from the input's own scale, so the message sits 2^-8 below q0
+   * whatever its scale; the circuit's SlotsToCoeffs constant carries the
+   * default scale's F, so the output scale is scale F / C->F (the input scale
+   * exactly when it is the default) */
+  const long double fr = roundl((long double)q0 / ldexpl(scale, BTP_LOGMSG));
+  const u64 F = fr < 1 ? 1 : (u64)fr;
+  if (out_scale) *out_scale = scale * (long double)F / (long double)C->F;
   u64 *x = (u64 *)malloc(sizeof(u64) * 2 * N);
   for (int comp = 0; comp < 2; comp++)
-    for (int i = 0; i < N; i++) x[(size_t)comp * N + i] = mulmod(ct[(size_t)comp * (level + 1) * N + i], C->F % q0, q0);
+    for (int i = 0; i < N; i++) x[(size_t)comp * N + i] = mulmod(ct[(size_t)comp * (level + 1) * N + i], F % q0, q0);
   /* EvkDenseToSparse at level 0 */
   {
     u64 *k0 = (u64 *)malloc(sizeof(u64) * N), *k1 = (u64 *)malloc(sizeof(u64) * N);

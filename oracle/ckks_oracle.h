@@ -209,10 +209,12 @@ typedef struct oracle_btp {
   const uint64_t *const *gks;
   const uint64_t *d2s, *s2d; /* EvkDenseToSparse (level 0), EvkSparseToDense */
 } oracle_btp;
-/* ct: [2][level+1][N] (scheme); out: [2][L_scheme][N] at the residual top
- * level.  Returns 0, or -1 when a key is missing or a level does not match. */
+/* ct: [2][level+1][N] (scheme) at `scale`; out: [2][L_scheme][N] at the
+ * residual top level, at *out_scale (= scale when it is the default scale;
+ * ScaleDown's F comes from the input scale).  Returns 0, or -1 when a key is
+ * missing or a level does not match. */
 int oracle_bootstrap(const oracle_ctx *sc, const oracle_ctx *bc, const oracle_btp_circuit *C, const oracle_btp *P,
-                     int level, const uint64_t *ct, uint64_t *out);
+                     int level, long double scale, const uint64_t *ct, uint64_t *out, long double *out_scale);
 
 /* coefficient-wise helpers used by tests */
 void oracle_mul_coeffs(const oracle_ctx *ctx, const int *mods, int nl,

@@ -74,7 +74,8 @@ def _load():
         "oracle_eval_poly_ldp": (ctypes.c_int, [vp, ctypes.c_int, _u64p, ctypes.POINTER(ctypes.c_longdouble), _dblp,
                                                 ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_longdouble), _u64p,
                                                 _u64p, ctypes.POINTER(ctypes.c_longdouble)]),
-        "oracle_bootstrap": (ctypes.c_int, [vp, vp, vp, ctypes.POINTER(OracleBtp), ctypes.c_int, _u64p, _u64p]),
+        "oracle_bootstrap": (ctypes.c_int, [vp, vp, vp, ctypes.POINTER(OracleBtp), ctypes.c_int, ctypes.c_longdouble,
+                                            _u64p, _u64p, ctypes.POINTER(ctypes.c_longdouble)]),
         "oracle_btp_chain": (ctypes.c_int, [ctypes.c_int, _u64p, ctypes.c_int, ctypes.c_int, _intp, ctypes.c_int,
                                             _u64p]),
         "oracle_btp_cos": (None, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_longdouble)]),
@@ -305,12 +306,13 @@ class Oracle:
             raise ValueError("level < depth")
         return out[:2 * (lv + 1) * self.N].reshape(2, lv + 1, self.N).copy(), lv, osc.value
 
-    def bootstrap(self, boot, circuit, keys, ct, level):
+    def bootstrap(self, boot, circuit, keys, ct, level, scale):
         """Bootstrap restated (oracle_bootstrap): self = the scheme's oracle,
         boot = the bootstrapping chain's oracle, circuit = BtpCircuit (the
         oracle's own constants and diagonals), keys = dict(rlk, gks {galEl:
-        key}, d2s, s2d) of the bootstrapping chain, ct [2][level+1][N].
-        Returns [2][L][N] at the residual top level."""
+        key}, d2s, s2d) of the bootstrapping chain, ct [2][level+1][N] at
+        `scale`.  Returns ([2][L][N] at the residual top level, its scale as
+        numpy longdouble)."""
         keep = []
 
         def u64arr(a):
@@ -327,10 +329,12 @@ class Oracle:
         P.d2s, P.s2d = u64arr(keys["d2s"]), u64arr(keys["s2d"])
         ct = np.ascontiguousarray(ct, dtype=np.uint64)
         out = np.zeros((2, self.L, self.N), dtype=np.uint64)
-        rc = lib().oracle_bootstrap(self._h, boot._h, circuit._h, ctypes.byref(P), level, _p(ct), _p(out))
+        osc = ctypes.c_longdouble(0)
+        rc = lib().oracle_bootstrap(self._h, boot._h, circuit._h, ctypes.byref(P), level, ctypes.c_longdouble(scale),
+                                    _p(ct), _p(out), ctypes.byref(osc))
         if rc != 0:
             raise ValueError("oracle_bootstrap: missing key or level mismatch")
-        return out
+        return out, np.longdouble(osc.value)
 
     def eval_poly_ld(self, ct, level, scale, coeffs, cheb, target, rlk):
         """eval_poly with 80-bit scales (numpy longdouble in and out, not via double)."""

@@ -290,8 +290,8 @@ class CpuStream:
             elif op == "Bootstrap":
                 x, l, s = cts[a[0]]
                 boot, circ, keys = self.bootstrappers[a[1]]
-                y = o.bootstrap(boot, circ, keys, np.ascontiguousarray(x[:, :l + 1]), l)
-                cts[ret] = (y, self.L - 1, s)
+                y, ys = o.bootstrap(boot, circ, keys, np.ascontiguousarray(x[:, :l + 1]), l, s)
+                cts[ret] = (y, self.L - 1, LD(ys))
             else:
                 raise RuntimeError(f"cpu replay: unsupported op {op}")
             if stop_after is not None and fi == stop_after:

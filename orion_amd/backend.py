@@ -179,6 +179,7 @@ SIGNATURES = {
     "ImportKeyBundle": ([c_void_p, c_ulong], c_int),
     "OrionHipProfile": ([c_int], None),
     "OrionHipProfileRead": ([c_char_p, P(ctypes.c_long), P(c_double), P(c_double), c_int], c_int),
+    "OrionHipProfileReadStrict": ([P(c_double), c_int], c_int),
     "OrionHipProfileReset": ([], None),
     "OrionHipNTT": ([P(c_ulong), c_int, c_int, P(c_int), c_int], c_int),
 }
@@ -214,7 +215,10 @@ def load_library(path=LIB_PATH):
         raise RuntimeError(
             f"HIP backend library not found at {path}: build it with "
             "`python orion_amd/build.py` (no CPU fallback exists)")
-    import torch  # noqa: F401  (one HIP runtime per process; see above)
+    try:
+        import torch  # noqa: F401  (one HIP runtime per process; see above)
+    except ImportError:  # no torch: this library's own runtime is the only one
+        pass
     lib = ctypes.CDLL(path)
     rt = _hip_runtimes()
     if len(rt) > 1:
@@ -515,11 +519,14 @@ class HipLibrary:
         launches = (ctypes.c_long * n)()
         ms = (c_double * n)()
         byts = (c_double * n)()
+        strict = (c_double * n)()
         k = self.lib.OrionHipProfileRead(names, launches, ms, byts, n)
+        self.lib.OrionHipProfileReadStrict(strict, n)
         out = {}
         for i in range(max(k, 0)):
             nm = names.raw[32 * i:32 * i + 32].split(b"\0")[0].decode()
-            out[nm] = dict(launches=int(launches[i]), ms=float(ms[i]), bytes=float(byts[i]))
+            out[nm] = dict(launches=int(launches[i]), ms=float(ms[i]), bytes=float(byts[i]),
+                           strict_bytes=float(strict[i]))
         return out
 
     def _chk(self, rc, name):

@@ -218,6 +218,10 @@ struct Ciphertext {
   Poly poly;
   int level = 0;
   long double scale = 1;
+  // copy-on-write: handles made by RescaleNew share the rescaled input's
+  // buffer (Lattigo returns a copy, evaluator.go:92-99); the first in-place op
+  // on either one, while both are alive, copies it first (Context::inplace_ct)
+  std::shared_ptr<char> share;
 };
 
 struct Plaintext {
@@ -303,7 +307,7 @@ class HandlePool {  // lowest-free-id reuse (minheap.go:46-64)
 struct ProfRec {
   int cat;
   hipEvent_t e0, e1;
-  double bytes;
+  double bytes, strict;
 };
 static const char* kProfNames[] = {"ntt_fwd", "ntt_inv", "elementwise", "basis_ext", "ks_mac", "automorph",
                                    "tensor", "rescale_prep", "lt_bsgs", "lt_giant", "ntt_bext"};
@@ -373,7 +377,10 @@ struct Context {
   unsigned prof = 0;  // bit mask of profiled kernel categories
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> ev_free;
-  double prof_launch[P_NCAT] = {0}, prof_ms[P_NCAT] = {0}, prof_bytes[P_NCAT] = {0};
+  // prof_bytes: the kernel's algorithmic bytes (for the NTT: 16 N per
+  // limb-transform + 8 N per epilogue operand or addend it reads, the
+  // "fused" model); prof_strict: SURVEY §8d's 16 N per limb-transform alone
+  double prof_launch[P_NCAT] = {0}, prof_ms[P_NCAT] = {0}, prof_bytes[P_NCAT] = {0}, prof_strict[P_NCAT] = {0};
 
   ~Context() {
     hipDeviceSynchronize();
@@ -423,9 +430,9 @@ struct Context {
   struct Scope {
     Context* c;
     int cat;
-    double bytes;
+    double bytes, strict;
     hipEvent_t e0 = nullptr;
-    Scope(Context* ctx, int k, double b) : c(ctx), cat(k), bytes(b) {
+    Scope(Context* ctx, int k, double b, double st = -1) : c(ctx), cat(k), bytes(b), strict(st < 0 ? b : st) {
       if (c->prof & (1u << cat)) {
         e0 = c->ev();
         hipEventRecord(e0, c->stream);
@@ -435,7 +442,7 @@ struct Context {
       if (e0) {
         hipEvent_t e1 = c->ev();
         hipEventRecord(e1, c->stream);
-        c->prof_recs.push_back(ProfRec{cat, e0, e1, bytes});
+        c->prof_recs.push_back(ProfRec{cat, e0, e1, bytes, strict});
         if (c->prof_recs.size() > 20000) c->prof_flush();
       }
     }
@@ -449,6 +456,7 @@ struct Context {
       prof_launch[r.cat] += 1;
       prof_ms[r.cat] += ms;
       prof_bytes[r.cat] += r.bytes;
+      prof_strict[r.cat] += r.strict;
       ev_free.push_back(r.e0);
       ev_free.push_back(r.e1);
     }
@@ -551,14 +559,49 @@ struct Context {
   // older handle a replay would apply the op again to its own output, and the
   // handle's level and scale would advance once (at capture) while its data
   // changes at every launch
-  Ciphertext& inplace_ct(int id) {
+  // a ciphertext an op is about to modify in place; cow = false: the caller
+  // replaces the whole buffer (no copy of a shared one is needed)
+  Ciphertext& inplace_ct(int id, bool cow = true) {
     Ciphertext& a = cts.get(id);
     if (capturing && !capture_born.count(id))
       throw std::runtime_error("in-place op on ciphertext " + std::to_string(id) +
                                ", which predates the graph capture (a replay would reapply it): clone it inside the "
                                "capture first");
+    if (cow && a.share) {
+      if (a.share.use_count() > 1) a.poly = clone(a).poly;  // the other handle keeps the old buffer
+      a.share.reset();
+    }
     return a;
   }
+  // RescaleNew's result: a second handle on a's (just rescaled) buffer, when
+  // nothing else (a captured graph) holds that buffer
+  Ciphertext alias(Ciphertext& a) {
+    if (!defer_on || !a.poly.buf || a.poly.buf.use_count() != 1) return clone(a);
+    if (!a.share) a.share = std::make_shared<char>(0);
+    Ciphertext y;
+    y.poly = a.poly;
+    y.level = a.level;
+    y.scale = a.scale;
+    y.share = a.share;
+    return y;
+  }
+
+  // -- deferred rotate-and-add, behind the unchanged C-ABI -------------------
+  // The frontend's `out += out.roll(k)` (linear.py:72-73 -> tensors.py:244-258,
+  // :139-167) issues RotateNew(x, k) -> r, AddCiphertext(x, r) and, when the
+  // temporary CipherTensor dies, DeleteCiphertext(r).  RotateNew only records
+  // the rotation (r gets its metadata, no buffer); the AddCiphertext that adds
+  // r into its own source records the sum; when r is then deleted unread, the
+  // pair runs as one key switch whose ModDown store adds into x
+  // (rotate_add_inplace), and r's contents are never formed.  Any other C-ABI
+  // call first runs what is pending as the op-by-op path would (defer_flush
+  // at the API layer).  ORION_DEFER=0 turns this and RescaleNew's aliasing off.
+  struct Deferred {
+    int kind = 0;  // 1: r = Rotate(x, k) pending; 2: and x += r pending
+    int x = -1, r = -1, k = 0;
+  };
+  Deferred dfr;
+  bool defer_on = getenv("ORION_DEFER") ? atoi(getenv("ORION_DEFER")) != 0 : true;
 
   // lazily built tables, keys and host transfers synchronise, which would
   // invalidate an open capture (and leave HIP's stream state unusable): refuse
@@ -826,10 +869,14 @@ struct Context {
   void ntt_io(NttIO io, bool inv, double src_per_job = 0) {
     prep_io(io);
     const bool bx = io.pro == NTT_PRO_BEXT;
-    // (+ 8 N for the subtract-and-scale operand, + 4 N for an automorphism's
-    // scatter index, + 8 N for the word it is added to)
+    // fused model: + 8 N for the subtract-and-scale operand, + 8 N for the word
+    // a rotate-and-add store adds to; an automorphism's scatter index is a
+    // table shared by every limb and image of the Galois element, amortised
+    // like the twiddles and not counted.  strict: 16 N per
+    // limb-transform, whatever the prologue and epilogue read
     const double per = (bx ? (src_per_job + 1) * 8.0 * N : 16.0 * N) + (io.epi != NTT_EPI_STORE ? 8.0 * N : 0.0) +
-                       (epi_aut(io.epi) ? 4.0 * N : 0.0) + (io.epi == NTT_EPI_SUBSCALE_AUT_ACC ? 8.0 * N : 0.0);
+                       (io.epi == NTT_EPI_SUBSCALE_AUT_ACC ? 8.0 * N : 0.0);
+    const double strict = 16.0 * N;
     const int cat = bx ? P_NTT_BEXT : inv ? P_NTT_INV : P_NTT_FWD;
     if (two_pass(io.jobs, inv, io.pro, io.epi, io.epi != NTT_EPI_STORE && io.ex.p == io.dst.p)) {
       Poly scratch;
@@ -838,7 +885,7 @@ struct Context {
         scratch = alloc(1, 1, chunk);
         io.mid = ls(scratch, 0, 1, {0}, {0});
         io.mid_compact = 1;
-        Scope sc(this, cat, per * io.jobs);
+        Scope sc(this, cat, per * io.jobs, strict * io.jobs);
         for (int j0 = 0; j0 < io.jobs; j0 += chunk) {
           io.job0 = j0;
           io.njob = std::min(chunk, io.jobs - j0);
@@ -857,7 +904,7 @@ struct Context {
         scratch = alloc(io.dst.ncomp, io.dst.nlimb, io.dst.nbatch);
         io.mid = ls(scratch, 0, io.dst.ncomp, iota(0, io.dst.nlimb), std::vector<int>(io.dst.mod, io.dst.mod + io.dst.nlimb));
       }
-      Scope sc(this, cat, per * io.jobs);
+      Scope sc(this, cat, per * io.jobs, strict * io.jobs);
       const bool small = io.jobs <= ntt2s_below;
       if (io.ifuse && !small) throw std::runtime_error("NTT: a fused INTT columns pass needs the latency kernels");
       if (small ? orion_launch_ntt2s(logN, io, d_tb, inv, stream) : orion_launch_ntt2(logN, io, d_tb, inv, stream))
@@ -872,7 +919,7 @@ struct Context {
       // the whole rounds on the one-pass kernel, the partial last round (the
       // fast float64 limbs: job order 2) on the two-pass kernels, which scale
       // with the job count instead of costing a whole limb's latency on every CU
-      Scope sc(this, cat, per * io.jobs);
+      Scope sc(this, cat, per * io.jobs, strict * io.jobs);
       NttIO a = io;
       a.njob = io.jobs - tail;
       if (orion_launch_ntt_io(logN, a, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
@@ -896,7 +943,7 @@ struct Context {
     }
     // algorithmic bytes per limb-transform: read + write the limb (16 N), + 8 N
     // for the epilogue's second operand (per, above)
-    Scope sc(this, cat, per * io.dst.ncomp * io.dst.nlimb * io.dst.nbatch);
+    Scope sc(this, cat, per * io.dst.ncomp * io.dst.nlimb * io.dst.nbatch, strict * io.dst.ncomp * io.dst.nlimb * io.dst.nbatch);
     if (orion_launch_ntt_io(logN, io, d_tb, inv, stream)) throw std::runtime_error("NTT launch failed");
     log_ntt(1, io, inv);
   }
@@ -1367,6 +1414,12 @@ struct Context {
     rlk = gen_evk(s2, sk, L - 1);
     have_rlk = true;
   }
+  // LoadRotationKey's whole keys, for the ones it cut on the device
+  struct HostKey {
+    int level = 0;
+    std::vector<u64> words;  // [digit][2][level+1+K][N]
+  };
+  std::map<u64, HostKey> gk_host;
   int hinted_level(u64 g) const {
     auto it = key_hint.find(g);
     return it == key_hint.end() ? L - 1 : it->second;
@@ -1376,6 +1429,16 @@ struct Context {
   void gen_galois(u64 g, int level) {
     auto have = gks.find(g);
     if (have != gks.end() && have->second.level >= level) return;
+    auto hk = gk_host.find(g);
+    if (hk != gk_host.end() && hk->second.level >= level) {  // a loaded key, cut at load: the whole key
+      no_capture("uploading a loaded rotation key past its cut level");
+      const int kl = hk->second.level, kb = (kl + 1 + K - 1) / K;
+      Poly k = alloc(2 * kb, kl + 1 + K, 1);
+      upload(k, hk->second.words);
+      gks[g] = EvKey{k, kl};
+      gk_host.erase(hk);
+      return;
+    }
     if (!have_sk)
       throw std::runtime_error(have == gks.end() ? "secret key not generated"
                                                  : "galois key " + std::to_string(g) + " covers level " +
@@ -1700,6 +1763,15 @@ struct Context {
   }
 
   Ciphertext rotate(const Ciphertext& a, int k) { return apply_galois(a, galois_element(k)); }
+  // sigma_{5^k}(a) into out's buffer (allocated here when it has none)
+  void rotate_into(const Ciphertext& a, int k, Ciphertext& out) {
+    const u64 g = galois_element(k);
+    const int level = a.level, B = a.poly.B;
+    const EvKey& key = galois_key(g, level);
+    if (!out.poly.buf) out.poly = new_ct(level, B, a.scale).poly;
+    out.level = level;
+    keyswitch(lsq(a.poly, 1, 1, level), level, B, key.k, key.level, out.poly, a.poly.ptr(), nullptr, g);
+  }
   // sigma_g(a): key switch of c1 with the Galois key of g, + c0, NTT-domain permutation
   // (g = 2N - 1 is the complex conjugation of the slots)
   Ciphertext apply_galois(const Ciphertext& a, u64 g) {
@@ -1788,6 +1860,7 @@ struct Context {
     // run its slots without per-slot branches (LT_DENSE; the products with it
     // add zero)
     {
+      if (T.sdiags.empty()) throw std::runtime_error("linear transform has no diagonals loaded");
       const Poly& any = T.sdiags.begin()->second;
       Poly z = alloc(any.ncomp, any.nlimb, any.B);
       HIPCHK(hipMemsetAsync(z.ptr(), 0, (size_t)any.ncomp * any.nlimb * any.B * N * sizeof(u64), stream));
@@ -2476,25 +2549,14 @@ struct Context {
     B->slots = ns;
     B->gap = n / ns;
     const long double PI = 3.14159265358979323846264338327950288L;
-    // EvalMod: the Chebyshev interpolant of a cos(2 pi (K u - 1/4) / 2^r) at
-    // the degree+1 Chebyshev nodes of [-1, 1], a = (2 pi)^(-1/2^r); after the r
-    // double angles y <- 2 y^2 - a^(2^(i+1)) it is sin(2 pi x) / (2 pi)
+    // EvalMod: Lattigo's default Mod1Type CosDiscrete [U] -- a cos(2 pi (x -
+    // 1/4) / 2^r), a = (2 pi)^(-1/2^r), interpolated at nodes on the integers
+    // the ModRaise overflow takes (x = K u; hostmath.cpp cos_discrete_cheb,
+    // nodes within 2^-LogMessageRatio of each integer); after the r double
+    // angles y <- 2 y^2 - a^(2^(i+1)) it is sin(2 pi x) / (2 pi)
     const long double a = powl(2 * PI, -1.0L / (long double)(1 << B->r));
-    {
-      const int d = B->degree, m = d + 1;
-      std::vector<long double> fx(m), c(m, 0);
-      for (int k = 0; k < m; ++k) {
-        const long double u = cosl(PI * (k + 0.5L) / m);
-        fx[k] = a * cosl(2 * PI * (B->K * u - 0.25L) / (long double)(1 << B->r));
-      }
-      for (int j = 0; j < m; ++j) {
-        long double acc = 0;
-        for (int k = 0; k < m; ++k) acc += fx[k] * cosl(PI * j * (k + 0.5L) / m);
-        c[j] = acc * (j == 0 ? 1.0L : 2.0L) / m;
-      }
-      B->cosp.cheb = true;
-      B->cosp.c = c;
-    }
+    B->cosp.cheb = true;
+    B->cosp.c = cos_discrete_cheb(B->K, B->degree, B->r, ldexp(1.0, -BT::kLogMsgRatio));
     {
       long double v = a;
       for (int i = 0; i < B->r; ++i) B->dac.push_back(v = v * v);
@@ -2714,13 +2776,19 @@ struct Context {
     if (it == btps.end()) throw std::runtime_error("no bootstrapper found for slot count: " + std::to_string(ns));
     Bootstrapper& bt = *it->second;
     const int B = in.poly.B;
-    // ScaleDown: F times the level-0 residues (an integer: no level)
+    // ScaleDown (Lattigo ScaleDown [U]): F = round(q0 / (2^LogMessageRatio
+    // scale)) times the level-0 residues (an integer: no level), F from the
+    // input's own scale so the message sits 2^-8 below q0 whatever its scale;
+    // SlotsToCoeffs carries the default scale's F (bt.F), so the output scale
+    // is scale F / bt.F -- the input scale exactly when it is the default
+    const long double fr = roundl((long double)mods[0] / ldexpl(in.scale, Bootstrapper::kLogMsgRatio));
+    const u64 F = fr < 1 ? 1 : (u64)fr;
     Poly x = alloc(2, 1, B);
-    std::vector<u64> f{bt.F % mods[0]};
+    std::vector<u64> f{F % mods[0]};
     ew1(EW_SCALE, lsq(x, 0, 2, 0), lsq(in.poly, 0, 2, 0), &f);
     Ciphertext o = bt.bc->run_circuit(bt, x, B);
     if (o.level != L - 1) throw std::logic_error("bootstrapping circuit did not end at the residual top level");
-    Ciphertext out = new_ct(L - 1, B, in.scale);
+    Ciphertext out = new_ct(L - 1, B, in.scale * (long double)F / (long double)bt.F);
     // the residual limbs hold the same primes in both contexts
     const LimbSet ol = lsq(out.poly, 0, 2, L - 1);
     if (bt.gap > 1) {  // post-scale (an integer: no level)
@@ -2777,10 +2845,42 @@ static void capture_guard(const char* fn) {
     throw std::runtime_error(std::string(fn) + " is not allowed while capturing a graph");
   if (g_debug_sync && g && !g->capturing && g->stream) (void)hipStreamSynchronize(g->stream);
 }
+static int ct_ct_op(int i0, int i1, int op, bool inplace);
+// runs a deferred rotation (and the addition recorded after it) exactly as
+// the op-by-op calls would have (Context::Deferred)
+static void defer_flush() {
+  if (!g || !g->dfr.kind) return;
+  Context& c = *g;
+  const Context::Deferred d = c.dfr;
+  c.dfr = Context::Deferred();
+  c.rotate_into(c.cts.get(d.x), d.k, c.cts.get(d.r));
+  if (d.kind == 2) ct_ct_op(d.x, d.r, EW_ADD, true);
+}
+// C-ABI calls that leave a pending rotation pending: host metadata reads
+// (the deferred result has its level, scale and batch already), error
+// strings, and the calls that match it themselves (AddCiphertext,
+// DeleteCiphertext); every other call runs it first
+static bool defer_keeps(const char* fn) {
+  static const std::set<std::string> keep = {
+      "AddCiphertext", "DeleteCiphertext", "DeletePlaintext", "GetCiphertextScale", "GetCiphertextScaleF",
+      "GetCiphertextLevel", "GetCiphertextSlots", "GetCiphertextDegree", "GetCiphertextBatch", "GetPlaintextScale",
+      "GetPlaintextLevel", "GetPlaintextSlots", "GetPlaintextBatch", "GetLiveCiphertexts", "GetLivePlaintexts",
+      "GetModuliChain", "GaloisElement"};
+  return keep.count(fn) != 0;
+}
+static void defer_gate(const char* fn) {
+  if (!g || !g->dfr.kind) return;
+  if (!strcmp(fn, "NewScheme") || !strcmp(fn, "DeleteScheme")) {  // the scheme and its handles go away
+    g->dfr = Context::Deferred();
+    return;
+  }
+  if (!defer_keeps(fn)) defer_flush();
+}
 #define API_BEGIN                                  \
   std::lock_guard<std::recursive_mutex> lk_(g_mu); \
   try {                                            \
-    capture_guard(__func__);
+    capture_guard(__func__);                       \
+    defer_gate(__func__);
 #define API_END(errval)          \
   }                              \
   catch (const std::exception& e) { \
@@ -2926,7 +3026,17 @@ void DeletePlaintext(int id) {
 }
 void DeleteCiphertext(int id) {
   API_BEGIN
-  ctx().cts.del(id);
+  Context& c = ctx();
+  const Context::Deferred d = c.dfr;
+  if (d.kind && id == d.r) {
+    c.dfr = Context::Deferred();
+    // the rotation dies unread: kind 1 needs no work at all; kind 2 is
+    // x += Rotate(x, k) with the addition in the key switch's store
+    if (d.kind == 2) c.rotate_add_inplace(c.cts.get(d.x), d.k);
+  } else if (d.kind && id == d.x) {
+    defer_flush();
+  }
+  c.cts.del(id);
   API_END_VOID
 }
 
@@ -3209,7 +3319,7 @@ int Negate(int id) {
 int Rotate(int id, int k) {
   API_BEGIN
   Context& c = ctx();
-  Ciphertext& a = c.inplace_ct(id);
+  Ciphertext& a = c.inplace_ct(id, false);  // the rotation replaces a (buffer and copy-on-write share)
   a = c.rotate(a, k);
   return id;
   API_END(-1)
@@ -3217,7 +3327,18 @@ int Rotate(int id, int k) {
 int RotateNew(int id, int k) {
   API_BEGIN
   Context& c = ctx();
-  return c.cts.add(c.rotate(c.cts.get(id), k));
+  Ciphertext& a = c.cts.get(id);
+  if (!c.defer_on) return c.cts.add(c.rotate(a, k));
+  // deferred (Context::Deferred): the key is made (or checked) now, so a
+  // missing key fails here as in the op-by-op path; r gets no buffer yet
+  c.galois_key(c.galois_element(k), a.level);
+  Ciphertext r;
+  r.level = a.level;
+  r.scale = a.scale;
+  r.poly.B = a.poly.B;
+  const int rid = c.cts.add(std::move(r));
+  c.dfr = Context::Deferred{1, id, rid, k};
+  return rid;
   API_END(-1)
 }
 int OrionHipRotateAdd(int id, int k) {
@@ -3239,7 +3360,7 @@ int RescaleNew(int id) {  // evaluator.go:92-99: rescales the input in place, re
   Context& c = ctx();
   Ciphertext& a = c.inplace_ct(id);
   c.rescale_inplace(a);
-  return c.cts.add(c.clone(a));
+  return c.cts.add(c.alias(a));  // copy-on-write: the copy is made only if both are later written
   API_END(-1)
 }
 
@@ -3422,6 +3543,13 @@ static int ct_ct_op(int i0, int i1, int op, bool inplace) {
 }
 int AddCiphertext(int a, int b) {
   API_BEGIN
+  Context& c = ctx();
+  if (c.dfr.kind == 1 && a == c.dfr.x && b == c.dfr.r) {  // x += (pending) Rotate(x, k): record the sum
+    c.inplace_ct(a);
+    c.dfr.kind = 2;
+    return a;
+  }
+  defer_flush();
   return ct_ct_op(a, b, EW_ADD, true);
   API_END(-1)
 }
@@ -3443,7 +3571,7 @@ int SubCiphertextNew(int a, int b) {
 int MulRelinCiphertext(int a, int b) {
   API_BEGIN
   Context& c = ctx();
-  c.inplace_ct(a);
+  c.inplace_ct(a, false);  // the product replaces a (buffer and copy-on-write share)
   Ciphertext r = c.mul_relin(c.cts.get(a), c.cts.get(b));
   if (r.poly.B != c.cts.get(a).poly.B) throw std::runtime_error("in-place op cannot grow the batch");
   c.cts.get(a) = std::move(r);
@@ -3643,7 +3771,12 @@ void LoadRotationKey(char* data, unsigned long len, unsigned long galEl) {
       memcpy(dst, src, sizeof(u64) * (size_t)(tl + 1) * c.N);
       memcpy(dst + (size_t)(tl + 1) * c.N, src + (size_t)(level + 1) * c.N, sizeof(u64) * (size_t)c.K * c.N);
     }
-    host.swap(sc);
+    // the whole key stays in host memory (as Lattigo keeps it,
+    // lineartransform.go:143-159): a later use above tl uploads it whole
+    c.gk_host[galEl] = Context::HostKey{level, std::move(host)};
+    host = std::move(sc);
+  } else {
+    c.gk_host.erase(galEl);
   }
   Poly k = c.alloc(2 * tbeta, tl + 1 + c.K, 1);
   c.upload(k, host);
@@ -3700,6 +3833,7 @@ void RemovePlaintextDiagonals(int tid) {
 void RemoveRotationKeys(void) {
   API_BEGIN
   ctx().gks.clear();
+  ctx().gk_host.clear();
   API_END_VOID
 }
 
@@ -3742,16 +3876,16 @@ int EvaluatePolynomial(int ct, int poly, unsigned long outScale) {
   API_END(-1)
 }
 // polyeval.go:91-167: composite minimax sign coefficients (compile-time, host),
-// cached per (degrees, prec, logalpha, logerr) like minimaxSignMap; the last
-// polynomial is mapped from [-1, 1] to [0, 1] (halved, + 0.5, inside
-// minimax_sign_composite).  The Remez restatement works in binary128 whatever
-// `prec` asks for: at prec >= 113 (orion's default is 128) the doubles are the
-// prec-bit computation's (tests/golden/minimax_sign.json).
+// cached per (degrees, prec, logalpha, logerr) like minimaxSignMap; every fit
+// absorbs the scheme error 2^-logerr, and the last polynomial is mapped from
+// [-1, 1] to [0, 1] (halved, + 0.5, inside minimax_sign_composite).  The Remez
+// restatement works in binary128 / double-binary128 whatever `prec` asks for:
+// at prec >= 113 (orion's default is 128) the doubles are the prec-bit
+// computation's (tests/golden/minimax_sign.json).
 static std::map<std::string, std::vector<double>> g_minimax_cache;
 ArrayResultDouble GenerateMinimaxSignCoeffs(int* degrees, int n, int prec, int logalpha, int logerr, int debug) {
   ArrayResultDouble r{nullptr, 0};
   API_BEGIN
-  (void)debug;
   std::vector<int> deg;
   for (int i = 0; i < n; ++i) deg.push_back(degrees[i]);
   if (deg.empty()) throw std::runtime_error("at least one degree is required");
@@ -3760,7 +3894,7 @@ ArrayResultDouble GenerateMinimaxSignCoeffs(int* degrees, int n, int prec, int l
   key += "|" + std::to_string(prec) + "|" + std::to_string(logalpha) + "|" + std::to_string(logerr);
   auto it = g_minimax_cache.find(key);
   if (it == g_minimax_cache.end()) {
-    std::vector<std::vector<double>> polys = minimax_sign_composite(deg, logalpha);
+    std::vector<std::vector<double>> polys = minimax_sign_composite(deg, logalpha, logerr, nullptr, debug != 0);
     std::vector<double> flat;
     for (auto& p : polys) flat.insert(flat.end(), p.begin(), p.end());
     it = g_minimax_cache.emplace(key, flat).first;
@@ -4199,7 +4333,7 @@ void OrionHipProfileReset(void) {
   API_BEGIN
   Context& c = ctx();
   c.prof_flush();
-  for (int i = 0; i < P_NCAT; ++i) c.prof_launch[i] = c.prof_ms[i] = c.prof_bytes[i] = 0;
+  for (int i = 0; i < P_NCAT; ++i) c.prof_launch[i] = c.prof_ms[i] = c.prof_bytes[i] = c.prof_strict[i] = 0;
   API_END_VOID
 }
 int OrionHipProfileRead(char* names, long* launches, double* ms, double* bytes, int max) {
@@ -4214,6 +4348,15 @@ int OrionHipProfileRead(char* names, long* launches, double* ms, double* bytes, 
     ms[i] = c.prof_ms[i];
     bytes[i] = c.prof_bytes[i];
   }
+  return n;
+  API_END(-1)
+}
+int OrionHipProfileReadStrict(double* strict, int max) {
+  API_BEGIN
+  Context& c = ctx();
+  c.prof_flush();
+  int n = std::min(max, (int)P_NCAT);
+  for (int i = 0; i < n; ++i) strict[i] = c.prof_strict[i];
   return n;
   API_END(-1)
 }

@@ -1,3 +1,4 @@
+#include <cstdio>
 // hostmath.cpp -- see hostmath.h.
 #include "hostmath.h"
 
@@ -247,38 +248,17 @@ int64_t Prng::gaussian(double sigma, double bound) {
 
 namespace orion {
 // ---------------------------------------------------------------------------
-// composite minimax approximation of sign (polyeval.go:91-167 ->
-// Lattigo v6 bignum.GenMinimaxCompositePolynomial [U], restated; the fixture
-// tests/golden/minimax_sign.json is the same construction at `prec` = 128
-// bits in mpmath, tools/gen_minimax.py):
-//   stage i: p_i = the odd minimax fit of 1 on [a_i, 1] (= the minimax
-//   approximation of sign on [-1, -a_i] U [a_i, 1], whose even Chebyshev
-//   coefficients vanish), degree d_i, error E_i; p_i /= 1 + E_i;
-//   a_{i+1} = (1 - E_i) / (1 + E_i); a_0 = 2^-logalpha.
-// The Remez exchange runs in binary128 (__float128, 113 bits: every stage's
-// minimax polynomial is unique, so once converged far below float64
-// resolution each coefficient rounds to the same double as the 128-bit
-// computation).
+// composite minimax approximation of sign (polyeval.go:91-167 -> Lattigo v6
+// circuits/ckks/minimax.GenMinimaxCompositePolynomial and utils/bignum.Remez
+// [U], restated below; the fixture tests/golden/minimax_sign.json is the same
+// construction at `prec` = 128 bits in mpmath, tools/gen_minimax.py).  The
+// Remez exchange runs in binary128 (__float128, 113 bits), its linear system
+// in double-binary128.
 // ---------------------------------------------------------------------------
 namespace {
 typedef __float128 qf;
 
 qf qabs(qf x) { return x < 0 ? -x : x; }
-// sum_k c_k T_{2k+1}(x) and its derivative (T_m' = m U_{m-1})
-void cheb_odd_eval(const std::vector<qf>& c, qf x, qf& s, qf& ds) {
-  qf t0 = 1, t1 = x, u0 = 1, u1 = 2 * x;
-  s = ds = 0;
-  size_t k = 0;
-  for (int m = 1; k < c.size(); ++m) {
-    if (m & 1) {
-      s += c[k] * t1;
-      ds += c[k] * m * u0;
-      ++k;
-    }
-    const qf t2 = 2 * x * t1 - t0, u2 = 2 * x * u1 - u0;
-    t0 = t1, t1 = t2, u0 = u1, u1 = u2;
-  }
-}
 // double-binary128 (~226 bits) for the Remez linear system alone: the last
 // stages fit 1 on a short interval near 1 (a = 0.952 for orion's ReLU), where
 // the Chebyshev columns are nearly dependent and binary128 loses the float64
@@ -353,103 +333,264 @@ std::vector<dq> solve(std::vector<std::vector<dq>> A) {
   }
   return x;
 }
-// Chebyshev-spaced point j of m on [a, 1] (the starting reference and the scan grid)
-qf cheb_pt(qf a, int j, int m) {
-  return (a + 1) / 2 - (1 - a) / 2 * (qf)cosl(3.14159265358979323846264338327950288L * j / m);
+// bignum.Remez [U] (Lattigo v6 utils/bignum/remez.go, the multi-interval
+// Remez of Lee et al., eprint 2020/552), restated: the degree-D approximation
+// of sign in the Chebyshev basis T_0 .. T_D evaluated at x itself (the basis
+// orion's GenerateChebyshev evaluates on [-1, 1], polyeval.go:49-60), D =
+// (nodes over all intervals) - 2:
+//   start: each interval's `nodes` Chebyshev points of the first kind;
+//   iterate (at most maxIters): solve p(x_i) + (-1)^i E = sign(x_i); take the
+//   extreme points of p - sign (each interval's ends and the zeros of p');
+//   drop same-signed neighbours but the larger; while more than D + 2 remain,
+//   drop the smaller end point when one too many, else the adjacent pair with
+//   the smallest |e_i| + |e_{i+1}|; MaxErr / MinErr = the largest / smallest
+//   |e| of the new nodes; stop once (MaxErr - MinErr) / MinErr <= threshold.
+// The coefficients returned are those of the last solve (the polynomial whose
+// extreme points MaxErr measured).
+struct RemezOut {
+  std::vector<dq> coeffs;  // T_0 .. T_D
+  qf maxerr = 0, minerr = 0;
+  int iters = 0;
+};
+// sum_j c_j T_j(x) and its derivative (T_j' = j U_{j-1})
+void cheb_eval_full(const std::vector<qf>& c, qf x, qf& s, qf& ds) {
+  qf t0 = 1, t1 = x, u0 = 1, u1 = 2 * x;  // T_0, T_1, U_0, U_1
+  s = c[0];
+  ds = 0;
+  for (size_t j = 1; j < c.size(); ++j) {
+    s += c[j] * t1;
+    ds += c[j] * (qf)(int)j * u0;
+    const qf t2 = 2 * x * t1 - t0, u2 = 2 * x * u1 - u0;
+    t0 = t1, t1 = t2, u0 = u1, u1 = u2;
+  }
 }
-// odd minimax fit of 1 on [a, 1] with n odd terms T_1 .. T_{2n-1}:
-// coefficients (double-binary128), sets err
-std::vector<dq> remez_sign(int n, qf a, qf& err) {
-  std::vector<qf> xs(n + 1), c(n, 0);
-  std::vector<dq> cd(n);
-  for (int i = 0; i <= n; ++i) xs[i] = cheb_pt(a, i, n);
-  const int G = 64 * n;
-  std::vector<qf> grid(G + 1), dg(G + 1);
-  for (int j = 0; j <= G; ++j) grid[j] = cheb_pt(a, j, G);
-  const qf tol_rel = 1 / (qf)18446744073709551616.0L;  // 2^-64
-  const qf tol_abs = tol_rel * tol_rel * 65536 * 2;    // 2^-111: binary128's floor
-  int done = 0;
-  for (int it = 0; it < 60; ++it) {
-    std::vector<std::vector<dq>> A(n + 1, std::vector<dq>(n + 2));
-    for (int i = 0; i <= n; ++i) {
-      for (int k = 0; k < n; ++k) A[i][k] = cheb_T_dq(2 * k + 1, xs[i]);
-      A[i][n] = to_dq((i & 1) ? -1 : 1);
-      A[i][n + 1] = to_dq(1);
+// pi and cos in binary128 (the nodes' positions must be exact to the
+// format, or the early-stopped iterate moves: cosl has 64 bits)
+const qf kPiQ = (qf)3.141592653589793 + (qf)1.2246467991473532e-16 + (qf)-2.9947698097183397e-33;
+qf cosq_(qf x) {  // |x| <= pi: Taylor series, terms below 2^-120
+  qf x2 = x * x, term = 1, sum = 1;
+  for (int k = 1; k < 60; ++k) {
+    term = -term * x2 / (qf)((2 * k - 1) * (2 * k));
+    sum += term;
+    if (qabs(term) < (qf)ldexpl(1.0L, -124)) break;
+  }
+  return sum;
+}
+RemezOut remez_sign_multi(const std::vector<std::pair<qf, qf>>& iv, int nodes_per, qf threshold, int max_iters,
+                          bool debug) {
+  const int nI = (int)iv.size(), nn = nodes_per * nI, D = nn - 2;
+  std::vector<qf> xs;
+  for (auto& I : iv)  // ascending: x_{n-k} = mid + half cos((k - 1/2) pi / n), k = 1..n
+    for (int i = 0; i < nodes_per; ++i) {
+      const int k = nodes_per - i;
+      xs.push_back((I.first + I.second) / 2 +
+                   (I.second - I.first) / 2 * cosq_(kPiQ * ((qf)k - (qf)0.5) / (qf)nodes_per));
+    }
+  auto sgn = [](qf x) -> qf { return x < 0 ? -1 : (x > 0 ? 1 : 0); };
+  const int G = 64 * (D + 2);
+  std::vector<std::vector<qf>> grids(nI);
+  for (int t = 0; t < nI; ++t)
+    for (int j = 0; j <= G; ++j)
+      grids[t].push_back((iv[t].first + iv[t].second) / 2 -
+                         (iv[t].second - iv[t].first) / 2 * cosq_(kPiQ * (qf)j / (qf)G));
+  RemezOut out;
+  std::vector<qf> c(D + 1, 0);
+  for (int it = 0; it < max_iters; ++it) {
+    std::vector<std::vector<dq>> A(nn, std::vector<dq>(nn + 1));
+    for (int i = 0; i < nn; ++i) {
+      for (int j = 0; j <= D; ++j) A[i][j] = cheb_T_dq(j, xs[i]);
+      A[i][D + 1] = to_dq((i & 1) ? -1 : 1);
+      A[i][nn] = to_dq(sgn(xs[i]));
     }
     std::vector<dq> sol = solve(A);
-    for (int k = 0; k < n; ++k) cd[k] = sol[k], c[k] = sol[k].hi + sol[k].lo;
-    const qf E = qabs(sol[n].hi + sol[n].lo);
-    // extrema of e = p - 1: the endpoints and the zeros of p' (bisection)
+    out.coeffs.assign(sol.begin(), sol.begin() + D + 1);
+    for (int j = 0; j <= D; ++j) c[j] = sol[j].hi + sol[j].lo;
+    out.iters = it + 1;
+    // extreme points of e = p - sign, interval by interval
+    std::vector<qf> px, pv;
     qf s, ds;
-    for (int j = 0; j <= G; ++j) cheb_odd_eval(c, grid[j], s, dg[j]);
-    std::vector<qf> ex{grid[0]};
-    for (int j = 0; j < G; ++j) {
-      if (!(dg[j] == 0 || (dg[j] > 0) != (dg[j + 1] > 0))) continue;
-      qf lo = grid[j], hi = grid[j + 1];
-      const bool up = dg[j] > 0;
-      for (int b = 0; b < 90; ++b) {
-        const qf m = (lo + hi) / 2;
-        cheb_odd_eval(c, m, s, ds);
-        if ((ds > 0) == up) lo = m; else hi = m;
-      }
-      ex.push_back((lo + hi) / 2);
-    }
-    ex.push_back(grid[G]);
-    std::vector<qf> px, pv;  // alternating points, the larger of equal-sign neighbours
-    for (qf x : ex) {
-      cheb_odd_eval(c, x, s, ds);
-      const qf v = s - 1;
-      if (!px.empty() && (v >= 0) == (pv.back() >= 0)) {
+    auto push = [&](qf x) {
+      cheb_eval_full(c, x, s, ds);
+      const qf v = s - sgn(x);
+      if (!px.empty() && (v >= 0) == (pv.back() >= 0)) {  // same sign as the previous: keep the larger
         if (qabs(v) > qabs(pv.back())) px.back() = x, pv.back() = v;
-        continue;
+        return;
       }
       px.push_back(x);
       pv.push_back(v);
+    };
+    for (int t = 0; t < nI; ++t) {
+      const std::vector<qf>& g = grids[t];
+      std::vector<qf> dg(G + 1);
+      for (int j = 0; j <= G; ++j) cheb_eval_full(c, g[j], s, dg[j]);
+      push(g[0]);
+      for (int j = 0; j < G; ++j) {
+        if (!(dg[j] == 0 || (dg[j] > 0) != (dg[j + 1] > 0))) continue;
+        if (dg[j] == 0 && j == 0) continue;
+        qf lo = g[j], hi = g[j + 1];
+        const bool up = dg[j] > 0;
+        for (int b = 0; b < 100; ++b) {
+          const qf m = (lo + hi) / 2;
+          cheb_eval_full(c, m, s, ds);
+          if ((ds > 0) == up) lo = m; else hi = m;
+        }
+        push((lo + hi) / 2);
+      }
+      push(g[G]);
     }
-    while ((int)px.size() > n + 1) {  // drop the smaller end extremum
-      if (qabs(pv.front()) < qabs(pv.back()))
-        px.erase(px.begin()), pv.erase(pv.begin());
-      else
-        px.pop_back(), pv.pop_back();
+    const size_t found = px.size();
+    {  // the levelled error below the arithmetic's resolution (a constant fit
+       // on a short interval near 1): converged as far as it can be measured
+      qf E = qabs(sol[D + 1].hi + sol[D + 1].lo), vmax = 0;
+      for (qf v : pv) vmax = qabs(v) > vmax ? qabs(v) : vmax;
+      if (vmax < (qf)ldexpl(1.0L, -100)) {
+        out.maxerr = vmax > E ? vmax : E, out.minerr = E;
+        if (debug) fprintf(stderr, "Iteration: %2d - error %.3Le below 2^-100: stop\n", it, (long double)vmax);
+        break;
+      }
     }
-    if ((int)px.size() < n + 1) throw std::runtime_error("minimax: Remez lost the alternation");
-    qf emax = 0;
-    for (qf v : pv) emax = qabs(v) > emax ? qabs(v) : emax;
-    err = emax;
+    while ((int)px.size() > nn) {
+      if ((int)px.size() == nn + 1) {  // one too many: the smaller end point
+        if (qabs(pv.front()) < qabs(pv.back()))
+          px.erase(px.begin()), pv.erase(pv.begin());
+        else
+          px.pop_back(), pv.pop_back();
+        continue;
+      }
+      size_t m = 0;
+      qf best = qabs(pv[0]) + qabs(pv[1]);
+      for (size_t i = 1; i + 1 < px.size(); ++i)
+        if (qabs(pv[i]) + qabs(pv[i + 1]) < best) best = qabs(pv[i]) + qabs(pv[i + 1]), m = i;
+      px.erase(px.begin() + m, px.begin() + m + 2);
+      pv.erase(pv.begin() + m, pv.begin() + m + 2);
+    }
+    if ((int)px.size() < nn) throw std::runtime_error("minimax: Remez lost the alternation");
+    out.maxerr = 0, out.minerr = qabs(pv[0]);
+    for (qf v : pv) {
+      out.maxerr = qabs(v) > out.maxerr ? qabs(v) : out.maxerr;
+      out.minerr = qabs(v) < out.minerr ? qabs(v) : out.minerr;
+    }
     xs = px;
-    // converged: the levelled error E matches the true maximum (relative,
-    // or absolute for stages whose error is far below float64); two more
-    // exchanges after the threshold (quadratic convergence)
-    if (emax - E <= tol_rel * emax || emax - E <= tol_abs) {
-      if (++done == 3) return cd;
-    }
+    const qf nerr = (out.maxerr - out.minerr) / out.minerr;
+    if (debug) fprintf(stderr, "Iteration: %2d - %.6Le (nodes %d, alternating extreme points %zu)\n", it, (long double)nerr, nn, found);
+    if (nerr <= threshold) break;
   }
-  throw std::runtime_error("minimax: Remez did not converge");
+  return out;
 }
 }  // namespace
 
-std::vector<std::vector<double>> minimax_sign_composite(const std::vector<int>& degrees, int logalpha) {
+// circuits/ckks/minimax.GenMinimaxCompositePolynomial [U], restated:
+//   e = 2^-logerr (the scheme error the fit absorbs), a_0 = 2^-logalpha;
+//   stage 0 fits sign on [-1 - e, -a_0 + e] U [a_0 - e, 1 + e];
+//   stage i > 0: the previous stage's coefficients are divided by
+//   1 + MaxErr (so its image [1 - MaxErr, 1 + MaxErr] lands in
+//   [a_i, 1], a_i = (1 - MaxErr) / (1 + MaxErr)), and stage i fits sign on
+//   [-1 - e, -a_i + e] U [a_i - e, 1 + e];
+//   the last stage keeps its coefficients; every stage has
+//   1 + (d + 1) / 2 nodes per interval, Remez threshold 2^-logalpha, at most
+//   50 iterations; each coefficient vector is the first d + 1 of T_0 .. T_D.
+// orion (polyeval.go:136-143): the last polynomial halved, + 0.5 on T_0.
+std::vector<std::vector<double>> minimax_sign_composite(const std::vector<int>& degrees, int logalpha, int logerr,
+                                                        std::vector<double>* stage_err, bool debug) {
   std::vector<std::vector<double>> out;
-  qf a = (qf)ldexpl(1.0L, -logalpha);
+  const qf alpha = (qf)ldexpl(1.0L, -logalpha), e = (qf)ldexpl(1.0L, -logerr);
+  qf a = alpha;
+  RemezOut prev;
+  std::vector<std::vector<dq>> polys;
   for (size_t i = 0; i < degrees.size(); ++i) {
     const int d = degrees[i];
     if (d < 1) throw std::runtime_error("minimax: degrees must be >= 1");
-    qf err = 0;
-    std::vector<dq> c = remez_sign((d - 1) / 2 + 1, a, err);
-    if (!(err < 1)) throw std::runtime_error("minimax: degree too small for the interval");
-    const dq s = to_dq(1) + to_dq(err);
-    std::vector<dq> p(d + 1, to_dq(0));
-    for (size_t k = 0; k < c.size(); ++k) p[2 * k + 1] = c[k] / s;
-    const dq an = (to_dq(1) - to_dq(err)) / s;
-    a = an.hi + an.lo;
-    if (i + 1 == degrees.size()) {  // orion (polyeval.go:136-143): halved, + 0.5 (in prec bits, then rounded)
-      for (dq& v : p) v = v / to_dq(2);
-      p[0] = p[0] + to_dq(0.5);
+    if (i > 0) {
+      const dq maxI = to_dq(1) + to_dq(prev.maxerr), minI = to_dq(1) - to_dq(prev.maxerr);
+      for (dq& v : polys.back()) v = v / maxI;  // interval normalisation
+      const dq an = minI / maxI;
+      a = an.hi + an.lo;
     }
-    std::vector<double> pd(d + 1);
-    for (int k = 0; k <= d; ++k) pd[k] = (double)(p[k].hi + p[k].lo);
+    std::vector<std::pair<qf, qf>> iv = {{-1 - e, -a + e}, {a - e, 1 + e}};
+    if (debug)
+      fprintf(stderr, "P[%zu]\nInterval: [%.12Lf, %.12Lf] U [%.12Lf, %.12Lf]\n", i, (long double)iv[0].first,
+              (long double)iv[0].second, (long double)iv[1].first, (long double)iv[1].second);
+    prev = remez_sign_multi(iv, 1 + ((d + 1) >> 1), alpha, 50, debug);
+    if (debug) fprintf(stderr, "MaxErr %.6Le MinErr %.6Le\n", (long double)prev.maxerr, (long double)prev.minerr);
+    if (!(prev.maxerr < 1)) throw std::runtime_error("minimax: degree too small for the interval");
+    polys.emplace_back(prev.coeffs.begin(), prev.coeffs.begin() + d + 1);
+    // sign is odd and the interval set symmetric: the even coefficients are
+    // zero up to the exchange's rounding, and are set to zero
+    for (int j = 0; j <= d; j += 2) polys.back()[j] = to_dq(0);
+    if (stage_err) stage_err->push_back((double)prev.maxerr);
+  }
+  std::vector<dq>& last = polys.back();
+  for (dq& v : last) v = v / to_dq(2);
+  last[0] = last[0] + to_dq(0.5);
+  for (auto& p : polys) {
+    std::vector<double> pd;
+    for (const dq& v : p) pd.push_back((double)(v.hi + v.lo));
     out.push_back(pd);
   }
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// EvalMod's cosine polynomial, Lattigo v6 mod1 CosDiscrete (the default
+// Mod1Type; circuits/ckks/mod1 ApproximateCos, after Han-Ki [U]), restated:
+// g(x) = a cos(2 pi (x - 1/4) / 2^r), a = (2 pi)^(-1/2^r), interpolated at
+// nodes clustered on the integers the ModRaise overflow takes, i in
+// [-(K-1), K-1]: d_i Chebyshev nodes of the first kind in [i - dev, i + dev]
+// (the integer itself when d_i = 1), d_i = 1 each and the degree + 1 - (2K - 1)
+// remaining nodes handed out greedily to the integer with the largest
+// interpolation-error bound dev^d_i / 2^(d_i - 1) * prod_{j != i} |i - j|^d_j
+// (d_{-i} = d_i; the centre takes single nodes); returned as Chebyshev
+// coefficients of u = x / K on [-1, 1] (solved in double-binary128: the
+// system at integer nodes has condition ~1e10), rounded to long double.
+// ---------------------------------------------------------------------------
+namespace {
+qf cos_reduced(qf x) {  // any x: reduced into [-pi, pi] first
+  const qf two_pi = 2 * kPiQ;
+  const long double k = roundl((long double)(x / two_pi));
+  return cosq_(x - (qf)k * two_pi);
+}
+qf sqrt_q(qf v) {  // binary128 square root: Newton from the long double one
+  qf y = (qf)sqrtl((long double)v);
+  for (int i = 0; i < 3; ++i) y = (y + v / y) / 2;
+  return y;
+}
+}  // namespace
+std::vector<long double> cos_discrete_cheb(int K, int degree, int r, double dev) {
+  const int n = degree + 1;
+  if (K < 1 || n < 2 * K - 1) throw std::runtime_error("CosDiscrete: degree + 1 must be >= 2K - 1");
+  std::vector<int> d(K, 1);  // nodes at +-i (d[0]: the centre)
+  int tot = 2 * K - 1;
+  while (tot < n) {
+    int best = -1;
+    long double bb = 0;
+    for (int i = 0; i < K; ++i) {
+      if (i > 0 && tot + 2 > n) continue;
+      long double lb = d[i] * log2l((long double)dev) - (d[i] - 1);
+      for (int j = -(K - 1); j < K; ++j)
+        if (j != i) lb += d[j < 0 ? -j : j] * log2l((long double)(i > j ? i - j : j - i));
+      if (best < 0 || lb > bb) best = i, bb = lb;
+    }
+    d[best] += 1;
+    tot += best == 0 ? 1 : 2;
+  }
+  std::vector<qf> xs;
+  for (int i = -(K - 1); i < K; ++i) {
+    const int di = d[i < 0 ? -i : i];
+    for (int j = 0; j < di; ++j)
+      xs.push_back(di == 1 ? (qf)i : (qf)i + (qf)dev * cosq_(kPiQ * (qf)(2 * j + 1) / (qf)(2 * di)));
+  }
+  qf a = 1 / (2 * kPiQ);
+  for (int i = 0; i < r; ++i) a = sqrt_q(a);
+  const qf sc = (qf)(1 << r);
+  std::vector<std::vector<dq>> A(n, std::vector<dq>(n + 1));
+  for (int k = 0; k < n; ++k) {
+    const qf u = xs[k] / (qf)K;
+    for (int j = 0; j < n; ++j) A[k][j] = cheb_T_dq(j, u);
+    A[k][n] = to_dq(a * cos_reduced(2 * kPiQ * (xs[k] - (qf)0.25) / sc));
+  }
+  std::vector<dq> c = solve(A);
+  std::vector<long double> out(n);
+  for (int j = 0; j < n; ++j) out[j] = (long double)(c[j].hi + c[j].lo);
   return out;
 }
 }  // namespace orion

@@ -37,11 +37,13 @@ std::vector<Cplx> special_fft_twiddles(int logN, bool inverse);
 // discrete Gaussian cumulative table: t[i] = floor(2^64 * P(X <= -bound + i)),
 // i < 2 bound, P(x) proportional to exp(-x^2 / (2 sigma^2)) on |x| <= bound
 void gauss_cdt(double sigma, int bound, u64* t);
-// composite minimax sign approximation on [-1, -2^-logalpha] U [2^-logalpha, 1]:
-// one Chebyshev coefficient vector (T_0..T_d) per degree; every stage is
-// divided by 1 + its minimax error (Lattigo's construction), the last one is
-// then mapped to [0, 1] (halved, + 0.5: orion's polyeval.go:136-143)
-std::vector<std::vector<double>> minimax_sign_composite(const std::vector<int>& degrees, int logalpha);
+// composite minimax sign approximation (Lattigo v6 GenMinimaxCompositePolynomial
+// [U], restated in hostmath.cpp): one Chebyshev coefficient vector per degree;
+// every fit absorbs a scheme error 2^-logerr, each stage but the last is
+// divided by 1 + its maximum error, the last is halved and + 0.5 (orion,
+// polyeval.go:136-143); stage_err (optional): each stage's maximum error
+std::vector<std::vector<double>> minimax_sign_composite(const std::vector<int>& degrees, int logalpha, int logerr,
+                                                        std::vector<double>* stage_err = nullptr, bool debug = false);
 // 256-bit ChaCha20 key of the encryption sampler, from the scheme seed
 void enc_key_from_seed(u64 seed, uint32_t key[8]);
 
@@ -58,4 +60,7 @@ class Prng {
   u64 s_[4];
 };
 
+// EvalMod's cosine polynomial (Lattigo v6 mod1 CosDiscrete [U], restated in
+// hostmath.cpp): Chebyshev coefficients on [-1, 1] of u = x / K
+std::vector<long double> cos_discrete_cheb(int K, int degree, int r, double dev);
 }  // namespace orion

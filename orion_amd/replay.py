@@ -15,6 +15,10 @@ deliberate differences:
 
 Handles recorded in the trace are mapped to the library's own handles at the
 events that create them, so deletes and lowest-free-id reuse replay exactly.
+Every other call goes through its own C-ABI entry, in the stream's order: the
+rotate-and-add fusion of `out += out.roll(k)` (RotateNew, AddCiphertext,
+DeleteCiphertext) and RescaleNew's copy-on-write result happen inside the
+library, behind the unchanged calls (backend.hip Context::Deferred, alias).
 """
 import json
 import os
@@ -56,50 +60,6 @@ _CT_OPS = {
 _NEW_CT = ("EvaluateLinearTransform", "EvaluatePolynomial", "Bootstrap", "Negate")
 
 
-def _dead_after(events, i, hid):
-    """Whether ciphertext id hid is read by no event after index i before it
-    is redefined or deleted."""
-    for e in events[i + 1:]:
-        kinds = _CT_OPS.get(e["op"], ())
-        if e["op"] == "SetCiphertextScale" and e["args"][0] == hid:
-            return False
-        if any(k == "ct" and v == hid for k, v in zip(kinds, e["args"])):
-            return False
-        if e.get("ret") == hid or (e["op"] == "DeleteCiphertext" and e["args"][0] == hid):
-            return True
-    return True
-
-
-def rotate_add_pairs(events, output_ids=()):
-    """{index of a RotateNew(x, k) -> r: index of the AddCiphertext(x, r) -> x
-    right after it}, for the pairs whose rotation r is read by nothing else
-    (LoLA's rotate-and-sum, lola.py's hybrid output rotations): the replay
-    runs such a pair as one OrionHipRotateAdd(x, k), x += Rotate(x, k)."""
-    ev, out = events, {}
-    outputs = set(output_ids)
-    fwd = [i for i, e in enumerate(ev) if e["phase"] == "forward"]
-    for a, b in zip(fwd, fwd[1:]):
-        r, s = ev[a], ev[b]
-        if r["op"] != "RotateNew" or s["op"] != "AddCiphertext":
-            continue
-        x, rid = r["args"][0], r["ret"]
-        if s["args"] != [x, rid] or s["ret"] != x or rid == x or rid in outputs:
-            continue
-        if _dead_after(ev, b, rid):
-            out[a] = b
-    return out
-
-
-def rescale_aliases(events, output_ids=()):
-    """Indices of the RescaleNew(x) -> y whose input x is read by nothing
-    afterwards: Lattigo's RescaleNew rescales x in place and returns a copy
-    (evaluator.go:92-99), and when x is dead the replay runs Rescale(x) and
-    lets y name x's ciphertext, with no copy."""
-    outputs = set(output_ids)
-    return {i for i, e in enumerate(events) if e["phase"] == "forward" and e["op"] == "RescaleNew"
-            and e["args"][0] not in outputs and e["ret"] != e["args"][0] and _dead_after(events, i, e["args"][0])}
-
-
 class OrionStream:
     """A compiled Orion model as an op stream bound to one HipLibrary."""
 
@@ -116,11 +76,6 @@ class OrionStream:
         self.pt_map, self.ct_map, self.lt_map, self.poly_map = {}, {}, {}, {}
         self.input_level = self.meta["input_level"]
         self._events = self.trace["events"]
-        # ORION_REPLAY_FUSE=0: every op through its own C-ABI call
-        self.fuse = os.environ.get("ORION_REPLAY_FUSE", "1") != "0"
-        self._rot_add = rotate_add_pairs(self._events, self.meta.get("output_ids", []))
-        self._rescale_alias = rescale_aliases(self._events, self.meta.get("output_ids", []))
-
 
     # -- setup: keys + evaluator (key_generator.py:10-15, evaluator.py:2-6) ---
     def keygen(self, with_po2=True):
@@ -203,24 +158,11 @@ class OrionStream:
         skipped_pts = set()
         owned = set()
         fi = -1
-        fuse = self.fuse and hook is None and stop_after is None
-        skip = set()
-        for ei, ev in enumerate(self._events):
+        for ev in self._events:
             if ev["phase"] != "forward":
                 continue
             fi += 1
-            if ei in skip:
-                continue
             op, args, ret = ev["op"], ev["args"], ev["ret"]
-            if fuse and ei in self._rot_add:  # x += Rotate(x, k): one call, the addition in the key switch's store
-                lib.OrionHipRotateAdd(ct_map[args[0]], args[1])
-                skip.add(self._rot_add[ei])
-                continue
-            if fuse and ei in self._rescale_alias:  # y = RescaleNew(x), x dead: rescale x in place, y names it
-                h = ct_map.pop(args[0])
-                lib.Rescale(h)
-                ct_map[ret] = h
-                continue
             if op in ("Decrypt", "Decode"):  # debug decryptions of the fork: not operator semantics
                 if op == "Decrypt":
                     skipped_pts.add(ret)

@@ -58,53 +58,59 @@ def test_fixture_integrity(name):
                                   "SetCiphertextScale"}
 
 
-@pytest.mark.parametrize("name,pairs", [("lola_n15", 10), ("lola_n13", "all"), ("mlp_n13", None), ("mlp_n14", None),
-                                        ("resnet20_n13", None)])
-def test_rotate_add_pairs(name, pairs):
-    """The replay's RotateNew + AddCiphertext fusion (OrionHipRotateAdd) takes
-    exactly the pairs x += Rotate(x, k) whose rotation nothing else reads:
-    LoLA's rotate-and-sum steps (all of its RotateNew).  Every taken pair is adjacent, adds into
-    the rotation's own input, and the rotation's handle is not read again
-    before it is redefined or deleted."""
-    from orion_amd.replay import rotate_add_pairs, _CT_OPS
-    t, _ = load(name)
-    ev = t["events"]
-    got = rotate_add_pairs(ev, t["meta"].get("output_ids", []))
-    if pairs == "all":
-        pairs = sum(e["phase"] == "forward" and e["op"] == "RotateNew" for e in ev)
-    if pairs is not None:
-        assert len(got) == pairs
-    for a, b in got.items():
-        r, s = ev[a], ev[b]
-        assert r["op"] == "RotateNew" and s["op"] == "AddCiphertext"
-        assert s["args"] == [r["args"][0], r["ret"]] and s["ret"] == r["args"][0]
-        for e in ev[b + 1:]:
-            if e.get("ret") == r["ret"] or (e["op"] == "DeleteCiphertext" and e["args"][0] == r["ret"]):
-                break
-            kinds = _CT_OPS.get(e["op"], ())
-            assert not any(k == "ct" and v == r["ret"] for k, v in zip(kinds, e["args"]))
-    # a rotation read again later is never fused
-    x = [{"phase": "forward", "op": "RotateNew", "args": [2, 4], "ret": 1},
-         {"phase": "forward", "op": "AddCiphertext", "args": [2, 1], "ret": 2},
-         {"phase": "forward", "op": "AddCiphertext", "args": [3, 1], "ret": 3}]
-    assert rotate_add_pairs(x) == {}
-    assert rotate_add_pairs(x[:2]) == {0: 1}
+# C-ABI calls that leave a deferred rotation pending (backend.hip defer_keeps)
+_DEFER_KEEPS = {"AddCiphertext", "DeleteCiphertext", "DeletePlaintext", "GetCiphertextScale", "GetCiphertextScaleF",
+                "GetCiphertextLevel", "GetCiphertextSlots", "GetCiphertextDegree", "GetCiphertextBatch",
+                "GetPlaintextScale", "GetPlaintextLevel", "GetPlaintextSlots", "GetPlaintextBatch",
+                "GetLiveCiphertexts", "GetLivePlaintexts", "GetModuliChain", "GaloisElement"}
 
 
-@pytest.mark.parametrize("name", ["lola_n15", "lola_n13", "mlp_n13", "mlp_n14", "resnet20_n13"])
-def test_rescale_aliases(name):
-    """The replay runs RescaleNew(x) -> y as an in-place Rescale(x) named y
-    only when nothing reads x afterwards (LoLA: all three)."""
-    from orion_amd.replay import rescale_aliases, _CT_OPS
+def deferred_rotations(events):
+    """Model of the library's deferral (backend.hip Context::Deferred) over a
+    stream of C-ABI calls: (rotate-and-adds fused in the key switch's store,
+    rotations dropped unread, rotations run on their own)."""
+    fused = dropped = plain = 0
+    st = None  # (kind, x, r)
+    for e in events:
+        op, args = e["op"], e["args"]
+        if st is not None:
+            kind, x, r = st
+            if op == "AddCiphertext" and kind == 1 and args == [x, r]:
+                st = (2, x, r)
+                continue
+            if op == "DeleteCiphertext" and args[0] == r:
+                fused += kind == 2
+                dropped += kind == 1
+                st = None
+                continue
+            if op not in _DEFER_KEEPS or (op == "DeleteCiphertext" and args[0] == x) or op == "AddCiphertext":
+                plain += 1
+                st = None
+        if op == "RotateNew":
+            st = (1, args[0], e["ret"])
+    return fused, dropped, plain + (st is not None)
+
+
+@pytest.mark.parametrize("name,fused", [("lola_n15", 10), ("lola_n13", "all"), ("mlp_n13", None),
+                                        ("mlp_n14", None), ("resnet20_n13", None)])
+def test_reference_stream_hits_deferred_rotate_add(name, fused):
+    """The frontend's own calls (the recorded stream as the fork issues it,
+    debug Decrypt/Decode included) reach the library's deferred rotate-and-add
+    for every `out += out.roll(k)` of LoLA (linear.py:72-73): RotateNew,
+    AddCiphertext into its source, DeleteCiphertext of the rotation -- so the
+    op-by-op replay the bench times runs them as one key switch each."""
     t, _ = load(name)
-    ev = t["events"]
-    got = rescale_aliases(ev, t["meta"].get("output_ids", []))
-    if name.startswith("lola"):
-        assert len(got) == sum(e["phase"] == "forward" and e["op"] == "RescaleNew" for e in ev)
-    for i in got:
-        x = ev[i]["args"][0]
-        for e in ev[i + 1:]:
-            if e.get("ret") == x or (e["op"] == "DeleteCiphertext" and e["args"][0] == x):
-                break
-            kinds = _CT_OPS.get(e["op"], ())
-            assert not any(k == "ct" and v == x for k, v in zip(kinds, e["args"]))
+    ev = [e for e in t["events"] if e["phase"] == "forward"]
+    f, d, p = deferred_rotations(ev)
+    n_rot = sum(e["op"] == "RotateNew" for e in ev)
+    assert f + d + p == n_rot
+    if fused == "all":
+        fused = n_rot
+    if fused is not None:
+        assert f == fused and p == 0
+    # a rotation read again, or its source written first, runs on its own
+    x = [{"op": "RotateNew", "args": [2, 4], "ret": 1}, {"op": "AddCiphertext", "args": [2, 1], "ret": 2},
+         {"op": "AddCiphertext", "args": [3, 1], "ret": 3}, {"op": "DeleteCiphertext", "args": [1], "ret": None}]
+    assert deferred_rotations(x) == (0, 0, 1)
+    assert deferred_rotations(x[:2] + x[3:]) == (1, 0, 0)
+    assert deferred_rotations([x[0], x[3]]) == (0, 1, 0)

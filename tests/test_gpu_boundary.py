@@ -241,6 +241,28 @@ def test_wire_format_rotation_key_and_diagonals(small):
     gkeys = {ge: lib.export_galois_key(ge) for ge in gels}
     assert np.array_equal(got, orc.lt_bsgs(x, level, idx, [pts[d] for d in idx], lib.GetLinearTransformN1(lt), gkeys))
 
+    # a key cut at load to its transform's level comes back whole -- the
+    # loaded key itself, which stays in host memory as Lattigo keeps it
+    # (lineartransform.go:143-159) -- for a rotation above that level
+    ge = gels[-1]
+    k = next(r for r in range(slots) if pow(5, r, 2 * N) == ge)
+    kb, _ = lib.GenerateAndSerializeRotationKey(ge)
+    lib.LoadRotationKey(kb, ge)
+    assert lib.GetGaloisKeyLevel(ge) == level
+    top = L - 1
+    y = rand_ct(rng, orc.moduli, top, N, B=1)
+    r = lib.export_ciphertext(lib.RotateNew(lib.import_ciphertext(y, 2.0 ** 40), k))[0]
+    assert lib.GetGaloisKeyLevel(ge) == top
+    gk = lib.export_galois_key(ge)
+    kw = kb.view(np.uint64)
+    for d in range(dnum):
+        for c in range(2):
+            # digit d, component c: its Q poly's top limb in the blob (Montgomery form)
+            off = 4 + 2 + d * (2 + 2 * (2 + (L + K) * (1 + N))) + c * (2 + (L + K) * (1 + N)) + 1 + top * (1 + N) + 1
+            for n in (0, 1, N // 3, N - 1):
+                assert int(kw[off + n]) == _mform(gk[d, c, top, n], orc.moduli[top]), (d, c, n)
+    assert np.array_equal(r, orc.rotate(y[0], ge, gk, top))
+
 
 def test_key_bundle_header_checks(torch_cuda):
     """ADVICE r1: the key bundle names its chain (logN, L, K, dnum, moduli);

@@ -379,27 +379,27 @@ def test_resnet20_n16_end_to_end(torch_cuda):
     st.lib.DeleteScheme()
 
 
-def test_replay_fusion_matches_op_by_op(torch_cuda):
-    """The replay's rewrites (rotate-and-add pairs as OrionHipRotateAdd,
-    dead-input RescaleNew as an in-place Rescale) give exactly the op-by-op
-    result, on LoLA N=2^13 at batch 5 (the latency kernels' scatter-add
-    store) and N=2^15 at batch 40 (the one-pass kernel's)."""
+def test_library_deferral_matches_undeferred(torch_cuda, monkeypatch):
+    """The library's own rewrites behind the unchanged C-ABI (RotateNew +
+    AddCiphertext + DeleteCiphertext as one key switch with the addition in
+    its store; RescaleNew's result sharing the rescaled input's buffer
+    copy-on-write) give exactly the result with them off (ORION_DEFER=0), on
+    the op-by-op replay of the reference stream: LoLA N=2^13 at batch 5 (the
+    latency kernels' scatter-add store) and N=2^15 at batch 40 (the one-pass
+    kernel's)."""
     import numpy as np
     from orion_amd.replay import OrionStream
     for name, B in (("lola_n13", 5), ("lola_n15", 40)):
-        st = OrionStream(name, seed=37)
-        st.keygen()
-        st.compile()
-        lib = st.lib
-        assert st._rot_add and st._rescale_alias
-        rng = np.random.default_rng(41)
-        imgs = rng.standard_normal((B,) + np.asarray(st.reference_input()).shape[1:]).astype(np.float32)
-        ct = st.encrypt_batch(imgs)
-        st.fuse = False
-        x = lib.CloneCiphertext(ct)
-        ref = lib.export_ciphertext(st.forward(x))
-        st.fuse = True
-        y = lib.CloneCiphertext(ct)
-        got = lib.export_ciphertext(st.forward(y))
-        assert np.array_equal(got, ref), name
-        lib.DeleteScheme()
+        outs = []
+        for defer in ("0", "1"):
+            monkeypatch.setenv("ORION_DEFER", defer)
+            st = OrionStream(name, seed=37)
+            st.keygen()
+            st.compile()
+            lib = st.lib
+            rng = np.random.default_rng(41)
+            imgs = rng.standard_normal((B,) + np.asarray(st.reference_input()).shape[1:]).astype(np.float32)
+            ct = st.encrypt_batch(imgs)
+            outs.append(lib.export_ciphertext(st.forward(ct)))
+            lib.DeleteScheme()
+        assert np.array_equal(outs[0], outs[1]), name

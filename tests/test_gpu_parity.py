@@ -511,8 +511,9 @@ def test_bootstrap_functional(torch_cuda, h):
     assert lib.GetCiphertextScaleF(out) == 2.0 ** 40
     dec = lib.decode_f64(lib.Decrypt(out))
     err = np.abs(dec - vals.astype(np.float64))
-    # Lattigo's default message ratio (2^8) and degree-30 cosine: the oracle's own
-    # run of this circuit measures 1.0e-5 / 1.8e-6 (tests/test_oracle.py)
+    # Lattigo's default message ratio (2^8) and degree-30 CosDiscrete cosine: the
+    # oracle's own run of this circuit measures 2.1e-8 / 4.6e-9 (tests/test_oracle.py)
+    print("bootstrap full h=%d err max %.3g mean %.3g" % (h, err.max(), err.mean()))
     assert err.max() < 1e-4 and err.mean() < 1e-5, (err.max(), err.mean())
     # the refreshed ciphertext computes: square and rescale
     sq = lib.MulRelinCiphertextNew(out, out)
@@ -535,8 +536,8 @@ def test_bootstrap_functional(torch_cuda, h):
         assert lib.GetCiphertextScaleF(out_s) == 2.0 ** 40
         exp_s = np.tile(sp[:, :ns], (1, n // ns)).astype(np.float64)
         err = np.abs(lib.decode_f64(lib.Decrypt(out_s)) - exp_s)
-        # the post-scale multiplies the error by the gap (64 at ns = 64: measured
-        # 6.1e-5 max / 1.4e-5 mean)
+        # the post-scale multiplies the error by the gap (64 at ns = 64)
+        print("bootstrap ns=%d h=%d err max %.3g mean %.3g" % (ns, h, err.max(), err.mean()))
         assert err.max() < 4e-4 and err.mean() < 1e-4, (ns, err.max(), err.mean())
     lib.DeleteBootstrappers()
     with pytest.raises(RuntimeError, match="no bootstrapper"):
@@ -550,7 +551,7 @@ def test_bootstrap_parity(torch_cuda, oracle_mod, sparse):
     restatement of Lattigo v6's default bootstrapping circuit
     (oracle_bootstrap: ScaleDown by F, EvkDenseToSparse, centred ModRaise,
     EvkSparseToDense, trace, 4 CoeffsToSlots transforms, conjugation, EvalMod
-    = degree-30 Chebyshev cosine + 3 double angles, 3 SlotsToCoeffs
+    = degree-30 CosDiscrete cosine + 3 double angles, 3 SlotsToCoeffs
     transforms, Orion's post-scale).  The oracle derives the prime chain, F,
     K, the cosine coefficients, the trace elements and every CoeffsToSlots /
     SlotsToCoeffs diagonal (special-FFT factorisation, constant spreading,
@@ -595,10 +596,21 @@ def test_bootstrap_parity(torch_cuda, oracle_mod, sparse):
     keys = bootstrap_keys(lib, ns)
     orc = oracle_mod.Oracle(13, lib.moduli(), len(BTP_LOGQ), len(logp))
     for b in range(2):
-        ref = orc.bootstrap(boot, circ, keys, x[b], 0)
+        ref, rsc = orc.bootstrap(boot, circ, keys, x[b], 0, 2.0 ** 40)
         assert np.array_equal(got[b], ref), b
+    assert lib.GetCiphertextScaleF(out) == 2.0 ** 40 == float(rsc)
     exp = np.tile(vals[:, :ns], (1, n // ns)).astype(np.float64)
-    assert np.abs(lib.decode_f64(lib.Decrypt(out)) - exp).max() < 1e-4
+    assert np.abs(lib.decode_f64(lib.Decrypt(out)) - exp).max() < 1e-6
+    # ScaleDown's F comes from the input's own scale (Lattigo's
+    # ScaleDown), so an input at another scale keeps the message ratio; the
+    # output scale carries F / F_default
+    ct2 = lib.Encrypt(lib.encode_batch(vals, 0, 1 << 38))
+    out2 = lib.Bootstrap(ct2, ns)
+    x2, got2 = lib.export_ciphertext(ct2), lib.export_ciphertext(out2)
+    ref2, rsc2 = orc.bootstrap(boot, circ, keys, x2[0], 0, 2.0 ** 38)
+    assert np.array_equal(got2[0], ref2)
+    assert lib.GetCiphertextScaleF(out2) == float(rsc2) and abs(float(rsc2) / 2.0 ** 38 - 1) < 1e-3
+    assert np.abs(lib.decode_f64(lib.Decrypt(out2)) - exp).max() < 1e-6
     lib.DeleteScheme()
 
 
@@ -825,12 +837,12 @@ def test_basis_extension_modes(torch_cuda, oracle_mod):
     lib.DeleteScheme()
 
 
-@pytest.mark.parametrize("env", [{"ORION_NTT_TAILSPLIT": "1"}, {"ORION_NTT_IFUSE": "0"}, {"ORION_NTT_AUT_FUSE": "0"},
-                                 {"ORION_BEXT_MODES": "0", "ORION_NTT_IFUSE_MAXR": "1000"}])
+@pytest.mark.parametrize("env", [{}, {"ORION_NTT_TAILSPLIT": "1"}, {"ORION_NTT_IFUSE": "0"},
+                                 {"ORION_NTT_AUT_FUSE": "0"}, {"ORION_BEXT_MODES": "0", "ORION_NTT_IFUSE_MAXR": "1000"}])
 @pytest.mark.parametrize("B", [2, 12, 40])
 def test_runtime_switch_parity(torch_cuda, oracle_mod, env, B, monkeypatch):
-    """The non-default NTT / basis-extension paths behind the runtime switches
-     stay bit-exact: the partial-round split (B=40 at
+    """The default environment and the non-default NTT / basis-extension
+    paths behind the runtime switches stay bit-exact: the partial-round split (B=40 at
     N=2^15 leaves 144- and 80-job tails), the unfused INTT + prologue NTT,
     the lazy-only basis extension, the INTT fusion with no redundancy limit,
     and the rotation's automorphism as its own launch; and the fused
@@ -872,4 +884,108 @@ def test_runtime_switch_parity(torch_cuda, oracle_mod, env, B, monkeypatch):
         rot = orc.rotate(ref, g, gk, level - 1)
         assert np.array_equal(got_r[b], rot), b
         assert np.array_equal(got_a[b], (ref + rot) % qs), b
+    lib.DeleteScheme()
+
+
+@pytest.mark.parametrize("B", [1, 64])
+def test_deferred_rotate_add_plain_calls(torch_cuda, oracle_mod, B):
+    """The frontend's `out += out.roll(k)` (linear.py:72-73) as the plain
+    C-ABI calls it issues -- RotateNew(x, k) -> r, AddCiphertext(x, r),
+    DeleteCiphertext(r) -- runs as one key switch with the addition in its
+    store (backend.hip Context::Deferred), bit-exact against orc.rotate + add,
+    at B=64 (one-pass kernel) and B=1 (latency kernels).  Every way out of
+    the deferral computes what the op-by-op calls would: the rotation read
+    after the addition, the rotation read before it, the source written
+    before the addition, the rotation deleted unread, and RescaleNew's
+    copy-on-write result with either handle written afterwards."""
+    from orion_amd.backend import HipLibrary
+    logq, logp = [60, 40, 40, 40, 40, 40], [60, 60]
+    lib = HipLibrary().new_scheme(15, logq, logp, 40, h=192, seed=616)
+    mods = lib.moduli()
+    orc = oracle_mod.Oracle(15, mods, len(logq), len(logp))
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    rng = np.random.default_rng(6160 + B)
+    level = 3
+    qs = np.array(mods[:level + 1], dtype=np.uint64)[:, None]
+    x = rand_ct(rng, mods, level, orc.N, B=B)
+    chk = (0, B - 1)
+
+    def fresh():
+        return lib.import_ciphertext(x, 2.0 ** 40)
+
+    k = 512
+    g = int(lib.GaloisElement(k))
+    lib.AddRotationKey(k)
+    gk = lib.export_galois_key(g)
+    rot = {b: orc.rotate(x[b], g, gk, level) for b in chk}
+    # 1. the frontend's sequence: fused
+    a = fresh()
+    lib.OrionHipProfileReset()
+    lib.OrionHipProfile(1)
+    r = lib.RotateNew(a, k)
+    assert lib.AddCiphertext(a, r) == a
+    lib.DeleteCiphertext(r)
+    lib.OrionHipProfile(0)
+    prof = lib.profile_read()
+    # no separate addition, no separate permutation: both in the ModDown's store
+    assert prof["elementwise"]["launches"] == 0 and prof["automorph"]["launches"] == 0, prof
+    assert prof["ks_mac"]["launches"] >= 1, prof
+    got = lib.export_ciphertext(a)
+    for b in chk:
+        assert np.array_equal(got[b], (x[b] + rot[b]) % qs), b
+    lib.DeleteCiphertext(a)
+    # 2. the rotation read after the addition
+    a = fresh()
+    r = lib.RotateNew(a, k)
+    lib.AddCiphertext(a, r)
+    gr, ga = lib.export_ciphertext(r), lib.export_ciphertext(a)
+    for b in chk:
+        assert np.array_equal(gr[b], rot[b]) and np.array_equal(ga[b], (x[b] + rot[b]) % qs), b
+    lib.DeleteCiphertext(r)
+    lib.DeleteCiphertext(a)
+    # 3. the source written before the addition (the rotation sees the old x)
+    a = fresh()
+    r = lib.RotateNew(a, k)
+    lib.MulScalarInt(a, 3)
+    lib.AddCiphertext(a, r)
+    lib.DeleteCiphertext(r)
+    ga = lib.export_ciphertext(a)
+    for b in chk:
+        assert np.array_equal(ga[b], (x[b] * 3 % qs + rot[b]) % qs), b
+    # 4. the rotation deleted unread; metadata reads keep it pending
+    r = lib.RotateNew(a, k)
+    assert lib.GetCiphertextLevel(r) == level and lib.GetCiphertextBatch(r) == B
+    lib.DeleteCiphertext(r)
+    assert np.array_equal(lib.export_ciphertext(a), ga)
+    # 5. a rotation added into another ciphertext runs on its own
+    c = fresh()
+    r = lib.RotateNew(a, k)
+    lib.AddCiphertext(c, r)
+    lib.DeleteCiphertext(r)
+    gc = lib.export_ciphertext(c)
+    for b in chk:
+        assert np.array_equal(gc[b], (x[b] + orc.rotate(ga[b], g, gk, level)) % qs), b
+    lib.DeleteCiphertext(a)
+    lib.DeleteCiphertext(c)
+    # 6. RescaleNew: y shares x's rescaled buffer until one of them is written
+    a = fresh()
+    y = lib.RescaleNew(a)
+    resc = {b: orc.rescale(x[b], level) for b in chk}
+    lib.MulScalarInt(a, 5)
+    gy, ga = lib.export_ciphertext(y), lib.export_ciphertext(a)
+    q1 = qs[:level]
+    for b in chk:
+        assert np.array_equal(gy[b], resc[b]) and np.array_equal(ga[b], resc[b] * 5 % q1), b
+    lib.DeleteCiphertext(y)
+    y = lib.RescaleNew(a)
+    lib.MulScalarInt(y, 7)
+    gy, ga = lib.export_ciphertext(y), lib.export_ciphertext(a)
+    q2 = qs[:level - 1]
+    for b in chk:
+        exp = orc.rescale(resc[b] * 5 % q1, level - 1)
+        assert np.array_equal(ga[b], exp) and np.array_equal(gy[b], exp * 7 % q2), b
+    lib.DeleteCiphertext(a)
+    lib.MulScalarInt(y, 1)  # sole owner now: in place, no copy
+    assert np.array_equal(lib.export_ciphertext(y), gy)
     lib.DeleteScheme()

@@ -1,10 +1,13 @@
 """GenerateMinimaxSignCoeffs (polyeval.go:91-167): composite minimax
 approximation of sign on [-1, -2^-logalpha] U [2^-logalpha, 1], host-side
 compile-time work, so it runs on the CPU.  Parity with Lattigo v6's
-GenMinimaxCompositePolynomial [U] is UNPINNED (not in this image; logerr is
-ignored here): the fixture (tools/gen_minimax.py ->
-tests/golden/minimax_sign.json) is this backend's own construction computed
-again in mpmath at `prec` bits, so the first test pins the arithmetic (the
+GenMinimaxCompositePolynomial [U] is UNPINNED (not in this image, DESIGN.md
+§2): both this backend (hostmath.cpp) and the fixture generator
+(tools/gen_minimax.py -> tests/golden/minimax_sign.json, mpmath at `prec`
+bits) restate Lattigo's construction -- every interval widened by the scheme
+error 2^-logerr, the multi-interval Remez stopped at Lattigo's threshold
+(MaxErr - MinErr) / MinErr <= 2^-logalpha, each stage but the last divided by
+1 + MaxErr -- so the first test pins the arithmetic of that restatement (the
 doubles must be equal), not Lattigo-equality.  The other checks
 are the contract the caller (orion/nn/activation.py:201-260, _Sign / ReLU)
 relies on -- one Chebyshev coefficient vector per degree, intermediate stages
@@ -27,7 +30,7 @@ def lib():
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "minimax_sign.json")
 
 
-@pytest.mark.parametrize("case", range(3))
+@pytest.mark.parametrize("case", range(4))
 def test_minimax_sign_matches_prec_bit_fixture(lib, case):
     c = json.load(open(GOLDEN))["cases"][case]
     got = np.array(lib.GenerateMinimaxSignCoeffs(c["degrees"], c["prec"], c["logalpha"], c["logerr"], 0))
@@ -73,3 +76,19 @@ def test_minimax_default_relu_precision(lib):
     assert np.abs(sign - np.sign(x)).max() < 2.0 ** -12
     # cached: the same call returns the same coefficients
     assert np.array_equal(np.array(lib.GenerateMinimaxSignCoeffs(degrees, 128, 6, 12, 0)), flat)
+
+
+def test_minimax_sign_depends_on_logerr(lib):
+    """logerr (orion's _Sign default 12, activation.py:207-231) widens every
+    fit interval by 2^-logerr, as Lattigo's GenMinimaxCompositePolynomial
+    does: the coefficients change with it, and the composite still maps
+    inputs perturbed by up to 2^-logerr to the right side."""
+    degrees = [15, 15, 27]
+    a = np.array(lib.GenerateMinimaxSignCoeffs(degrees, 128, 6, 12, 0))
+    b = np.array(lib.GenerateMinimaxSignCoeffs(degrees, 128, 6, 8, 0))
+    assert a.shape == b.shape and not np.array_equal(a, b)
+    polys = np.split(b, np.cumsum([d + 1 for d in degrees])[:-1])
+    e = 2.0 ** -8
+    x = np.concatenate([np.linspace(2.0 ** -6 - e, 1 + e, 20001), -np.linspace(2.0 ** -6 - e, 1 + e, 20001)])
+    out = _composite(polys, x)
+    assert np.abs(out - (x > 0)).max() < 1e-4

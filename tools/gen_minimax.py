@@ -1,21 +1,24 @@
 """Composite minimax sign coefficients at `prec` bits (mpmath), the fixture
 that pins GenerateMinimaxSignCoeffs (/root/reference/orion/backend/lattigo/
-polyeval.go:90-167 -> Lattigo v6 bignum.GenMinimaxCompositePolynomial [U]).
+polyeval.go:90-167 -> Lattigo v6 circuits/ckks/minimax.
+GenMinimaxCompositePolynomial and utils/bignum.Remez [U]).
 
 Restated algorithm [U] (Lattigo v6.2.0 is not vendored; this follows its
-published construction):
-  stage i (degree d_i, interval [-1, -a_i] U [a_i, 1], a_0 = 2^-logalpha):
-    p_i = the degree-d_i minimax approximation of sign on that interval set,
-          in the Chebyshev basis on [-1, 1]; sign is odd and the interval set
-          symmetric, so p_i is odd (Lattigo zeroes the even coefficients) and
-          is the odd minimax fit of 1 on [a_i, 1]; E_i = its error;
-    p_i <- p_i / (1 + E_i)                   (its image stays inside [-1, 1])
-    a_{i+1} = (1 - E_i) / (1 + E_i)          (the image of [a_i, 1])
+published construction, the same one orion_amd/csrc/hostmath.cpp restates):
+  e = 2^-logerr, alpha = 2^-logalpha, a_0 = alpha;
+  stage i (degree d_i): the multi-interval Remez approximation of sign on
+    [-1 - e, -a_i + e] U [a_i - e, 1 + e] in the Chebyshev basis T_0 .. T_D
+    evaluated at x (D = 2 (1 + (d_i + 1) // 2) - 2: 1 + (d_i + 1) // 2 nodes
+    per interval), started on each interval's Chebyshev nodes of the first
+    kind, exchanging on the extreme points of the error (interval ends and
+    the zeros of p'; same-signed neighbours keep the larger; surplus points
+    leave as the smaller end point or the adjacent pair with the smallest
+    error sum), stopped once (MaxErr - MinErr) / MinErr <= alpha (at most 50
+    iterations); the first d_i + 1 coefficients, the even ones set to zero;
+  stage i < last: divided by 1 + MaxErr_i; a_{i+1} = (1 - MaxErr_i) / (1 + MaxErr_i);
   orion (polyeval.go:136-143): the last polynomial halved, + 0.5 on T_0.
-The minimax polynomial of each stage is unique, so a Remez exchange converged
-far below float64 resolution gives Lattigo's coefficients up to its own
-stopping threshold; each coefficient is rounded to float64 once (big.Float
-.Float64: round to nearest even, as mpmath's float()).
+Each coefficient is rounded to float64 once (big.Float.Float64: round to
+nearest even, as mpmath's float()).
 
 Usage: python tools/gen_minimax.py  ->  tests/golden/minimax_sign.json
 """
@@ -26,105 +29,126 @@ import mpmath as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = [([15, 15, 27], 128, 6, 12),   # orion.nn.activation._Sign / ReLU defaults (ResNet-20)
+         ([15, 15, 27], 128, 6, 8),    # the same with a larger scheme error
          ([7, 15], 128, 4, 12),
          ([31], 128, 3, 12)]
 
 
-def cheb_odd(c, x):
-    """sum_k c_k T_{2k+1}(x) and its derivative."""
-    t0, t1 = mp.mpf(1), x
-    u0, u1 = mp.mpf(1), 2 * x  # U_0, U_1
-    s = ds = mp.mpf(0)
-    k = 0
-    m = 1
-    while k < len(c):
-        if m & 1:
-            s += c[k] * t1
-            ds += c[k] * m * u0  # T_m' = m U_{m-1}
-            k += 1
+def cheb_full(c, x):
+    """sum_j c_j T_j(x) and its derivative (T_j' = j U_{j-1})."""
+    t0, t1, u0, u1 = mp.mpf(1), x, mp.mpf(1), 2 * x
+    s, ds = c[0], mp.mpf(0)
+    for j in range(1, len(c)):
+        s += c[j] * t1
+        ds += c[j] * j * u0
         t0, t1 = t1, 2 * x * t1 - t0
         u0, u1 = u1, 2 * x * u1 - u0
-        m += 1
     return s, ds
 
 
-def remez_odd_one(n, a, tol):
-    """Odd minimax fit p = sum_{k<n} c_k T_{2k+1} of 1 on [a, 1]: (c, E)."""
-    xs = [(a + 1) / 2 - (1 - a) / 2 * mp.cos(mp.pi * i / n) for i in range(n + 1)]
-    grid = [(a + 1) / 2 - (1 - a) / 2 * mp.cos(mp.pi * j / (64 * n)) for j in range(64 * n + 1)]
-    done = 0
-    for _ in range(60):
-        A = mp.matrix(n + 1, n + 1)
-        b = mp.matrix(n + 1, 1)
+def sgn(x):
+    return mp.mpf(-1) if x < 0 else (mp.mpf(1) if x > 0 else mp.mpf(0))
+
+
+def remez_multi(iv, nodes_per, threshold, max_iters=50):
+    nn = nodes_per * len(iv)
+    D = nn - 2
+    xs = []
+    for a, b in iv:
+        for i in range(nodes_per):
+            k = nodes_per - i
+            xs.append((a + b) / 2 + (b - a) / 2 * mp.cos(mp.pi * (k - mp.mpf(0.5)) / nodes_per))
+    G = 64 * (D + 2)
+    grids = [[(a + b) / 2 - (b - a) / 2 * mp.cos(mp.pi * j / G) for j in range(G + 1)] for a, b in iv]
+    coeffs = maxerr = minerr = None
+    for _ in range(max_iters):
+        A = mp.matrix(nn, nn)
+        rhs = mp.matrix(nn, 1)
         for i, x in enumerate(xs):
-            for k in range(n):
-                A[i, k] = mp.chebyt(2 * k + 1, x)
-            A[i, n] = (-1) ** i
-            b[i] = 1
-        sol = mp.lu_solve(A, b)
-        c = [sol[k] for k in range(n)]
-        E = abs(sol[n])
-        # extrema of e = p - 1: the endpoints and the zeros of p' between them
-        d = [cheb_odd(c, x)[1] for x in grid]
-        ex = [grid[0]]
-        for j in range(len(grid) - 1):
-            if d[j] == 0 or (d[j] > 0) != (d[j + 1] > 0):
-                ex.append(mp.findroot(lambda x: cheb_odd(c, x)[1], (grid[j], grid[j + 1]), solver="anderson"))
-        ex.append(grid[-1])
-        ev = [cheb_odd(c, x)[0] - 1 for x in ex]
-        # keep an alternating set of n + 1 points with the largest errors
+            for j in range(D + 1):
+                A[i, j] = mp.chebyt(j, x)
+            A[i, D + 1] = -1 if i & 1 else 1
+            rhs[i] = sgn(x)
+        sol = mp.lu_solve(A, rhs)
+        coeffs = [sol[j] for j in range(D + 1)]
         pts = []
-        for x, v in zip(ex, ev):
+
+        def push(x):
+            v = cheb_full(coeffs, x)[0] - sgn(x)
             if pts and (v >= 0) == (pts[-1][1] >= 0):
                 if abs(v) > abs(pts[-1][1]):
                     pts[-1] = (x, v)
-                continue
+                return
             pts.append((x, v))
-        while len(pts) > n + 1:
-            if abs(pts[0][1]) < abs(pts[-1][1]):
-                pts.pop(0)
-            else:
-                pts.pop()
-        emax = max(abs(v) for _, v in pts)
-        if len(pts) < n + 1:
-            raise RuntimeError("Remez: lost alternation")
+
+        for g in grids:
+            dg = [cheb_full(coeffs, x)[1] for x in g]
+            push(g[0])
+            for j in range(G):
+                if not (dg[j] == 0 or (dg[j] > 0) != (dg[j + 1] > 0)):
+                    continue
+                if dg[j] == 0 and j == 0:
+                    continue
+                lo, hi, up = g[j], g[j + 1], dg[j] > 0
+                for _b in range(100):
+                    m = (lo + hi) / 2
+                    if (cheb_full(coeffs, m)[1] > 0) == up:
+                        lo = m
+                    else:
+                        hi = m
+                push((lo + hi) / 2)
+            push(g[-1])
+        E = abs(sol[D + 1])
+        vmax = max(abs(v) for _, v in pts)
+        if vmax < mp.ldexp(1, -100):  # below the arithmetic's resolution
+            maxerr, minerr = max(vmax, E), E
+            break
+        while len(pts) > nn:
+            if len(pts) == nn + 1:
+                if abs(pts[0][1]) < abs(pts[-1][1]):
+                    pts.pop(0)
+                else:
+                    pts.pop()
+                continue
+            m = min(range(len(pts) - 1), key=lambda i: (abs(pts[i][1]) + abs(pts[i + 1][1]), i))
+            del pts[m:m + 2]
+        if len(pts) < nn:
+            raise RuntimeError("Remez lost the alternation")
+        maxerr = max(abs(v) for _, v in pts)
+        minerr = min(abs(v) for _, v in pts)
         xs = [x for x, _ in pts]
-        rel = (emax - E) / emax
-        if rel <= tol or emax - E <= mp.ldexp(1, 16) * mp.eps:  # relative, or absolute (values ~1)
-            done += 1  # quadratic convergence: two more exchanges after the threshold
-            if done == 3:
-                return c, emax
-    raise RuntimeError("Remez did not converge: n %d a %s rel %s" % (n, mp.nstr(a, 8), mp.nstr(rel, 5)))
+        if (maxerr - minerr) / minerr <= threshold:
+            break
+    return coeffs, maxerr, minerr
 
 
-def composite(degrees, prec, logalpha):
+def composite(degrees, prec, logalpha, logerr):
     with mp.workprec(prec):
-        a = mp.ldexp(mp.mpf(1), -logalpha)
-        tol = mp.ldexp(mp.mpf(1), -(prec // 2))
-        out = []
-        for d in degrees:
-            n = (d - 1) // 2 + 1
-            c, E = remez_odd_one(n, a, tol)
-            s = 1 + E
-            p = [mp.mpf(0)] * (d + 1)
-            for k in range(n):
-                p[2 * k + 1] = c[k] / s
-            a = (1 - E) / s
-            out.append((p, E))
-        last = out[-1][0]
-        for i in range(len(last)):
-            last[i] = last[i] / 2
+        alpha, e = mp.ldexp(mp.mpf(1), -logalpha), mp.ldexp(mp.mpf(1), -logerr)
+        a = alpha
+        polys, errs = [], []
+        for i, d in enumerate(degrees):
+            if i:
+                maxI, minI = 1 + errs[-1], 1 - errs[-1]
+                polys[-1] = [v / maxI for v in polys[-1]]
+                a = minI / maxI
+            c, maxerr, _ = remez_multi([(-1 - e, -a + e), (a - e, 1 + e)], 1 + ((d + 1) >> 1), alpha)
+            p = [mp.mpf(0) if j % 2 == 0 else c[j] for j in range(d + 1)]
+            polys.append(p)
+            errs.append(maxerr)
+        last = [v / 2 for v in polys[-1]]
         last[0] += mp.mpf(0.5)
-        return [[float(v) for v in p] for p, _ in out], [float(E) for _, E in out]
+        polys[-1] = last
+        return [[float(v) for v in p] for p in polys], [float(E) for E in errs]
 
 
 def main():
     cases = []
     for degrees, prec, logalpha, logerr in CASES:
-        polys, errs = composite(degrees, prec, logalpha)
+        polys, errs = composite(degrees, prec, logalpha, logerr)
         cases.append({"degrees": degrees, "prec": prec, "logalpha": logalpha, "logerr": logerr,
                       "stage_errors": errs, "coeffs": polys})
-        print(degrees, "stage errors", errs)
+        print(degrees, logalpha, logerr, "stage errors", errs)
     path = os.path.join(ROOT, "tests", "golden", "minimax_sign.json")
     with open(path, "w") as f:
         json.dump({"generator": "tools/gen_minimax.py (mpmath %s, Remez at prec bits)" % mp.__version__,

@@ -9,9 +9,13 @@ and SQ counter passes) and writes
 
 HBM bytes follow MI355X_MICROARCH.md (HBM/rocprofv3): FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide
-coalesced reads, so it is doubled.  Algorithmic bytes of an NTT call = 16 N
-per limb-transform (24 N with the subtract-and-scale epilogue), for the
-one-pass kernels and the two-pass pairs (ntt2.hip) alike.  The one-pass
+coalesced reads, so it is doubled.  Algorithmic bytes of an NTT call, two
+models (the same two bench.py reports): strict = 16 N per
+limb-transform; fused = 16 N + 8 N per epilogue operand or addend read (the
+subtract-and-scale operand, the word a rotate-and-add store adds to; the
+automorphism's scatter index is a batch-shared table, excluded like the
+twiddles).  Both hold for the one-pass kernels and the two-pass pairs
+(ntt2.hip) alike; the traffic ratio is taken against the fused bytes.  The one-pass
 kernels are persistent (one workgroup per CU walks the jobs), so the
 limb-transform count of a dispatch comes from the library's call log
 (ORION_NTT_LOG, one file per pass: gpurun_out/prof_<tag>/ntt_log_<pass>.txt),
@@ -92,10 +96,10 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
             return [tuple(int(v) for v in ln.split()[:3]) for ln in f if ln.strip()]
 
     # the log's epilogue field (backend.hip log_ntt; 0/1 in logs before the
-    # automorphism epilogues): extra algorithmic bytes per coefficient over the
-    # 16 of a plain transform -- the subtract-and-scale operand (8), the
-    # scatter index (4) and the word the scatter adds to (8)
-    EPI_BYTES = {0: 0.0, 1: 8.0, 2: 12.0, 3: 20.0}
+    # automorphism epilogues): extra fused-model bytes per coefficient over the
+    # 16 of a plain transform -- the subtract-and-scale operand (8) and the word
+    # the scatter adds to (8); the scatter index is not counted
+    EPI_BYTES = {0: 0.0, 1: 8.0, 2: 8.0, 3: 16.0}
     EPI_NAME = {0: "store", 1: "sub", 2: "sub-aut", 3: "sub-aut-acc"}
 
     def ntt_log_full(name):
@@ -164,7 +168,7 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
     tr = sorted(rows(kt), key=lambda r: int(r["Start_Timestamp"])) if os.path.exists(kt) else []
     tr = [r for r in tr if "ntt" in r["Kernel_Name"]]
     n_l = 0
-    n_us = n_b = 0.0
+    n_us = n_b = n_s = 0.0
     klog = ntt_log("kt")
     if klog is not None:
         for call, r, alg, jobs in priced(tr, klog):
@@ -174,6 +178,7 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
             if alg is not None:
                 n_l += 1
                 n_b += alg
+                n_s += 16.0 * N * jobs
     # NTT time by launch class (kt pass): direction, kernel (one-pass / two-pass
     # pair), epilogue, prologue, integer-path share, jobs in multiples of CUs
     classes = {}
@@ -187,18 +192,24 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
             fam = fam or ("1pass" if f[0] == 1 else "2pass")
             key = (f"{'inv' if f[3] else 'fwd'} {fam} "
                    f"{EPI_NAME.get(f[2], 'sub')} pro{f[4]} int{round(f[5] / f[1], 2)} jobs{f[1]}")
-            c = classes.setdefault(key, {"calls": 0, "us": 0.0, "bytes": 0.0})
+            c = classes.setdefault(key, {"calls": 0, "us": 0.0, "bytes": 0.0, "strict_bytes": 0.0})
             c["us"] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
             if alg is not None:
                 c["calls"] += 1
                 c["bytes"] += alg
+                c["strict_bytes"] += 16.0 * N * jobs
         for c in classes.values():
             c["GBps"] = round(c["bytes"] / (c["us"] * 1e-6) / 1e9, 1) if c["us"] else None
+            c["GBps_strict"] = round(c["strict_bytes"] / (c["us"] * 1e-6) / 1e9, 1) if c["us"] else None
             c["us_per_call"] = round(c["us"] / max(c["calls"], 1), 1)
             c["us"] = round(c["us"], 1)
     trace = {"launches": n_l, "avg_launch_us": n_us / n_l if n_l else None,
              "algorithmic_bytes_per_launch": n_b / n_l if n_l else None,
-             "achieved_GBps": n_b / (n_us * 1e-6) / 1e9 if n_us else None}
+             "strict_bytes_per_launch": n_s / n_l if n_l else None,
+             "achieved_GBps": n_b / (n_us * 1e-6) / 1e9 if n_us else None,
+             "achieved_GBps_strict": n_s / (n_us * 1e-6) / 1e9 if n_us else None,
+             "frac_fused": n_b / (n_us * 1e-6) / 1e9 / 8000.0 if n_us else None,
+             "frac_strict": n_s / (n_us * 1e-6) / 1e9 / 8000.0 if n_us else None}
     # VALU roofline of the VALU-bound kernels: the fraction of SIMD cycles in
     # which a VALU instruction was executing, sum over waves of
     # SQ_ACTIVE_INST_VALU (quad-cycles, so x4) / (elapsed cycles x 1024 SIMDs);
