@@ -470,9 +470,15 @@ int launch_ntt_ring(const NttIO& io, const DeviceTables* tb, bool inverse, hipSt
   return -1;
 }
 
+// NTT_ONLY15 (register-usage experiments only, never shipped): instantiate
+// the N = 2^15 Standard-ring kernels alone, so one compile takes seconds
 template <int LOGN>
 int launch_ntt(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
+#ifdef NTT_ONLY15
+  return io.ci ? -1 : launch_ntt_ring<LOGN, false>(io, tb, inverse, st);
+#else
   return io.ci ? launch_ntt_ring<LOGN, true>(io, tb, inverse, st) : launch_ntt_ring<LOGN, false>(io, tb, inverse, st);
+#endif
 }
 
 template <int LOGN, bool CI>
@@ -492,7 +498,9 @@ void init_lds_ring() {
 template <int LOGN>
 void init_lds() {
   init_lds_ring<LOGN, false>();
+#ifndef NTT_ONLY15
   init_lds_ring<LOGN, true>();
+#endif
 }
 
 }  // namespace
@@ -500,8 +508,10 @@ void init_lds() {
 // host entry: NTT (inverse=false) or INTT with the fused prologue / epilogue of io
 int orion_launch_ntt_io(int logN, const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t st) {
   switch (logN) {
+#ifndef NTT_ONLY15
     case 13: return launch_ntt<13>(io, tb, inverse, st);
     case 14: return launch_ntt<14>(io, tb, inverse, st);
+#endif
     case 15: return launch_ntt<15>(io, tb, inverse, st);
     default: return -1;
   }
@@ -519,8 +529,10 @@ int orion_launch_ntt(int logN, const LimbSet& s, const DeviceTables* tb, bool in
 // allow >64 KiB dynamic LDS for the N = 2^14, 2^15 kernels; size the
 // persistent grid: ORION_NTT_PERSIST workgroups per CU (0 = one per job)
 int orion_ntt_init() {
+#ifndef NTT_ONLY15
   init_lds<13>();
   init_lds<14>();
+#endif
   init_lds<15>();
   const char* e = getenv("ORION_NTT_PERSIST");
   const int per_cu = e ? atoi(e) : 1;

@@ -46,6 +46,10 @@ __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, u64 v, int voff
 #ifndef NTT_INT_CUT
 #define NTT_INT_CUT 1
 #endif
+// 1: the inverse (GS) butterfly with the cut quotient too, values in [0, 4q)
+#ifndef NTT_INV_CUT
+#define NTT_INV_CUT 0
+#endif
 struct IntArith {
   typedef u64 T;
   typedef ulonglong2 W;
@@ -77,22 +81,56 @@ struct IntArith {
     }
   }
   // Harvey GS butterfly, values in [0, 2q).  (The cut quotient of the forward
-  // butterfly, with values in [0, 4q), spills the inverse kernel: 128 VGPRs +
-  // 172-196 B of scratch per lane at N = 2^15 in every formulation tried --
-  // cut, the nq form, fenced after every butterfly -- against 120 VGPRs here.)
+  // butterfly, with values in [0, 4q), spilled the inverse kernel in round 4:
+  // 128 VGPRs + 172-196 B of scratch per lane at N = 2^15 -- against 120 VGPRs
+  // here; NTT_INV_CUT retries it with a shorter twiddle prefetch ring.)
+  // NTT_INV_CUT: values in [0, 4q): s = x + y < 8q reduced once into [0, 4q),
+  // Y = cut Shoup of x - y + 4q < 8q (result in [0, 4q)), 8 instead of ~10
+  // 32-bit multiplies and no 64-bit subtraction in the product
   __device__ __forceinline__ void gs(T& X, T& Y, const W& w, bool) const {
     const u64 x = X, y = Y;
     const u64 s = x + y;
-    X = s >= q2 ? s - q2 : s;
-    Y = shoup_lazy(x - y + q2, w.x, w.y, q);
+    if constexpr (NTT_INV_CUT == 3) {  // cut quotient, the product in 64-bit form
+      X = s >= q4 ? s - q4 : s;
+      const u64 a = x - y + q4;
+      const u32 a0 = (u32)a, a1 = (u32)(a >> 32), s0 = (u32)w.y, s1 = (u32)(w.y >> 32);
+      const u64 m1 = (u64)a1 * s0;
+      const u64 m2 = (u64)a0 * s1 + (u32)m1;
+      const u64 qh = (u64)a1 * s1 + ((m1 >> 32) + (m2 >> 32));
+      Y = a * w.x - qh * q;
+    } else if constexpr (NTT_INV_CUT == 2) {  // the nq form of the full quotient: values stay in [0, 2q)
+      X = s >= q2 ? s - q2 : s;
+      Y = shoup_lazy_nq(x - y + q2, w.x, w.y, nq);
+    } else if constexpr (NTT_INV_CUT) {
+      X = s >= q4 ? s - q4 : s;
+      Y = shoup_cut_nq(x - y + q4, w.x, w.y, nq);
+    } else {
+      X = s >= q2 ? s - q2 : s;
+      Y = shoup_lazy(x - y + q2, w.x, w.y, q);
+    }
   }
-  // the last GS stage with N^-1 folded in (inputs in [0, 2q), outputs in [0, 2q))
+  // the last GS stage with N^-1 folded in (inputs in [0, 2q) / [0, 4q) with
+  // NTT_INV_CUT, outputs in [0, 2q) / [0, 4q))
   __device__ __forceinline__ void gs_last(T& X, T& Y) const {
     const u64 x = X, y = Y;
-    X = shoup_lazy(x + y, ninv, ninv_s, q);
-    Y = shoup_lazy(x - y + q2, wl, wl_s, q);
+    if constexpr (NTT_INV_CUT == 3) {
+      X = shoup_lazy(x + y, ninv, ninv_s, q);
+      Y = shoup_lazy(x - y + q4, wl, wl_s, q);
+    } else if constexpr (NTT_INV_CUT == 2) {
+      X = shoup_lazy_nq(x + y, ninv, ninv_s, nq);
+      Y = shoup_lazy_nq(x - y + q2, wl, wl_s, nq);
+    } else if constexpr (NTT_INV_CUT) {
+      X = shoup_cut_nq(x + y, ninv, ninv_s, nq);
+      Y = shoup_cut_nq(x - y + q4, wl, wl_s, nq);
+    } else {
+      X = shoup_lazy(x + y, ninv, ninv_s, q);
+      Y = shoup_lazy(x - y + q2, wl, wl_s, q);
+    }
   }
-  __device__ __forceinline__ u64 final_inv_folded(T x) const { return x >= q ? x - q : x; }
+  __device__ __forceinline__ u64 final_inv_folded(T x) const {
+    if constexpr (NTT_INV_CUT == 1) x = x >= q2 ? x - q2 : x;  // (3: gs_last ends in [0, 2q))
+    return x >= q ? x - q : x;
+  }
   __device__ __forceinline__ T reduce_round(T x) const { return x; }  // lazy range is invariant
   __device__ __forceinline__ u64 final_fwd(T x) const {
     if constexpr (NTT_INT_CUT) x = x >= q4 ? x - q4 : x;

@@ -511,10 +511,11 @@ def test_bootstrap_functional(torch_cuda, h):
     assert lib.GetCiphertextScaleF(out) == 2.0 ** 40
     dec = lib.decode_f64(lib.Decrypt(out))
     err = np.abs(dec - vals.astype(np.float64))
-    # Lattigo's default message ratio (2^8) and degree-30 CosDiscrete cosine: the
-    # oracle's own run of this circuit measures 2.1e-8 / 4.6e-9 (tests/test_oracle.py)
+    # Lattigo's default message ratio (2^8) and degree-30 CosDiscrete cosine:
+    # measured 8.5e-8 / 1.3e-8 (h = 32) and 1.0e-7 / 1.3e-8 (h = 192), r05b; the
+    # Chebyshev-node cosine of round 4 gave ~1e-5 max
     print("bootstrap full h=%d err max %.3g mean %.3g" % (h, err.max(), err.mean()))
-    assert err.max() < 1e-4 and err.mean() < 1e-5, (err.max(), err.mean())
+    assert err.max() < 2.5e-7 and err.mean() < 3e-8, (err.max(), err.mean())
     # the refreshed ciphertext computes: square and rescale
     sq = lib.MulRelinCiphertextNew(out, out)
     lib.Rescale(sq)
@@ -536,9 +537,11 @@ def test_bootstrap_functional(torch_cuda, h):
         assert lib.GetCiphertextScaleF(out_s) == 2.0 ** 40
         exp_s = np.tile(sp[:, :ns], (1, n // ns)).astype(np.float64)
         err = np.abs(lib.decode_f64(lib.Decrypt(out_s)) - exp_s)
-        # the post-scale multiplies the error by the gap (64 at ns = 64)
+        # the post-scale multiplies the error by the gap (64 at ns = 64); measured
+        # (r05b) ns = 1024: 1.3e-7 / 2.2e-8, ns = 64: 6.1e-7 / 1.1e-7 -- bars at ~2x
         print("bootstrap ns=%d h=%d err max %.3g mean %.3g" % (ns, h, err.max(), err.mean()))
-        assert err.max() < 4e-4 and err.mean() < 1e-4, (ns, err.max(), err.mean())
+        bar = {64: (1.3e-6, 2.2e-7)}.get(ns, (3e-7, 5e-8))
+        assert err.max() < bar[0] and err.mean() < bar[1], (ns, err.max(), err.mean())
     lib.DeleteBootstrappers()
     with pytest.raises(RuntimeError, match="no bootstrapper"):
         lib.Bootstrap(ct, n)
@@ -609,7 +612,9 @@ def test_bootstrap_parity(torch_cuda, oracle_mod, sparse):
     x2, got2 = lib.export_ciphertext(ct2), lib.export_ciphertext(out2)
     ref2, rsc2 = orc.bootstrap(boot, circ, keys, x2[0], 0, 2.0 ** 38)
     assert np.array_equal(got2[0], ref2)
-    assert lib.GetCiphertextScaleF(out2) == float(rsc2) and abs(float(rsc2) / 2.0 ** 38 - 1) < 1e-3
+    # F is 4x the default's: the output comes back near the default scale (as
+    # Lattigo's does), carrying F's rounding
+    assert lib.GetCiphertextScaleF(out2) == float(rsc2) and abs(float(rsc2) / 2.0 ** 40 - 1) < 1e-3
     assert np.abs(lib.decode_f64(lib.Decrypt(out2)) - exp).max() < 1e-6
     lib.DeleteScheme()
 

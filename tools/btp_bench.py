@@ -1,8 +1,9 @@
 """Bootstrapping latency/throughput on the GPU: Bootstrap
 of B level-0 ciphertexts at N = 2^LOGN for each slot count in SLOTS (default
 N/2 and N/16); residual chain [60] + [40]x5, bootstrapping chain = residual +
-SlotsToCoeffs 3 (40-bit), EvalMod 9 (60-bit), CoeffsToSlots 3 (55-bit), P =
-[61] x 8 (logPs).  Sparse slot counts run the n-point circuit (trace, one
+Lattigo v6's default circuit [U]: SlotsToCoeffs 3 (39-bit), EvalMod 8 (60-bit:
+the degree-30 CosDiscrete cosine + 3 double angles), CoeffsToSlots 4 (56-bit),
+P = [61] x 8 (logPs).  Sparse slot counts run the n-point circuit (trace, one
 packed EvalMod) and the post-scale; their inputs have slots >= n zeroed and
 their outputs are checked against the replicated n slots.  Prints one JSON
 line per (slots, batch) (the first call generates the rotation keys and is
