@@ -20,14 +20,23 @@
 
 namespace {
 
+// columns per cols-pass workgroup at N = 2^15, rows per rows-pass workgroup:
+// a launch of J jobs runs J 256/CW (J 2^R/RW) workgroups, and with a few jobs
+// (one image) the time is that of the CUs holding the most workgroups
+#ifndef NTT2S_CW15
+#define NTT2S_CW15 8
+#endif
+#ifndef NTT2S_RW
+#define NTT2S_RW 4
+#endif
 template <int LOGN>
 struct S2 {
   static constexpr int R = LOGN - 8;            // row bits: the cols pass transforms 2^R-point columns
-  static constexpr int CW = LOGN == 15 ? 8 : 4;  // columns per cols-pass workgroup
+  static constexpr int CW = LOGN == 15 ? NTT2S_CW15 : 4;  // columns per cols-pass workgroup
   static constexpr int H = 1 << (R - 1);         // butterflies per column per stage
   static constexpr int CT = CW * H;              // cols-pass threads (512)
   static constexpr int CTILES = 256 / CW;        // cols-pass workgroups per limb
-  static constexpr int RW = 4;                   // rows per rows-pass workgroup
+  static constexpr int RW = NTT2S_RW;           // rows per rows-pass workgroup
   static constexpr int RT = RW * 128;            // rows-pass threads (512)
   static constexpr int RTILES = (1 << R) / RW;   // rows-pass workgroups per limb
   static constexpr int CT4 = CW << (R - 2);      // radix-4 cols-pass threads (256)
