@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("ORION_BENCH_BATCH", 64)))
+    # the GPU's batch as P concurrent pipelines of batch/P images each (peer
+    # contexts sharing the keys, their ops interleaved on P HIP streams)
+    ap.add_argument("--pipelines", type=int, default=int(os.environ.get("ORION_BENCH_PIPELINES", 2)))
     ap.add_argument("--workload", default="lola_n15")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     # profiler passes: skip the client-side, batch-1 and hipGraph measurements
@@ -260,6 +263,10 @@ def main():
 
     from orion_amd.replay import OrionStream
     lib_seed = 2024
+    P = max(1, args.pipelines)
+    if args.batch % P:
+        print(f"bench.py: --batch {args.batch} is not a multiple of --pipelines {P}", file=sys.stderr)
+        sys.exit(2)
     st = OrionStream(args.workload, seed=lib_seed + rank, device=local)
     lib = st.lib
     torch_stream = torch.cuda.Stream()
@@ -287,28 +294,69 @@ def main():
             lib.OrionHipSynchronize()
 
         bundle_bytes = odist.broadcast_bundle(dist, lambda: lib.KeyBundleBytes(0), export, load, device)
+    # peer pipelines: copies of the keys (and the secret on rank 0), their own
+    # HIP streams, pools and handles, the same compiled transforms
+    peers = [st] + [OrionStream(args.workload, peer_of=st) for _ in range(P - 1)]
+    for p in peers[1:]:
+        p.compile(gen_keys=False)
     t_setup = time.perf_counter() - t_setup
 
-    # this rank's shard of synthetic images (MNIST-shaped, N(0,1), seed 42 + rank)
+    # this rank's shard of synthetic images (MNIST-shaped, N(0,1), seed 42 + rank),
+    # batch / P images per pipeline
     g = torch.Generator().manual_seed(42 + rank)
     imgs = torch.randn(args.batch, 1, 28, 28, generator=g).numpy()
     imgs[0] = st.reference_input().reshape(1, 28, 28)
-    ct = st.encrypt_batch(imgs)  # public-key encryption (ranks > 0 hold the broadcast pk, no sk)
+    bp = args.batch // P
+    cts = [p.encrypt_batch(imgs[i * bp:(i + 1) * bp]) for i, p in enumerate(peers)]  # public-key encryption
+    ct = cts[0]
     lib.OrionHipSynchronize()
 
     def step():
-        return st.forward(ct)
+        """one pass of the op stream over the GPU's batch: P pipelines' ops interleaved"""
+        if P == 1:
+            return [st.forward(ct)]
+        return OrionStream.forward_interleaved(list(zip(peers, cts)))
+
+    def delete(outs):
+        for p, o in zip(peers, outs):
+            p.use()
+            lib.DeleteCiphertext(o)
+        st.use()
+
+    def profile(mask):
+        for p in peers:
+            p.use()
+            lib.OrionHipProfile(mask)
+        st.use()
+
+    def profile_reset():
+        for p in peers:
+            p.use()
+            lib.OrionHipProfileReset()
+        st.use()
+        lib.OrionHipProfileClock()
+
+    def profile_read():
+        tot = {}
+        for p in peers:
+            p.use()
+            for k, v in lib.profile_read().items():
+                t = tot.setdefault(k, dict(launches=0, ms=0.0, bytes=0.0, strict_bytes=0.0))
+                for f in t:
+                    t[f] += v[f]
+        st.use()
+        return tot
 
     dump_maps("setup")
     stage("warmup")
 
     for _ in range(args.warmup):
-        lib.DeleteCiphertext(step())
+        delete(step())
     lib.OrionHipSynchronize()
 
     stage("timed")
-    lib.OrionHipProfileReset()
-    lib.OrionHipProfile(0b11)  # HIP events around the NTT launches only (the roofline kernel)
+    profile_reset()
+    profile(0b11)  # HIP events around the NTT launches only (the roofline kernel)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -320,8 +368,9 @@ def main():
     lib.OrionHipSynchronize()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    lib.OrionHipProfile(0)
-    prof = lib.profile_read()
+    profile(0)
+    prof = profile_read()
+    ntt_union_ms = lib.profile_union(0b11)  # wall clock with an NTT (forward or inverse) of any pipeline running
     if dist:
         dist.barrier()
         dt = odist.max_over_ranks(dist, dt, device)
@@ -330,9 +379,9 @@ def main():
     # reference input; each rank's output ciphertext for it is gathered to
     # rank 0, which holds the only secret key, and decrypted there
     exp = st.arrays["expected_output"].reshape(-1)
-    out0 = lib.export_ciphertext(outs[-1])[0]
-    level0 = lib.GetCiphertextLevel(outs[-1])
-    scale0 = lib.GetCiphertextScaleF(outs[-1])
+    out0 = lib.export_ciphertext(outs[-1][0])[0]
+    level0 = lib.GetCiphertextLevel(outs[-1][0])
+    scale0 = lib.GetCiphertextScaleF(outs[-1][0])
     shards = [out0]
     if dist:
         t = torch.from_numpy(out0.view(np.int64).copy()).to(device if not rehearse else "cpu")
@@ -353,13 +402,22 @@ def main():
             maes.append(float(np.abs(vals - exp).mean()))
         mae = max(maes)
     for o in outs:
-        lib.DeleteCiphertext(o)
-    # one extra, fully profiled step (outside the timed region) for the per-kernel breakdown
-    lib.OrionHipProfileReset()
+        delete(o)
+    # one extra, fully profiled step (outside the timed region) for the per-kernel
+    # breakdown: the whole batch on ONE pipeline, so every kernel has the GPU to
+    # itself (with P pipelines the timed region's launches overlap each other)
+    ct_all = st.encrypt_batch(imgs) if P > 1 else ct
+    if P > 1:
+        lib.DeleteCiphertext(st.forward(ct_all))  # warm: this batch size's buffers
+        lib.OrionHipSynchronize()
+    profile_reset()
     lib.OrionHipProfile(1)
-    lib.DeleteCiphertext(step())
+    lib.DeleteCiphertext(st.forward(ct_all))
+    lib.OrionHipSynchronize()
     lib.OrionHipProfile(0)
     breakdown = lib.profile_read()
+    if P > 1:
+        lib.DeleteCiphertext(ct_all)
 
     client_ms, b1_ms, graph_step = None, None, None
     dump_maps("extras")
@@ -371,7 +429,10 @@ def main():
         dvals = torch.zeros(args.batch, st.slots, dtype=torch.float32, device=device)
         dvals[:, :imgs[0].size] = torch.from_numpy(imgs.reshape(args.batch, -1)).to(device)
         torch.cuda.synchronize()
-        out_ct = step()
+        st.use()
+        ct_full = st.encrypt_batch(imgs)
+        out_ct = st.forward(ct_full)  # the whole batch's output, on one context
+        lib.DeleteCiphertext(ct_full)
         dout = torch.empty(args.batch, lib.slots, dtype=torch.float64, device=device)  # DecodeDevice: [B][slots]
 
         def client(fn, reps=5):
@@ -428,17 +489,28 @@ def main():
         # the batched step as a hipGraph replay (reported beside the line; the
         # value above is the stream-launched step the NTT events are timed on)
         stage("extras: batched graph capture + replay")
-        gid, g_out = st.capture(ct)
-        lib.OrionHipGraphLaunch(gid)
+        gids = [p.capture(c) for p, c in zip(peers, cts)]  # one graph per pipeline, each on its stream
+
+        def launch_all():
+            for p, (gid, _) in zip(peers, gids):
+                p.use()
+                lib.OrionHipGraphLaunch(gid)
+            st.use()
+
+        launch_all()
         lib.OrionHipSynchronize()
         t1 = time.perf_counter()
         for _ in range(args.steps):
-            lib.OrionHipGraphLaunch(gid)
+            launch_all()
         lib.OrionHipSynchronize()
         g_ms = (time.perf_counter() - t1) / args.steps * 1e3
-        graph_step = {"ms_per_step": round(g_ms, 3), "images_per_s": round(args.batch / g_ms * 1e3, 3)}
-        lib.OrionHipGraphDestroy(gid)
-        lib.DeleteCiphertext(g_out)
+        graph_step = {"ms_per_step": round(g_ms, 3), "images_per_s": round(args.batch / g_ms * 1e3, 3),
+                      "graphs": P}
+        for p, (gid, g_out) in zip(peers, gids):
+            p.use()
+            lib.OrionHipGraphDestroy(gid)
+            lib.DeleteCiphertext(g_out)
+        st.use()
 
     stage("report")
     images = args.batch * world * args.steps
@@ -448,8 +520,26 @@ def main():
     n_ms = sum(p.get("ms", 0.0) for p in ntt)
     n_bytes = sum(p.get("bytes", 0.0) for p in ntt)  # fused model (epilogue operands/addends counted)
     n_strict = sum(p.get("strict_bytes", 0.0) for p in ntt)  # 16 N per limb-transform
-    achieved = (n_strict / (n_ms / 1e3)) / 1e9 if n_ms > 0 else 0.0
-    achieved_fused = (n_bytes / (n_ms / 1e3)) / 1e9 if n_ms > 0 else 0.0
+    # with P pipelines the NTT launches of one overlap the other's kernels, so
+    # the bytes are divided by the wall-clock time during which at least one
+    # NTT ran (the union of the launch intervals; = the summed durations at P = 1)
+    n_time = ntt_union_ms if P > 1 and ntt_union_ms > 0 else n_ms
+    achieved = (n_strict / (n_time / 1e3)) / 1e9 if n_time > 0 else 0.0
+    achieved_fused = (n_bytes / (n_time / 1e3)) / 1e9 if n_time > 0 else 0.0
+    solo_line = None
+    if P > 1:
+        sn = [breakdown.get("ntt_fwd", {}), breakdown.get("ntt_inv", {})]
+        s_ms = sum(p.get("ms", 0.0) for p in sn)
+        s_strict = sum(p.get("strict_bytes", 0.0) for p in sn)
+        s_bytes = sum(p.get("bytes", 0.0) for p in sn)
+        s_launch = sum(p.get("launches", 0) for p in sn)
+        solo_line = {"definition": "the whole batch on one pipeline (no concurrent kernels), the profiled "
+                                   "breakdown step outside the timed region; 16 N per limb-transform / summed "
+                                   "launch time",
+                     "achieved": round(s_strict / (s_ms / 1e3) / 1e9, 1) if s_ms else None,
+                     "frac": round(s_strict / (s_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if s_ms else None,
+                     "frac_fused": round(s_bytes / (s_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if s_ms else None,
+                     "launches": s_launch, "avg_launch_us": round(s_ms / max(s_launch, 1) * 1e3, 2)}
     total_prof_ms = sum(p["ms"] for p in breakdown.values())
     bd_ntt_ms = breakdown.get("ntt_fwd", {}).get("ms", 0) + breakdown.get("ntt_inv", {}).get("ms", 0)
     traffic = None
@@ -498,11 +588,20 @@ def main():
                                    f"LogP=[60,60], input level {st.input_level}, Standard ring",
                        "batch_per_gpu": args.batch, "global_batch": args.batch * world,
                        "parallelism": f"replicas x{world} (image shards), keys RCCL-broadcast"
-                                      + (" (rehearsal: gloo, shared GPUs)" if rehearse else "")},
+                                      + (" (rehearsal: gloo, shared GPUs)" if rehearse else "")
+                                      + (f"; per GPU {P} concurrent pipelines of {args.batch // P} images "
+                                         "(peer contexts sharing the keys, ops interleaved on their HIP streams)"
+                                         if P > 1 else "")},
             "roofline": {"bound": "hbm", "kernel": "ntt (fwd+inv: one-pass, 1 limb per workgroup; two-pass for partial-round launches)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "definition": "strict (SURVEY 8d): 16 N bytes per limb-transform / HIP-event launch time",
+                         "definition": "strict (SURVEY 8d): 16 N bytes per limb-transform / NTT time from HIP events "
+                                       "over the timed region" + (f" -- with {P} pipelines the wall-clock union of the "
+                                       "NTT launch intervals (launches of one pipeline overlap the other's kernels)"
+                                       if P > 1 else " (summed launch durations)"),
+                         "pipelines": P,
+                         "ntt_summed_launch_ms": round(n_ms, 3), "ntt_wall_ms": round(n_time, 3),
+                         "single_pipeline": solo_line,
                          "achieved_fused": round(achieved_fused, 1),
                          "frac_fused": round(achieved_fused / HBM_PEAK_GBS, 4),
                          "definition_fused": "16 N per limb-transform + 8 N per epilogue operand or addend read "

@@ -161,7 +161,16 @@ int OrionHipSetDevice(int device);
 void OrionHipSetSeed(unsigned long seed);                /* keygen / encryption PRNG seed */
 void OrionHipSetStream(void *hipStream);                  /* NULL = library-owned stream */
 void *OrionHipGetStream(void);
-int OrionHipSynchronize(void);
+/* peer pipelines: OrionHipPeerCreate makes a second context on the scheme's
+ * chain with copies of its keys and its own stream, buffer pool and handle
+ * heaps (returns its id; the scheme's context is 0); OrionHipPeerSelect(id)
+ * makes every following call act on that context.  Ops issued to two
+ * contexts alternately run concurrently on the GPU.  DeleteScheme removes
+ * every peer. */
+int OrionHipPeerCreate(void);
+int OrionHipPeerSelect(int id);
+int OrionHipPeerCount(void);
+int OrionHipSynchronize(void); /* drains every context's stream */
 /* hipGraph capture of an op stream issued through this ABI: every call between
  * Begin and End is recorded into one graph (returned id), which Launch replays
  * on the library stream with one launch, into the same buffers (the pool pins
@@ -277,6 +286,12 @@ int OrionHipProfileRead(char *names, long *launches, double *ms, double *bytes, 
  * equal to their algorithmic bytes) */
 int OrionHipProfileReadStrict(double *strict, int max);
 void OrionHipProfileReset(void);
+/* union timing across contexts (peer pipelines): ProfileClock records the
+ * reference and drops the collected intervals; ProfileUnion returns the
+ * wall-clock length (ms) of the union of the intervals of every context's
+ * profiled launches of the categories in `mask` since then */
+void OrionHipProfileClock(void);
+double OrionHipProfileUnion(unsigned mask);
 
 /* raw kernel entry for the roofline microbenchmark and parity tests:
  * in-place NTT/INTT of `nlimb` limbs x `batch` images at device pointer

@@ -139,6 +139,9 @@ SIGNATURES = {
     "OrionHipSetSeed": ([c_ulong], None),
     "OrionHipSetStream": ([c_void_p], None),
     "OrionHipGetStream": ([], c_void_p),
+    "OrionHipPeerCreate": ([], c_int),
+    "OrionHipPeerSelect": ([c_int], c_int),
+    "OrionHipPeerCount": ([], c_int),
     "OrionHipSynchronize": ([], c_int),
     "OrionHipGraphBegin": ([], c_int),
     "OrionHipGraphEnd": ([], c_int),
@@ -181,6 +184,8 @@ SIGNATURES = {
     "OrionHipProfileRead": ([c_char_p, P(ctypes.c_long), P(c_double), P(c_double), c_int], c_int),
     "OrionHipProfileReadStrict": ([P(c_double), c_int], c_int),
     "OrionHipProfileReset": ([], None),
+    "OrionHipProfileClock": ([], None),
+    "OrionHipProfileUnion": ([ctypes.c_uint], c_double),
     "OrionHipNTT": ([P(c_ulong), c_int, c_int, P(c_int), c_int], c_int),
 }
 
@@ -528,6 +533,14 @@ class HipLibrary:
             out[nm] = dict(launches=int(launches[i]), ms=float(ms[i]), bytes=float(byts[i]),
                            strict_bytes=float(strict[i]))
         return out
+
+    def profile_union(self, mask):
+        """ms of wall clock with at least one profiled launch of a category in
+        `mask` running, over every context, since OrionHipProfileClock."""
+        v = self.lib.OrionHipProfileUnion(mask)
+        if v < 0:
+            raise RuntimeError(f"OrionHipProfileUnion: {self.lib.OrionHipLastError().decode()}")
+        return v
 
     def _chk(self, rc, name):
         if rc is None or (isinstance(rc, int) and rc < 0):

@@ -315,6 +315,17 @@ static const char* kProfNames[] = {"ntt_fwd", "ntt_inv", "elementwise", "basis_e
 // priced (ns + 1) 8 N per limb-transform (+ 8 N for a subtract-and-scale epilogue)
 enum { P_NTT_FWD = 0, P_NTT_INV, P_EW, P_BEXT, P_MAC, P_AUT, P_TENSOR, P_RSPREP, P_LTMAC, P_LTGIANT, P_NTT_BEXT, P_NCAT };
 
+// wall-clock intervals of the profiled launches of every context (peer
+// pipelines run concurrently), relative to one reference event
+// (OrionHipProfileClock): the union per category is the time the GPU spent
+// with at least one such launch running (OrionHipProfileUnion)
+struct ProfIv {
+  int cat;
+  float t0, t1;
+};
+static hipEvent_t g_prof_ref = nullptr;
+static std::vector<ProfIv> g_prof_iv;
+
 // ---------------------------------------------------------------------------
 // context
 // ---------------------------------------------------------------------------
@@ -453,6 +464,12 @@ struct Context {
     for (auto& r : prof_recs) {
       float ms = 0;
       hipEventElapsedTime(&ms, r.e0, r.e1);
+      if (g_prof_ref) {
+        float a0 = 0, a1 = 0;
+        hipEventElapsedTime(&a0, g_prof_ref, r.e0);
+        hipEventElapsedTime(&a1, g_prof_ref, r.e1);
+        g_prof_iv.push_back(ProfIv{r.cat, a0, a1});
+      }
       prof_launch[r.cat] += 1;
       prof_ms[r.cat] += ms;
       prof_bytes[r.cat] += r.bytes;
@@ -1345,6 +1362,24 @@ struct Context {
   void import_secret(const std::vector<int64_t>& s) {
     sk = secret_poly(s);
     have_sk = true;
+  }
+  // copies of another context's keys (same chain) in this context's pool
+  void adopt_keys(const Context& o) {
+    if (o.mods != mods) throw std::runtime_error("peer context: another modulus chain");
+    HIPCHK(hipStreamSynchronize(o.stream));
+    auto cp = [&](const Poly& src) {
+      Poly d = alloc(src.ncomp, src.nlimb, src.B);
+      HIPCHK(hipMemcpyAsync(d.ptr(), src.ptr(), (size_t)src.ncomp * src.nlimb * src.B * N * 8,
+                            hipMemcpyDeviceToDevice, stream));
+      return d;
+    };
+    if (o.have_sk) sk = cp(o.sk), have_sk = true;
+    if (o.have_pk) pk = cp(o.pk), have_pk = true;
+    if (o.have_rlk) rlk = cp(o.rlk), have_rlk = true;
+    for (auto& kv : o.gks) gks[kv.first] = EvKey{cp(kv.second.k), kv.second.level};
+    key_hint = o.key_hint;
+    gk_host = o.gk_host;
+    HIPCHK(hipStreamSynchronize(stream));
   }
   LimbSet full(const Poly& P, int c0, int nc) const { return ls(P, c0, nc, iota(0, L + K), iota(0, L + K)); }
 
@@ -2807,7 +2842,11 @@ struct Context {
   }
 };
 
-static std::unique_ptr<Context> g;
+// the scheme's context ([0]) and its peer pipelines ([1..], OrionHipPeerCreate:
+// the same chain and keys, their own stream, pool and handles); g is the one
+// the C-ABI calls act on (OrionHipPeerSelect)
+static std::vector<std::unique_ptr<Context>> g_ctxs;
+static Context* g = nullptr;
 static std::recursive_mutex g_mu;
 
 static Context& ctx() {
@@ -2865,7 +2904,7 @@ static bool defer_keeps(const char* fn) {
       "AddCiphertext", "DeleteCiphertext", "DeletePlaintext", "GetCiphertextScale", "GetCiphertextScaleF",
       "GetCiphertextLevel", "GetCiphertextSlots", "GetCiphertextDegree", "GetCiphertextBatch", "GetPlaintextScale",
       "GetPlaintextLevel", "GetPlaintextSlots", "GetPlaintextBatch", "GetLiveCiphertexts", "GetLivePlaintexts",
-      "GetModuliChain", "GaloisElement"};
+      "GetModuliChain", "GaloisElement", "OrionHipPeerSelect", "OrionHipPeerCount"};
   return keep.count(fn) != 0;
 }
 static void defer_gate(const char* fn) {
@@ -2949,9 +2988,10 @@ void OrionHipSetStream(void* s) {
 
 void* OrionHipGetStream(void) { return g ? (void*)g->stream : nullptr; }
 
-int OrionHipSynchronize(void) {
+int OrionHipSynchronize(void) {  // every context's stream (peer pipelines included)
   API_BEGIN
-  HIPCHK(hipStreamSynchronize(ctx().stream));
+  ctx();
+  for (auto& p : g_ctxs) HIPCHK(hipStreamSynchronize(p->stream));
   return 0;
   API_END(-1)
 }
@@ -3002,8 +3042,10 @@ void NewScheme(int logN, int* logQ, int lenQ, int* logP, int lenP, int logScale,
   // the CI NTT folds/unfolds inside the one-pass kernels (N <= 2^15 per CU)
   if (ci && (logN < 13 || logN > 15))
     throw std::runtime_error("ConjugateInvariant ring: logN must be 13..15 in this build");
-  g.reset();
-  g.reset(new Context());
+  g = nullptr;
+  g_ctxs.clear();
+  g_ctxs.emplace_back(new Context());
+  g = g_ctxs[0].get();
   g->stream = g_user_stream;
   g->prng = Prng(g_seed);
   g->setup(logN, std::vector<int>(logQ, logQ + lenQ), std::vector<int>(logP, logP + lenP), logScale, h, ci);
@@ -3013,9 +3055,40 @@ void NewScheme(int logN, int* logQ, int lenQ, int* logP, int lenP, int logScale,
 
 void DeleteScheme(void) {
   API_BEGIN
-  g.reset();
+  g = nullptr;
+  while (!g_ctxs.empty()) g_ctxs.pop_back();  // peers first
   API_END_VOID
 }
+
+// A peer pipeline: a second context on the same chain with copies of the
+// scheme's keys (secret, public, relinearisation, Galois), its own stream,
+// buffer pool and handle heaps.  Ops issued to two contexts alternately run
+// concurrently on the GPU (their kernels share the CUs), which fills the
+// partial rounds and desynchronises the load and compute phases of the
+// one-limb-per-CU NTT.  Returns the peer's id (the scheme's context is 0).
+int OrionHipPeerCreate(void) {
+  API_BEGIN
+  if (g_ctxs.empty()) throw std::runtime_error("scheme not initialised: call NewScheme first");
+  Context& c0 = *g_ctxs[0];
+  std::unique_ptr<Context> p(new Context());
+  p->prng = Prng(c0.prng.next());
+  p->init_moduli(c0.logN, c0.mods, c0.logQ_bits, c0.logP_bits, c0.logScale, c0.h, c0.ci);
+  p->adopt_keys(c0);
+  p->seed_encryption(g_seed + 0x9e3779b97f4a7c15ull * g_ctxs.size());
+  g_ctxs.push_back(std::move(p));
+  return (int)g_ctxs.size() - 1;
+  API_END(-1)
+}
+int OrionHipPeerSelect(int id) {
+  std::lock_guard<std::recursive_mutex> lk_(g_mu);
+  if (id < 0 || id >= (int)g_ctxs.size()) {
+    g_last_error = "no such peer context: " + std::to_string(id);
+    return -1;
+  }
+  g = g_ctxs[id].get();
+  return 0;
+}
+int OrionHipPeerCount(void) { return (int)g_ctxs.size(); }
 
 void FreeCArray(void* p) { free(p); }
 
@@ -4328,6 +4401,43 @@ void OrionHipProfile(int enable) {
   if (!enable) c.prof_flush();
   c.prof = enable == 1 ? 0xffffffffu : (unsigned)enable;  // 1 = all categories, else a bit mask
   API_END_VOID
+}
+// the reference of the union timing: recorded on the current context's
+// stream; the intervals collected so far are dropped
+void OrionHipProfileClock(void) {
+  API_BEGIN
+  Context& c = ctx();
+  for (auto& p : g_ctxs) p->prof_flush();
+  g_prof_iv.clear();
+  if (!g_prof_ref) HIPCHK(hipEventCreate(&g_prof_ref));
+  HIPCHK(hipEventRecord(g_prof_ref, c.stream));
+  HIPCHK(hipEventSynchronize(g_prof_ref));
+  API_END_VOID
+}
+// the union of the wall-clock intervals of every context's profiled launches
+// of the categories in `mask` since OrionHipProfileClock (ms): e.g. the time
+// at least one NTT ran while two pipelines interleave
+double OrionHipProfileUnion(unsigned mask) {
+  API_BEGIN
+  for (auto& p : g_ctxs) p->prof_flush();
+  std::vector<std::pair<float, float>> iv;
+  for (const ProfIv& r : g_prof_iv)
+    if (mask & (1u << r.cat)) iv.push_back({r.t0, r.t1});
+  std::sort(iv.begin(), iv.end());
+  double tot = 0;
+  float b = 0, e = 0;
+  bool open = false;
+  for (auto& x : iv) {
+    if (!open || x.first > e) {
+      if (open) tot += e - b;
+      b = x.first, e = x.second, open = true;
+    } else if (x.second > e) {
+      e = x.second;
+    }
+  }
+  if (open) tot += e - b;
+  return tot;
+  API_END(-1.0)
 }
 void OrionHipProfileReset(void) {
   API_BEGIN

@@ -63,22 +63,38 @@ _NEW_CT = ("EvaluateLinearTransform", "EvaluatePolynomial", "Bootstrap", "Negate
 class OrionStream:
     """A compiled Orion model as an op stream bound to one HipLibrary."""
 
-    def __init__(self, name, lib=None, seed=2024, device=None, root=GOLDEN, synthetic_diagonals=False):
+    def __init__(self, name, lib=None, seed=2024, device=None, root=GOLDEN, synthetic_diagonals=False,
+                 peer_of=None):
+        """peer_of: another OrionStream whose scheme (and keys) this one shares
+        as a peer pipeline (OrionHipPeerCreate): its own stream, buffer pool
+        and handles, so the two can run concurrently (forward_interleaved)."""
         self.name = name
         self.trace, self.arrays = load_stream(name, root)
         self.meta = self.trace["meta"]
         cfg = self.meta["config"]
-        self.lib = lib or HipLibrary()
-        self.lib.new_scheme(cfg["logn"], cfg["logq"], cfg["logp"], cfg["logscale"], h=cfg["h"], seed=seed,
-                            device=device, ringtype=cfg.get("ringtype", "standard"))
+        if peer_of is not None:
+            self.lib = peer_of.lib
+            self.ctx_id = self.lib._chk(self.lib.OrionHipPeerCreate(), "OrionHipPeerCreate")
+        else:
+            self.lib = lib or HipLibrary()
+            self.lib.new_scheme(cfg["logn"], cfg["logq"], cfg["logp"], cfg["logscale"], h=cfg["h"], seed=seed,
+                                device=device, ringtype=cfg.get("ringtype", "standard"))
+            self.ctx_id = 0
+        self.use()
         self.slots = self.meta["slots"]
         self.synthetic = synthetic_diagonals
         self.pt_map, self.ct_map, self.lt_map, self.poly_map = {}, {}, {}, {}
         self.input_level = self.meta["input_level"]
         self._events = self.trace["events"]
 
+    def use(self):
+        """Make this pipeline's context the one the library's calls act on."""
+        if self.lib.OrionHipPeerCount() > 1 or self.ctx_id:
+            self.lib._chk(self.lib.OrionHipPeerSelect(self.ctx_id), "OrionHipPeerSelect")
+
     # -- setup: keys + evaluator (key_generator.py:10-15, evaluator.py:2-6) ---
     def keygen(self, with_po2=True):
+        self.use()
         lib = self.lib
         lib.NewKeyGenerator()
         lib.GenerateSecretKey()
@@ -95,6 +111,7 @@ class OrionStream:
 
     # -- compile phase: bias plaintexts + linear transforms + their keys --------
     def compile(self, gen_keys=True):
+        self.use()
         lib = self.lib
         rng = np.random.default_rng(7)
         for ev in self._events:
@@ -134,6 +151,7 @@ class OrionStream:
     def encrypt_batch(self, images):
         """images: (B, ...) array; each image flattened into the slots the way
         orion's encoder pads it (encoder.py:29-42)."""
+        self.use()
         imgs = np.asarray(images, dtype=np.float32).reshape(len(images), -1)
         enc = [e for e in self.input_events() if e["op"] == "Encode"][0]
         level, scale = enc["args"][1], enc["args"][2]
@@ -152,6 +170,36 @@ class OrionStream:
         """hook(event, handle): called after every replayed op (debugging).
         stop_after: index of a forward event; the handle that event produced is
         returned (the stream's other temporaries are deleted)."""
+        self.use()
+        it = self.forward_iter(ct_in, hook, stop_after)
+        while True:
+            try:
+                next(it)
+            except StopIteration as e:
+                return e.value
+
+    @staticmethod
+    def forward_interleaved(pairs):
+        """Run the forward passes of several pipelines [(stream, ct_in), ...]
+        (peer contexts of one scheme) op by op in turn, so their kernels run
+        concurrently on the GPU; returns their outputs in order."""
+        its = [(st, st.forward_iter(ct)) for st, ct in pairs]
+        outs = [None] * len(its)
+        live = list(range(len(its)))
+        while live:
+            for i in list(live):
+                st, it = its[i]
+                st.use()
+                try:
+                    next(it)
+                except StopIteration as e:
+                    outs[i] = e.value
+                    live.remove(i)
+        return outs
+
+    def forward_iter(self, ct_in, hook=None, stop_after=None):
+        """forward() one op at a time: yields after every library call that
+        enqueues GPU work; the generator's return value is the output."""
         lib = self.lib
         in_ids = self.meta["input_ids"]
         ct_map = {in_ids[0]: ct_in}
@@ -190,6 +238,7 @@ class OrionStream:
                 cargs.append(ct_map[a] if k == "ct" else self.pt_map[a] if k == "pt" else
                              self.lt_map[a] if k == "lt" else self.poly_map[a] if k == "poly" else a)
             h = getattr(lib, op)(*cargs)
+            yield
             if hook is not None:
                 hook(ev, h)
             if ret is not None:
@@ -210,6 +259,7 @@ class OrionStream:
         re-runs every kernel of the pass on ct_in's current contents and
         rewrites the output handle; the clone keeps in-place ops off ct_in.
         Run forward() once first (keys, tables and LT plans are made then)."""
+        self.use()
         lib = self.lib
         lib.OrionHipGraphBegin()
         try:
@@ -227,6 +277,7 @@ class OrionStream:
 
     def decrypt_output(self, ct, n_out=None):
         """Decrypt + decode a batch output; returns (B, n_out) floats."""
+        self.use()
         lib = self.lib
         B = lib.GetCiphertextBatch(ct)
         pt = lib.Decrypt(ct)

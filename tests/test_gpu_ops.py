@@ -403,3 +403,44 @@ def test_library_deferral_matches_undeferred(torch_cuda, monkeypatch):
             outs.append(lib.export_ciphertext(st.forward(ct)))
             lib.DeleteScheme()
         assert np.array_equal(outs[0], outs[1]), name
+
+
+def test_peer_pipelines_interleaved(torch_cuda):
+    """Peer pipelines (OrionHipPeerCreate / OrionHipPeerSelect): a second
+    context on the scheme's chain with copies of its keys, its own stream,
+    pool and handles.  Two pipelines replayed op by op in turn
+    (OrionStream.forward_interleaved, their kernels concurrent on the GPU)
+    give, for the same input ciphertext, exactly the single pipeline's output
+    -- LoLA N=2^13 at batch 3 and N=2^15 at batch 4; DeleteScheme removes the
+    peers."""
+    import numpy as np
+    from orion_amd.replay import OrionStream
+    for name, B in (("lola_n13", 3), ("lola_n15", 4)):
+        st = OrionStream(name, seed=91)
+        st.keygen()
+        st.compile()
+        st2 = OrionStream(name, peer_of=st)
+        st2.compile()
+        lib = st.lib
+        assert lib.OrionHipPeerCount() == 2 and st2.ctx_id == 1
+        rng = np.random.default_rng(92)
+        imgs = rng.standard_normal((B,) + np.asarray(st.reference_input()).shape[1:]).astype(np.float32)
+        ct = st.encrypt_batch(imgs)
+        x, scale = lib.export_ciphertext(ct), lib.GetCiphertextScaleF(ct)
+        st2.use()
+        ct2 = lib.import_ciphertext(x, scale)
+        st.use()
+        ref = lib.export_ciphertext(st.forward(lib.CloneCiphertext(ct)))
+        outs = OrionStream.forward_interleaved([(st, ct), (st2, ct2)])
+        st.use()
+        got0 = lib.export_ciphertext(outs[0])
+        st2.use()
+        got1 = lib.export_ciphertext(outs[1])
+        assert np.array_equal(got0, ref) and np.array_equal(got1, ref), name
+        # the peer decrypts with its copy of the secret
+        dec = st2.decrypt_output(outs[1])
+        exp = st.arrays["expected_output"].reshape(-1)
+        assert dec.shape[0] == B
+        st.use()
+        lib.DeleteScheme()
+        assert lib.OrionHipPeerCount() == 0
