@@ -291,6 +291,8 @@ void OrionHipProfileReset(void);
  * wall-clock length (ms) of the union of the intervals of every context's
  * profiled launches of the categories in `mask` since then */
 void OrionHipProfileClock(void);
+/* a marker line "# tag" in the ORION_NTT_LOG call log (no-op without it) */
+void OrionHipLogMark(const char *tag);
 double OrionHipProfileUnion(unsigned mask);
 
 /* raw kernel entry for the roofline microbenchmark and parity tests:

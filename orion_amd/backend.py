@@ -185,6 +185,7 @@ SIGNATURES = {
     "OrionHipProfileReadStrict": ([P(c_double), c_int], c_int),
     "OrionHipProfileReset": ([], None),
     "OrionHipProfileClock": ([], None),
+    "OrionHipLogMark": ([c_char_p], None),
     "OrionHipProfileUnion": ([ctypes.c_uint], c_double),
     "OrionHipNTT": ([P(c_ulong), c_int, c_int, P(c_int), c_int], c_int),
 }

@@ -325,6 +325,18 @@ struct ProfIv {
 };
 static hipEvent_t g_prof_ref = nullptr;
 static std::vector<ProfIv> g_prof_iv;
+// ORION_NTT_LOG: one line per NTT call for tools/pmc_summary.py -- one
+// line-buffered file for the whole process, so the lines of every context
+// (peer pipelines) stay in call order, which is dispatch order
+static FILE* ntt_log_file() {
+  static FILE* const f = []() -> FILE* {
+    const char* p = getenv("ORION_NTT_LOG");
+    FILE* h = p && *p ? fopen(p, "a") : nullptr;
+    if (h) setvbuf(h, nullptr, _IOLBF, 0);
+    return h;
+  }();
+  return f;
+}
 
 // ---------------------------------------------------------------------------
 // context
@@ -424,7 +436,6 @@ struct Context {
     }
     for (auto e : ev_free) hipEventDestroy(e);
     if (own_stream && stream) hipStreamDestroy(stream);
-    if (ntt_log) fclose(ntt_log);
   }
 
   // -- profiling -----------------------------------------------------------
@@ -775,14 +786,8 @@ struct Context {
   // tools/pmc_summary.py can price each dispatch of a rocprofv3 pass with its
   // limb-transform count (persistent launches have fewer workgroups than
   // jobs) and break the NTT time down by launch class
-  FILE* ntt_log = nullptr;
-  bool ntt_log_init = false;
   void log_ntt(int family, const NttIO& io, bool inv) {
-    if (!ntt_log_init) {
-      ntt_log_init = true;
-      const char* p = getenv("ORION_NTT_LOG");
-      if (p && *p) ntt_log = fopen(p, "a");
-    }
+    FILE* const ntt_log = ntt_log_file();
     if (!ntt_log) return;
     int nint = 0;
     for (int l = 0; l < io.dst.nlimb; ++l) nint += host_tb.mc[io.dst.mod[l]].f64 ? 0 : 1;
@@ -4438,6 +4443,11 @@ double OrionHipProfileUnion(unsigned mask) {
   if (open) tot += e - b;
   return tot;
   API_END(-1.0)
+}
+// a marker line ("# tag") in the NTT call log (bench.py brackets its timed
+// region, so a kernel trace can be cut to it)
+void OrionHipLogMark(const char* tag) {
+  if (FILE* f = ntt_log_file()) fprintf(f, "# %s\n", tag ? tag : "");
 }
 void OrionHipProfileReset(void) {
   API_BEGIN

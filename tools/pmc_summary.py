@@ -88,12 +88,30 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
     ntt_alg = ntt_fetch = ntt_write = 0.0
     def ntt_log(name):
         """The pass's NTT calls in order (bench.py run with ORION_NTT_LOG):
-        (dispatches, jobs, subtract-and-scale epilogue)."""
+        (dispatches, jobs, subtract-and-scale epilogue); marker lines skipped."""
         p = os.path.join(d, f"ntt_log_{name}.txt")
         if not os.path.exists(p):
             return None
         with open(p) as f:
-            return [tuple(int(v) for v in ln.split()[:3]) for ln in f if ln.strip()]
+            return [tuple(int(v) for v in ln.split()[:3]) for ln in f if ln.strip() and not ln.startswith("#")]
+
+    def log_window(name, tag):
+        """[c0, c1): the calls between the log's last "# <tag> begin" and
+        "# <tag> end" markers (bench.py: "timed" = the timed steps, "solo" =
+        the profiled step of the whole batch on one pipeline), or None."""
+        p = os.path.join(d, f"ntt_log_{name}.txt")
+        if not os.path.exists(p):
+            return None
+        i, c0, win = 0, None, None
+        with open(p) as f:
+            for ln in f:
+                if ln.startswith(f"# {tag} begin"):
+                    c0 = i
+                elif ln.startswith(f"# {tag} end") and c0 is not None:
+                    win = (c0, i)
+                elif ln.strip() and not ln.startswith("#"):
+                    i += 1
+        return win
 
     # the log's epilogue field (backend.hip log_ntt; 0/1 in logs before the
     # automorphism epilogues): extra fused-model bytes per coefficient over the
@@ -108,7 +126,7 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
         if not os.path.exists(p):
             return None
         with open(p) as f:
-            return [tuple(int(v) for v in ln.split()) for ln in f if ln.strip()]
+            return [tuple(int(v) for v in ln.split()) for ln in f if ln.strip() and not ln.startswith("#")]
 
     def priced(dispatches, log):
         """Pair the pass's NTT dispatches (in issue order) with its logged calls:
@@ -165,13 +183,31 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
     # duration = the dispatches' summed time, priced with the logged
     # limb-transform counts; setup calls (keygen, < 64 jobs) are excluded
     kt = os.path.join(d, "kt_kernel_trace.csv")
-    tr = sorted(rows(kt), key=lambda r: int(r["Start_Timestamp"])) if os.path.exists(kt) else []
+    # issue order (Dispatch_Id): with peer pipelines the kernels of two streams
+    # start out of call order, but they are dispatched in it
+    tr = sorted(rows(kt), key=lambda r: int(r["Dispatch_Id"])) if os.path.exists(kt) else []
     tr = [r for r in tr if "ntt" in r["Kernel_Name"]]
     n_l = 0
     n_us = n_b = n_s = 0.0
     klog = ntt_log("kt")
+    win = log_window("kt", "timed")
+    swin = log_window("kt", "solo")
+    w_iv, w_b, w_s, w_l = [], 0.0, 0.0, 0
+    s_us, s_b, s_s, s_l = 0.0, 0.0, 0.0, 0
     if klog is not None:
         for call, r, alg, jobs in priced(tr, klog):
+            if win and win[0] <= call < win[1]:  # bench.py's timed steps: every NTT call counts
+                w_iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+                if alg is not None:
+                    w_l += 1
+                    w_b += alg
+                    w_s += 16.0 * N * jobs
+            if swin and swin[0] <= call < swin[1]:  # the single-pipeline step the bench's roofline is taken on
+                s_us += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+                if alg is not None:
+                    s_l += 1
+                    s_b += alg
+                    s_s += 16.0 * N * jobs
             if jobs < 64:
                 continue
             n_us += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
@@ -179,6 +215,26 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
                 n_l += 1
                 n_b += alg
                 n_s += 16.0 * N * jobs
+    # the timed window: the wall-clock union of its NTT dispatch intervals (the
+    # bench line's definition with peer pipelines) and their summed durations
+    timed = None
+    if w_iv:
+        w_iv.sort()
+        union = 0
+        b, e = w_iv[0]
+        for x0, x1 in w_iv[1:]:
+            if x0 > e:
+                union += e - b
+                b, e = x0, x1
+            else:
+                e = max(e, x1)
+        union += e - b
+        summed = sum(x1 - x0 for x0, x1 in w_iv)
+        timed = {"calls": w_l, "union_us": union / 1e3, "summed_us": summed / 1e3,
+                 "strict_bytes": w_s, "fused_bytes": w_b,
+                 "frac_strict_union": w_s / (union * 1e-9) / 1e9 / 8000.0 if union else None,
+                 "frac_fused_union": w_b / (union * 1e-9) / 1e9 / 8000.0 if union else None,
+                 "frac_strict_summed": w_s / (summed * 1e-9) / 1e9 / 8000.0 if summed else None}
     # NTT time by launch class (kt pass): direction, kernel (one-pass / two-pass
     # pair), epilogue, prologue, integer-path share, jobs in multiples of CUs
     classes = {}
@@ -209,7 +265,13 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
              "achieved_GBps": n_b / (n_us * 1e-6) / 1e9 if n_us else None,
              "achieved_GBps_strict": n_s / (n_us * 1e-6) / 1e9 if n_us else None,
              "frac_fused": n_b / (n_us * 1e-6) / 1e9 / 8000.0 if n_us else None,
-             "frac_strict": n_s / (n_us * 1e-6) / 1e9 / 8000.0 if n_us else None}
+             "frac_strict": n_s / (n_us * 1e-6) / 1e9 / 8000.0 if n_us else None,
+             "timed_window": timed,
+             "solo_window": {"calls": s_l, "avg_launch_us": s_us / s_l if s_l else None,
+                             "strict_bytes_per_launch": s_s / s_l if s_l else None,
+                             "frac_strict": s_s / (s_us * 1e-6) / 1e9 / 8000.0 if s_us else None,
+                             "frac_fused": s_b / (s_us * 1e-6) / 1e9 / 8000.0 if s_us else None}
+             if s_l else None}
     # VALU roofline of the VALU-bound kernels: the fraction of SIMD cycles in
     # which a VALU instruction was executing, sum over waves of
     # SQ_ACTIVE_INST_VALU (quad-cycles, so x4) / (elapsed cycles x 1024 SIMDs);
