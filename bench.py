@@ -263,7 +263,7 @@ def main():
 
     from orion_amd.replay import OrionStream
     lib_seed = 2024
-    P = max(1, args.pipelines)
+    P = max(1, min(args.pipelines, args.batch))  # (a batch of one image runs on one pipeline)
     if args.batch % P:
         print(f"bench.py: --batch {args.batch} is not a multiple of --pipelines {P}", file=sys.stderr)
         sys.exit(2)

@@ -854,7 +854,7 @@ struct Context {
   // N = 2^16 ModDowns onto 20-30 Q limbs measured slower fused)
   double ntt_ifuse_maxr = getenv("ORION_NTT_IFUSE_MAXR") ? atof(getenv("ORION_NTT_IFUSE_MAXR")) : 8.0;
   bool on_ntt2s(int jobs, bool inv, int pro, int epi, bool inplace_sub) {
-    return (logN == 15 || logN == 16) && !ci && ntt2_chunk <= 0 && jobs <= ntt2s_below &&
+    return (logN == 15 || logN == 16) && !ci && jobs <= ntt2s_below &&
            two_pass(jobs, inv, pro, epi, inplace_sub);
   }
   // the INTT iio (load prologue, store epilogue) and then the forward fio whose
@@ -902,7 +902,10 @@ struct Context {
     const int cat = bx ? P_NTT_BEXT : inv ? P_NTT_INV : P_NTT_FWD;
     if (two_pass(io.jobs, inv, io.pro, io.epi, io.epi != NTT_EPI_STORE && io.ex.p == io.dst.p)) {
       Poly scratch;
-      if (ntt2_chunk > 0 && io.jobs > 0) {  // chunks of jobs through one reused compact scratch
+      // large launches in chunks of jobs through one reused compact scratch
+      // (the intermediate can stay in the Infinity Cache); the latency
+      // kernels' small launches are never chunked
+      if (ntt2_chunk > 0 && io.jobs > std::max(ntt2_chunk, ntt2s_below) && !io.ifuse) {
         const int chunk = std::min(ntt2_chunk, io.jobs);
         scratch = alloc(1, 1, chunk);
         io.mid = ls(scratch, 0, 1, {0}, {0});
@@ -1647,7 +1650,7 @@ struct Context {
   // a kernel with the automorphism-scatter epilogue (NTT_EPI_SUBSCALE_AUT):
   // the one-pass kernel with the load prologue, or the radix-4 latency kernels
   bool aut_epi_ok(int jobs, int pro) {
-    if (ci || ntt2_chunk > 0 || ntt_tailsplit) return false;
+    if (ci || ntt_tailsplit) return false;
     if (!two_pass(jobs, false, pro, NTT_EPI_SUBSCALE, false)) return logN <= 15 && pro == NTT_PRO_LOAD;
     return jobs <= ntt2s_below && NTT2S_R4;
   }
