@@ -25,6 +25,12 @@
 
 namespace {
 
+// timing-only ablation (tools/build_ablation.py; 0 in the product): bit 0 =
+// the forward rows pass's per-lane (second-phase) twiddles replaced by one
+// loaded twiddle, bit 1 = the same for the inverse rows pass's first phase
+#ifndef NTT2_TW_ABLATE
+#define NTT2_TW_ABLATE 0
+#endif
 constexpr int A_STRIDE = 18;   // cols pass LDS: [2^R rows][18] u64, conflict-free both ways
 constexpr int B_STRIDE = 272;  // rows pass LDS: [16 rows][256 + 16 pad] u64
 __device__ __forceinline__ int b_lds(int rr, int col) { return rr * B_STRIDE + col + (col >> 4); }
@@ -160,12 +166,15 @@ __device__ __forceinline__ void fwd_rows(const NttIO& io, int job, int c, int l,
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 16; ++j) a[j] = from_bits<typename A::T>(lds[b_lds(rr, 16 * jc + j)]);
+  [[maybe_unused]] const typename A::W w_abl = ar.tw(tw, (1 << (LOGN - 4)) + (row << 4), 0);
 #pragma unroll
   for (int d = 3; d >= 0; --d) {
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       if (!((j >> d) & 1))
-        ar.ct(a[j], a[j | (1 << d)], ar.tw(tw, (1 << (LOGN - 1 - d)) + ((row << (7 - d)) | ((16 * jc + j) >> (d + 1))), 0));
+        ar.ct(a[j], a[j | (1 << d)],
+              (NTT2_TW_ABLATE & 1) ? w_abl
+                                   : ar.tw(tw, (1 << (LOGN - 1 - d)) + ((row << (7 - d)) | ((16 * jc + j) >> (d + 1))), 0));
   }
   u64* dst = row_ptr(io.dst, c, l, b) + (row << 8) + 16 * jc;
   if constexpr (EPI == NTT_EPI_STORE) {
@@ -202,12 +211,15 @@ __device__ __forceinline__ void inv_rows(const NttIO& io, int job, int c, int l,
     a[j] = ar.from_u64(x.x);
     a[j + 1] = ar.from_u64(x.y);
   }
+  [[maybe_unused]] const typename A::W w_abl = ar.tw(tw, (1 << (LOGN - 4)) + (row << 4), 0);
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       if (!((j >> d) & 1))
-        ar.gs(a[j], a[j | (1 << d)], ar.tw(tw, (1 << (LOGN - 1 - d)) + ((row << (7 - d)) | ((16 * jc + j) >> (d + 1))), 0),
+        ar.gs(a[j], a[j | (1 << d)],
+              (NTT2_TW_ABLATE & 2) ? w_abl
+                                   : ar.tw(tw, (1 << (LOGN - 1 - d)) + ((row << (7 - d)) | ((16 * jc + j) >> (d + 1))), 0),
               (d & 1) == 1);
   }
   reduce16<A>(a, ar);
