@@ -290,7 +290,13 @@ class HandlePool {  // lowest-free-id reuse (minheap.go:46-64)
   void reset() {
     map_.clear();
     free_.clear();
-    next_ = 0;
+    next_ = base_;
+  }
+  // ids from base on (a peer context's handles live in a range of their own,
+  // so a handle passed to the wrong context is "not found", never another object)
+  void set_base(int b) {
+    base_ = b;
+    reset();
   }
   std::vector<int> live() const {
     std::vector<int> v;
@@ -301,7 +307,7 @@ class HandlePool {  // lowest-free-id reuse (minheap.go:46-64)
  private:
   std::map<int, std::unique_ptr<T>> map_;
   std::set<int> free_;
-  int next_ = 0;
+  int base_ = 0, next_ = 0;
 };
 
 struct ProfRec {
@@ -3083,6 +3089,9 @@ int OrionHipPeerCreate(void) {
   p->init_moduli(c0.logN, c0.mods, c0.logQ_bits, c0.logP_bits, c0.logScale, c0.h, c0.ci);
   p->adopt_keys(c0);
   p->seed_encryption(g_seed + 0x9e3779b97f4a7c15ull * g_ctxs.size());
+  const int base = (int)g_ctxs.size() << 20;
+  p->pts.set_base(base), p->cts.set_base(base), p->lts.set_base(base), p->polys.set_base(base);
+  p->next_graph = base;
   g_ctxs.push_back(std::move(p));
   return (int)g_ctxs.size() - 1;
   API_END(-1)

@@ -411,8 +411,8 @@ def test_peer_pipelines_interleaved(torch_cuda):
     pool and handles.  Two pipelines replayed op by op in turn
     (OrionStream.forward_interleaved, their kernels concurrent on the GPU)
     give, for the same input ciphertext, exactly the single pipeline's output
-    -- LoLA N=2^13 at batch 3 and N=2^15 at batch 4; DeleteScheme removes the
-    peers."""
+    -- LoLA N=2^13 at batch 3 and N=2^15 at batch 4; a peer's handles are
+    unknown to context 0; DeleteScheme removes the peers."""
     import numpy as np
     from orion_amd.replay import OrionStream
     for name, B in (("lola_n13", 3), ("lola_n15", 4)):
@@ -437,6 +437,12 @@ def test_peer_pipelines_interleaved(torch_cuda):
         st2.use()
         got1 = lib.export_ciphertext(outs[1])
         assert np.array_equal(got0, ref) and np.array_equal(got1, ref), name
+        # each context's handles live in a range of their own: a peer's handle
+        # passed to context 0 is unknown there, never another ciphertext
+        assert outs[0] < 1 << 20 <= outs[1] < 2 << 20, (outs, name)
+        st.use()
+        with pytest.raises(RuntimeError, match="handle not found"):
+            lib.GetCiphertextLevel(outs[1])
         # the peer decrypts with its copy of the secret
         dec = st2.decrypt_output(outs[1])
         exp = st.arrays["expected_output"].reshape(-1)
