@@ -170,6 +170,10 @@ void *OrionHipGetStream(void);
 int OrionHipPeerCreate(void);
 int OrionHipPeerSelect(int id);
 int OrionHipPeerCount(void);
+/* Peer pipelines: the current context's stream waits (on the GPU) for the
+ * work enqueued so far on context `peer`'s stream (an event recorded there).
+ * A frontend uses it to start one pipeline behind another.  0 or -1. */
+int OrionHipStreamWaitPeer(int peer);
 int OrionHipSynchronize(void); /* drains every context's stream */
 /* hipGraph capture of an op stream issued through this ABI: every call between
  * Begin and End is recorded into one graph (returned id), which Launch replays

@@ -142,6 +142,7 @@ SIGNATURES = {
     "OrionHipPeerCreate": ([], c_int),
     "OrionHipPeerSelect": ([c_int], c_int),
     "OrionHipPeerCount": ([], c_int),
+    "OrionHipStreamWaitPeer": ([c_int], c_int),
     "OrionHipSynchronize": ([], c_int),
     "OrionHipGraphBegin": ([], c_int),
     "OrionHipGraphEnd": ([], c_int),

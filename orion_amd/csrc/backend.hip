@@ -3106,6 +3106,20 @@ int OrionHipPeerSelect(int id) {
   return 0;
 }
 int OrionHipPeerCount(void) { return (int)g_ctxs.size(); }
+int OrionHipStreamWaitPeer(int peer) {
+  API_BEGIN
+  if (peer < 0 || peer >= (int)g_ctxs.size()) throw std::runtime_error("no such peer context: " + std::to_string(peer));
+  Context& c = ctx();
+  Context& p = *g_ctxs[peer];
+  if (&p == &c) return 0;
+  hipEvent_t e;
+  HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(e, p.stream));
+  HIPCHK(hipStreamWaitEvent(c.stream, e, 0));
+  HIPCHK(hipEventDestroy(e));  // (released once the wait has completed)
+  return 0;
+  API_END(-1)
+}
 
 void FreeCArray(void* p) { free(p); }
 

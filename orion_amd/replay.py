@@ -179,17 +179,30 @@ class OrionStream:
                 return e.value
 
     @staticmethod
-    def forward_interleaved(pairs):
+    def forward_interleaved(pairs, lag=0):
         """Run the forward passes of several pipelines [(stream, ct_in), ...]
         (peer contexts of one scheme) op by op in turn, so their kernels run
-        concurrently on the GPU; returns their outputs in order."""
+        concurrently on the GPU; returns their outputs in order.  lag > 0:
+        pipeline i starts once pipeline 0 has issued i * lag ops, and its
+        stream first waits on the GPU for the work pipeline 0 has enqueued by
+        then (OrionHipStreamWaitPeer), so the pipelines run phase-shifted."""
         its = [(st, st.forward_iter(ct)) for st, ct in pairs]
         outs = [None] * len(its)
         live = list(range(len(its)))
+        issued = 0  # pipeline 0's ops so far
+        started = set([0]) if lag > 0 else set(range(len(its)))
         while live:
             for i in list(live):
                 st, it = its[i]
+                if i not in started:
+                    if issued < i * lag and 0 in live:
+                        continue
+                    st.use()
+                    st.lib.OrionHipStreamWaitPeer(pairs[0][0].ctx_id)
+                    started.add(i)
                 st.use()
+                if i == 0:
+                    issued += 1
                 try:
                     next(it)
                 except StopIteration as e:

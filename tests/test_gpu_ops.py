@@ -411,8 +411,9 @@ def test_peer_pipelines_interleaved(torch_cuda):
     pool and handles.  Two pipelines replayed op by op in turn
     (OrionStream.forward_interleaved, their kernels concurrent on the GPU)
     give, for the same input ciphertext, exactly the single pipeline's output
-    -- LoLA N=2^13 at batch 3 and N=2^15 at batch 4; a peer's handles are
-    unknown to context 0; DeleteScheme removes the peers."""
+    -- LoLA N=2^13 at batch 3 and N=2^15 at batch 4, also with the peer
+    started 3 ops behind; a peer's handles are unknown to context 0;
+    DeleteScheme removes the peers."""
     import numpy as np
     from orion_amd.replay import OrionStream
     for name, B in (("lola_n13", 3), ("lola_n15", 4)):
@@ -431,6 +432,18 @@ def test_peer_pipelines_interleaved(torch_cuda):
         ct2 = lib.import_ciphertext(x, scale)
         st.use()
         ref = lib.export_ciphertext(st.forward(lib.CloneCiphertext(ct)))
+        # phase-shifted: the peer starts 3 ops behind, its stream waiting on the
+        # GPU for context 0's work so far (OrionHipStreamWaitPeer)
+        ca = lib.CloneCiphertext(ct)
+        st2.use()
+        cb = lib.CloneCiphertext(ct2)
+        outs_lag = OrionStream.forward_interleaved([(st, ca), (st2, cb)], lag=3)
+        st.use()
+        assert np.array_equal(lib.export_ciphertext(outs_lag[0]), ref), name
+        lib.DeleteCiphertext(outs_lag[0])
+        st2.use()
+        assert np.array_equal(lib.export_ciphertext(outs_lag[1]), ref), name
+        lib.DeleteCiphertext(outs_lag[1])
         outs = OrionStream.forward_interleaved([(st, ct), (st2, ct2)])
         st.use()
         got0 = lib.export_ciphertext(outs[0])
