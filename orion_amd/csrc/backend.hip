@@ -95,6 +95,9 @@ class DevicePool {
     } else {
       hipError_t e = hipMalloc(&p, bytes);
       if (e != hipSuccess) {  // release the cache once and retry (not while capturing: trim synchronises)
+        // clear the failed call's error: HIP keeps it as the thread's last
+        // error, and a later launch check (hipGetLastError) would report it
+        (void)hipGetLastError();
         if (tracking_) throw std::runtime_error("device memory exhausted during graph capture");
         trim();
         HIPCHK(hipMalloc(&p, bytes));
@@ -859,6 +862,11 @@ struct Context {
   // target) / source limbs times the INTT's own columns work (ResNet's
   // N = 2^16 ModDowns onto 20-30 Q limbs measured slower fused)
   double ntt_ifuse_maxr = getenv("ORION_NTT_IFUSE_MAXR") ? atof(getenv("ORION_NTT_IFUSE_MAXR")) : 8.0;
+  // 2 or 4: the fused forward runs a workgroup of that many 256-thread groups
+  // per segment of targets sharing their sources, which finishes the sources'
+  // INTT columns once for the segment (ntt2s_ifwd_cols_p); 1: one target per
+  // workgroup, the sources' columns redone for each (ntt2s_ifwd_cols)
+  int ntt_ifuse_p = getenv("ORION_NTT_IFUSE_P") ? atoi(getenv("ORION_NTT_IFUSE_P")) : 2;
   bool on_ntt2s(int jobs, bool inv, int pro, int epi, bool inplace_sub) {
     return (logN == 15 || logN == 16) && !ci && jobs <= ntt2s_below &&
            two_pass(jobs, inv, pro, epi, inplace_sub);
@@ -892,6 +900,23 @@ struct Context {
     }
     fio.ifuse = 1;
     fio.imid = iio.dst;
+    if (NTT2S_R4 && (ntt_ifuse_p == 2 || ntt_ifuse_p == 4)) {
+      // segments: runs of target limbs on the same basis-extension table (the
+      // same source limbs; the rescale prep has one source), at most G each
+      int k = 0;
+      for (int l = 0; l < fio.dst.nlimb;) {
+        int e = l + 1;
+        while (e < fio.dst.nlimb && e - l < ntt_ifuse_p &&
+               (fio.pro != NTT_PRO_BEXT || fio.bx_tab[e] == fio.bx_tab[l]))
+          ++e;
+        fio.tg_l0[k] = (unsigned char)l;
+        fio.tg_n[k] = (unsigned char)(e - l);
+        ++k;
+        l = e;
+      }
+      fio.ntg = k;
+      fio.tgroup = ntt_ifuse_p;
+    }
     ntt_io(fio, false, src_per_job);
   }
   void ntt_io(NttIO io, bool inv, double src_per_job = 0) {
@@ -2934,16 +2959,20 @@ static void defer_gate(const char* fn) {
   try {                                            \
     capture_guard(__func__);                       \
     defer_gate(__func__);
+// (a failed call's HIP error is read off here, so that it is reported once,
+// by this call, and not again by the next call's launch checks)
 #define API_END(errval)          \
   }                              \
   catch (const std::exception& e) { \
     g_last_error = e.what();     \
+    (void)hipGetLastError();     \
     return errval;               \
   }
 #define API_END_VOID                \
   }                                 \
   catch (const std::exception& e) { \
     g_last_error = e.what();        \
+    (void)hipGetLastError();        \
   }
 
 template <class T, class U>

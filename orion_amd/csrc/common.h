@@ -598,6 +598,12 @@ struct NttIO {
   // their inverse columns pass itself, in registers and LDS
   int ifuse;
   LimbSet imid;
+  // ifuse, radix-4, tgroup = G > 1 (ntt2s_ifwd_cols_p): a workgroup of G x 256
+  // threads per (component, image) row, target segment and column tile; the
+  // ntg segments (consecutive target limbs that read the same source limbs)
+  // start at limb tg_l0[k] and hold tg_n[k] <= G targets
+  int tgroup, ntg;
+  unsigned char tg_l0[ORION_MAXLIMB], tg_n[ORION_MAXLIMB];
   const u32* aut;  // NTT_EPI_SUBSCALE_AUT: the scatter index (N entries)
 };
 

@@ -22,6 +22,8 @@
 // thread; the remaining 12 stages run in LDS on aligned 4096-element blocks
 // (64 KiB, two workgroups per CU).  Twiddles of the stage with half-length h
 // are tw[h + j], j < h (n doubles2 per direction, L2 resident).
+#include <cstdio>
+
 #include "common.h"
 
 namespace {
@@ -386,5 +388,7 @@ int orion_launch_enc_sample(const LimbSet& r, const EncSampler& sp, const Device
 
 int orion_launch_modraise(const LimbSet& out, const LimbSet& in, const DeviceTables* tb, int N, hipStream_t st) {
   modraise_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)(out.ncomp * out.nbatch)), 256, 0, st>>>(out, in, tb, N);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fprintf(stderr, "orion_launch_modraise: %s\n", hipGetErrorString(e));
+  return e == hipSuccess ? 0 : -1;
 }

@@ -342,9 +342,9 @@ __device__ __forceinline__ void gs4(const A& ar, typename A::T (&x)[4], const ty
 template <class A, int LOGN>
 __device__ __forceinline__ void s_fwd_cols4_core(const NttIO& io, int job, int c, int l, int b, int tile,
                                                  typename A::T (&x)[4], const A& ar, __amdgpu_buffer_rsrc_t tw,
-                                                 u64* lds) {
+                                                 u64* lds, int t) {
   constexpr int N = 1 << LOGN, R = S2<LOGN>::R, CW = S2<LOGN>::CW, NS = R / 2;
-  const int t = threadIdx.x, cl = t % CW, j = t / CW, col = tile * CW + cl;
+  const int cl = t % CW, j = t / CW, col = tile * CW + cl;
   typename A::W wa[NS], wb[NS], wc[NS], wl[2];
 #pragma unroll
   for (int st = 0; st < NS; ++st) {
@@ -394,7 +394,7 @@ __device__ __forceinline__ void s_fwd_cols4(const NttIO& io, int job, int c, int
   typename A::T x[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) x[i] = fwd_load<A, PRO>(io, c, l, b, col + ((j + i * Q) << 8), mc, ar, tb);
-  s_fwd_cols4_core<A, LOGN>(io, job, c, l, b, tile, x, ar, tw, lds);
+  s_fwd_cols4_core<A, LOGN>(io, job, c, l, b, tile, x, ar, tw, lds, (int)threadIdx.x);
 }
 
 // forward rows pass, radix 4: thread (rr, kk), kk < 64
@@ -516,9 +516,9 @@ __device__ __forceinline__ void s_inv_rows4(const NttIO& io, int job, int c, int
 template <class A0, class A1, int LOGN, bool TWO>
 __device__ __forceinline__ void s_inv_cols4_src(const u64* m0, const u64* m1, const A0& a0, const A1& a1,
                                                 __amdgpu_buffer_rsrc_t tw0, __amdgpu_buffer_rsrc_t tw1, u64* lds,
-                                                typename A0::T (&x)[4], typename A1::T (&y)[4]) {
+                                                typename A0::T (&x)[4], typename A1::T (&y)[4], int t, int tile) {
   constexpr int N = 1 << LOGN, R = S2<LOGN>::R, CW = S2<LOGN>::CW, NS = R / 2, Q = 1 << (R - 2);
-  const int t = threadIdx.x, cl = t % CW, j = t / CW, col = blockIdx.x % S2<LOGN>::CTILES * CW + cl;
+  const int cl = t % CW, j = t / CW, col = tile * CW + cl;
   typename A0::W wa0[NS], wb0[NS], wc0[NS], wl0;
   typename A1::W wa1[NS], wb1[NS], wc1[NS], wl1;
 #pragma unroll
@@ -587,23 +587,25 @@ __device__ __forceinline__ void s_inv_cols4_src(const u64* m0, const u64* m1, co
 template <class A0, int LOGN>
 __device__ __forceinline__ void s_inv_cols4_src2(const u64* m0, const u64* m1, const A0& a0, int mod1, bool two,
                                                  const DeviceTables* __restrict__ tb, __amdgpu_buffer_rsrc_t tw0,
-                                                 u64* lds, u64 (&v)[2][4]) {
+                                                 u64* lds, u64 (&v)[2][4], int t, int tile) {
   typename A0::T x[4];
   if (!two) {
     typename A0::T y[4];
-    s_inv_cols4_src<A0, A0, LOGN, false>(m0, m0, a0, a0, tw0, tw0, lds, x, y);
+    s_inv_cols4_src<A0, A0, LOGN, false>(m0, m0, a0, a0, tw0, tw0, lds, x, y, t, tile);
   } else {
     const ModConst& mc1 = tb->mc[mod1];
     if (mc1.f64) {
       const F64Arith a1(mc1);
       double y[4];
-      s_inv_cols4_src<A0, F64Arith, LOGN, true>(m0, m1, a0, a1, tw0, twr_s(tb->inv_d[mod1], 8 << LOGN), lds, x, y);
+      s_inv_cols4_src<A0, F64Arith, LOGN, true>(m0, m1, a0, a1, tw0, twr_s(tb->inv_d[mod1], 8 << LOGN), lds, x, y, t,
+                                                  tile);
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[1][i] = a1.final_inv(y[i]);
     } else {
       const IntArith a1(mc1);
       u64 y[4];
-      s_inv_cols4_src<A0, IntArith, LOGN, true>(m0, m1, a0, a1, tw0, twr_s(tb->inv[mod1], 16 << LOGN), lds, x, y);
+      s_inv_cols4_src<A0, IntArith, LOGN, true>(m0, m1, a0, a1, tw0, twr_s(tb->inv[mod1], 16 << LOGN), lds, x, y, t,
+                                                  tile);
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[1][i] = a1.final_inv(y[i]);
     }
@@ -642,9 +644,11 @@ __global__ void __launch_bounds__(NTT2S_R4 ? S2<LOGN>::CT4 : S2<LOGN>::CT)
   u64 v[2][NE];
   if constexpr (NTT2S_R4) {
     if (mc0.f64)
-      s_inv_cols4_src2<F64Arith, LOGN>(p0, p1, F64Arith(mc0), m1, ns > 1, tb, twr_s(tb->inv_d[m0], 8 << LOGN), lds, v);
+      s_inv_cols4_src2<F64Arith, LOGN>(p0, p1, F64Arith(mc0), m1, ns > 1, tb, twr_s(tb->inv_d[m0], 8 << LOGN), lds, v,
+                                       (int)threadIdx.x, tile);
     else
-      s_inv_cols4_src2<IntArith, LOGN>(p0, p1, IntArith(mc0), m1, ns > 1, tb, twr_s(tb->inv[m0], 16 << LOGN), lds, v);
+      s_inv_cols4_src2<IntArith, LOGN>(p0, p1, IntArith(mc0), m1, ns > 1, tb, twr_s(tb->inv[m0], 16 << LOGN), lds, v,
+                                       (int)threadIdx.x, tile);
   } else {
     u64 xa[2] = {0, 0}, xb[2] = {0, 0};
     if (mc0.f64)
@@ -677,10 +681,94 @@ __global__ void __launch_bounds__(NTT2S_R4 ? S2<LOGN>::CT4 : S2<LOGN>::CT)
       typename A::T x[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) x[i] = ar.from_u64(o[i]);
-      s_fwd_cols4_core<A, LOGN>(io, job, c, l, b, tile, x, ar, tw, lds);
+      s_fwd_cols4_core<A, LOGN>(io, job, c, l, b, tile, x, ar, tw, lds, (int)threadIdx.x);
     } else {
       s_fwd_cols_core<A, LOGN>(io, job, c, l, b, tile, ar.from_u64(o[0]), ar.from_u64(o[1]), ar, tw, lds);
     }
+  };
+  if (mc.f64)
+    fwd(F64Arith(mc), twr_s(tb->fwd_d[mod], 8 << LOGN));
+  else
+    fwd(IntArith(mc), twr_s(tb->fwd[mod], 16 << LOGN));
+}
+
+// the same with the sources' INTT columns shared by a segment of G targets
+// (NttIO.tgroup = G > 1, radix-4; targets that read the same source limbs): a
+// workgroup of G groups of 256 threads per (row, segment, column tile) runs
+// the sources' INTT columns once -- source s on group s, concurrently -- then
+// every group forms its own target's prologue from the shared values and runs
+// that target's forward columns stages.  The arithmetic is ntt2s_ifwd_cols's
+// (bit-identical); the columns work that kernel redoes for every target is
+// done once per segment, on as many threads per workgroup as targets.
+template <int LOGN>
+__device__ __forceinline__ void idle_inv_cols4_barriers() {  // the barriers of s_inv_cols4_src
+  constexpr int R = S2<LOGN>::R, NS = R / 2;
+#pragma unroll
+  for (int k = 0; k < NS - 1 + (R & 1); ++k) __syncthreads();
+}
+template <int LOGN, int PRO, int G>
+__global__ void __launch_bounds__(G * S2<LOGN>::CT4) ntt2s_ifwd_cols_p(NttIO io, const DeviceTables* __restrict__ tb) {
+  static_assert(NTT2S_R4 || LOGN < 0, "radix-4 only");
+  constexpr int CT = S2<LOGN>::CT4, REG = S2<LOGN>::CW << S2<LOGN>::R;  // LDS words per group
+  __shared__ u64 lds[G * REG + 2 * 4 * CT];
+  u64* const sb = lds + G * REG;  // the sources' INTT values, [source][element][thread]
+  const int grp = threadIdx.x / CT, t = threadIdx.x % CT;  // (group-uniform, so wave-uniform)
+  const int tile = blockIdx.x % S2<LOGN>::CTILES, q = blockIdx.x / S2<LOGN>::CTILES;
+  const int seg = q % io.ntg, row = q / io.ntg;
+  const int b = row % io.dst.nbatch, c = row / io.dst.nbatch;
+  // surplus groups of a short segment redo its last target (identical stores)
+  const int l = arg_byte(io.tg_l0, seg) + min(grp, arg_byte(io.tg_n, seg) - 1);
+  int sl0 = 0, ns = 1, ti = 0;
+  const BasisExtTable* __restrict__ T = nullptr;
+  if constexpr (PRO == NTT_PRO_BEXT) {
+    const int kt = arg_byte(io.bx_tab, l);
+    ti = arg_byte(io.bx_t, l);
+    sl0 = arg_byte(io.bx_s0, kt);
+    T = io.bx + kt;
+    ns = T->ns;
+  }
+  // phase 1: group s < ns finishes source s's INTT columns on this tile
+  if (grp < ns) {
+    const int ms = arg_byte(io.src.mod, sl0 + grp);
+    const u64* p = row_ptr(io.imid, c, sl0 + grp, b);
+    const ModConst& mcs = tb->mc[ms];
+    auto inv = [&](const auto& ar, __amdgpu_buffer_rsrc_t tw) {
+      using A = std::decay_t<decltype(ar)>;
+      typename A::T x[4], y[4];
+      s_inv_cols4_src<A, A, LOGN, false>(p, p, ar, ar, tw, tw, lds + grp * REG, x, y, t, tile);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sb[(grp * 4 + i) * CT + t] = ar.final_inv(x[i]);
+    };
+    if (mcs.f64)
+      inv(F64Arith(mcs), twr_s(tb->inv_d[ms], 8 << LOGN));
+    else
+      inv(IntArith(mcs), twr_s(tb->inv[ms], 16 << LOGN));
+  } else {
+    idle_inv_cols4_barriers<LOGN>();
+  }
+  __syncthreads();  // sb complete; the group regions are free for the forward stages
+  const int mod = arg_byte(io.dst.mod, l);
+  const ModConst mc = tb->mc[mod];
+  u64 o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const u64 v0 = sb[i * CT + t];
+    if constexpr (PRO == NTT_PRO_BEXT) {
+      u64 x[2] = {v0, ns > 1 ? sb[(4 + i) * CT + t] : 0}, y[2];
+      const u64 vv = bext_prep<2>(T, x, y);
+      o[i] = bext_target_sel<2>(T->tgt + ti, ns, y, vv);
+    } else {  // NTT_PRO_RESCALE
+      const u64 qL = tb->mc[io.modL].q, h = qL >> 1;
+      const u64 hm = barrett128(0, h, mc);
+      o[i] = sub_mod(barrett128(0, add_mod(v0, h, qL), mc), hm, mc.q);
+    }
+  }
+  auto fwd = [&](const auto& ar, __amdgpu_buffer_rsrc_t tw) {
+    using A = std::decay_t<decltype(ar)>;
+    typename A::T x[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = ar.from_u64(o[i]);
+    s_fwd_cols4_core<A, LOGN>(io, 0, c, l, b, tile, x, ar, tw, lds + grp * REG, t);
   };
   if (mc.f64)
     fwd(F64Arith(mc), twr_s(tb->fwd_d[mod], 8 << LOGN));
@@ -770,7 +858,7 @@ __global__ void __launch_bounds__(NTT2S_R4 ? S2<LOGN>::CT4 : S2<LOGN>::CT)
       const int t = threadIdx.x, cl = t % CW, j = t / CW, col = tile * CW + cl;
       typename A::T x[4], y[4];
       const u64* m = mid_row_s(io, job, c, l, b);
-      s_inv_cols4_src<A, A, LOGN, false>(m, m, ar, ar, tw, tw, lds, x, y);
+      s_inv_cols4_src<A, A, LOGN, false>(m, m, ar, ar, tw, tw, lds, x, y, t, tile);
       u64* dst = row_ptr(io.dst, c, l, b);
 #pragma unroll
       for (int i = 0; i < 4; ++i) dst[col + ((j + i * Q) << 8)] = ar.final_inv(x[i]);
@@ -803,7 +891,31 @@ int launch2s(const NttIO& io, const DeviceTables* tb, bool inverse, bool rows_on
     if (!rows_only) hipLaunchKernelGGL(ntt2s_inv_cols<LOGN>, ga, ba, 0, st, io, tb);
     return 0;
   }
-  if (io.ifuse) {
+  if (io.ifuse && io.tgroup > 1) {
+    if (io.mid_compact || !io.imid.p || io.job0 != 0 || jobs != total || io.ntg < 1) return -1;
+    const dim3 gg(io.dst.ncomp * io.dst.nbatch * io.ntg * S2<LOGN>::CTILES);
+    if constexpr (NTT2S_R4) {
+      const bool bx = io.pro == NTT_PRO_BEXT;
+      if (!bx && io.pro != NTT_PRO_RESCALE) return -1;
+      if (io.tgroup == 2) {
+        const dim3 bg(2 * S2<LOGN>::CT4);
+        if (bx)
+          hipLaunchKernelGGL((ntt2s_ifwd_cols_p<LOGN, NTT_PRO_BEXT, 2>), gg, bg, 0, st, io, tb);
+        else
+          hipLaunchKernelGGL((ntt2s_ifwd_cols_p<LOGN, NTT_PRO_RESCALE, 2>), gg, bg, 0, st, io, tb);
+      } else if (io.tgroup == 4) {
+        const dim3 bg(4 * S2<LOGN>::CT4);
+        if (bx)
+          hipLaunchKernelGGL((ntt2s_ifwd_cols_p<LOGN, NTT_PRO_BEXT, 4>), gg, bg, 0, st, io, tb);
+        else
+          hipLaunchKernelGGL((ntt2s_ifwd_cols_p<LOGN, NTT_PRO_RESCALE, 4>), gg, bg, 0, st, io, tb);
+      } else {
+        return -1;
+      }
+    } else {
+      return -1;
+    }
+  } else if (io.ifuse) {
     if (io.mid_compact || !io.imid.p) return -1;
     if (io.pro == NTT_PRO_BEXT)
       hipLaunchKernelGGL((ntt2s_ifwd_cols<LOGN, NTT_PRO_BEXT>), ga, ba, 0, st, io, tb);
