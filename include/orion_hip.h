@@ -174,6 +174,13 @@ int OrionHipPeerCount(void);
  * work enqueued so far on context `peer`'s stream (an event recorded there).
  * A frontend uses it to start one pipeline behind another.  0 or -1. */
 int OrionHipStreamWaitPeer(int peer);
+
+/* Device-memory pools of the process (one per context: the scheme's, its
+ * peers', the bootstrappers'): out[0] bytes held (handed out + cached),
+ * out[1] their peak, out[2] hipMalloc calls, out[3] cache trims forced by a
+ * failed hipMalloc (each trims every pool), out[4] bytes cached.  Writes
+ * min(n, 5) values; returns 5. */
+int OrionHipPoolStats(double* out, int n);
 int OrionHipSynchronize(void); /* drains every context's stream */
 /* hipGraph capture of an op stream issued through this ABI: every call between
  * Begin and End is recorded into one graph (returned id), which Launch replays

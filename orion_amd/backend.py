@@ -143,6 +143,7 @@ SIGNATURES = {
     "OrionHipPeerSelect": ([c_int], c_int),
     "OrionHipPeerCount": ([], c_int),
     "OrionHipStreamWaitPeer": ([c_int], c_int),
+    "OrionHipPoolStats": ([P(c_double), c_int], c_int),
     "OrionHipSynchronize": ([], c_int),
     "OrionHipGraphBegin": ([], c_int),
     "OrionHipGraphEnd": ([], c_int),
@@ -394,6 +395,14 @@ class HipLibrary:
         self._chk(self.lib.OrionHipBootstrapExport(slots, w, arg, out.ctypes.data_as(c_void_p), n),
                   "OrionHipBootstrapExport")
         return out
+
+    def pool_stats(self):
+        """Device-memory pools (OrionHipPoolStats): bytes held and their peak,
+        hipMalloc calls, trims after a failed hipMalloc, bytes cached."""
+        v = (c_double * 5)()
+        self.lib.OrionHipPoolStats(v, 5)
+        return {"held_bytes": v[0], "peak_bytes": v[1], "hipmalloc_calls": int(v[2]), "trims": int(v[3]),
+                "cached_bytes": v[4]}
 
     def export_ciphertext(self, ct):
         B, lvl = self.GetCiphertextBatch(ct), self.GetCiphertextLevel(ct)

@@ -94,14 +94,20 @@ class DevicePool {
       it->second.pop_back();
     } else {
       hipError_t e = hipMalloc(&p, bytes);
-      if (e != hipSuccess) {  // release the cache once and retry (not while capturing: trim synchronises)
-        // clear the failed call's error: HIP keeps it as the thread's last
-        // error, and a later launch check (hipGetLastError) would report it
+      if (e != hipSuccess) {
+        // release the caches of every pool on the device (the scheme's,
+        // its peers' and the bootstrappers' contexts) and retry -- not while
+        // capturing: trim synchronises.  The failed call's error is cleared:
+        // HIP keeps it as the thread's last error, and a later launch check
+        // (hipGetLastError) would report it
         (void)hipGetLastError();
         if (tracking_) throw std::runtime_error("device memory exhausted during graph capture");
-        trim();
+        for (DevicePool* q : registry()) q->trim();
         HIPCHK(hipMalloc(&p, bytes));
       }
+      stats()[2] += 1;
+      held_ += bytes;
+      add_held((double)bytes);
     }
     if (tracking_) touched_[p] = bytes;
     // debugging: every buffer handed out holds garbage, not stale or zero pages
@@ -141,8 +147,32 @@ class DevicePool {
   void trim() {
     hipDeviceSynchronize();
     for (auto& kv : free_)
-      for (void* p : kv.second) hipFree(p);
+      for (void* p : kv.second) hipFree(p), held_ -= kv.first, add_held(-(double)kv.first);
     free_.clear();
+    stats()[3] += 1;
+  }
+  DevicePool() { registry().push_back(this); }
+  DevicePool(const DevicePool&) = delete;
+  DevicePool& operator=(const DevicePool&) = delete;
+  // every pool of the process (one per context), and process-wide counters:
+  // device bytes held by the pools (handed out + cached), their peak,
+  // hipMalloc calls, cache trims after a failed hipMalloc
+  static std::vector<DevicePool*>& registry() {
+    static std::vector<DevicePool*> r;
+    return r;
+  }
+  static double* stats() {
+    static double st[4] = {0, 0, 0, 0};
+    return st;
+  }
+  static void add_held(double d) {
+    stats()[0] += d;
+    if (stats()[0] > stats()[1]) stats()[1] = stats()[0];
+  }
+  size_t cached() const {
+    size_t c = 0;
+    for (auto& kv : free_) c += kv.first * kv.second.size();
+    return c;
   }
   // graph capture: record every buffer handed out until end_track()
   void begin_track() {
@@ -184,9 +214,13 @@ class DevicePool {
     for (auto& kv : parked_) free_[kv.second].push_back(kv.first);
     parked_.clear();
     trim();
+    stats()[0] -= (double)held_;  // (buffers still handed out are released with their owners)
+    auto& r = registry();
+    r.erase(std::remove(r.begin(), r.end(), this), r.end());
   }
 
  private:
+  size_t held_ = 0;
   std::unordered_map<size_t, std::vector<void*>> free_;
   bool tracking_ = false;
   std::unordered_map<void*, size_t> touched_, parked_;
@@ -3135,6 +3169,15 @@ int OrionHipPeerSelect(int id) {
   return 0;
 }
 int OrionHipPeerCount(void) { return (int)g_ctxs.size(); }
+int OrionHipPoolStats(double* out, int n) {
+  std::lock_guard<std::recursive_mutex> lk_(g_mu);
+  double cached = 0;
+  for (DevicePool* q : DevicePool::registry()) cached += (double)q->cached();
+  const double v[5] = {DevicePool::stats()[0], DevicePool::stats()[1], DevicePool::stats()[2], DevicePool::stats()[3],
+                       cached};
+  for (int i = 0; i < n && i < 5; ++i) out[i] = v[i];
+  return 5;
+}
 int OrionHipStreamWaitPeer(int peer) {
   API_BEGIN
   if (peer < 0 || peer >= (int)g_ctxs.size()) throw std::runtime_error("no such peer context: " + std::to_string(peer));

@@ -63,7 +63,7 @@ def main():
                                       f"{st.forward_op_counts().get('Bootstrap', 0)} bootstraps)",
                           "batch": B, "s_per_batch": round(dt, 3), "images_per_s": round(B / dt, 3),
                           "mae_vs_cleartext": mae, "argmax_ok": bool(np.argmax(res[0]) == np.argmax(exp)),
-                          "setup_s": round(setup, 1)}), flush=True)
+                          "setup_s": round(setup, 1), "pools": st.lib.pool_stats()}), flush=True)
         st.lib.DeleteCiphertext(out)
         st.lib.DeleteCiphertext(ct)
 
