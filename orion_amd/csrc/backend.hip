@@ -101,7 +101,8 @@ class DevicePool {
         // HIP keeps it as the thread's last error, and a later launch check
         // (hipGetLastError) would report it
         (void)hipGetLastError();
-        if (tracking_) throw std::runtime_error("device memory exhausted during graph capture");
+        for (DevicePool* q : registry())
+          if (q->tracking_) throw std::runtime_error("device memory exhausted during graph capture");
         for (DevicePool* q : registry()) q->trim();
         HIPCHK(hipMalloc(&p, bytes));
       }
