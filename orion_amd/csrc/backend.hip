@@ -909,7 +909,9 @@ struct Context {
   // the INTT iio (load prologue, store epilogue) and then the forward fio whose
   // BEXT / RESCALE prologue reads the INTT's output (fio.src = iio.dst); ns_max:
   // the most source limbs one target reads
-  void intt_then_fwd(NttIO iio, NttIO fio, int ns_max, double src_per_job = 0) {
+  // whether intt_then_fwd(iio, fio, ns_max) takes the fused path (the INTT's
+  // rows pass alone, its columns pass inside the forward's latency kernels)
+  bool ifuse_ok(const NttIO& iio, const NttIO& fio, int ns_max) {
     const int ij = iio.dst.ncomp * iio.dst.nlimb * iio.dst.nbatch;
     const int fj = fio.dst.ncomp * fio.dst.nlimb * fio.dst.nbatch;
     bool same = iio.dst.p == fio.src.p && iio.dst.nlimb == fio.src.nlimb && iio.dst.ncomp == fio.src.ncomp &&
@@ -919,16 +921,23 @@ struct Context {
       same = iio.dst.pos[l] == fio.src.pos[l] && iio.dst.mod[l] == fio.src.mod[l];
     const bool inplace_sub = fio.epi != NTT_EPI_STORE && fio.ex.p == fio.dst.p;
     const double redo = (double)fio.dst.nlimb * ns_max / std::max(1, iio.dst.nlimb);
-    if (!ntt_ifuse || redo > ntt_ifuse_maxr || !same || iio.pro != NTT_PRO_LOAD || iio.epi != NTT_EPI_STORE ||
-        (fio.pro != NTT_PRO_BEXT && fio.pro != NTT_PRO_RESCALE) ||
-        !on_ntt2s(ij, true, NTT_PRO_LOAD, NTT_EPI_STORE, false) || !on_ntt2s(fj, false, fio.pro, fio.epi, inplace_sub)) {
+    return ntt_ifuse && redo <= ntt_ifuse_maxr && same && iio.pro == NTT_PRO_LOAD && iio.epi == NTT_EPI_STORE &&
+           (fio.pro == NTT_PRO_BEXT || fio.pro == NTT_PRO_RESCALE) &&
+           on_ntt2s(ij, true, NTT_PRO_LOAD, NTT_EPI_STORE, false) && on_ntt2s(fj, false, fio.pro, fio.epi, inplace_sub);
+  }
+  // rows_done: the caller's kernel already stored the INTT's rows-pass
+  // intermediate in iio.dst (ks_mac_rows_kernel); only the fused path is valid then
+  void intt_then_fwd(NttIO iio, NttIO fio, int ns_max, double src_per_job = 0, bool rows_done = false) {
+    if (!ifuse_ok(iio, fio, ns_max)) {
+      if (rows_done) throw std::runtime_error("NTT: rows pass done, but the fused forward is not available");
       ntt_io(iio, true);
       ntt_io(fio, false, src_per_job);
       return;
     }
+    const int ij = iio.dst.ncomp * iio.dst.nlimb * iio.dst.nbatch;
     prep_io(iio);
     iio.mid = iio.dst;  // the rows pass leaves its intermediate in the INTT's own output rows
-    {
+    if (!rows_done) {
       Scope sc(this, P_NTT_INV, 16.0 * N * ij);
       if (orion_launch_ntt2s(logN, iio, d_tb, true, stream, true)) throw std::runtime_error("NTT launch failed");
       log_ntt(4, iio, true);
@@ -1678,7 +1687,7 @@ struct Context {
   void mac_groups(const LimbSet& o, long long out_gstride, const LimbSet& d, long long d_gstride,
                   const LimbSet& own, long long own_gstride, const std::vector<const u64*>& keys,
                   const std::vector<int>& klvl, int beta, const u64* add0 = nullptr, long long add_gstride = 0,
-                  int add_nq = 0, const u64* add1 = nullptr) {
+                  int add_nq = 0, const u64* add1 = nullptr, int rows_from = 0) {
     const int G = (int)keys.size();
     for (int g0 = 0; g0 < G; g0 += ORION_MAXGROUP) {
       const int ng = std::min(ORION_MAXGROUP, G - g0);
@@ -1694,6 +1703,8 @@ struct Context {
       mg.add0 = add0 ? add0 + g0 * add_gstride : nullptr;
       mg.add1 = add1 ? add1 + g0 * add_gstride : nullptr;
       mg.add_nq = add0 ? add_nq : 0;
+      mg.rows_from = rows_from;
+      mg.logN = logN;
       for (int j = 0; j < mg.add_nq; ++j) {  // P mod q_j: ModDown(u + P*a) = ModDown(u) + a exactly
         u64 P = 1;
         for (int k = 0; k < K; ++k) P = hm_mulmod(P, mods[L + k] % mods[o.mod[j]], mods[o.mod[j]]);
@@ -1734,7 +1745,27 @@ struct Context {
   // out = sigma_g of that (a rotation's NTT-domain automorphism), applied in
   // the final NTT's store when its kernel can scatter, else by automorph();
   // aut_acc: out += sigma_g(...) instead
-  void moddown(const LimbSet& x, int level, const LimbSet& out, u64 aut_g = 0, bool aut_acc = false) {
+  // whether moddown(x, level, out, aut_g) runs its P limbs' INTT as the fused
+  // latency path, so that the gadget product before it may store those limbs
+  // after the INTT's rows pass (keyswitch, ks_mac_rows_kernel)
+  bool moddown_rows_fusable(const LimbSet& x, int level, const LimbSet& out, u64 aut_g, bool aut_acc) {
+    if (!mac_rows || (logN != 15 && logN != 16) || !NTT2S_R4) return false;
+    const int nc = x.ncomp, B = x.nbatch, jobs = nc * B * (level + 1);
+    if (!fuse_bext(jobs, K, NTT_EPI_SUBSCALE)) return false;
+    const bool scatter = aut_g && ntt_aut_fuse && aut_epi_ok(jobs, NTT_PRO_BEXT);
+    if (aut_g && !scatter) return false;
+    LimbSet xp = limbs(x, level + 1, K);
+    NttIO io = nio(out, xp);
+    io.pro = NTT_PRO_BEXT;
+    io.epi = !scatter ? NTT_EPI_SUBSCALE : aut_acc ? NTT_EPI_SUBSCALE_AUT_ACC : NTT_EPI_SUBSCALE_AUT;
+    io.ex = limbs(x, 0, level + 1);
+    return ifuse_ok(nio(xp, xp), io, K);
+  }
+  // 1: keyswitch's gadget product stores the P limbs through the ModDown
+  // INTT's rows pass when the ModDown takes the fused latency path
+  int mac_rows = getenv("ORION_MAC_ROWS") ? atoi(getenv("ORION_MAC_ROWS")) : 1;
+  void moddown(const LimbSet& x, int level, const LimbSet& out, u64 aut_g = 0, bool aut_acc = false,
+               bool rows_done = false) {
     const int nc = x.ncomp, B = x.nbatch, jobs = nc * B * (level + 1);
     LimbSet xp = limbs(x, level + 1, K);
     const bool fused = fuse_bext(jobs, K, NTT_EPI_SUBSCALE);
@@ -1767,8 +1798,9 @@ struct Context {
       for (int j = 0; j <= level; ++j) io.bx_tab[j] = 0, io.bx_t[j] = (unsigned char)j;
       io.bx_s0[0] = 0;
       epilogue(io);
-      intt_then_fwd(nio(xp, xp), io, K, K);
+      intt_then_fwd(nio(xp, xp), io, K, K, rows_done);
     } else {
+      if (rows_done) throw std::runtime_error("moddown: rows pass done, but the fused path is not taken");
       ntt(xp, true);
       Poly ext = alloc(nc, level + 1, B);
       LimbSet le = lsq(ext, 0, nc, level);
@@ -1794,9 +1826,11 @@ struct Context {
     Poly D = decompose(c, level, B);
     Poly u = alloc(2, level + 1 + K, B);
     const int beta = (level + 1 + K - 1) / K;
-    mac_groups(lsqp(u, 0, 2, level, level), 0, lsqp(D, 0, beta, level, level), 0, c, 0, {key.ptr()}, {klvl}, beta,
-               add0, 0, add0 ? level + 1 : 0, add1);
-    moddown(lsqp(u, 0, 2, level, level), level, lsq(out, 0, 2, level), aut_g, aut_acc);
+    const LimbSet uq = lsqp(u, 0, 2, level, level), oq = lsq(out, 0, 2, level);
+    const bool rows = moddown_rows_fusable(uq, level, oq, aut_g, aut_acc);
+    mac_groups(uq, 0, lsqp(D, 0, beta, level, level), 0, c, 0, {key.ptr()}, {klvl}, beta, add0, 0,
+               add0 ? level + 1 : 0, add1, rows ? level + 1 : 0);
+    moddown(uq, level, oq, aut_g, aut_acc, rows);
   }
   std::vector<u64> p_mod_q(int level) const {
     std::vector<u64> v;

@@ -241,6 +241,10 @@ struct MacGroups {  // ks_mac_kernel: group g uses key[g], made for level klvl[g
   int add_nq;
   const u64* add1;
   u64 add_s[ORION_MAXLIMB], add_ss[ORION_MAXLIMB];
+  // rows_from > 0 (ks_mac_rows_kernel, N = 2^logN, logN 15 or 16): out limbs
+  // l >= rows_from (the P limbs, read only by the ModDown's INTT) are stored
+  // after the INTT's radix-4 rows pass, as its intermediate (ntt2s_rows.h)
+  int rows_from, logN;
 };
 
 // BSGS linear transform plan (device-resident, one per LinTrans): giants in

@@ -9,6 +9,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "ntt2s_rows.h"
 
 // timing-only ablation of lt_bsgs (0 in the product): bit 0 skips the giant
 // inner products of moduli below 2^48, bit 1 skips the baby gadget products,
@@ -259,8 +260,9 @@ __global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, c
 // decomposition, group stride own_gstride) instead of D, so the decomposition
 // never copies them.  out comps 0/1 of group g at out.p + g*out_gstride.
 // key layout [digit][2][klvl+1+K][N] (common.h key_pos).
-__global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, LimbSet own, MacGroups G, int beta,
-                                                     const DeviceTables* __restrict__ tb, int N) {
+template <bool ROWS>
+__device__ __forceinline__ void ks_mac_body(LimbSet& out, LimbSet& D, LimbSet& own, MacGroups& G, int beta,
+                                            const DeviceTables* __restrict__ tb, int N, u64* lds) {
   const int row = blockIdx.y;
   const int bi = row % out.nbatch;
   const int r = row / out.nbatch;
@@ -333,8 +335,47 @@ __global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, Lim
     r1.x = add_mod(r1.x, mac_reduce_small(s1x, mc), q);
     r1.y = add_mod(r1.y, mac_reduce_small(s1y, mc), q);
   }
+  if constexpr (ROWS) {
+    if (l >= G.rows_from) {  // (block-uniform) a P limb: the ModDown INTT's rows pass, here
+      // the block's 512 coefficients are rows 2 bx and 2 bx + 1 of both
+      // components: staged in LDS as 4 rows (comp-major), then thread
+      // (rr, kk) runs the radix-4 inverse rows steps on elements 4 kk .. 4 kk + 3
+      const int t = threadIdx.x, lrw = (2 * t) >> 8, col = (2 * t) & 255;
+      lds[lrw * 256 + col] = r0.x, lds[lrw * 256 + col + 1] = r0.y;
+      lds[(2 + lrw) * 256 + col] = r1.x, lds[(2 + lrw) * 256 + col + 1] = r1.y;
+      __syncthreads();
+      const int rr = t >> 6, kk = t & 63, row = 2 * blockIdx.x + (rr & 1);
+      u64* const lr = lds + rr * 256;
+      u64* const mid = op + row_off(out, rr >> 1, l, bi) + (row << 8);
+      auto rows = [&](const auto& ar, __amdgpu_buffer_rsrc_t tw) {
+        using A = std::decay_t<decltype(ar)>;
+        typename A::T x[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = ar.from_u64(lr[4 * kk + i]);
+        if (G.logN == 15)
+          inv_rows4_core<A, 15>(x, row, kk, ar, tw, lr, mid);
+        else
+          inv_rows4_core<A, 16>(x, row, kk, ar, tw, lr, mid);
+      };
+      if (mc.f64)
+        rows(F64Arith(mc), twr_s(tb->inv_d[m], 8 * N));
+      else
+        rows(IntArith(mc), twr_s(tb->inv[m], 16 * N));
+      return;
+    }
+  }
   *(ulonglong2*)(op + row_off(out, 0, l, bi) + n) = r0;
   *(ulonglong2*)(op + row_off(out, 1, l, bi) + n) = r1;
+}
+__global__ void __launch_bounds__(256) ks_mac_kernel(LimbSet out, LimbSet D, LimbSet own, MacGroups G, int beta,
+                                                     const DeviceTables* __restrict__ tb, int N) {
+  ks_mac_body<false>(out, D, own, G, beta, tb, N, nullptr);
+}
+// the same, the P limbs' results through the INTT's rows pass (MacGroups.rows_from)
+__global__ void __launch_bounds__(256) ks_mac_rows_kernel(LimbSet out, LimbSet D, LimbSet own, MacGroups G, int beta,
+                                                          const DeviceTables* __restrict__ tb, int N) {
+  __shared__ u64 lds[4 * 256];
+  ks_mac_body<true>(out, D, own, G, beta, tb, N, lds);
 }
 
 // NTT-domain automorphism: o[j] = a[idx[j]]  (optionally o += a[idx[j]])
@@ -812,6 +853,11 @@ int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const LimbSet& own
   const int rows = ngroup * out.nlimb * out.nbatch;
   if (rows == 0) return 0;
   if (ngroup > ORION_MAXGROUP) return -1;
+  if (G.rows_from > 0) {
+    if ((G.logN != 15 && G.logN != 16) || N != (1 << G.logN) || ngroup != 1) return -1;
+    hipLaunchKernelGGL(ks_mac_rows_kernel, ew_grid(N, rows), dim3(256), 0, st, out, D, own, G, beta, tb, N);
+    return 0;
+  }
   hipLaunchKernelGGL(ks_mac_kernel, ew_grid(N, rows), dim3(256), 0, st, out, D, own, G, beta, tb, N);
   return 0;
 }

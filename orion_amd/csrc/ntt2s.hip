@@ -17,6 +17,7 @@
 
 #include "common.h"
 #include "ntt_arith.h"
+#include "ntt2s_rows.h"
 
 namespace {
 
@@ -43,9 +44,6 @@ struct S2 {
   static constexpr int RT4 = RW * 64;            // radix-4 rows-pass threads (256)
 };
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t twr_s(const void* t, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)t, 0, bytes, 0x00020000);
-}
 
 // lower index of butterfly k of a stage on bit `bit` (pairs lo, lo + 2^bit)
 [[maybe_unused]] __device__ __forceinline__ int lo_of(int k, int bit) { return ((k >> bit) << (bit + 1)) | (k & ((1 << bit) - 1)); }
@@ -318,26 +316,6 @@ __device__ __forceinline__ void s_inv_cols_src2(const u64* m0, const u64* m1, co
 // set {j, j + 2^(R-2), j + 2^(R-1), j + 3 2^(R-2)} -- so ntt2s_ifwd_cols needs
 // no exchange between its inverse and forward halves.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int ins2(int j, int lo) {  // j with zero bits inserted at lo, lo + 1
-  return ((j >> lo) << (lo + 2)) | (j & ((1 << lo) - 1));
-}
-template <class A>
-__device__ __forceinline__ void ct4(const A& ar, typename A::T (&x)[4], const typename A::W& wa,
-                                    const typename A::W& wb, const typename A::W& wc) {
-  ar.ct(x[0], x[2], wa);  // upper stage: (e0, e2), (e1, e3)
-  ar.ct(x[1], x[3], wa);
-  ar.ct(x[0], x[1], wb);  // lower stage: (e0, e1), (e2, e3)
-  ar.ct(x[2], x[3], wc);
-}
-template <class A>
-__device__ __forceinline__ void gs4(const A& ar, typename A::T (&x)[4], const typename A::W& wa,
-                                    const typename A::W& wb, const typename A::W& wc, bool red_lo, bool red_hi) {
-  ar.gs(x[0], x[1], wa, red_lo);  // lower stage: (e0, e1), (e2, e3)
-  ar.gs(x[2], x[3], wb, red_lo);
-  ar.gs(x[0], x[2], wc, red_hi);  // upper stage: (e0, e2), (e1, e3)
-  ar.gs(x[1], x[3], wc, red_hi);
-}
-
 // forward columns pass, radix 4: thread (cl, j), j < 2^(R-2)
 template <class A, int LOGN>
 __device__ __forceinline__ void s_fwd_cols4_core(const NttIO& io, int job, int c, int l, int b, int tile,
@@ -470,45 +448,15 @@ __device__ __forceinline__ void s_fwd_rows4(const NttIO& io, int job, int c, int
 }
 
 // inverse rows pass, radix 4 (first): steps on bits (0, 1) .. (6, 7)
+// (inv_rows4_core, ntt2s_rows.h)
 template <class A, int LOGN>
 __device__ __forceinline__ void s_inv_rows4(const NttIO& io, int job, int c, int l, int b, int tile, const A& ar,
                                             __amdgpu_buffer_rsrc_t tw, u64* lds) {
-  constexpr int N = 1 << LOGN;
   const int t = threadIdx.x, rr = t >> 6, kk = t & 63, row = tile * S2<LOGN>::RW + rr;
-  typename A::W wa[4], wb[4], wc[4];
-#pragma unroll
-  for (int st = 0; st < 4; ++st) {
-    const int lb = 2 * st, g = kk >> lb;
-    wa[st] = ar.tw(tw, (row << (7 - lb)) | (2 * g), N >> (lb + 1));
-    wb[st] = ar.tw(tw, (row << (7 - lb)) | (2 * g + 1), N >> (lb + 1));
-    wc[st] = ar.tw(tw, (row << (6 - lb)) | g, N >> (lb + 2));
-  }
   const u64* src = row_ptr(io.src, c, l, b) + (row << 8) + 4 * kk;
   const ulonglong2 v01 = *(const ulonglong2*)src, v23 = *(const ulonglong2*)(src + 2);
   typename A::T x[4] = {ar.from_u64(v01.x), ar.from_u64(v01.y), ar.from_u64(v23.x), ar.from_u64(v23.y)};
-  u64* lr = lds + rr * 256;
-#pragma unroll
-  for (int st = 0; st < 4; ++st) {
-    const int lb = 2 * st, hb = lb + 1;
-    const int e0 = ins2(kk, lb), e1 = e0 + (1 << lb), e2 = e0 + (1 << hb), e3 = e2 + (1 << lb);
-    if (st > 0) {
-      x[0] = from_bits<typename A::T>(lr[e0]);
-      x[1] = from_bits<typename A::T>(lr[e1]);
-      x[2] = from_bits<typename A::T>(lr[e2]);
-      x[3] = from_bits<typename A::T>(lr[e3]);
-    }
-    gs4(ar, x, wa[st], wb[st], wc[st], false, true);
-    if (st < 3) {  // (a thread writes back only the words it read: one barrier per step)
-      lr[e0] = to_bits(x[0]);
-      lr[e1] = to_bits(x[1]);
-      lr[e2] = to_bits(x[2]);
-      lr[e3] = to_bits(x[3]);
-      __syncthreads();
-    }
-  }
-  u64* mid = mid_row_s(io, job, c, l, b) + (row << 8);  // the last step's elements: kk + 64 i
-#pragma unroll
-  for (int i = 0; i < 4; ++i) mid[kk + 64 * i] = to_bits(ar.reduce_round(x[i]));
+  inv_rows4_core<A, LOGN>(x, row, kk, ar, tw, lds + rr * 256, mid_row_s(io, job, c, l, b) + (row << 8));
 }
 
 // inverse columns pass, radix 4 (second), up to two source limbs interleaved

@@ -1,0 +1,76 @@
+// ntt2s_rows.h -- the radix-4 steps shared by the latency NTT kernels
+// (ntt2s.hip) and the kernels that end in an inverse rows pass of their own
+// output (kernels.hip: ks_mac's P limbs).  Device code only.
+#pragma once
+#include "common.h"
+#include "ntt_arith.h"
+
+namespace {
+
+// a twiddle table (t, bytes) as a buffer resource
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t twr_s(const void* t, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)t, 0, bytes, 0x00020000);
+}
+
+__device__ __forceinline__ int ins2(int j, int lo) {  // j with zero bits inserted at lo, lo + 1
+  return ((j >> lo) << (lo + 2)) | (j & ((1 << lo) - 1));
+}
+template <class A>
+__device__ __forceinline__ void ct4(const A& ar, typename A::T (&x)[4], const typename A::W& wa,
+                                    const typename A::W& wb, const typename A::W& wc) {
+  ar.ct(x[0], x[2], wa);  // upper stage: (e0, e2), (e1, e3)
+  ar.ct(x[1], x[3], wa);
+  ar.ct(x[0], x[1], wb);  // lower stage: (e0, e1), (e2, e3)
+  ar.ct(x[2], x[3], wc);
+}
+template <class A>
+__device__ __forceinline__ void gs4(const A& ar, typename A::T (&x)[4], const typename A::W& wa,
+                                    const typename A::W& wb, const typename A::W& wc, bool red_lo, bool red_hi) {
+  ar.gs(x[0], x[1], wa, red_lo);  // lower stage: (e0, e1), (e2, e3)
+  ar.gs(x[2], x[3], wb, red_lo);
+  ar.gs(x[0], x[2], wc, red_hi);  // upper stage: (e0, e2), (e1, e3)
+  ar.gs(x[1], x[3], wc, red_hi);
+}
+
+// the inverse rows pass (the first pass of the two-pass INTT, ntt2s.hip) of
+// one 256-element row: thread kk holds elements 4kk .. 4kk + 3 in x, lr is
+// the row's 256 words of LDS (a thread writes back only the words it read, so
+// one barrier per step, and none before the first), mid the row's
+// intermediate (element kk + 64 i of the last step).  row: the row's index in
+// the limb (the twiddles of its groups)
+template <class A, int LOGN>
+__device__ __forceinline__ void inv_rows4_core(typename A::T (&x)[4], int row, int kk, const A& ar,
+                                               __amdgpu_buffer_rsrc_t tw, u64* lr, u64* mid) {
+  constexpr int N = 1 << LOGN;
+  typename A::W wa[4], wb[4], wc[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int lb = 2 * st, g = kk >> lb;
+    wa[st] = ar.tw(tw, (row << (7 - lb)) | (2 * g), N >> (lb + 1));
+    wb[st] = ar.tw(tw, (row << (7 - lb)) | (2 * g + 1), N >> (lb + 1));
+    wc[st] = ar.tw(tw, (row << (6 - lb)) | g, N >> (lb + 2));
+  }
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int lb = 2 * st, hb = lb + 1;
+    const int e0 = ins2(kk, lb), e1 = e0 + (1 << lb), e2 = e0 + (1 << hb), e3 = e2 + (1 << lb);
+    if (st > 0) {
+      x[0] = from_bits<typename A::T>(lr[e0]);
+      x[1] = from_bits<typename A::T>(lr[e1]);
+      x[2] = from_bits<typename A::T>(lr[e2]);
+      x[3] = from_bits<typename A::T>(lr[e3]);
+    }
+    gs4(ar, x, wa[st], wb[st], wc[st], false, true);
+    if (st < 3) {
+      lr[e0] = to_bits(x[0]);
+      lr[e1] = to_bits(x[1]);
+      lr[e2] = to_bits(x[2]);
+      lr[e3] = to_bits(x[3]);
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) mid[kk + 64 * i] = to_bits(ar.reduce_round(x[i]));
+}
+
+}  // namespace
