@@ -1764,6 +1764,9 @@ struct Context {
   // 1: keyswitch's gadget product stores the P limbs through the ModDown
   // INTT's rows pass when the ModDown takes the fused latency path
   int mac_rows = getenv("ORION_MAC_ROWS") ? atoi(getenv("ORION_MAC_ROWS")) : 1;
+  // 1: lt_bsgs / lt_giant take their workgroups in XCD-aware order (every
+  // coefficient block's diagonals and keys read into one XCD's L2)
+  int lt_xcd = getenv("ORION_LT_XCD") ? atoi(getenv("ORION_LT_XCD")) : 1;
   void moddown(const LimbSet& x, int level, const LimbSet& out, u64 aut_g = 0, bool aut_acc = false,
                bool rows_done = false) {
     const int nc = x.ncomp, B = x.nbatch, jobs = nc * B * (level + 1);
@@ -2077,6 +2080,7 @@ struct Context {
         memset(&Bb, 0, sizeof(Bb));
         Bb.nb = std::min(LT_MAXB, nb - s0);
         Bb.s0 = s0;
+        Bb.xcd = lt_xcd && (N / 256) % 8 == 0;
         Bb.beta = beta;
         Bb.K = K;
         Bb.level = level;
@@ -2133,6 +2137,7 @@ struct Context {
         G.level = level;
         G.L = L;
         G.has_zero = (has_g0 && g0 == 0) ? 1 : 0;
+        G.xcd = lt_xcd && (N / 256) % 8 == 0;
         G.d_gstride = (long long)beta * Dg.comp_stride();
         G.own_gstride = T1q.comp_stride();
         G.t0_gstride = Tt.comp_stride();

@@ -262,6 +262,7 @@ struct LtBabies {  // the baby steps of register slots [s0, s0 + nb) of one lt_b
   int klvl[LT_MAXB];        // level the key was made for
   int nb, s0, beta, K, level, L;
   u64 pq[ORION_MAXLIMB], pqs[ORION_MAXLIMB];  // P mod q_l and Shoup companion (0 on the P limbs)
+  int xcd;  // 1: XCD-aware block order (lt_xcd_decode)
 };
 struct LtGiants {  // the nonzero giant steps of one lt_giant launch
   const u64* key[ORION_MAXGROUP];
@@ -269,6 +270,7 @@ struct LtGiants {  // the nonzero giant steps of one lt_giant launch
   int klvl[ORION_MAXGROUP];
   int ng, beta, K, level, L, has_zero;
   long long d_gstride, own_gstride, t0_gstride;
+  int xcd;  // 1: XCD-aware block order (lt_xcd_decode)
 };
 
 // ---------------------------------------------------------------------------

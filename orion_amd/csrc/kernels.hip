@@ -14,7 +14,8 @@
 // timing-only ablation of lt_bsgs (0 in the product): bit 0 skips the giant
 // inner products of moduli below 2^48, bit 1 skips the baby gadget products,
 // bit 2 the giant products of the integer-path (>= 2^48) moduli, bit 3 their
-// baby gadget products
+// baby gadget products, bit 4 replaces the giants' diagonal loads by values
+// formed in registers
 #ifndef LT_ABLATE
 #define LT_ABLATE 0
 #endif
@@ -443,6 +444,23 @@ __device__ __forceinline__ void mac_add1(MacAcc& a, u64 x) {
   a.c += (a.lo < x);
 }
 
+// XCD-aware block order for the grids (images, coefficient blocks, limbs) of
+// lt_bsgs / lt_giant: workgroups go round-robin to the 8 XCDs by linear id,
+// so with the image index fastest every XCD would see every coefficient block
+// and fill its own L2 with all of the blocks' shared words (diagonals, keys).
+// Here linear id L runs on XCD L % 8 over coefficient blocks = XCD (mod 8),
+// images fastest: each block's shared words are read into one XCD's L2 only.
+// (x, y, z) = (image, coefficient block, limb); needs gridDim.y % 8 == 0.
+__device__ __forceinline__ void lt_xcd_decode(int& x, int& y, int& z) {
+  const unsigned gx = gridDim.x, gy = gridDim.y;
+  const unsigned lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const unsigned xcd = lin & 7, k = lin >> 3, cpx = gy >> 3;
+  x = (int)(k % gx);
+  const unsigned rest = k / gx;
+  y = (int)((rest % cpx) * 8 + xcd);
+  z = (int)(rest / cpx);
+}
+
 // Hoisted BSGS linear transform, baby steps and giant inner products fused
 // (lintrans MultiplyByDiagMatrixBSGS):
 //   rot_s  = sigma_s( gadget(D, key_s) + (P * ct0, 0) )   s != 0   (QP, hoisted key switch)
@@ -459,9 +477,11 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
                                              const LtBabies& Bb, const LtPlan* __restrict__ P, int g0, int g1,
                                              int accumulate, const LimbSet& ptl, const DeviceTables* __restrict__ tb,
                                              int N, int z0) {
-  const int bi = blockIdx.x;
-  const int n = blockIdx.y * blockDim.x + threadIdx.x;
-  const int l = z0 + blockIdx.z;
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (Bb.xcd) lt_xcd_decode(bx, by, bz);
+  const int bi = bx;
+  const int n = by * blockDim.x + threadIdx.x;
+  const int l = z0 + bz;
   if (n >= N) return;
   const int m = arg_byte(t0.mod, l);
   const ModConst mc = tb->mc[m];
@@ -519,7 +539,7 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
         }
         u64 pv[MB];
 #pragma unroll
-        for (int s = 0; s < MB; ++s) pv[s] = (LT_DENSE || ((mask >> s) & 1ull)) ? gld(P->pt[g][Bb.s0 + s], po) : 0;
+        for (int s = 0; s < MB; ++s) pv[s] = (LT_DENSE || ((mask >> s) & 1ull)) ? ((LT_ABLATE & 16) ? (u64)(po + 977 * s + g) : gld(P->pt[g][Bb.s0 + s], po)) : 0;
         MacD a0, a1;
         macd_zero(a0), macd_zero(a1);
 #pragma unroll
@@ -565,7 +585,7 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
       }
       u64 pv[MB];
 #pragma unroll
-      for (int s = 0; s < MB; ++s) pv[s] = (LT_DENSE || ((mask >> s) & 1ull)) ? gld(P->pt[g][Bb.s0 + s], po) : 0;
+      for (int s = 0; s < MB; ++s) pv[s] = (LT_DENSE || ((mask >> s) & 1ull)) ? ((LT_ABLATE & 16) ? (u64)(po + 977 * s + g) : gld(P->pt[g][Bb.s0 + s], po)) : 0;
       MacW a0, a1;
       macw_zero(a0), macw_zero(a1);
 #pragma unroll
@@ -604,7 +624,7 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
     // their latencies overlap (the branches are wave-uniform)
     u64 pv[MB];
 #pragma unroll
-    for (int s = 0; s < MB; ++s) pv[s] = (LT_DENSE || ((mask >> s) & 1ull)) ? gld(P->pt[g][Bb.s0 + s], po) : 0;
+    for (int s = 0; s < MB; ++s) pv[s] = (LT_DENSE || ((mask >> s) & 1ull)) ? ((LT_ABLATE & 16) ? (u64)(po + 977 * s + g) : gld(P->pt[g][Bb.s0 + s], po)) : 0;
     MacAcc a0, a1;
     mac_zero(a0), mac_zero(a1);
 #pragma unroll
@@ -648,9 +668,11 @@ template <int IB>
 __global__ void __launch_bounds__(256) lt_giant_kernel(LimbSet acc, LimbSet D, LimbSet own, LimbSet t0, LimbSet z,
                                                        LtGiants G, const DeviceTables* __restrict__ tb, int N) {
   constexpr int CH = LT_GIANT_CH > 0 ? LT_GIANT_CH : (IB >= 4 ? 2 : 4);  // digits per load chunk
-  const int b0 = blockIdx.x * IB;
-  const int n = blockIdx.y * blockDim.x + threadIdx.x;
-  const int l = blockIdx.z;
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (G.xcd) lt_xcd_decode(bx, by, bz);
+  const int b0 = bx * IB;
+  const int n = by * blockDim.x + threadIdx.x;
+  const int l = bz;
   if (n >= N) return;
   const int nb = acc.nbatch - b0 < IB ? acc.nbatch - b0 : IB;  // uniform
   const int m = arg_byte(acc.mod, l);
