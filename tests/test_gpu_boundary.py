@@ -67,6 +67,25 @@ def test_handle_heap_lowest_free_reuse(torch_cuda):
     lib.DeleteScheme()
 
 
+def test_pool_stats_reuse(torch_cuda):
+    """OrionHipPoolStats: the device pools cache freed buffers by size, so a
+    second identical op reuses them (no new hipMalloc); held >= cached and the
+    peak bounds the held bytes; no trim happens at this size."""
+    from orion_amd.backend import HipLibrary
+    lib = HipLibrary().new_scheme(13, [50, 40, 40], [60], 40, h=64, seed=9)
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    ct = lib.Encrypt(lib.encode_batch(np.ones((2, 8), np.float32), 2, 1 << 40))
+    lib.DeleteCiphertext(lib.MulRelinCiphertextNew(ct, ct))  # warm the size classes
+    a = lib.pool_stats()
+    lib.DeleteCiphertext(lib.MulRelinCiphertextNew(ct, ct))
+    b = lib.pool_stats()
+    assert b["hipmalloc_calls"] == a["hipmalloc_calls"], (a, b)
+    assert b["trims"] == 0 and 0 < b["cached_bytes"] <= b["held_bytes"] <= b["peak_bytes"], b
+    lib.DeleteScheme()
+
+
 def test_stream_switch_bit_exact(small, torch_cuda):
     """OrionHipSetStream between two ops (the pool reuses buffers
     across streams): the old stream is drained at the switch, so a result
