@@ -103,7 +103,7 @@ class DevicePool {
         (void)hipGetLastError();
         for (DevicePool* q : registry())
           if (q->tracking_) throw std::runtime_error("device memory exhausted during graph capture");
-        for (DevicePool* q : registry()) q->trim();
+        for (DevicePool* q : registry()) q->trim(true);
         HIPCHK(hipMalloc(&p, bytes));
       }
       stats()[2] += 1;
@@ -145,12 +145,13 @@ class DevicePool {
       }
     }
   }
-  void trim() {
+  // forced: after a failed hipMalloc (counted in stats()[3])
+  void trim(bool forced = false) {
     hipDeviceSynchronize();
     for (auto& kv : free_)
       for (void* p : kv.second) hipFree(p), held_ -= kv.first, add_held(-(double)kv.first);
     free_.clear();
-    stats()[3] += 1;
+    if (forced) stats()[3] += 1;
   }
   DevicePool() { registry().push_back(this); }
   DevicePool(const DevicePool&) = delete;

@@ -70,7 +70,7 @@ def test_handle_heap_lowest_free_reuse(torch_cuda):
 def test_pool_stats_reuse(torch_cuda):
     """OrionHipPoolStats: the device pools cache freed buffers by size, so a
     second identical op reuses them (no new hipMalloc); held >= cached and the
-    peak bounds the held bytes; no trim happens at this size."""
+    peak bounds the held bytes; no forced trim happens at this size."""
     from orion_amd.backend import HipLibrary
     lib = HipLibrary().new_scheme(13, [50, 40, 40], [60], 40, h=64, seed=9)
     lib.GenerateSecretKey()
@@ -82,7 +82,7 @@ def test_pool_stats_reuse(torch_cuda):
     lib.DeleteCiphertext(lib.MulRelinCiphertextNew(ct, ct))
     b = lib.pool_stats()
     assert b["hipmalloc_calls"] == a["hipmalloc_calls"], (a, b)
-    assert b["trims"] == 0 and 0 < b["cached_bytes"] <= b["held_bytes"] <= b["peak_bytes"], b
+    assert b["trims"] == a["trims"] and 0 < b["cached_bytes"] <= b["held_bytes"] <= b["peak_bytes"], b
     lib.DeleteScheme()
 
 
