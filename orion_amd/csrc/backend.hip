@@ -2123,6 +2123,11 @@ struct Context {
     // 4. giant key switches and the automorphism-accumulation (lt_giant)
     Poly acc = alloc(2, nqp, B);
     LimbSet la = lsqp(acc, 0, 2, level, level);
+    Ciphertext out = new_ct(level, B, ct.scale * (long double)mods[T.level]);
+    const LimbSet lo = lsq(out.poly, 0, 2, level);
+    // one lt_giant launch: it may store the P limbs through the final
+    // ModDown INTT's rows pass (as keyswitch's gadget product does)
+    const bool rows = nzg > 0 && nzg <= ORION_MAXGROUP && moddown_rows_fusable(la, level, lo, 0, false);
     LimbSet z = lsqp(Tt, ng - 1, 2, level, level);  // the zero giant: (c0, c1) at comps ng-1, 2ng-1
     z.comp_stride = (long long)ng * Tt.comp_stride();
     if (nzg > 0) {
@@ -2139,6 +2144,8 @@ struct Context {
         G.L = L;
         G.has_zero = (has_g0 && g0 == 0) ? 1 : 0;
         G.xcd = lt_xcd && (N / 256) % 8 == 0;
+        G.rows_from = rows ? level + 1 : 0;
+        G.logN = logN;
         G.d_gstride = (long long)beta * Dg.comp_stride();
         G.own_gstride = T1q.comp_stride();
         G.t0_gstride = Tt.comp_stride();
@@ -2171,8 +2178,7 @@ struct Context {
       copy(la, z);
     }
     // 5.
-    Ciphertext out = new_ct(level, B, ct.scale * (long double)mods[T.level]);
-    moddown(la, level, lsq(out.poly, 0, 2, level));
+    moddown(la, level, lo, 0, false, rows);
     return out;
   }
 

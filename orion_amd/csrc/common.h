@@ -271,6 +271,10 @@ struct LtGiants {  // the nonzero giant steps of one lt_giant launch
   int ng, beta, K, level, L, has_zero;
   long long d_gstride, own_gstride, t0_gstride;
   int xcd;  // 1: XCD-aware block order (lt_xcd_decode)
+  // rows_from > 0 (lt_giant_kernel<IB, true>, N = 2^logN, logN 15 or 16): acc
+  // limbs l >= rows_from (the P limbs, read only by the final ModDown's INTT)
+  // are stored after the INTT's radix-4 rows pass (ntt2s_rows.h)
+  int rows_from, logN;
 };
 
 // ---------------------------------------------------------------------------

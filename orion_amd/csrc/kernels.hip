@@ -664,7 +664,7 @@ lt_bsgs_kernel16(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb, con
 // Each thread takes one coefficient of IB images: the automorphism index, the
 // key words and every pointer step are shared by the IB images, so the key
 // reads from L2 and the scalar address work per product drop IB-fold.
-template <int IB>
+template <int IB, bool ROWS>
 __global__ void __launch_bounds__(256) lt_giant_kernel(LimbSet acc, LimbSet D, LimbSet own, LimbSet t0, LimbSet z,
                                                        LtGiants G, const DeviceTables* __restrict__ tb, int N) {
   constexpr int CH = LT_GIANT_CH > 0 ? LT_GIANT_CH : (IB >= 4 ? 2 : 4);  // digits per load chunk
@@ -781,8 +781,52 @@ __global__ void __launch_bounds__(256) lt_giant_kernel(LimbSet acc, LimbSet D, L
       x0 = add_mod(x0, z.p[row_off(z, 0, l, b0 + b) + n], mc.q);
       x1 = add_mod(x1, z.p[row_off(z, 1, l, b0 + b) + n], mc.q);
     }
-    acc.p[row_off(acc, 0, l, b0 + b) + n] = x0;
-    acc.p[row_off(acc, 1, l, b0 + b) + n] = x1;
+    r0[b] = x0, r1[b] = x1;
+  }
+  if constexpr (ROWS) {
+    if (l >= G.rows_from) {  // (block-uniform) a P limb: the final ModDown INTT's rows pass, here
+      // the block's 256 coefficients are row `by` of the limb, for 2 nb
+      // (image, component) rows q = 2 b + c: staged in LDS, then 4 rows at a
+      // time, thread (rr, kk) runs the radix-4 inverse rows steps on elements
+      // 4 kk .. 4 kk + 3 of row q0 + rr and stores the INTT's intermediate in
+      // place of the row.  A group past the last row works on a spare LDS row
+      // of its own and stores nothing, so every thread keeps the barriers.
+      constexpr int NR = 2 * IB > 4 ? 2 * IB : 4;
+      __shared__ u64 lds[NR * 256];
+      const int t = threadIdx.x;
+#pragma unroll
+      for (int b = 0; b < IB; ++b)
+        if (b < nb) lds[(2 * b) * 256 + t] = r0[b], lds[(2 * b + 1) * 256 + t] = r1[b];
+      __syncthreads();
+      const int rr = t >> 6, kk = t & 63;
+      for (int q0 = 0; q0 < 2 * nb; q0 += 4) {  // (uniform)
+        const int q = q0 + rr;
+        const bool live = q < 2 * nb;
+        u64* const lr = lds + q * 256;
+        u64* const mid = acc.p + row_off(acc, q & 1, l, b0 + (live ? q >> 1 : 0)) + (by << 8);
+        auto rows = [&](const auto& ar, __amdgpu_buffer_rsrc_t tw) {
+          using A = std::decay_t<decltype(ar)>;
+          typename A::T x[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) x[i] = ar.from_u64(lr[4 * kk + i]);
+          if (G.logN == 15)
+            inv_rows4_core<A, 15>(x, by, kk, ar, tw, lr, mid, live);
+          else
+            inv_rows4_core<A, 16>(x, by, kk, ar, tw, lr, mid, live);
+        };
+        if (mc.f64)
+          rows(F64Arith(mc), twr_s(tb->inv_d[m], 8 * N));
+        else
+          rows(IntArith(mc), twr_s(tb->inv[m], 16 * N));
+      }
+      return;
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < IB; ++b) {
+    if (b >= nb) break;
+    acc.p[row_off(acc, 0, l, b0 + b) + n] = r0[b];
+    acc.p[row_off(acc, 1, l, b0 + b) + n] = r1[b];
   }
 }
 
@@ -916,7 +960,12 @@ int orion_launch_lt_giant(const LimbSet& acc, const LimbSet& D, const LimbSet& o
   if (G.ng > ORION_MAXGROUP) return -1;
   constexpr int IB = LT_GIANT_IB;
   dim3 g((acc.nbatch + IB - 1) / IB, (N + 255) / 256, acc.nlimb);
-  hipLaunchKernelGGL(lt_giant_kernel<IB>, g, dim3(256), 0, st, acc, D, own, t0, z, G, tb, N);
+  if (G.rows_from > 0) {
+    if ((G.logN != 15 && G.logN != 16) || N != (1 << G.logN)) return -1;
+    hipLaunchKernelGGL((lt_giant_kernel<IB, true>), g, dim3(256), 0, st, acc, D, own, t0, z, G, tb, N);
+    return 0;
+  }
+  hipLaunchKernelGGL((lt_giant_kernel<IB, false>), g, dim3(256), 0, st, acc, D, own, t0, z, G, tb, N);
   return 0;
 }
 

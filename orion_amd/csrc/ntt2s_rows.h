@@ -40,7 +40,7 @@ __device__ __forceinline__ void gs4(const A& ar, typename A::T (&x)[4], const ty
 // the limb (the twiddles of its groups)
 template <class A, int LOGN>
 __device__ __forceinline__ void inv_rows4_core(typename A::T (&x)[4], int row, int kk, const A& ar,
-                                               __amdgpu_buffer_rsrc_t tw, u64* lr, u64* mid) {
+                                               __amdgpu_buffer_rsrc_t tw, u64* lr, u64* mid, bool store = true) {
   constexpr int N = 1 << LOGN;
   typename A::W wa[4], wb[4], wc[4];
 #pragma unroll
@@ -69,8 +69,10 @@ __device__ __forceinline__ void inv_rows4_core(typename A::T (&x)[4], int row, i
       __syncthreads();
     }
   }
+  if (store) {  // (store = false: a thread group that only keeps the barriers)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) mid[kk + 64 * i] = to_bits(ar.reduce_round(x[i]));
+    for (int i = 0; i < 4; ++i) mid[kk + 64 * i] = to_bits(ar.reduce_round(x[i]));
+  }
 }
 
 }  // namespace
