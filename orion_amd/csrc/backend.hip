@@ -2073,12 +2073,6 @@ struct Context {
     const bool has_g0 = T.gorder.back() == 0;
     const int nzg = ng - (has_g0 ? 1 : 0);
     Poly Tt = alloc(2 * ng, nqp, B);
-    Poly T1q = alloc(std::max(nzg, 1), level + 1, B);
-    // one lt_bsgs launch for all giants: it may end the giants' c1 rows on the
-    // P limbs through the giants' ModDown INTT's rows pass
-    const bool bsgs_rows = nzg > 0 && nb <= LT_MAXB && T.n_plan == 1 &&
-                           moddown_rows_fusable(lsqp(Tt, ng, nzg, level, level), level, lsq(T1q, 0, nzg, level), 0,
-                                                false);
     {
       const Poly& pt0 = T.diags.begin()->second.poly;
       LimbSet ptl = lsqp(pt0, 0, 1, level, T.level, 1);
@@ -2088,8 +2082,6 @@ struct Context {
         Bb.nb = std::min(LT_MAXB, nb - s0);
         Bb.s0 = s0;
         Bb.xcd = lt_xcd && (N / 256) % 8 == 0;
-        Bb.rows_nz = bsgs_rows ? nzg : 0;
-        Bb.logN = logN;
         Bb.beta = beta;
         Bb.K = K;
         Bb.level = level;
@@ -2139,7 +2131,8 @@ struct Context {
     LimbSet z = lsqp(Tt, ng - 1, 2, level, level);  // the zero giant: (c0, c1) at comps ng-1, 2ng-1
     z.comp_stride = (long long)ng * Tt.comp_stride();
     if (nzg > 0) {
-      moddown(lsqp(Tt, ng, nzg, level, level), level, lsq(T1q, 0, nzg, level), 0, false, bsgs_rows);
+      Poly T1q = alloc(nzg, level + 1, B);
+      moddown(lsqp(Tt, ng, nzg, level, level), level, lsq(T1q, 0, nzg, level));
       Poly Dg = decompose(lsq(T1q, 0, nzg, level), level, B);
       for (int g0 = 0; g0 < nzg; g0 += ORION_MAXGROUP) {
         LtGiants G;

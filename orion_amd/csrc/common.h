@@ -263,10 +263,6 @@ struct LtBabies {  // the baby steps of register slots [s0, s0 + nb) of one lt_b
   int nb, s0, beta, K, level, L;
   u64 pq[ORION_MAXLIMB], pqs[ORION_MAXLIMB];  // P mod q_l and Shoup companion (0 on the P limbs)
   int xcd;  // 1: XCD-aware block order (lt_xcd_decode)
-  // rows_nz > 0 (lt_bsgs_rows_kernel*, one launch for all giants, g0 = 0; N =
-  // 2^logN, logN 15 or 16): on the P limbs the c1 rows of giants [0, rows_nz)
-  // -- read only by the ModDown's INTT -- end through its radix-4 rows pass
-  int rows_nz, logN;
 };
 struct LtGiants {  // the nonzero giant steps of one lt_giant launch
   const u64* key[ORION_MAXGROUP];

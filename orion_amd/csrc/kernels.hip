@@ -644,45 +644,6 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
   }
 }
 
-// the giants' c1 rows on a P limb (rows_nz of them, stored by this block:
-// row `by` of each) through the ModDown INTT's radix-4 rows pass, in place,
-// 4 rows at a time (the block's own global stores are visible to it after
-// the barrier); Q-limb blocks return at once
-__device__ __forceinline__ void lt_bsgs_rows_tail(const LimbSet& t1, const LtBabies& Bb,
-                                                  const DeviceTables* __restrict__ tb, int N, int z0, u64* lds) {
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (Bb.xcd) lt_xcd_decode(bx, by, bz);
-  const int l = z0 + bz;
-  if (l <= Bb.level) return;  // (block-uniform)
-  const int m = arg_byte(t1.mod, l);
-  const ModConst& mc = tb->mc[m];
-  const int t = threadIdx.x, rr = t >> 6, kk = t & 63;
-  const long long ro = row_off(t1, 0, l, bx) + ((long long)by << 8);
-  u64* const lr = lds + rr * 256;
-  for (int q0 = 0; q0 < Bb.rows_nz; q0 += 4) {
-    __syncthreads();  // the giants' stores done; the previous round's LDS reads done
-    const int q = q0 + rr;
-    const bool live = q < Bb.rows_nz;
-    u64* const row = t1.p + (long long)(live ? q : 0) * t1.comp_stride + ro;
-    auto rows = [&](const auto& ar, __amdgpu_buffer_rsrc_t tw) {
-      using A = std::decay_t<decltype(ar)>;
-      typename A::T x[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) x[i] = ar.from_u64(row[4 * kk + i]);
-      // (the in-place stores come after the steps' 3 barriers, so every
-      // thread of the row has read its words by then)
-      if (Bb.logN == 15)
-        inv_rows4_core<A, 15>(x, by, kk, ar, tw, lr, row, live);
-      else
-        inv_rows4_core<A, 16>(x, by, kk, ar, tw, lr, row, live);
-    };
-    if (mc.f64)
-      rows(F64Arith(mc), twr_s(tb->inv_d[m], 8 * N));
-    else
-      rows(IntArith(mc), twr_s(tb->inv[m], 16 * N));
-  }
-}
-
 // MB = 8 at 4 waves per SIMD (<= 128 VGPRs); MB = 16 holds twice the babies
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LT_WAVES8)))
 lt_bsgs_kernel8(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb, const LtPlan* __restrict__ P, int g0,
@@ -693,23 +654,6 @@ __global__ void __launch_bounds__(256)
 lt_bsgs_kernel16(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb, const LtPlan* __restrict__ P, int g0,
                  int g1, int accumulate, LimbSet ptl, const DeviceTables* __restrict__ tb, int N, int z0) {
   lt_bsgs_body<16>(t0, t1, D, ct, Bb, P, g0, g1, accumulate, ptl, tb, N, z0);
-}
-// the same, ending with the P limbs' c1 rows through the ModDown INTT's rows pass (LtBabies.rows_nz)
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LT_WAVES8)))
-lt_bsgs_rows_kernel8(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb, const LtPlan* __restrict__ P,
-                     int g0, int g1, int accumulate, LimbSet ptl, const DeviceTables* __restrict__ tb, int N,
-                     int z0) {
-  __shared__ u64 lds[4 * 256];
-  lt_bsgs_body<8>(t0, t1, D, ct, Bb, P, g0, g1, accumulate, ptl, tb, N, z0);
-  lt_bsgs_rows_tail(t1, Bb, tb, N, z0, lds);
-}
-__global__ void __launch_bounds__(256)
-lt_bsgs_rows_kernel16(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb, const LtPlan* __restrict__ P,
-                      int g0, int g1, int accumulate, LimbSet ptl, const DeviceTables* __restrict__ tb, int N,
-                      int z0) {
-  __shared__ u64 lds[4 * 256];
-  lt_bsgs_body<16>(t0, t1, D, ct, Bb, P, g0, g1, accumulate, ptl, tb, N, z0);
-  lt_bsgs_rows_tail(t1, Bb, tb, N, z0, lds);
 }
 
 // Giant steps of a hoisted BSGS transform, key switches and accumulation fused:
@@ -988,18 +932,10 @@ int orion_launch_lt_bsgs(const LimbSet& t0, const LimbSet& t1, const LimbSet& D,
                          const LtBabies& Bb, const LtPlan* plan, int g0, int g1, int accumulate, const LimbSet& ptl,
                          const DeviceTables* tb, int N, hipStream_t st) {
   if (Bb.nb < 1 || Bb.nb > LT_MAXB || g1 <= g0) return -1;
-  if (Bb.rows_nz > 0 && (g0 != 0 || Bb.rows_nz > g1 || (Bb.logN != 15 && Bb.logN != 16) || N != (1 << Bb.logN)))
-    return -1;
   auto launch = [&](int z0, int nz) {
     if (nz <= 0) return;
     dim3 g(t0.nbatch, (N + 255) / 256, nz);
-    if (Bb.rows_nz > 0 && Bb.nb <= 8)
-      hipLaunchKernelGGL(lt_bsgs_rows_kernel8, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate, ptl,
-                         tb, N, z0);
-    else if (Bb.rows_nz > 0)
-      hipLaunchKernelGGL(lt_bsgs_rows_kernel16, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate,
-                         ptl, tb, N, z0);
-    else if (Bb.nb <= 8)
+    if (Bb.nb <= 8)
       hipLaunchKernelGGL(lt_bsgs_kernel8, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate, ptl, tb,
                          N, z0);
     else
