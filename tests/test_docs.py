@@ -1,0 +1,31 @@
+"""Documentation contract (CPU): every runtime switch the library, bench.py or
+the package reads (ORION_* environment variables) is listed in
+INTEGRATION.md §7, so a maintainer switching from the reference sees every
+knob the backend honours."""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _switches():
+    found = set()
+    srcs = [os.path.join(ROOT, "bench.py")]
+    for d in ("orion_amd", os.path.join("orion_amd", "csrc")):
+        for f in os.listdir(os.path.join(ROOT, d)):
+            if f.endswith((".py", ".hip", ".cpp", ".h")):
+                srcs.append(os.path.join(ROOT, d, f))
+    pat = re.compile(r'(?:getenv\(|environ\.get\(|environ\[)"(ORION_[A-Z0-9_]+)"')
+    for p in srcs:
+        with open(p) as fh:
+            found.update(pat.findall(fh.read()))
+    return found
+
+
+def test_every_runtime_switch_documented():
+    with open(os.path.join(ROOT, "INTEGRATION.md")) as fh:
+        doc = fh.read()
+    switches = _switches()
+    assert len(switches) > 20
+    missing = sorted(v for v in switches if v not in doc)
+    assert not missing, missing
