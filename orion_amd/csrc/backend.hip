@@ -848,8 +848,13 @@ struct Context {
     if (logN != 15 || ci) return false;
     if (ntt_impl == 2 || jobs < ntt2_below) return true;
     const bool plain = (pro == NTT_PRO_LOAD || pro == NTT_PRO_BEXT) && epi == NTT_EPI_STORE;
-    return (inv || (ntt2_tail_fwd == 1 && plain) || (ntt2_tail_fwd == 2 && !inplace_sub)) && ntt2_tail(jobs);
+    return (inv || (ntt2_tail_fwd == 1 && plain) || (ntt2_tail_fwd == 2 && !inplace_sub) ||
+            (ntt2_tail_aut && epi_aut(epi) && pro == NTT_PRO_LOAD)) &&
+           ntt2_tail(jobs);
   }
+  // 1: the partial-round rule above also moves the rotations' scatter-store
+  // ModDown NTTs (NTT_EPI_SUBSCALE_AUT[_ACC]) onto the two-pass kernels
+  int ntt2_tail_aut = getenv("ORION_NTT2_TAIL_AUT") ? atoi(getenv("ORION_NTT2_TAIL_AUT")) : 0;
   // the fused basis extension (NTT_PRO_BEXT) pays on the two-pass kernels
   // only: in the one-pass kernel, one CU per limb, every target re-forms the
   // shared y_i and float quotient and loads ns source limbs in its memory
@@ -1729,8 +1734,9 @@ struct Context {
   // the one-pass kernel with the load prologue, or the radix-4 latency kernels
   bool aut_epi_ok(int jobs, int pro) {
     if (ci || ntt_tailsplit) return false;
-    if (!two_pass(jobs, false, pro, NTT_EPI_SUBSCALE, false)) return logN <= 15 && pro == NTT_PRO_LOAD;
-    return jobs <= ntt2s_below && NTT2S_R4;
+    if (!two_pass(jobs, false, pro, NTT_EPI_SUBSCALE_AUT, false)) return logN <= 15 && pro == NTT_PRO_LOAD;
+    if (jobs <= ntt2s_below) return NTT2S_R4;
+    return pro == NTT_PRO_LOAD && ntt2_tail_aut;  // the large two-pass kernels (ntt2.hip), load prologue
   }
   u64 galois_inverse(u64 g) const {
     const u64 M = nthroot;

@@ -181,6 +181,33 @@ __device__ __forceinline__ void fwd_rows(const NttIO& io, int job, int c, int l,
 #pragma unroll
     for (int j = 0; j < 16; j += 2)
       *(ulonglong2*)(dst + j) = make_ulonglong2(ar.final_fwd(a[j]), ar.final_fwd(a[j + 1]));
+  } else if constexpr (epi_aut(EPI)) {
+    // (ex - y) * s_l stored at position aut[e] of the limb (added to the word
+    // there for _ACC): the rotation's NTT-domain automorphism in the ModDown's
+    // store, as in the one-pass and latency kernels
+    const u64* ex = row_ptr(io.ex, c, l, b) + (row << 8) + 16 * jc;
+    const u32* ai = io.aut + (row << 8) + 16 * jc;
+    u64* const d = row_ptr(io.dst, c, l, b);
+    const u64 s = io.s[l], ss = io.ss[l];
+#pragma unroll
+    for (int j = 0; j < 16; j += 4) {
+      const uint4 ix = *(const uint4*)(ai + j);
+      const ulonglong2 e01 = *(const ulonglong2*)(ex + j), e23 = *(const ulonglong2*)(ex + j + 2);
+      u64 o0 = shoup_mul(sub_mod(e01.x, ar.final_fwd(a[j]), mc.q), s, ss, mc.q);
+      u64 o1 = shoup_mul(sub_mod(e01.y, ar.final_fwd(a[j + 1]), mc.q), s, ss, mc.q);
+      u64 o2 = shoup_mul(sub_mod(e23.x, ar.final_fwd(a[j + 2]), mc.q), s, ss, mc.q);
+      u64 o3 = shoup_mul(sub_mod(e23.y, ar.final_fwd(a[j + 3]), mc.q), s, ss, mc.q);
+      if constexpr (EPI == NTT_EPI_SUBSCALE_AUT_ACC) {
+        o0 = add_mod(o0, d[ix.x], mc.q);
+        o1 = add_mod(o1, d[ix.y], mc.q);
+        o2 = add_mod(o2, d[ix.z], mc.q);
+        o3 = add_mod(o3, d[ix.w], mc.q);
+      }
+      d[ix.x] = o0;
+      d[ix.y] = o1;
+      d[ix.z] = o2;
+      d[ix.w] = o3;
+    }
   } else {  // NTT_EPI_SUBSCALE: dst = (ex - y) * s_l
     const u64* ex = row_ptr(io.ex, c, l, b) + (row << 8) + 16 * jc;
     const u64 s = io.s[l], ss = io.ss[l];
@@ -388,6 +415,10 @@ int launch2(const NttIO& io, const DeviceTables* tb, bool inverse, hipStream_t s
     hipLaunchKernelGGL((ntt2_fwd_rows<LOGN, NTT_EPI_STORE>), gb, bb, 0, st, io, tb);
   else if (io.epi == NTT_EPI_SUBSCALE)
     hipLaunchKernelGGL((ntt2_fwd_rows<LOGN, NTT_EPI_SUBSCALE>), gb, bb, 0, st, io, tb);
+  else if (io.epi == NTT_EPI_SUBSCALE_AUT && io.aut)
+    hipLaunchKernelGGL((ntt2_fwd_rows<LOGN, NTT_EPI_SUBSCALE_AUT>), gb, bb, 0, st, io, tb);
+  else if (io.epi == NTT_EPI_SUBSCALE_AUT_ACC && io.aut)
+    hipLaunchKernelGGL((ntt2_fwd_rows<LOGN, NTT_EPI_SUBSCALE_AUT_ACC>), gb, bb, 0, st, io, tb);
   else
     return -1;
   return 0;
