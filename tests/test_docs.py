@@ -29,3 +29,15 @@ def test_every_runtime_switch_documented():
     assert len(switches) > 20
     missing = sorted(v for v in switches if v not in doc)
     assert not missing, missing
+
+
+def test_every_extension_entry_point_documented():
+    """every OrionHip* entry point include/orion_hip.h declares is in INTEGRATION.md"""
+    import re as _re
+    with open(os.path.join(ROOT, "include", "orion_hip.h")) as fh:
+        names = set(_re.findall(r"\b(OrionHip[A-Za-z0-9]+)\s*\(", fh.read()))
+    with open(os.path.join(ROOT, "INTEGRATION.md")) as fh:
+        doc = fh.read()
+    assert len(names) > 20
+    missing = sorted(n for n in names if n not in doc)
+    assert not missing, missing
