@@ -1600,7 +1600,11 @@ struct Context {
   // positions at lvl_alloc = level.  Digit i's own Q limbs (l / K == i) equal
   // c's and are not written: every consumer (ks_mac, lt_bsgs, lt_giant) reads
   // them from c.
-  Poly decompose(const LimbSet& c, int level, int B) {
+  // want_cols_only: if the decomposition takes the fused latency path, its
+  // forward NTT stops after the columns pass (the caller's gadget product runs
+  // the rows pass, ks_mac_full_kernel); *cols_only tells whether it did
+  Poly decompose(const LimbSet& c, int level, int B, bool want_cols_only = false, bool* cols_only = nullptr) {
+    if (cols_only) *cols_only = false;
     const int nc = c.ncomp;
     const int beta = (level + 1 + K - 1) / K;
     const int nqp = level + 1 + K;
@@ -1636,6 +1640,10 @@ struct Context {
           io.bx_tab[l] = (unsigned char)i;
           io.bx_t[l] = (unsigned char)(j < lo ? j : j - ns);
           srcs += ns;
+        }
+        if (want_cols_only && ifuse_ok(iio, io, K)) {
+          io.cols_only = 1;
+          if (cols_only) *cols_only = true;
         }
         intt_then_fwd(iio, io, K, srcs / (double)tpos.size());
         return D;
@@ -1693,7 +1701,7 @@ struct Context {
   void mac_groups(const LimbSet& o, long long out_gstride, const LimbSet& d, long long d_gstride,
                   const LimbSet& own, long long own_gstride, const std::vector<const u64*>& keys,
                   const std::vector<int>& klvl, int beta, const u64* add0 = nullptr, long long add_gstride = 0,
-                  int add_nq = 0, const u64* add1 = nullptr, int rows_from = 0) {
+                  int add_nq = 0, const u64* add1 = nullptr, int rows_from = 0, bool fwd_rows = false) {
     const int G = (int)keys.size();
     for (int g0 = 0; g0 < G; g0 += ORION_MAXGROUP) {
       const int ng = std::min(ORION_MAXGROUP, G - g0);
@@ -1711,6 +1719,8 @@ struct Context {
       mg.add_nq = add0 ? add_nq : 0;
       mg.rows_from = rows_from;
       mg.logN = logN;
+      mg.fwd_rows = (fwd_rows && rows_from > 0) ? 1 : 0;
+      if (fwd_rows && rows_from == 0) throw std::runtime_error("mac_groups: forward rows without the ModDown rows pass");
       for (int j = 0; j < mg.add_nq; ++j) {  // P mod q_j: ModDown(u + P*a) = ModDown(u) + a exactly
         u64 P = 1;
         for (int k = 0; k < K; ++k) P = hm_mulmod(P, mods[L + k] % mods[o.mod[j]], mods[o.mod[j]]);
@@ -1771,6 +1781,8 @@ struct Context {
   // 1: keyswitch's gadget product stores the P limbs through the ModDown
   // INTT's rows pass when the ModDown takes the fused latency path
   int mac_rows = getenv("ORION_MAC_ROWS") ? atoi(getenv("ORION_MAC_ROWS")) : 1;
+  // 1: ... and runs the decomposition NTT's forward rows pass itself
+  int mac_fwd_rows = getenv("ORION_MAC_FWD_ROWS") ? atoi(getenv("ORION_MAC_FWD_ROWS")) : 0;
   // 1: lt_bsgs / lt_giant take their workgroups in XCD-aware order (every
   // coefficient block's diagonals and keys read into one XCD's L2)
   int lt_xcd = getenv("ORION_LT_XCD") ? atoi(getenv("ORION_LT_XCD")) : 1;
@@ -1833,13 +1845,18 @@ struct Context {
   void keyswitch(const LimbSet& c, int level, int B, const Poly& key, int klvl, const Poly& out,
                  const u64* add0 = nullptr, const u64* add1 = nullptr, u64 aut_g = 0, bool aut_acc = false) {
     if (klvl < level) throw std::runtime_error("evaluation key made for a lower level");
-    Poly D = decompose(c, level, B);
     Poly u = alloc(2, level + 1 + K, B);
+    // when the gadget product runs the ModDown INTT's rows pass, it can run
+    // the decomposition NTT's forward rows pass too (ORION_MAC_FWD_ROWS)
+    const bool rows_q = mac_fwd_rows && moddown_rows_fusable(lsqp(u, 0, 2, level, level), level,
+                                                             lsq(out, 0, 2, level), aut_g, aut_acc);
+    bool fwd_rows = false;
+    Poly D = decompose(c, level, B, rows_q, &fwd_rows);
     const int beta = (level + 1 + K - 1) / K;
     const LimbSet uq = lsqp(u, 0, 2, level, level), oq = lsq(out, 0, 2, level);
     const bool rows = moddown_rows_fusable(uq, level, oq, aut_g, aut_acc);
     mac_groups(uq, 0, lsqp(D, 0, beta, level, level), 0, c, 0, {key.ptr()}, {klvl}, beta, add0, 0,
-               add0 ? level + 1 : 0, add1, rows ? level + 1 : 0);
+               add0 ? level + 1 : 0, add1, rows ? level + 1 : 0, fwd_rows);
     moddown(uq, level, oq, aut_g, aut_acc, rows);
   }
   std::vector<u64> p_mod_q(int level) const {

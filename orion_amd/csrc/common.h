@@ -245,6 +245,10 @@ struct MacGroups {  // ks_mac_kernel: group g uses key[g], made for level klvl[g
   // l >= rows_from (the P limbs, read only by the ModDown's INTT) are stored
   // after the INTT's radix-4 rows pass, as its intermediate (ntt2s_rows.h)
   int rows_from, logN;
+  // fwd_rows (with rows_from, one group): the decomposition's target rows of
+  // D hold its forward NTT's columns-pass intermediate; the gadget product
+  // runs their forward rows pass itself, in LDS, before the products
+  int fwd_rows;
 };
 
 // BSGS linear transform plan (device-resident, one per LinTrans): giants in
@@ -614,6 +618,9 @@ struct NttIO {
   // start at limb tg_l0[k] and hold tg_n[k] <= G targets
   int tgroup, ntg;
   unsigned char tg_l0[ORION_MAXLIMB], tg_n[ORION_MAXLIMB];
+  // forward latency launch (ntt2s): the columns pass alone -- the rows pass
+  // runs in the consumer (the key switch's gadget product, MacGroups.fwd_rows)
+  int cols_only;
   const u32* aut;  // NTT_EPI_SUBSCALE_AUT: the scatter index (N entries)
 };
 

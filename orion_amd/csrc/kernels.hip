@@ -261,7 +261,7 @@ __global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, c
 // decomposition, group stride own_gstride) instead of D, so the decomposition
 // never copies them.  out comps 0/1 of group g at out.p + g*out_gstride.
 // key layout [digit][2][klvl+1+K][N] (common.h key_pos).
-template <bool ROWS>
+template <bool ROWS, bool FR = false>
 __device__ __forceinline__ void ks_mac_body(LimbSet& out, LimbSet& D, LimbSet& own, MacGroups& G, int beta,
                                             const DeviceTables* __restrict__ tb, int N, u64* lds) {
   const int row = blockIdx.y;
@@ -296,6 +296,41 @@ __device__ __forceinline__ void ks_mac_body(LimbSet& out, LimbSet& D, LimbSet& o
   const int kl = G.klvl[g];
   const long long kstride = (long long)(kl + 1 + G.K) * N;
   const u64* kp = key + (long long)key_pos(m, G.L, kl) * N + n;
+  // FR: the decomposition's forward NTT stopped after its columns pass; rows
+  // 2 bx and 2 bx + 1 of every non-own digit's row set go through the
+  // forward rows pass here, 4 rows at a time (groups past the last row keep
+  // the barriers on their own LDS row), into fr = [digit][2 rows][256]
+  [[maybe_unused]] const u64* fr = nullptr;
+  if constexpr (FR) {
+    u64* const frw = lds + 4 * 256;
+    const int t = threadIdx.x, rr = t >> 6, kk = t & 63;
+    for (int q0 = 0; q0 < 2 * beta; q0 += 4) {  // (uniform)
+      if (q0 > 0) __syncthreads();  // the previous round's exchange reads done
+      const int q = q0 + rr, i = q >> 1, rw = 2 * blockIdx.x + (q & 1);
+      const bool live = q < 2 * beta && i != owndigit;
+      const u64* const src = dp + row_off(D, live ? i : 0, l, bi) + ((long long)rw << 8);
+      auto rows = [&](const auto& ar, __amdgpu_buffer_rsrc_t tw) {
+        using A = std::decay_t<decltype(ar)>;
+        typename A::T x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = from_bits<typename A::T>(live ? src[kk + 64 * k] : 0);
+        if (G.logN == 15)
+          fwd_rows4_core<A, 15>(x, rw, kk, ar, tw, lds + rr * 256);
+        else
+          fwd_rows4_core<A, 16>(x, rw, kk, ar, tw, lds + rr * 256);
+        if (live) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) frw[q * 256 + 4 * kk + k] = ar.final_fwd(x[k]);
+        }
+      };
+      if (mc.f64)
+        rows(F64Arith(mc), twr_s(tb->fwd_d[m], 8 * N));
+      else
+        rows(IntArith(mc), twr_s(tb->fwd[m], 16 * N));
+    }
+    __syncthreads();  // fr complete
+    fr = frw;
+  }
   // moduli below 2^52 (block-uniform): the digits' products are reduced once
   // at the end (mac_reduce_small takes up to 128), not once per chunk of 4
   const bool small = KS_MAC_ACC && mc.bar_k <= 52 && beta <= 120;
@@ -307,8 +342,14 @@ __device__ __forceinline__ void ks_mac_body(LimbSet& out, LimbSet& D, LimbSet& o
     for (int u = 0; u < KS_CH; ++u) {
       const int i = i0 + u;
       if (i < beta) {
-        d[u] = i == owndigit ? *(const ulonglong2*)(own.p + g * G.own_gstride + row_off(own, 0, l, bi) + n)
-                             : *(const ulonglong2*)(dp + row_off(D, i, l, bi) + n);
+        if (i == owndigit) {
+          d[u] = *(const ulonglong2*)(own.p + g * G.own_gstride + row_off(own, 0, l, bi) + n);
+        } else if constexpr (FR) {  // this thread's 2 coefficients: local 2t, 2t + 1 of the block's 2 rows
+          const int lt = 2 * (int)threadIdx.x;
+          d[u] = make_ulonglong2(fr[(2 * i + (lt >> 8)) * 256 + (lt & 255)], fr[(2 * i + (lt >> 8)) * 256 + (lt & 255) + 1]);
+        } else {
+          d[u] = *(const ulonglong2*)(dp + row_off(D, i, l, bi) + n);
+        }
         kb[u] = *(const ulonglong2*)(kp + (2 * i + 0) * kstride);
         ka[u] = *(const ulonglong2*)(kp + (2 * i + 1) * kstride);
       }
@@ -377,6 +418,13 @@ __global__ void __launch_bounds__(256) ks_mac_rows_kernel(LimbSet out, LimbSet D
                                                           const DeviceTables* __restrict__ tb, int N) {
   __shared__ u64 lds[4 * 256];
   ks_mac_body<true>(out, D, own, G, beta, tb, N, lds);
+}
+// the same, and before the products the decomposition's forward rows pass
+// (MacGroups.fwd_rows; dynamic LDS: (4 + 2 beta) rows of 256 words)
+__global__ void __launch_bounds__(256) ks_mac_full_kernel(LimbSet out, LimbSet D, LimbSet own, MacGroups G, int beta,
+                                                          const DeviceTables* __restrict__ tb, int N) {
+  extern __shared__ u64 lds_dyn[];
+  ks_mac_body<true, true>(out, D, own, G, beta, tb, N, lds_dyn);
 }
 
 // NTT-domain automorphism: o[j] = a[idx[j]]  (optionally o += a[idx[j]])
@@ -921,6 +969,12 @@ int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const LimbSet& own
   if (ngroup > ORION_MAXGROUP) return -1;
   if (G.rows_from > 0) {
     if ((G.logN != 15 && G.logN != 16) || N != (1 << G.logN) || ngroup != 1) return -1;
+    if (G.fwd_rows) {
+      if (beta > 16 || G.d_gstride) return -1;
+      hipLaunchKernelGGL(ks_mac_full_kernel, ew_grid(N, rows), dim3(256), (size_t)(4 + 2 * beta) * 256 * 8, st, out, D,
+                         own, G, beta, tb, N);
+      return 0;
+    }
     hipLaunchKernelGGL(ks_mac_rows_kernel, ew_grid(N, rows), dim3(256), 0, st, out, D, own, G, beta, tb, N);
     return 0;
   }

@@ -379,42 +379,12 @@ __device__ __forceinline__ void s_fwd_cols4(const NttIO& io, int job, int c, int
 template <class A, int LOGN, int EPI>
 __device__ __forceinline__ void s_fwd_rows4(const NttIO& io, int job, int c, int l, int b, int tile, const ModConst& mc,
                                             const A& ar, __amdgpu_buffer_rsrc_t tw, u64* lds) {
-  constexpr int N = 1 << LOGN;
   const int t = threadIdx.x, rr = t >> 6, kk = t & 63, row = tile * S2<LOGN>::RW + rr;
-  typename A::W wa[4], wb[4], wc[4];
-#pragma unroll
-  for (int st = 0; st < 4; ++st) {
-    const int hb = 7 - 2 * st, g = kk >> (hb - 1);
-    wa[st] = ar.tw(tw, (row << (7 - hb)) | g, N >> (hb + 1));
-    wb[st] = ar.tw(tw, (row << (8 - hb)) | (2 * g), N >> hb);
-    wc[st] = ar.tw(tw, (row << (8 - hb)) | (2 * g + 1), N >> hb);
-  }
   const u64* mid = mid_row_s(io, job, c, l, b) + (row << 8);
   typename A::T x[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) x[i] = from_bits<typename A::T>(mid[kk + 64 * i]);
-  u64* lr = lds + rr * 256;
-#pragma unroll
-  for (int st = 0; st < 4; ++st) {
-    const int hb = 7 - 2 * st, lb = hb - 1;
-    const int e0 = ins2(kk, lb), e1 = e0 + (1 << lb), e2 = e0 + (1 << hb), e3 = e2 + (1 << lb);
-    if (st > 0) {
-      x[0] = from_bits<typename A::T>(lr[e0]);
-      x[1] = from_bits<typename A::T>(lr[e1]);
-      x[2] = from_bits<typename A::T>(lr[e2]);
-      x[3] = from_bits<typename A::T>(lr[e3]);
-    }
-    ct4(ar, x, wa[st], wb[st], wc[st]);
-    if (st == 1)
-      for (int i = 0; i < 4; ++i) x[i] = ar.reduce_round(x[i]);
-    if (st < 3) {  // (a thread writes back only the words it read: one barrier per step)
-      lr[e0] = to_bits(x[0]);
-      lr[e1] = to_bits(x[1]);
-      lr[e2] = to_bits(x[2]);
-      lr[e3] = to_bits(x[3]);
-      __syncthreads();
-    }
-  }
+  fwd_rows4_core<A, LOGN>(x, row, kk, ar, tw, lds + rr * 256);
   // the last step's elements: columns 4kk .. 4kk + 3
   u64* dst = row_ptr(io.dst, c, l, b) + (row << 8) + 4 * kk;
   u64 o[4];
@@ -879,6 +849,10 @@ int launch2s(const NttIO& io, const DeviceTables* tb, bool inverse, bool rows_on
     hipLaunchKernelGGL((ntt2s_fwd_cols<LOGN, NTT_PRO_RESCALE>), ga, ba, 0, st, io, tb);
   else
     return -1;
+  if (io.cols_only) {  // the rows pass runs in the consumer
+    if (io.epi != NTT_EPI_STORE) return -1;
+    return 0;
+  }
   if (io.epi == NTT_EPI_STORE)
     hipLaunchKernelGGL((ntt2s_fwd_rows<LOGN, NTT_EPI_STORE>), gb, bb, 0, st, io, tb);
   else if (io.epi == NTT_EPI_SUBSCALE)

@@ -32,6 +32,45 @@ __device__ __forceinline__ void gs4(const A& ar, typename A::T (&x)[4], const ty
   ar.gs(x[1], x[3], wc, red_hi);
 }
 
+// the forward rows pass (the second pass of the two-pass NTT, ntt2s.hip) of
+// one 256-element row: x holds the intermediate's elements kk + 64 i on entry
+// and the last step's elements 4 kk .. 4 kk + 3 (lazy range) on return; lr is
+// the row's 256 words of LDS (one barrier per step but the last)
+template <class A, int LOGN>
+__device__ __forceinline__ void fwd_rows4_core(typename A::T (&x)[4], int row, int kk, const A& ar,
+                                               __amdgpu_buffer_rsrc_t tw, u64* lr) {
+  constexpr int N = 1 << LOGN;
+  typename A::W wa[4], wb[4], wc[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int hb = 7 - 2 * st, g = kk >> (hb - 1);
+    wa[st] = ar.tw(tw, (row << (7 - hb)) | g, N >> (hb + 1));
+    wb[st] = ar.tw(tw, (row << (8 - hb)) | (2 * g), N >> hb);
+    wc[st] = ar.tw(tw, (row << (8 - hb)) | (2 * g + 1), N >> hb);
+  }
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int hb = 7 - 2 * st, lb = hb - 1;
+    const int e0 = ins2(kk, lb), e1 = e0 + (1 << lb), e2 = e0 + (1 << hb), e3 = e2 + (1 << lb);
+    if (st > 0) {
+      x[0] = from_bits<typename A::T>(lr[e0]);
+      x[1] = from_bits<typename A::T>(lr[e1]);
+      x[2] = from_bits<typename A::T>(lr[e2]);
+      x[3] = from_bits<typename A::T>(lr[e3]);
+    }
+    ct4(ar, x, wa[st], wb[st], wc[st]);
+    if (st == 1)
+      for (int i = 0; i < 4; ++i) x[i] = ar.reduce_round(x[i]);
+    if (st < 3) {  // (a thread writes back only the words it read: one barrier per step)
+      lr[e0] = to_bits(x[0]);
+      lr[e1] = to_bits(x[1]);
+      lr[e2] = to_bits(x[2]);
+      lr[e3] = to_bits(x[3]);
+      __syncthreads();
+    }
+  }
+}
+
 // the inverse rows pass (the first pass of the two-pass INTT, ntt2s.hip) of
 // one 256-element row: thread kk holds elements 4kk .. 4kk + 3 in x, lr is
 // the row's 256 words of LDS (a thread writes back only the words it read, so
