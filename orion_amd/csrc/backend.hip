@@ -1782,7 +1782,7 @@ struct Context {
   // INTT's rows pass when the ModDown takes the fused latency path
   int mac_rows = getenv("ORION_MAC_ROWS") ? atoi(getenv("ORION_MAC_ROWS")) : 1;
   // 1: ... and runs the decomposition NTT's forward rows pass itself
-  int mac_fwd_rows = getenv("ORION_MAC_FWD_ROWS") ? atoi(getenv("ORION_MAC_FWD_ROWS")) : 0;
+  int mac_fwd_rows = getenv("ORION_MAC_FWD_ROWS") ? atoi(getenv("ORION_MAC_FWD_ROWS")) : 1;
   // 1: lt_bsgs / lt_giant take their workgroups in XCD-aware order (every
   // coefficient block's diagonals and keys read into one XCD's L2)
   int lt_xcd = getenv("ORION_LT_XCD") ? atoi(getenv("ORION_LT_XCD")) : 1;
