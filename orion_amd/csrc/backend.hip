@@ -160,8 +160,10 @@ class DevicePool {
   // device bytes held by the pools (handed out + cached), their peak,
   // hipMalloc calls, cache trims after a failed hipMalloc
   static std::vector<DevicePool*>& registry() {
-    static std::vector<DevicePool*> r;
-    return r;
+    // never destroyed: contexts held in namespace-scope statics are torn down
+    // at library unload, possibly after a function-local static would be
+    static auto* r = new std::vector<DevicePool*>();
+    return *r;
   }
   static double* stats() {
     static double st[4] = {0, 0, 0, 0};
