@@ -558,8 +558,10 @@ def main():
             tj = json.load(f)
         # HBM bytes per algorithmic byte of the NTT launches, from the committed
         # rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/pmc_summary.py)
+        # (the solo window's ratio when the profile has one: the roofline's own step)
         if tj.get("workload") == args.workload and tj.get("batch") == args.batch and n_launch:
-            traffic = round(tj["hbm_bytes_per_algorithmic_byte"] * n_bytes / n_launch)
+            r = tj.get("hbm_bytes_per_algorithmic_byte_solo") or tj["hbm_bytes_per_algorithmic_byte"]
+            traffic = round(r * n_bytes / n_launch)
 
     valu = None
     vfile = os.path.join(ROOT, "profiles", "valu_roofline.json")

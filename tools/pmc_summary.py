@@ -86,6 +86,7 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
     N = 1 << logn
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     ntt_alg = ntt_fetch = ntt_write = 0.0
+    solo_alg = solo_fetch = solo_write = 0.0
     def ntt_log(name):
         """The pass's NTT calls in order (bench.py run with ORION_NTT_LOG):
         (dispatches, jobs, subtract-and-scale epilogue); marker lines skipped."""
@@ -168,16 +169,24 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
         if log is None:
             continue
         cnt = "FETCH_SIZE" if name == "pmc_fetch" else "WRITE_SIZE"
+        sw = log_window(name, "solo")  # the single-pipeline step the bench's roofline is taken on
         for call, drs, alg, jobs in priced(order, log):
             if jobs < 64:
                 continue
             v = sum(float(r["Counter_Value"]) for r in drs if r["Counter_Name"] == cnt)
+            solo = sw is not None and sw[0] <= call < sw[1]
             if cnt == "FETCH_SIZE":
                 ntt_fetch += 2 * v * 1024  # gfx950 counts half the bytes of wide reads
                 ntt_alg += alg or 0.0
+                if solo:
+                    solo_fetch += 2 * v * 1024
+                    solo_alg += alg or 0.0
             else:
                 ntt_write += v * 1024
+                if solo:
+                    solo_write += v * 1024
     ratio = (ntt_fetch + ntt_write) / ntt_alg if ntt_alg else None
+    ratio_solo = (solo_fetch + solo_write) / solo_alg if solo_alg else None
     # the batched NTT calls of the kernel trace, counted the way bench.py's HIP
     # events count them: one call = one one-pass dispatch or one two-pass pair,
     # duration = the dispatches' summed time, priced with the logged
@@ -298,7 +307,8 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
             json.dump({"tag": tag, "workload": workload, "batch": batch,
                        "definition": "valu_busy = sum SQ_ACTIVE_INST_VALU*4 / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs)",
                        "kernels": valu}, f, indent=1)
-    summary = {"tag": tag, "ntt_hbm_bytes_per_algorithmic_byte": ratio, "ntt_trace_batched": trace,
+    summary = {"tag": tag, "ntt_hbm_bytes_per_algorithmic_byte": ratio,
+               "ntt_hbm_bytes_per_algorithmic_byte_solo": ratio_solo, "ntt_trace_batched": trace,
                "ntt_classes": dict(sorted(classes.items(), key=lambda kv: -kv[1]["us"])), "valu": valu,
                "ntt_fetch_bytes_per_algorithmic_byte": ntt_fetch / ntt_alg if ntt_alg else None,
                "kernels": {k: dict(v) for k, v in per.items()}}
@@ -307,7 +317,9 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
     if ratio and not resnet:
         with open(os.path.join(out, "ntt_traffic.json"), "w") as f:
             json.dump({"tag": tag, "workload": workload, "batch": batch,
-                       "hbm_bytes_per_algorithmic_byte": round(ratio, 4)}, f, indent=1)
+                       "hbm_bytes_per_algorithmic_byte": round(ratio, 4),
+                       "hbm_bytes_per_algorithmic_byte_solo": round(ratio_solo, 4) if ratio_solo else None},
+                      f, indent=1)
     print(json.dumps({"tag": tag, "ntt_hbm_bytes_per_algorithmic_byte": ratio, "ntt_trace_batched": trace}))
 
 
