@@ -267,7 +267,6 @@ struct LtBabies {  // the baby steps of register slots [s0, s0 + nb) of one lt_b
   int nb, s0, beta, K, level, L;
   u64 pq[ORION_MAXLIMB], pqs[ORION_MAXLIMB];  // P mod q_l and Shoup companion (0 on the P limbs)
   int xcd;  // 1: XCD-aware block order (lt_xcd_decode)
-  int gsplit;  // > 1: grid x = images x gsplit, each block takes 1/gsplit of the giants (set by the launcher)
 };
 struct LtGiants {  // the nonzero giant steps of one lt_giant launch
   const u64* key[ORION_MAXGROUP];

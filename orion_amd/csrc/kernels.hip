@@ -520,23 +520,17 @@ __device__ __forceinline__ void lt_xcd_decode(int& x, int& y, int& z) {
 // coefficient in registers and loops over the giants: the rotations never
 // touch HBM, and every diagonal (shared by the batch; the image index is the
 // fastest grid dimension) is read from L2.
-template <int MB, bool SPLIT = false>
+template <int MB>
 __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const LimbSet& D, const LimbSet& ct,
                                              const LtBabies& Bb, const LtPlan* __restrict__ P, int g0, int g1,
                                              int accumulate, const LimbSet& ptl, const DeviceTables* __restrict__ tb,
                                              int N, int z0) {
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   if (Bb.xcd) lt_xcd_decode(bx, by, bz);
-  // giant split (small batches): part `bx % S` of the image's blocks rebuilds
-  // the babies and takes giants [ga, gb); outputs stay indexed from g0
-  int bi = bx, ga = g0, gb = g1;
-  if constexpr (SPLIT) {
-    const int S = Bb.gsplit, span = (g1 - g0 + S - 1) / S;
-    bi = bx / S, ga = g0 + (bx % S) * span, gb = min(g1, ga + span);
-  }
+  const int bi = bx;
   const int n = by * blockDim.x + threadIdx.x;
   const int l = z0 + bz;
-  if (n >= N || (SPLIT && ga >= gb)) return;
+  if (n >= N) return;
   const int m = arg_byte(t0.mod, l);
   const ModConst mc = tb->mc[m];
   const bool isq = l <= Bb.level;
@@ -584,7 +578,7 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
     // the giant loop instantiated with and without accumulation (uniform)
     auto giants = [&](auto acc_tag) {
       constexpr bool ACC = decltype(acc_tag)::value;
-      for (int g = ga; g < gb; ++g) {
+      for (int g = g0; g < g1; ++g) {
         const unsigned long long mask = P->mask[g] >> Bb.s0;
         u64 r0 = 0, r1 = 0;
         if (ACC) {
@@ -630,7 +624,7 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
 #pragma unroll
       for (int s = 0; s < MB; ++s) x0[s] = split30(x0[s]), x1[s] = split30(x1[s]);
     }
-    for (int g = ga; g < gb; ++g) {
+    for (int g = g0; g < g1; ++g) {
       const unsigned long long mask = P->mask[g] >> Bb.s0;
       u64 r0 = 0, r1 = 0;
       if (accumulate) {
@@ -667,7 +661,7 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
   }
   // moduli of at most 60 bits: 8 products per reduction (mac_reduce8)
   const bool acc8 = LT_INT_ACC8 && mc.bar_k <= 60;
-  for (int g = ga; g < gb; ++g) {
+  for (int g = g0; g < g1; ++g) {
     const unsigned long long mask = P->mask[g] >> Bb.s0;
     u64 r0 = 0, r1 = 0;
     if (accumulate) {
@@ -704,11 +698,6 @@ lt_bsgs_kernel8(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb, cons
                 int g1, int accumulate, LimbSet ptl, const DeviceTables* __restrict__ tb, int N, int z0) {
   lt_bsgs_body<8>(t0, t1, D, ct, Bb, P, g0, g1, accumulate, ptl, tb, N, z0);
 }
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LT_WAVES8)))
-lt_bsgs_kernel8s(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb, const LtPlan* __restrict__ P, int g0,
-                 int g1, int accumulate, LimbSet ptl, const DeviceTables* __restrict__ tb, int N, int z0) {
-  lt_bsgs_body<8, true>(t0, t1, D, ct, Bb, P, g0, g1, accumulate, ptl, tb, N, z0);
-}
 __global__ void __launch_bounds__(256)
 lt_bsgs_kernel16(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb, const LtPlan* __restrict__ P, int g0,
                  int g1, int accumulate, LimbSet ptl, const DeviceTables* __restrict__ tb, int N, int z0) {
@@ -723,19 +712,14 @@ lt_bsgs_kernel16(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb, con
 // Each thread takes one coefficient of IB images: the automorphism index, the
 // key words and every pointer step are shared by the IB images, so the key
 // reads from L2 and the scalar address work per product drop IB-fold.
-// GS > 1 (small batches, where each thread's chain of giants -- one round
-// trip per giant -- sets the time): GS groups of 256 threads per block take
-// every GS-th giant of the same coefficients, and group 0 sums the partial
-// results from LDS.
-template <int IB, bool ROWS, int GS = 1>
-__global__ void __launch_bounds__(256 * GS) lt_giant_kernel(LimbSet acc, LimbSet D, LimbSet own, LimbSet t0, LimbSet z,
-                                                            LtGiants G, const DeviceTables* __restrict__ tb, int N) {
+template <int IB, bool ROWS>
+__global__ void __launch_bounds__(256) lt_giant_kernel(LimbSet acc, LimbSet D, LimbSet own, LimbSet t0, LimbSet z,
+                                                       LtGiants G, const DeviceTables* __restrict__ tb, int N) {
   constexpr int CH = LT_GIANT_CH > 0 ? LT_GIANT_CH : (IB >= 4 ? 2 : 4);  // digits per load chunk
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   if (G.xcd) lt_xcd_decode(bx, by, bz);
   const int b0 = bx * IB;
-  const int grp = GS > 1 ? (int)threadIdx.x / 256 : 0;  // (wave-uniform)
-  const int n = by * 256 + (int)threadIdx.x % 256;
+  const int n = by * blockDim.x + threadIdx.x;
   const int l = bz;
   if (n >= N) return;
   const int nb = acc.nbatch - b0 < IB ? acc.nbatch - b0 : IB;  // uniform
@@ -757,10 +741,10 @@ __global__ void __launch_bounds__(256 * GS) lt_giant_kernel(LimbSet acc, LimbSet
       for (int b = 0; b < IB; ++b) mac_zero(a0[b]), mac_zero(a1[b]);
     }
     int cnt = 0;
-    int jn = grp < G.ng ? (int)G.idx[grp][n] : 0;
-    for (int g = grp; g < G.ng; g += GS) {
+    int jn = G.ng > 0 ? (int)G.idx[0][n] : 0;
+    for (int g = 0; g < G.ng; ++g) {
       const int j = jn;
-      if (g + GS < G.ng) jn = G.idx[g + GS][n];  // prefetch the next giant's index
+      if (g + 1 < G.ng) jn = G.idx[g + 1][n];  // prefetch the next giant's index
       const int klvl = G.klvl[g];
       const long long kstride = (long long)(klvl + 1 + G.K) * N;
       const u64* kp = G.key[g] + (long long)key_pos(m, G.L, klvl) * N + j;
@@ -837,31 +821,9 @@ __global__ void __launch_bounds__(256 * GS) lt_giant_kernel(LimbSet acc, LimbSet
   // of once per giant (the Barrett reduction is ~40 VALU ops per component)
   if (LT_GIANT_ACC && mc.bar_k <= 52) giants(std::true_type{});  // block-uniform
   else giants(std::false_type{});
-  if constexpr (GS > 1) {
-    __shared__ u64 red[(GS - 1) * 2 * IB * 256];
-    const int tt = (int)threadIdx.x % 256;
-    if (grp > 0) {
-#pragma unroll
-      for (int b = 0; b < IB; ++b)
-        if (b < nb) red[((grp - 1) * 2 * IB + 2 * b) * 256 + tt] = r0[b], red[((grp - 1) * 2 * IB + 2 * b + 1) * 256 + tt] = r1[b];
-    }
-    __syncthreads();
-    if (grp > 0) {
-      if (!(ROWS && l >= G.rows_from)) return;  // (block-uniform) only the rows tail needs every group
-    } else {
-#pragma unroll
-      for (int k = 0; k < GS - 1; ++k)
-#pragma unroll
-        for (int b = 0; b < IB; ++b)
-          if (b < nb) {
-            r0[b] = add_mod(r0[b], red[(k * 2 * IB + 2 * b) * 256 + tt], mc.q);
-            r1[b] = add_mod(r1[b], red[(k * 2 * IB + 2 * b + 1) * 256 + tt], mc.q);
-          }
-    }
-  }
 #pragma unroll
   for (int b = 0; b < IB; ++b) {
-    if (b >= nb || grp > 0) break;
+    if (b >= nb) break;
     u64 x0 = r0[b], x1 = r1[b];
     if (G.has_zero) {
       x0 = add_mod(x0, z.p[row_off(z, 0, l, b0 + b) + n], mc.q);
@@ -876,19 +838,16 @@ __global__ void __launch_bounds__(256 * GS) lt_giant_kernel(LimbSet acc, LimbSet
       // time, thread (rr, kk) runs the radix-4 inverse rows steps on elements
       // 4 kk .. 4 kk + 3 of row q0 + rr and stores the INTT's intermediate in
       // place of the row.  A group past the last row works on a spare LDS row
-      // of its own and stores nothing, so every thread keeps the barriers
-      // (with GS groups, 4 GS rows per round; group 0 holds the sums).
-      constexpr int NR = 2 * IB > 4 * GS ? 2 * IB : 4 * GS;
+      // of its own and stores nothing, so every thread keeps the barriers.
+      constexpr int NR = 2 * IB > 4 ? 2 * IB : 4;
       __shared__ u64 lds[NR * 256];
       const int t = threadIdx.x;
-      if (grp == 0) {
 #pragma unroll
-        for (int b = 0; b < IB; ++b)
-          if (b < nb) lds[(2 * b) * 256 + t] = r0[b], lds[(2 * b + 1) * 256 + t] = r1[b];
-      }
+      for (int b = 0; b < IB; ++b)
+        if (b < nb) lds[(2 * b) * 256 + t] = r0[b], lds[(2 * b + 1) * 256 + t] = r1[b];
       __syncthreads();
       const int rr = t >> 6, kk = t & 63;
-      for (int q0 = 0; q0 < 2 * nb; q0 += 4 * GS) {  // (uniform)
+      for (int q0 = 0; q0 < 2 * nb; q0 += 4) {  // (uniform)
         const int q = q0 + rr;
         const bool live = q < 2 * nb;
         u64* const lr = lds + q * 256;
@@ -913,7 +872,7 @@ __global__ void __launch_bounds__(256 * GS) lt_giant_kernel(LimbSet acc, LimbSet
   }
 #pragma unroll
   for (int b = 0; b < IB; ++b) {
-    if (b >= nb || grp > 0) break;
+    if (b >= nb) break;
     acc.p[row_off(acc, 0, l, b0 + b) + n] = r0[b];
     acc.p[row_off(acc, 1, l, b0 + b) + n] = r1[b];
   }
@@ -1027,28 +986,14 @@ int orion_launch_lt_bsgs(const LimbSet& t0, const LimbSet& t1, const LimbSet& D,
                          const LtBabies& Bb, const LtPlan* plan, int g0, int g1, int accumulate, const LimbSet& ptl,
                          const DeviceTables* tb, int N, hipStream_t st) {
   if (Bb.nb < 1 || Bb.nb > LT_MAXB || g1 <= g0) return -1;
-  // giant split: a launch of few blocks (small batches) is latency-bound on
-  // each thread's chain of giants (one diagonal round trip per giant), so the
-  // giants are spread over more blocks, each rebuilding the babies.
-  // ORION_LT_GSPLIT: 0 = auto (aim at 4096 blocks, at most 8 parts), n >= 1 = fixed
-  static const int gsplit_env = getenv("ORION_LT_GSPLIT") ? atoi(getenv("ORION_LT_GSPLIT")) : 0;
-  LtBabies bb = Bb;
-  {
-    const long long blocks = (long long)t0.nbatch * ((N + 255) / 256) * t0.nlimb;
-    int S = gsplit_env > 0 ? gsplit_env : (int)std::min<long long>(8, (4096 + blocks - 1) / blocks);
-    bb.gsplit = Bb.nb <= 8 ? std::max(1, std::min(S, g1 - g0)) : 1;  // (lt_bsgs_kernel16 does not split)
-  }
   auto launch = [&](int z0, int nz) {
     if (nz <= 0) return;
-    dim3 g(t0.nbatch * bb.gsplit, (N + 255) / 256, nz);
-    if (Bb.nb <= 8 && bb.gsplit > 1)
-      hipLaunchKernelGGL(lt_bsgs_kernel8s, g, dim3(256), 0, st, t0, t1, D, ct, bb, plan, g0, g1, accumulate, ptl, tb,
-                         N, z0);
-    else if (Bb.nb <= 8)
-      hipLaunchKernelGGL(lt_bsgs_kernel8, g, dim3(256), 0, st, t0, t1, D, ct, bb, plan, g0, g1, accumulate, ptl, tb,
+    dim3 g(t0.nbatch, (N + 255) / 256, nz);
+    if (Bb.nb <= 8)
+      hipLaunchKernelGGL(lt_bsgs_kernel8, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate, ptl, tb,
                          N, z0);
     else
-      hipLaunchKernelGGL(lt_bsgs_kernel16, g, dim3(256), 0, st, t0, t1, D, ct, bb, plan, g0, g1, accumulate, ptl, tb,
+      hipLaunchKernelGGL(lt_bsgs_kernel16, g, dim3(256), 0, st, t0, t1, D, ct, Bb, plan, g0, g1, accumulate, ptl, tb,
                          N, z0);
   };
   // ORION_LT_SPLIT=1 (timing diagnostics): three launches, limb 0, the middle
@@ -1068,28 +1013,9 @@ int orion_launch_lt_giant(const LimbSet& acc, const LimbSet& D, const LimbSet& o
                           const LimbSet& z, const LtGiants& G, const DeviceTables* tb, int N, hipStream_t st) {
   if (G.ng > ORION_MAXGROUP) return -1;
   constexpr int IB = LT_GIANT_IB;
-  if (G.rows_from > 0 && ((G.logN != 15 && G.logN != 16) || N != (1 << G.logN))) return -1;
-  // giant split for small batches (one image per block, GS groups of 256
-  // threads). ORION_LT_GIANT_SPLIT: 0 = auto (4 groups below 3 images), 1 = off, 2 or 4
-  static const int gs_env = getenv("ORION_LT_GIANT_SPLIT") ? atoi(getenv("ORION_LT_GIANT_SPLIT")) : 0;
-  const int gs = gs_env > 0 ? gs_env : (acc.nbatch <= 2 && G.ng >= 4 ? 4 : 1);
-  if (gs == 2 || gs == 4) {
-    dim3 g(acc.nbatch, (N + 255) / 256, acc.nlimb), blk(256 * gs);
-#define GIANT_SPLIT(GSV)                                                                                      \
-  if (G.rows_from > 0)                                                                                        \
-    hipLaunchKernelGGL((lt_giant_kernel<1, true, GSV>), g, blk, 0, st, acc, D, own, t0, z, G, tb, N);         \
-  else                                                                                                        \
-    hipLaunchKernelGGL((lt_giant_kernel<1, false, GSV>), g, blk, 0, st, acc, D, own, t0, z, G, tb, N);
-    if (gs == 2) {
-      GIANT_SPLIT(2)
-    } else {
-      GIANT_SPLIT(4)
-    }
-#undef GIANT_SPLIT
-    return 0;
-  }
   dim3 g((acc.nbatch + IB - 1) / IB, (N + 255) / 256, acc.nlimb);
   if (G.rows_from > 0) {
+    if ((G.logN != 15 && G.logN != 16) || N != (1 << G.logN)) return -1;
     hipLaunchKernelGGL((lt_giant_kernel<IB, true>), g, dim3(256), 0, st, acc, D, own, t0, z, G, tb, N);
     return 0;
   }
