@@ -246,28 +246,34 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
                  "frac_strict_summed": w_s / (summed * 1e-9) / 1e9 / 8000.0 if summed else None}
     # NTT time by launch class (kt pass): direction, kernel (one-pass / two-pass
     # pair), epilogue, prologue, integer-path share, jobs in multiples of CUs
-    classes = {}
+    # (all calls of >= 64 jobs; and the calls of the solo / timed windows alone)
+    classes, classes_solo, classes_timed = {}, {}, {}
     full = ntt_log_full("kt")
     if klog is not None and full is not None and len(full[0]) >= 6:
         for call, r, alg, jobs in priced(tr, klog):
             f = full[call]
-            if jobs < 64:
-                continue
             fam = {1: "1pass", 2: "2pass", 3: "2pass-s", 4: "rows-only"}.get(f[6]) if len(f) >= 7 else None
             fam = fam or ("1pass" if f[0] == 1 else "2pass")
             key = (f"{'inv' if f[3] else 'fwd'} {fam} "
                    f"{EPI_NAME.get(f[2], 'sub')} pro{f[4]} int{round(f[5] / f[1], 2)} jobs{f[1]}")
-            c = classes.setdefault(key, {"calls": 0, "us": 0.0, "bytes": 0.0, "strict_bytes": 0.0})
-            c["us"] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-            if alg is not None:
-                c["calls"] += 1
-                c["bytes"] += alg
-                c["strict_bytes"] += 16.0 * N * jobs
-        for c in classes.values():
-            c["GBps"] = round(c["bytes"] / (c["us"] * 1e-6) / 1e9, 1) if c["us"] else None
-            c["GBps_strict"] = round(c["strict_bytes"] / (c["us"] * 1e-6) / 1e9, 1) if c["us"] else None
-            c["us_per_call"] = round(c["us"] / max(c["calls"], 1), 1)
-            c["us"] = round(c["us"], 1)
+            dst = [classes] if jobs >= 64 else []
+            if swin and swin[0] <= call < swin[1]:
+                dst.append(classes_solo)
+            if win and win[0] <= call < win[1]:
+                dst.append(classes_timed)
+            for cl in dst:
+                c = cl.setdefault(key, {"calls": 0, "us": 0.0, "bytes": 0.0, "strict_bytes": 0.0})
+                c["us"] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+                if alg is not None:
+                    c["calls"] += 1
+                    c["bytes"] += alg
+                    c["strict_bytes"] += 16.0 * N * jobs
+        for cl in (classes, classes_solo, classes_timed):
+            for c in cl.values():
+                c["GBps"] = round(c["bytes"] / (c["us"] * 1e-6) / 1e9, 1) if c["us"] else None
+                c["GBps_strict"] = round(c["strict_bytes"] / (c["us"] * 1e-6) / 1e9, 1) if c["us"] else None
+                c["us_per_call"] = round(c["us"] / max(c["calls"], 1), 1)
+                c["us"] = round(c["us"], 1)
     trace = {"launches": n_l, "avg_launch_us": n_us / n_l if n_l else None,
              "algorithmic_bytes_per_launch": n_b / n_l if n_l else None,
              "strict_bytes_per_launch": n_s / n_l if n_l else None,
@@ -309,7 +315,9 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
                        "kernels": valu}, f, indent=1)
     summary = {"tag": tag, "ntt_hbm_bytes_per_algorithmic_byte": ratio,
                "ntt_hbm_bytes_per_algorithmic_byte_solo": ratio_solo, "ntt_trace_batched": trace,
-               "ntt_classes": dict(sorted(classes.items(), key=lambda kv: -kv[1]["us"])), "valu": valu,
+               "ntt_classes": dict(sorted(classes.items(), key=lambda kv: -kv[1]["us"])),
+               "ntt_classes_solo": dict(sorted(classes_solo.items(), key=lambda kv: -kv[1]["us"])),
+               "ntt_classes_timed": dict(sorted(classes_timed.items(), key=lambda kv: -kv[1]["us"])), "valu": valu,
                "ntt_fetch_bytes_per_algorithmic_byte": ntt_fetch / ntt_alg if ntt_alg else None,
                "kernels": {k: dict(v) for k, v in per.items()}}
     with open(os.path.join(out, f"{tag}_pmc_summary.json"), "w") as f:
