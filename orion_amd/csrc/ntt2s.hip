@@ -30,6 +30,10 @@ namespace {
 #ifndef NTT2S_RW
 #define NTT2S_RW 4
 #endif
+// 1: ntt2s_ifwd_cols_p fetches its forward twiddles before the INTT half
+#ifndef NTT2S_FWD_PREFETCH
+#define NTT2S_FWD_PREFETCH 0
+#endif
 template <int LOGN>
 struct S2 {
   static constexpr int R = LOGN - 8;            // row bits: the cols pass transforms 2^R-point columns
@@ -317,13 +321,14 @@ __device__ __forceinline__ void s_inv_cols_src2(const u64* m0, const u64* m1, co
 // no exchange between its inverse and forward halves.
 // ---------------------------------------------------------------------------
 // forward columns pass, radix 4: thread (cl, j), j < 2^(R-2)
+// the twiddles of thread row j's forward columns stages (wa/wb/wc per radix-4
+// step, wl for an odd last stage)
 template <class A, int LOGN>
-__device__ __forceinline__ void s_fwd_cols4_core(const NttIO& io, int job, int c, int l, int b, int tile,
-                                                 typename A::T (&x)[4], const A& ar, __amdgpu_buffer_rsrc_t tw,
-                                                 u64* lds, int t) {
-  constexpr int N = 1 << LOGN, R = S2<LOGN>::R, CW = S2<LOGN>::CW, NS = R / 2;
-  const int cl = t % CW, j = t / CW, col = tile * CW + cl;
-  typename A::W wa[NS], wb[NS], wc[NS], wl[2];
+__device__ __forceinline__ void s_fwd_cols4_tw(const A& ar, __amdgpu_buffer_rsrc_t tw, int j,
+                                               typename A::W (&wa)[S2<LOGN>::R / 2],
+                                               typename A::W (&wb)[S2<LOGN>::R / 2],
+                                               typename A::W (&wc)[S2<LOGN>::R / 2], typename A::W (&wl)[2]) {
+  constexpr int N = 1 << LOGN, R = S2<LOGN>::R, NS = R / 2;
 #pragma unroll
   for (int st = 0; st < NS; ++st) {
     const int hb = R - 1 - 2 * st, g = j >> (hb - 1);
@@ -332,6 +337,16 @@ __device__ __forceinline__ void s_fwd_cols4_core(const NttIO& io, int job, int c
     wc[st] = ar.tw(tw, 2 * g + 1, N >> (hb + 8));
   }
   if (R & 1) wl[0] = ar.tw(tw, 2 * j, N >> 9), wl[1] = ar.tw(tw, 2 * j + 1, N >> 9);
+}
+template <class A, int LOGN>
+__device__ __forceinline__ void s_fwd_cols4_run(const NttIO& io, int job, int c, int l, int b, int tile,
+                                                typename A::T (&x)[4], const A& ar,
+                                                const typename A::W (&wa)[S2<LOGN>::R / 2],
+                                                const typename A::W (&wb)[S2<LOGN>::R / 2],
+                                                const typename A::W (&wc)[S2<LOGN>::R / 2],
+                                                const typename A::W (&wl)[2], u64* lds, int t) {
+  constexpr int R = S2<LOGN>::R, CW = S2<LOGN>::CW, NS = R / 2;
+  const int cl = t % CW, j = t / CW, col = tile * CW + cl;
 #pragma unroll
   for (int st = 0; st < NS; ++st) {
     const int hb = R - 1 - 2 * st, lb = hb - 1;
@@ -362,6 +377,24 @@ __device__ __forceinline__ void s_fwd_cols4_core(const NttIO& io, int job, int c
   u64* mid = mid_row_s(io, job, c, l, b);
 #pragma unroll
   for (int i = 0; i < 4; ++i) mid[col + ((4 * j + i) << 8)] = to_bits(ar.reduce_round(x[i]));
+}
+template <class A, int LOGN>
+__device__ __forceinline__ void s_fwd_cols4_core(const NttIO& io, int job, int c, int l, int b, int tile,
+                                                 typename A::T (&x)[4], const A& ar, __amdgpu_buffer_rsrc_t tw,
+                                                 u64* lds, int t) {
+  constexpr int NS = S2<LOGN>::R / 2;
+  typename A::W wa[NS], wb[NS], wc[NS], wl[2];
+  s_fwd_cols4_tw<A, LOGN>(ar, tw, t / S2<LOGN>::CW, wa, wb, wc, wl);
+  s_fwd_cols4_run<A, LOGN>(io, job, c, l, b, tile, x, ar, wa, wb, wc, wl, lds, t);
+}
+// a twiddle word kept as two u64 (the float64 path's double in .x), so the
+// forward twiddles of either arithmetic can be fetched before the INTT half
+__device__ __forceinline__ ulonglong2 w_raw(double w) { return make_ulonglong2(__builtin_bit_cast(u64, w), 0); }
+__device__ __forceinline__ ulonglong2 w_raw(ulonglong2 w) { return w; }
+template <class A>
+__device__ __forceinline__ typename A::W w_of(ulonglong2 r) {
+  if constexpr (std::is_same_v<typename A::W, double>) return __builtin_bit_cast(double, r.x);
+  else return r;
 }
 template <class A, int LOGN, int PRO>
 __device__ __forceinline__ void s_fwd_cols4(const NttIO& io, int job, int c, int l, int b, int tile,
@@ -645,6 +678,26 @@ __global__ void __launch_bounds__(G * S2<LOGN>::CT4) ntt2s_ifwd_cols_p(NttIO io,
     T = io.bx + kt;
     ns = T->ns;
   }
+  const int mod = arg_byte(io.dst.mod, l);
+  const ModConst mc = tb->mc[mod];
+  // NTT2S_FWD_PREFETCH: the forward stages' twiddles are fetched before the
+  // INTT half, so their latency overlaps it (timing switch)
+  constexpr int NS = S2<LOGN>::R / 2;
+  [[maybe_unused]] ulonglong2 pw[3 * NS + 2];
+  if constexpr (NTT2S_FWD_PREFETCH) {
+    auto pre = [&](const auto& ar, __amdgpu_buffer_rsrc_t tw) {
+      using A = std::decay_t<decltype(ar)>;
+      typename A::W wa[NS], wb[NS], wc[NS], wl[2];
+      s_fwd_cols4_tw<A, LOGN>(ar, tw, t / S2<LOGN>::CW, wa, wb, wc, wl);
+#pragma unroll
+      for (int k = 0; k < NS; ++k) pw[k] = w_raw(wa[k]), pw[NS + k] = w_raw(wb[k]), pw[2 * NS + k] = w_raw(wc[k]);
+      if (S2<LOGN>::R & 1) pw[3 * NS] = w_raw(wl[0]), pw[3 * NS + 1] = w_raw(wl[1]);
+    };
+    if (mc.f64)
+      pre(F64Arith(mc), twr_s(tb->fwd_d[mod], 8 << LOGN));
+    else
+      pre(IntArith(mc), twr_s(tb->fwd[mod], 16 << LOGN));
+  }
   // phase 1: group s < ns finishes source s's INTT columns on this tile
   if (grp < ns) {
     const int ms = arg_byte(io.src.mod, sl0 + grp);
@@ -665,8 +718,6 @@ __global__ void __launch_bounds__(G * S2<LOGN>::CT4) ntt2s_ifwd_cols_p(NttIO io,
     idle_inv_cols4_barriers<LOGN>();
   }
   __syncthreads();  // sb complete; the group regions are free for the forward stages
-  const int mod = arg_byte(io.dst.mod, l);
-  const ModConst mc = tb->mc[mod];
   u64 o[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -686,7 +737,16 @@ __global__ void __launch_bounds__(G * S2<LOGN>::CT4) ntt2s_ifwd_cols_p(NttIO io,
     typename A::T x[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) x[i] = ar.from_u64(o[i]);
-    s_fwd_cols4_core<A, LOGN>(io, 0, c, l, b, tile, x, ar, tw, lds + grp * REG, t);
+    if constexpr (NTT2S_FWD_PREFETCH) {
+      typename A::W wa[NS], wb[NS], wc[NS], wl[2];
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+        wa[k] = w_of<A>(pw[k]), wb[k] = w_of<A>(pw[NS + k]), wc[k] = w_of<A>(pw[2 * NS + k]);
+      wl[0] = w_of<A>(pw[3 * NS]), wl[1] = w_of<A>(pw[3 * NS + 1]);
+      s_fwd_cols4_run<A, LOGN>(io, 0, c, l, b, tile, x, ar, wa, wb, wc, wl, lds + grp * REG, t);
+    } else {
+      s_fwd_cols4_core<A, LOGN>(io, 0, c, l, b, tile, x, ar, tw, lds + grp * REG, t);
+    }
   };
   if (mc.f64)
     fwd(F64Arith(mc), twr_s(tb->fwd_d[mod], 8 << LOGN));
