@@ -261,7 +261,7 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=device)
 
-    from orion_amd.replay import OrionStream
+    from orion_amd.replay import OrionStream, Pipelines
     lib_seed = 2024
     P = max(1, min(args.pipelines, args.batch))  # (a batch of one image runs on one pipeline)
     if args.batch % P:
@@ -294,87 +294,67 @@ def main():
             lib.OrionHipSynchronize()
 
         bundle_bytes = odist.broadcast_bundle(dist, lambda: lib.KeyBundleBytes(0), export, load, device)
-    # peer pipelines: copies of the keys (and the secret on rank 0), their own
-    # HIP streams, pools and handles, the same compiled transforms
-    peers = [st] + [OrionStream(args.workload, peer_of=st) for _ in range(P - 1)]
-    for p in peers[1:]:
-        p.compile(gen_keys=False)
     t_setup = time.perf_counter() - t_setup
 
-    # this rank's shard of synthetic images (MNIST-shaped, N(0,1), seed 42 + rank),
-    # batch / P images per pipeline
+    # this rank's shard of synthetic images (MNIST-shaped, N(0,1), seed 42 + rank)
     g = torch.Generator().manual_seed(42 + rank)
     imgs = torch.randn(args.batch, 1, 28, 28, generator=g).numpy()
     imgs[0] = st.reference_input().reshape(1, 28, 28)
     bp = args.batch // P
-    cts = [p.encrypt_batch(imgs[i * bp:(i + 1) * bp]) for i, p in enumerate(peers)]  # public-key encryption
-    ct = cts[0]
+    # P pipelines = P frontend threads, each running the unchanged op stream
+    # (forward() of the one compiled stream) on the batch/P images it encrypted
+    # itself; the library binds each thread to a context of its own (the
+    # scheme's keys and compiled transforms, its own HIP stream, pool and
+    # handles: OrionHipThreadPipelines), so their kernels overlap on the GPU
+    pipes = Pipelines(lib, P, device=local) if P > 1 else None
+    if pipes:
+        cts = pipes.run([(lambda i=i: st.encrypt_batch(imgs[i * bp:(i + 1) * bp])) for i in range(P)])
+    else:
+        cts = [st.encrypt_batch(imgs)]
+    # the whole batch on the scheme's own context (main thread): the
+    # single-pipeline timing and the per-kernel breakdown
+    ct_all = st.encrypt_batch(imgs) if P > 1 else cts[0]
     lib.OrionHipSynchronize()
 
     def step():
-        """one pass of the op stream over the GPU's batch: P pipelines' ops interleaved"""
+        """one pass of the op stream over the GPU's batch: P threads, one pipeline each"""
         if P == 1:
-            return [st.forward(ct)]
-        return OrionStream.forward_interleaved(list(zip(peers, cts)))
+            return [st.forward(cts[0])]
+        return pipes.run([(lambda c=c: st.forward(c)) for c in cts])
 
     def delete(outs):
-        for p, o in zip(peers, outs):
-            p.use()
-            lib.DeleteCiphertext(o)
-        st.use()
+        for o in outs:
+            lib.DeleteCiphertext(o)  # (a handle is deleted on its own context)
 
-    def profile(mask):
-        for p in peers:
-            p.use()
-            lib.OrionHipProfile(mask)
-        st.use()
-
-    def profile_reset():
-        for p in peers:
-            p.use()
-            lib.OrionHipProfileReset()
-        st.use()
-        lib.OrionHipProfileClock()
-
-    def profile_read():
-        tot = {}
-        for p in peers:
-            p.use()
-            for k, v in lib.profile_read().items():
-                t = tot.setdefault(k, dict(launches=0, ms=0.0, bytes=0.0, strict_bytes=0.0))
-                for f in t:
-                    t[f] += v[f]
-        st.use()
-        return tot
+    def timed(fn, steps):
+        """K steps of fn bracketed by barrier + synchronize; returns (seconds, outputs)"""
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        lib.OrionHipSynchronize()
+        t0 = time.perf_counter()
+        outs = [fn() for _ in range(steps)]
+        lib.OrionHipSynchronize()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, outs
 
     dump_maps("setup")
     stage("warmup")
-
     for _ in range(args.warmup):
         delete(step())
     lib.OrionHipSynchronize()
 
     stage("timed")
-    profile_reset()
-    profile(0b11)  # HIP events around the NTT launches only (the roofline kernel)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    lib.OrionHipSynchronize()
+    lib.OrionHipProfileReset()
+    lib.OrionHipProfileClock()
+    lib.OrionHipProfile(0b11)  # HIP events around the NTT launches only (the roofline kernel)
     lib.OrionHipLogMark("timed begin")  # (ORION_NTT_LOG: tools/pmc_summary.py cuts the trace to the timed steps)
-    t0 = time.perf_counter()
-    outs = []
-    for _ in range(args.steps):
-        outs.append(step())
-    lib.OrionHipSynchronize()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dt, outs = timed(step, args.steps)
     lib.OrionHipLogMark("timed end")
-    profile(0)
-    prof = profile_read()
+    lib.OrionHipProfile(0)
+    prof = lib.profile_read()
     ntt_union_ms = lib.profile_union(0b11)  # wall clock with an NTT (forward or inverse) of any pipeline running
     if dist:
-        dist.barrier()
         dt = odist.max_over_ranks(dist, dt, device)
 
     # correctness of the timed output: image 0 of every shard is the fixture's
@@ -405,14 +385,29 @@ def main():
         mae = max(maes)
     for o in outs:
         delete(o)
-    # one extra, fully profiled step (outside the timed region) for the per-kernel
-    # breakdown: the whole batch on ONE pipeline, so every kernel has the GPU to
-    # itself (with P pipelines the timed region's launches overlap each other)
-    ct_all = st.encrypt_batch(imgs) if P > 1 else ct
+
+    # the same K steps with the whole batch on ONE pipeline (the scheme's
+    # context, main thread): value_single_pipeline, and the roofline -- every
+    # NTT launch timed there has the GPU to itself (with P pipelines the
+    # launches of one overlap the other's kernels)
+    stage("timed single pipeline")
     if P > 1:
         lib.DeleteCiphertext(st.forward(ct_all))  # warm: this batch size's buffers
-        lib.OrionHipSynchronize()
-    profile_reset()
+    lib.OrionHipSynchronize()
+    lib.OrionHipProfileReset()
+    lib.OrionHipProfile(0b11)
+    lib.OrionHipLogMark("single begin")
+    dt1, outs1 = timed(lambda: st.forward(ct_all), args.steps)
+    lib.OrionHipLogMark("single end")
+    lib.OrionHipProfile(0)
+    prof1 = lib.profile_read()
+    if dist:
+        dt1 = odist.max_over_ranks(dist, dt1, device)
+    for o in outs1:
+        lib.DeleteCiphertext(o)
+    # one extra, fully profiled single-pipeline step (outside the timed
+    # regions) for the per-kernel breakdown
+    lib.OrionHipProfileReset()
     lib.OrionHipProfile(1)
     lib.OrionHipLogMark("solo begin")
     lib.DeleteCiphertext(st.forward(ct_all))
@@ -420,8 +415,6 @@ def main():
     lib.OrionHipLogMark("solo end")
     lib.OrionHipProfile(0)
     breakdown = lib.profile_read()
-    if P > 1:
-        lib.DeleteCiphertext(ct_all)
 
     client_ms, b1_ms, graph_step = None, None, None
     dump_maps("extras")
@@ -433,7 +426,6 @@ def main():
         dvals = torch.zeros(args.batch, st.slots, dtype=torch.float32, device=device)
         dvals[:, :imgs[0].size] = torch.from_numpy(imgs.reshape(args.batch, -1)).to(device)
         torch.cuda.synchronize()
-        st.use()
         ct_full = st.encrypt_batch(imgs)
         out_ct = st.forward(ct_full)  # the whole batch's output, on one context
         lib.DeleteCiphertext(ct_full)
@@ -493,13 +485,15 @@ def main():
         # the batched step as a hipGraph replay (reported beside the line; the
         # value above is the stream-launched step the NTT events are timed on)
         stage("extras: batched graph capture + replay")
-        gids = [p.capture(c) for p, c in zip(peers, cts)]  # one graph per pipeline, each on its stream
+        # one graph per pipeline, captured by its thread on its stream (one
+        # capture at a time); a launch runs on the stream of the context that
+        # captured the graph, whichever thread issues it
+        gids = ([pipes.run_one(i, lambda c=c: st.capture(c)) for i, c in enumerate(cts)] if pipes
+                else [st.capture(cts[0])])
 
         def launch_all():
-            for p, (gid, _) in zip(peers, gids):
-                p.use()
+            for gid, _ in gids:
                 lib.OrionHipGraphLaunch(gid)
-            st.use()
 
         launch_all()
         lib.OrionHipSynchronize()
@@ -510,43 +504,41 @@ def main():
         g_ms = (time.perf_counter() - t1) / args.steps * 1e3
         graph_step = {"ms_per_step": round(g_ms, 3), "images_per_s": round(args.batch / g_ms * 1e3, 3),
                       "graphs": P}
-        for p, (gid, g_out) in zip(peers, gids):
-            p.use()
+        for gid, g_out in gids:
             lib.OrionHipGraphDestroy(gid)
             lib.DeleteCiphertext(g_out)
-        st.use()
+    if pipes:
+        pipes.close()
 
     stage("report")
     images = args.batch * world * args.steps
     value = images / dt
-    ntt = [prof.get("ntt_fwd", {}), prof.get("ntt_inv", {})]
-    n_launch = sum(p.get("launches", 0) for p in ntt)
-    n_ms = sum(p.get("ms", 0.0) for p in ntt)
-    n_bytes = sum(p.get("bytes", 0.0) for p in ntt)  # fused model (epilogue operands/addends counted)
-    n_strict = sum(p.get("strict_bytes", 0.0) for p in ntt)  # 16 N per limb-transform
-    # with P pipelines the NTT launches of one overlap the other's kernels, so
-    # the bytes are divided by the wall-clock time during which at least one
-    # NTT ran (the union of the launch intervals; = the summed durations at P = 1)
+    value_single = args.batch * world * args.steps / dt1
+
+    def ntt_sums(pr):
+        ntt = [pr.get("ntt_fwd", {}), pr.get("ntt_inv", {})]
+        return (sum(p.get("launches", 0) for p in ntt), sum(p.get("ms", 0.0) for p in ntt),
+                sum(p.get("bytes", 0.0) for p in ntt),  # fused model (epilogue operands/addends counted)
+                sum(p.get("strict_bytes", 0.0) for p in ntt))  # 16 N per limb-transform
+    # the roofline: the single-pipeline timed region (every NTT launch with
+    # the GPU to itself; HIP events on the library stream the NTTs run on)
+    n_launch, n_ms, n_bytes, n_strict = ntt_sums(prof1)
     concurrent = None
     if P > 1:
-        # with P pipelines an NTT launch shares the GPU with the other pipelines'
-        # kernels, so per-launch durations describe the mix, not the kernel: the
-        # roofline (below) is taken over the profiled step of the whole batch on
-        # ONE pipeline; the timed region's own figures are reported beside it
+        # with P pipelines an NTT launch shares the GPU with the other
+        # pipelines' kernels, so its duration describes the mix, not the
+        # kernel: the P-pipeline timed region's own figures, beside the line.
+        # frac_union: the bytes over the wall-clock time at least one NTT ran
+        c_launch, c_ms, _, c_strict = ntt_sums(prof)
         concurrent = {"definition": "timed region, P pipelines: 16 N per limb-transform / the wall-clock union "
                                     "of the NTT launch intervals (frac_union), / the summed launch durations "
                                     "(frac_summed); NTTs overlap the other pipelines' kernels",
-                      "frac_union": round(n_strict / (ntt_union_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+                      "frac_union": round(c_strict / (ntt_union_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
                       if ntt_union_ms > 0 else None,
-                      "frac_summed": round(n_strict / (n_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if n_ms > 0 else None,
+                      "frac_summed": round(c_strict / (c_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if c_ms > 0 else None,
                       "ntt_union_ms_per_step": round(ntt_union_ms / args.steps, 3),
-                      "ntt_summed_launch_ms_per_step": round(n_ms / args.steps, 3),
-                      "launches": n_launch}
-        sn = [breakdown.get("ntt_fwd", {}), breakdown.get("ntt_inv", {})]
-        n_ms = sum(p.get("ms", 0.0) for p in sn)
-        n_strict = sum(p.get("strict_bytes", 0.0) for p in sn)
-        n_bytes = sum(p.get("bytes", 0.0) for p in sn)
-        n_launch = sum(p.get("launches", 0) for p in sn)
+                      "ntt_summed_launch_ms_per_step": round(c_ms / args.steps, 3),
+                      "launches": c_launch}
     achieved = (n_strict / (n_ms / 1e3)) / 1e9 if n_ms > 0 else 0.0
     achieved_fused = (n_bytes / (n_ms / 1e3)) / 1e9 if n_ms > 0 else 0.0
     total_prof_ms = sum(p["ms"] for p in breakdown.values())
@@ -589,6 +581,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "value_single_pipeline": round(value_single, 3),
+            "ms_per_step_single_pipeline": round(dt1 / args.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -600,17 +594,16 @@ def main():
                        "batch_per_gpu": args.batch, "global_batch": args.batch * world,
                        "parallelism": f"replicas x{world} (image shards), keys RCCL-broadcast"
                                       + (" (rehearsal: gloo, shared GPUs)" if rehearse else "")
-                                      + (f"; per GPU {P} concurrent pipelines of {args.batch // P} images "
-                                         "(peer contexts sharing the keys, ops interleaved on their HIP streams)"
+                                      + (f"; per GPU {P} frontend threads of {args.batch // P} images each, "
+                                         "each thread on a pipeline context of its own (the scheme's keys and "
+                                         "compiled transforms, its own HIP stream), kernels concurrent"
                                          if P > 1 else "")},
             "roofline": {"bound": "hbm", "kernel": "ntt (fwd+inv: one-pass, 1 limb per workgroup; two-pass for partial-round launches)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "definition": "strict (SURVEY 8d): 16 N bytes per limb-transform / the NTT launches' "
-                                       "HIP-event durations, "
-                                       + ("over the timed region" if P == 1 else
-                                          "over one profiled step of the whole batch on one pipeline (the "
-                                          "kernel with the GPU to itself; log window 'solo')"),
+                                       "HIP-event durations over the single-pipeline timed region (the whole "
+                                       "batch on one context: value_single_pipeline; log window 'single')",
                          "pipelines": P,
                          "concurrent": concurrent,
                          "achieved_fused": round(achieved_fused, 1),

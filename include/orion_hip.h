@@ -161,26 +161,48 @@ int OrionHipSetDevice(int device);
 void OrionHipSetSeed(unsigned long seed);                /* keygen / encryption PRNG seed */
 void OrionHipSetStream(void *hipStream);                  /* NULL = library-owned stream */
 void *OrionHipGetStream(void);
-/* peer pipelines: OrionHipPeerCreate makes a second context on the scheme's
- * chain with copies of its keys and its own stream, buffer pool and handle
- * heaps (returns its id; the scheme's context is 0); OrionHipPeerSelect(id)
- * makes every following call act on that context.  Ops issued to two
- * contexts alternately run concurrently on the GPU.  DeleteScheme removes
- * every peer. */
+/* Pipelines (thread-affine contexts).  The reference's scheme is a process
+ * singleton (orion/core/orion.py:323; Lattigo's global state, scheme.go:32);
+ * here each thread acts on one context of the scheme.  A pipeline is a context
+ * on the scheme's chain that shares the scheme's keys and reads its compiled
+ * objects (plaintexts, linear transforms, polynomials, bootstrappers), with
+ * its own HIP stream, buffer pool and handle range; calls acting on different
+ * contexts run concurrently (each holds only its own context's lock), so
+ * several threads each running the frontend's `net(ct)` overlap on the GPU.
+ *
+ * OrionHipThreadPipelines(n): n > 1 gives every thread other than the one that
+ * called NewScheme a pipeline of its own at its first call (up to n contexts,
+ * then shared round-robin); n <= 1 (default; or ORION_THREAD_PIPELINES=n in
+ * the environment) leaves every thread on the scheme's context.  Returns the
+ * previous setting.  OrionHipCurrentPipeline: the calling thread's context
+ * index (0 = the scheme's).  OrionHipPeerCreate makes a pipeline and returns
+ * its index without binding a thread; OrionHipPeerSelect(id) binds the
+ * calling thread to context id.  Handles are unique across contexts: a call
+ * naming another context's object orders its stream after that object's
+ * producer; deletes and metadata calls go to the handle's own context; an
+ * in-place op on another context's ciphertext is refused.  DeleteScheme
+ * removes every pipeline. */
+int OrionHipThreadPipelines(int n);
+int OrionHipCurrentPipeline(void);
 int OrionHipPeerCreate(void);
 int OrionHipPeerSelect(int id);
 int OrionHipPeerCount(void);
-/* Peer pipelines: the current context's stream waits (on the GPU) for the
- * work enqueued so far on context `peer`'s stream (an event recorded there).
+/* The calling thread's context's stream waits (on the GPU) for the work
+ * enqueued so far on context `peer`'s stream (an event recorded there).
  * A frontend uses it to start one pipeline behind another.  0 or -1. */
 int OrionHipStreamWaitPeer(int peer);
 
 /* Device-memory pools of the process (one per context: the scheme's, its
- * peers', the bootstrappers'): out[0] bytes held (handed out + cached),
- * out[1] their peak, out[2] hipMalloc calls, out[3] cache trims forced by a
- * failed hipMalloc (each trims every pool), out[4] bytes cached.  Writes
- * min(n, 5) values; returns 5. */
+ * pipelines', the bootstrappers'): out[0] bytes held (handed out + cached),
+ * out[1] their peak, out[2] hipMalloc calls, out[3] failed allocations that
+ * forced every pool to release its cache (then one retry), out[4] bytes
+ * cached; returns the number of fields. */
 int OrionHipPoolStats(double* out, int n);
+/* A cap on the bytes all pools hold together (0: none; also
+ * ORION_POOL_CAP_BYTES): an allocation past it takes the failed-hipMalloc
+ * path -- release every cache, retry once, else fail the call with "device
+ * memory exhausted".  Returns the previous cap. */
+double OrionHipPoolCap(double bytes);
 int OrionHipSynchronize(void); /* drains every context's stream */
 /* hipGraph capture of an op stream issued through this ABI: every call between
  * Begin and End is recorded into one graph (returned id), which Launch replays

@@ -139,6 +139,9 @@ SIGNATURES = {
     "OrionHipSetSeed": ([c_ulong], None),
     "OrionHipSetStream": ([c_void_p], None),
     "OrionHipGetStream": ([], c_void_p),
+    "OrionHipThreadPipelines": ([c_int], c_int),
+    "OrionHipCurrentPipeline": ([], c_int),
+    "OrionHipPoolCap": ([c_double], c_double),
     "OrionHipPeerCreate": ([], c_int),
     "OrionHipPeerSelect": ([c_int], c_int),
     "OrionHipPeerCount": ([], c_int),
@@ -396,9 +399,22 @@ class HipLibrary:
                   "OrionHipBootstrapExport")
         return out
 
+    def thread_pipelines(self, n):
+        """Thread-affine pipelines (OrionHipThreadPipelines): with n > 1 every
+        thread other than the scheme's gets a context of its own at its first
+        call -- the scheme's keys and compiled objects, its own stream, pool
+        and handles -- so threads each running the frontend's forward pass
+        overlap on the GPU.  Returns the previous setting."""
+        return int(self.lib.OrionHipThreadPipelines(int(n)))
+
+    def pool_cap(self, nbytes):
+        """Cap on the device bytes all pools hold (0: none); returns the previous cap."""
+        return float(self.lib.OrionHipPoolCap(float(nbytes)))
+
     def pool_stats(self):
         """Device-memory pools (OrionHipPoolStats): bytes held and their peak,
-        hipMalloc calls, trims after a failed hipMalloc, bytes cached."""
+        hipMalloc calls, failed allocations that forced a trim of every cache,
+        bytes cached."""
         v = (c_double * 5)()
         self.lib.OrionHipPoolStats(v, 5)
         return {"held_bytes": v[0], "peak_bytes": v[1], "hipmalloc_calls": int(v[2]), "trims": int(v[3]),

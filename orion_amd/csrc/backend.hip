@@ -9,12 +9,15 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <set>
+#include <shared_mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 #include <complex>
@@ -86,25 +89,53 @@ class DevicePool {
   bool poison_ = getenv("ORION_DEBUG_POISON") && atoi(getenv("ORION_DEBUG_POISON")) != 0;
 
  public:
+  // every pool of the process shares one lock: the pipelines' contexts run on
+  // threads of their own, a forced trim empties every pool, and a buffer can be
+  // released by another context's thread than the one that allocated it (keys
+  // and compiled objects are shared with the pipelines)
+  static std::recursive_mutex& mu() {
+    static auto* m = new std::recursive_mutex();
+    return *m;
+  }
+  // ORION_POOL_CAP_BYTES: the device bytes all pools together may hold; an
+  // allocation past it takes the failed-hipMalloc path (trim every pool's
+  // cache, retry once) -- the regression test of that path, and a way to run
+  // a workload inside a memory budget
+  static double& cap_ref() {
+    static double c = getenv("ORION_POOL_CAP_BYTES") ? atof(getenv("ORION_POOL_CAP_BYTES")) : 0;
+    return c;
+  }
+  static double cap_bytes() { return cap_ref(); }
   void* alloc(size_t bytes) {
+    std::lock_guard<std::recursive_mutex> lk(mu());
     void* p = nullptr;
     auto it = free_.find(bytes);
     if (it != free_.end() && !it->second.empty()) {
       p = it->second.back();
       it->second.pop_back();
     } else {
-      hipError_t e = hipMalloc(&p, bytes);
+      const bool over = cap_bytes() > 0 && stats()[0] + (double)bytes > cap_bytes();
+      hipError_t e = over ? hipErrorOutOfMemory : hipMalloc(&p, bytes);
       if (e != hipSuccess) {
         // release the caches of every pool on the device (the scheme's,
-        // its peers' and the bootstrappers' contexts) and retry -- not while
-        // capturing: trim synchronises.  The failed call's error is cleared:
-        // HIP keeps it as the thread's last error, and a later launch check
-        // (hipGetLastError) would report it
+        // its pipelines' and the bootstrappers' contexts) and retry -- not
+        // while capturing: trim synchronises.  The failed call's error is
+        // cleared: HIP keeps it as the thread's last error, and a later launch
+        // check (hipGetLastError) would report it
         (void)hipGetLastError();
         for (DevicePool* q : registry())
           if (q->tracking_) throw std::runtime_error("device memory exhausted during graph capture");
-        for (DevicePool* q : registry()) q->trim(true);
-        HIPCHK(hipMalloc(&p, bytes));
+        stats()[3] += 1;  // one forced trim per failed allocation, whatever the number of pools
+        for (DevicePool* q : registry()) q->trim();
+        if (cap_bytes() > 0 && stats()[0] + (double)bytes > cap_bytes())
+          throw std::runtime_error("device memory exhausted: " + std::to_string(bytes) + " more bytes exceed the pool cap (ORION_POOL_CAP_BYTES) with every cache released");
+        e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) {
+          (void)hipGetLastError();
+          throw std::runtime_error("device memory exhausted: hipMalloc of " + std::to_string(bytes) +
+                                   " bytes failed with every pool's cache released (" +
+                                   std::to_string((long long)stats()[0]) + " bytes held by live objects)");
+        }
       }
       stats()[2] += 1;
       held_ += bytes;
@@ -120,6 +151,7 @@ class DevicePool {
     return p;
   }
   void release(void* p, size_t bytes) {
+    std::lock_guard<std::recursive_mutex> lk(mu());
     if (pins_.count(p)) {
       parked_[p] = bytes;
       return;
@@ -136,6 +168,7 @@ class DevicePool {
   }
   // a capture that failed: buffers parked for it that no graph pins go back
   void unpark_unpinned(const std::vector<std::pair<void*, size_t>>& v) {
+    std::lock_guard<std::recursive_mutex> lk(mu());
     for (auto& pb : v) {
       if (pins_.count(pb.first)) continue;
       auto pk = parked_.find(pb.first);
@@ -145,20 +178,23 @@ class DevicePool {
       }
     }
   }
-  // forced: after a failed hipMalloc (counted in stats()[3])
-  void trim(bool forced = false) {
+  // free the cached (unused) buffers
+  void trim() {
+    std::lock_guard<std::recursive_mutex> lk(mu());
     hipDeviceSynchronize();
     for (auto& kv : free_)
       for (void* p : kv.second) hipFree(p), held_ -= kv.first, add_held(-(double)kv.first);
     free_.clear();
-    if (forced) stats()[3] += 1;
   }
-  DevicePool() { registry().push_back(this); }
+  DevicePool() {
+    std::lock_guard<std::recursive_mutex> lk(mu());
+    registry().push_back(this);
+  }
   DevicePool(const DevicePool&) = delete;
   DevicePool& operator=(const DevicePool&) = delete;
   // every pool of the process (one per context), and process-wide counters:
   // device bytes held by the pools (handed out + cached), their peak,
-  // hipMalloc calls, cache trims after a failed hipMalloc
+  // hipMalloc calls, failed allocations that forced a trim of every cache
   static std::vector<DevicePool*>& registry() {
     // never destroyed: contexts held in namespace-scope statics are torn down
     // at library unload, possibly after a function-local static would be
@@ -174,22 +210,26 @@ class DevicePool {
     if (stats()[0] > stats()[1]) stats()[1] = stats()[0];
   }
   size_t cached() const {
+    std::lock_guard<std::recursive_mutex> lk(mu());
     size_t c = 0;
     for (auto& kv : free_) c += kv.first * kv.second.size();
     return c;
   }
   // graph capture: record every buffer handed out until end_track()
   void begin_track() {
+    std::lock_guard<std::recursive_mutex> lk(mu());
     touched_.clear();
     tracking_ = true;
   }
   std::vector<std::pair<void*, size_t>> end_track() {
+    std::lock_guard<std::recursive_mutex> lk(mu());
     tracking_ = false;
     std::vector<std::pair<void*, size_t>> v(touched_.begin(), touched_.end());
     touched_.clear();
     return v;
   }
   void pin(const std::vector<std::pair<void*, size_t>>& v) {
+    std::lock_guard<std::recursive_mutex> lk(mu());
     for (auto& pb : v) {
       if (pins_[pb.first]++) continue;
       auto& fl = free_[pb.second];  // released during the capture: park it
@@ -203,6 +243,7 @@ class DevicePool {
     }
   }
   void unpin(const std::vector<std::pair<void*, size_t>>& v) {
+    std::lock_guard<std::recursive_mutex> lk(mu());
     for (auto& pb : v) {
       auto it = pins_.find(pb.first);
       if (it == pins_.end() || --it->second > 0) continue;
@@ -215,6 +256,7 @@ class DevicePool {
     }
   }
   ~DevicePool() {
+    std::lock_guard<std::recursive_mutex> lk(mu());
     for (auto& kv : parked_) free_[kv.second].push_back(kv.first);
     parked_.clear();
     trim();
@@ -259,6 +301,9 @@ struct Ciphertext {
   Poly poly;
   int level = 0;
   long double scale = 1;
+  // set when a deferred op that should have written this ciphertext failed:
+  // every later use of the handle reports it (deleting it stays possible)
+  std::string poison;
   // copy-on-write: handles made by RescaleNew share the rescaled input's
   // buffer (Lattigo returns a copy, evaluator.go:92-99); the first in-place op
   // on either one, while both are alive, copies it first (Context::inplace_ct)
@@ -303,10 +348,37 @@ struct LinTrans {
   ~LinTrans() = default;
 };
 
+// a handle's context: the scheme's context is 0, pipeline i holds the ids
+// [i << 20, (i + 1) << 20)
+enum { kCtxShift = 20, kMaxCtx = 64 };
+// birth stamps of pooled objects (HandlePool): a pipeline reading another
+// context's compiled object orders its stream after the object's producer only
+// when the object is younger than what it has already waited for
+static std::atomic<unsigned long long> g_birth{1};
+
 template <class T>
 class HandlePool {  // lowest-free-id reuse (minheap.go:46-64)
  public:
+  // another context's pool, by context index (nullptr: none); and the hook a
+  // foreign lookup runs: (owner index, the object's birth stamp, ciphertext?)
+  using Resolver = HandlePool<T>* (*)(int owner);
+  using Hook = void (*)(int owner, unsigned long long birth);
+  static Resolver& resolver() {
+    static Resolver r = nullptr;
+    return r;
+  }
+  static Hook& hook() {
+    static Hook h = nullptr;
+    return h;
+  }
+  // run on every object get() returns (a poisoned ciphertext throws)
+  using Check = void (*)(const T&);
+  static Check& check() {
+    static Check c = nullptr;
+    return c;
+  }
   int add(T&& v) {
+    std::lock_guard<std::mutex> lk(mu_);
     int id;
     if (!free_.empty()) {
       id = *free_.begin();
@@ -314,39 +386,92 @@ class HandlePool {  // lowest-free-id reuse (minheap.go:46-64)
     } else {
       id = next_++;
     }
-    map_[id] = std::make_unique<T>(std::move(v));
+    map_[id] = Entry{std::make_unique<T>(std::move(v)), g_birth.fetch_add(1)};
     if (born) born->insert(id);
     return id;
   }
   std::set<int>* born = nullptr;  // while set: ids handed out (graph capture)
+  // Handles are unique across the contexts of a scheme: an id of another
+  // context (a compiled plaintext or transform of the scheme read by a
+  // pipeline, a ciphertext handed from one thread to another) resolves to that
+  // context's object, after the hook has ordered this thread's stream after
+  // the object's producer
   T& get(int id) {
-    auto it = map_.find(id);
-    if (it == map_.end()) throw std::runtime_error("handle not found: " + std::to_string(id));
-    return *it->second;
+    const int own = id >> kCtxShift;
+    if (id >= 0 && own != (base_ >> kCtxShift)) {
+      HandlePool* o = resolver() ? resolver()(own) : nullptr;
+      if (!o || o == this) throw std::runtime_error("handle not found: " + std::to_string(id));
+      unsigned long long birth = 0;
+      T& v = o->get_local(id, &birth);
+      if (check()) check()(v);
+      if (hook()) hook()(own, birth);
+      return v;
+    }
+    T& v = get_local(id, nullptr);
+    if (check()) check()(v);
+    return v;
   }
-  bool has(int id) const { return map_.count(id) != 0; }
+  // a new stamp for an object changed in place (a transform's diagonals)
+  void touch(int id) {
+    const int own = id >> kCtxShift;
+    HandlePool* o = this;
+    if (id >= 0 && own != (base_ >> kCtxShift)) o = resolver() ? resolver()(own) : nullptr;
+    if (!o) throw std::runtime_error("handle not found: " + std::to_string(id));
+    std::lock_guard<std::mutex> lk(o->mu_);
+    auto it = o->map_.find(id);
+    if (it != o->map_.end()) it->second.birth = g_birth.fetch_add(1);
+  }
+  bool has(int id) const {
+    std::lock_guard<std::mutex> lk(mu_);
+    return map_.count(id) != 0;
+  }
+  // owner of id: this pool, or the pool of the context its id names
+  HandlePool* owner_pool(int id) {
+    const int own = id >> kCtxShift;
+    if (id < 0 || own == (base_ >> kCtxShift)) return this;
+    HandlePool* o = resolver() ? resolver()(own) : nullptr;
+    return o ? o : this;
+  }
   void del(int id) {
-    if (map_.erase(id)) free_.insert(id);
+    HandlePool* o = owner_pool(id);
+    std::lock_guard<std::mutex> lk(o->mu_);
+    if (o->map_.erase(id)) o->free_.insert(id);
   }
   void reset() {
+    std::lock_guard<std::mutex> lk(mu_);
     map_.clear();
     free_.clear();
     next_ = base_;
   }
-  // ids from base on (a peer context's handles live in a range of their own,
-  // so a handle passed to the wrong context is "not found", never another object)
+  // ids from base on (a pipeline's handles live in a range of their own)
   void set_base(int b) {
-    base_ = b;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      base_ = b;
+    }
     reset();
   }
   std::vector<int> live() const {
+    std::lock_guard<std::mutex> lk(mu_);
     std::vector<int> v;
     for (auto& kv : map_) v.push_back(kv.first);
     return v;
   }
 
  private:
-  std::map<int, std::unique_ptr<T>> map_;
+  struct Entry {
+    std::unique_ptr<T> obj;
+    unsigned long long birth = 0;
+  };
+  T& get_local(int id, unsigned long long* birth) {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = map_.find(id);
+    if (it == map_.end()) throw std::runtime_error("handle not found: " + std::to_string(id));
+    if (birth) *birth = it->second.birth;
+    return *it->second.obj;
+  }
+  mutable std::mutex mu_;
+  std::map<int, Entry> map_;
   std::set<int> free_;
   int base_ = 0, next_ = 0;
 };
@@ -372,6 +497,7 @@ struct ProfIv {
 };
 static hipEvent_t g_prof_ref = nullptr;
 static std::vector<ProfIv> g_prof_iv;
+static std::mutex g_prof_mu;  // g_prof_iv: every context's launches
 // ORION_NTT_LOG: one line per NTT call for tools/pmc_summary.py -- one
 // line-buffered file for the whole process, so the lines of every context
 // (peer pipelines) stay in call order, which is dispatch order
@@ -388,7 +514,18 @@ static FILE* ntt_log_file() {
 // ---------------------------------------------------------------------------
 // context
 // ---------------------------------------------------------------------------
+struct Context;
+static Context* scheme_ctx();  // the scheme's context (index 0), or nullptr
+
 struct Context {
+  // index in the scheme's registry (0: the scheme's context, > 0: a pipeline,
+  // -1: a bootstrapping context owned by another context); its device; the
+  // lock every C-ABI call acting on it holds
+  int index = -1, dev = 0;
+  std::recursive_mutex mu;
+  // per owner context: the birth stamp below which that context's objects are
+  // known complete on this context's stream (HandlePool::get's hook)
+  unsigned long long synced[kMaxCtx] = {0};
   int logN = 0, N = 0, L = 0, K = 0, dnum = 0, logScale = 0, h = 0;
   // ring (scheme.go:49-52): Standard Z[X]/(X^N + 1), N/2 complex slots, NthRoot
   // 2N; or ConjugateInvariant Z[X + X^-1]/(X^2N + 1) of degree N, N real
@@ -526,6 +663,7 @@ struct Context {
         float a0 = 0, a1 = 0;
         hipEventElapsedTime(&a0, g_prof_ref, r.e0);
         hipEventElapsedTime(&a1, g_prof_ref, r.e1);
+        std::lock_guard<std::mutex> lk(g_prof_mu);
         g_prof_iv.push_back(ProfIv{r.cat, a0, a1});
       }
       prof_launch[r.cat] += 1;
@@ -637,6 +775,13 @@ struct Context {
   // a ciphertext an op is about to modify in place; cow = false: the caller
   // replaces the whole buffer (no copy of a shared one is needed)
   Ciphertext& inplace_ct(int id, bool cow = true) {
+    // a buffer replaced here goes back to its owner's pool, which hands out
+    // buffers in its own stream's order only: another context's ciphertext is
+    // read, never changed
+    if (index >= 0 && id >= 0 && (id >> kCtxShift) != index)
+      throw std::runtime_error("in-place op on ciphertext " + std::to_string(id) + " of pipeline " +
+                               std::to_string(id >> kCtxShift) + " from pipeline " + std::to_string(index) +
+                               ": a ciphertext is changed only by the context (thread) that made it");
     Ciphertext& a = cts.get(id);
     if (capturing && !capture_born.count(id))
       throw std::runtime_error("in-place op on ciphertext " + std::to_string(id) +
@@ -1454,23 +1599,18 @@ struct Context {
     sk = secret_poly(s);
     have_sk = true;
   }
-  // copies of another context's keys (same chain) in this context's pool
+  // another context's keys (same chain), shared: the key polys are the same
+  // device buffers (read-only once made), the loaded keys' host copies the
+  // same host arrays
   void adopt_keys(const Context& o) {
-    if (o.mods != mods) throw std::runtime_error("peer context: another modulus chain");
+    if (o.mods != mods) throw std::runtime_error("pipeline context: another modulus chain");
     HIPCHK(hipStreamSynchronize(o.stream));
-    auto cp = [&](const Poly& src) {
-      Poly d = alloc(src.ncomp, src.nlimb, src.B);
-      HIPCHK(hipMemcpyAsync(d.ptr(), src.ptr(), (size_t)src.ncomp * src.nlimb * src.B * N * 8,
-                            hipMemcpyDeviceToDevice, stream));
-      return d;
-    };
-    if (o.have_sk) sk = cp(o.sk), have_sk = true;
-    if (o.have_pk) pk = cp(o.pk), have_pk = true;
-    if (o.have_rlk) rlk = cp(o.rlk), have_rlk = true;
-    for (auto& kv : o.gks) gks[kv.first] = EvKey{cp(kv.second.k), kv.second.level};
+    if (o.have_sk) sk = o.sk, have_sk = true;
+    if (o.have_pk) pk = o.pk, have_pk = true;
+    if (o.have_rlk) rlk = o.rlk, have_rlk = true;
+    gks = o.gks;
     key_hint = o.key_hint;
     gk_host = o.gk_host;
-    HIPCHK(hipStreamSynchronize(stream));
   }
   LimbSet full(const Poly& P, int c0, int nc) const { return ls(P, c0, nc, iota(0, L + K), iota(0, L + K)); }
 
@@ -1543,7 +1683,7 @@ struct Context {
   // LoadRotationKey's whole keys, for the ones it cut on the device
   struct HostKey {
     int level = 0;
-    std::vector<u64> words;  // [digit][2][level+1+K][N]
+    std::shared_ptr<const std::vector<u64>> words;  // [digit][2][level+1+K][N] (shared with the pipelines)
   };
   std::map<u64, HostKey> gk_host;
   int hinted_level(u64 g) const {
@@ -1555,12 +1695,29 @@ struct Context {
   void gen_galois(u64 g, int level) {
     auto have = gks.find(g);
     if (have != gks.end() && have->second.level >= level) return;
+    // a pipeline's keys are the scheme's: a key it lacks (made, loaded or
+    // raised to a higher level after the pipeline was created) is made by the
+    // scheme's context, with the scheme's randomness, and shared, so every
+    // context switches with the same key and a pipeline's output equals the
+    // scheme's bit for bit
+    Context* s = scheme_ctx();
+    if (index > 0 && s && s != this) {
+      no_capture("taking a Galois key from the scheme");
+      std::lock_guard<std::recursive_mutex> lk(s->mu);  // (a pipeline may wait on the scheme: index order)
+      s->gen_galois(g, level);
+      HIPCHK(hipStreamSynchronize(s->stream));
+      // the replaced key's buffer may return to the scheme's pool once this
+      // context lets go of it: this stream is done reading it first
+      if (have != gks.end()) HIPCHK(hipStreamSynchronize(stream));
+      gks[g] = s->gks.at(g);
+      return;
+    }
     auto hk = gk_host.find(g);
     if (hk != gk_host.end() && hk->second.level >= level) {  // a loaded key, cut at load: the whole key
       no_capture("uploading a loaded rotation key past its cut level");
       const int kl = hk->second.level, kb = (kl + 1 + K - 1) / K;
       Poly k = alloc(2 * kb, kl + 1 + K, 1);
-      upload(k, hk->second.words);
+      upload(k, *hk->second.words);
       gks[g] = EvKey{k, kl};
       gk_host.erase(hk);
       return;
@@ -2061,6 +2218,17 @@ struct Context {
     h2d(T.d_plan, plans.data(), nplan * sizeof(LtPlan));
     T.n_plan = nplan;
     T.plan_dirty = false;
+  }
+  // the device plans of every transform whose diagonals are all loaded (a
+  // pipeline reads the scheme's transforms and never builds their plans)
+  void build_dirty_plans() {
+    for (int id : lts.live()) {
+      LinTrans& T = lts.get(id);
+      if (!T.plan_dirty || T.giants.empty()) continue;
+      bool all = true;
+      for (int d : T.idx) all = all && T.diags.count(d & (slots - 1));
+      if (all) build_plan(T);
+    }
   }
 
   // BSGS linear transform (lintrans MultiplyByDiagMatrixBSGS restated; oracle_lt_bsgs).
@@ -2987,17 +3155,181 @@ struct Context {
   }
 };
 
-// the scheme's context ([0]) and its peer pipelines ([1..], OrionHipPeerCreate:
-// the same chain and keys, their own stream, pool and handles); g is the one
-// the C-ABI calls act on (OrionHipPeerSelect)
-static std::vector<std::unique_ptr<Context>> g_ctxs;
-static Context* g = nullptr;
-static std::recursive_mutex g_mu;
+// ---------------------------------------------------------------------------
+// the scheme's contexts: [0] the scheme's own, [1..] its pipelines
+// ---------------------------------------------------------------------------
+// A pipeline is a context on the scheme's chain that shares the scheme's keys
+// and reads the scheme's compiled objects (plaintexts, linear transforms,
+// polynomials), with its own HIP stream, buffer pool and handle range.  Each
+// thread acts on one context: the thread that made the scheme on the scheme's,
+// and, once OrionHipThreadPipelines(n > 1) is set (or ORION_THREAD_PIPELINES=n
+// is in the environment), every other thread on a pipeline of its own, made at
+// its first call (up to n contexts; further threads share them round-robin).
+// So several threads each running the unchanged frontend's `net(ct)` over their
+// own ciphertexts run their kernels concurrently on the GPU, each call holding
+// only its own context's lock.  Handles are unique across the contexts; calls
+// that only name a handle (deletes, metadata) go to the handle's context.
+//
+// Locks: g_reg (shared by every call, exclusive for NewScheme/DeleteScheme);
+// a context's mu for a call acting on it; a thread holding a pipeline's mu may
+// take the scheme's (keys, bootstrapping), never the other way round; the
+// handle pools' and device pools' locks are leaves.
+static std::unique_ptr<Context> g_slot[kMaxCtx];
+static std::atomic<int> g_nctx{0};
+static std::shared_mutex g_reg;
+static std::mutex g_create_mu;
+static std::atomic<unsigned long long> g_scheme_gen{1};
+static std::atomic<int> g_thread_pipes{getenv("ORION_THREAD_PIPELINES") ? atoi(getenv("ORION_THREAD_PIPELINES")) : 0};
+static std::atomic<unsigned> g_rr{0};
+static std::thread::id g_scheme_thread;
+static unsigned long g_seed = 0x0123456789abcdefull;
+struct ThreadBind {
+  Context* c = nullptr;
+  unsigned long long gen = 0;
+};
+static thread_local ThreadBind t_bind;
+static thread_local Context* t_act = nullptr;  // the context the running call acts on
+static thread_local int t_depth = 0;           // nesting of C-ABI calls (SubScalar -> AddScalar)
+static thread_local int t_dev = -1;            // this thread's HIP device, as last set here
+
+static Context* scheme_ctx() { return g_nctx.load() > 0 ? g_slot[0].get() : nullptr; }
+static Context* slot_ctx(int i) { return i >= 0 && i < g_nctx.load() ? g_slot[i].get() : nullptr; }
 
 static Context& ctx() {
-  if (!g) throw std::runtime_error("scheme not initialised: call NewScheme first");
-  return *g;
+  if (!t_act) throw std::runtime_error("scheme not initialised: call NewScheme first");
+  return *t_act;
 }
+
+// the caller's stream waits for everything queued on context `owner`'s stream
+static void wait_on(Context& me, Context& o) {
+  if (&me == &o) return;
+  hipEvent_t e;
+  HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(e, o.stream));
+  HIPCHK(hipStreamWaitEvent(me.stream, e, 0));
+  HIPCHK(hipEventDestroy(e));  // (released once the wait has completed)
+}
+// HandlePool hooks: a call reading another context's object orders its stream
+// after that object's producer.  A ciphertext (changed by the ops of its
+// context) always waits for its context's queued work; a compiled object
+// waits only when it is younger than what this context already waited for
+// (every object older than a pipeline was complete when it was made)
+static void foreign_order(int owner, unsigned long long birth, bool always) {
+  Context* me = t_act;
+  Context* o = slot_ctx(owner);
+  if (!me || !o || o == me) return;
+  if (!always && birth < me->synced[owner]) return;
+  if (me->capturing)
+    throw std::runtime_error("a captured op reads context " + std::to_string(owner) +
+                             "'s newer object: capture on the context that owns it, or run the stream once first");
+  const unsigned long long stamp = g_birth.load();
+  wait_on(*me, *o);
+  if (!always) me->synced[owner] = stamp;
+}
+static HandlePool<Ciphertext>* res_cts(int i) { Context* c = slot_ctx(i); return c ? &c->cts : nullptr; }
+static HandlePool<Plaintext>* res_pts(int i) { Context* c = slot_ctx(i); return c ? &c->pts : nullptr; }
+static HandlePool<LinTrans>* res_lts(int i) { Context* c = slot_ctx(i); return c ? &c->lts : nullptr; }
+static HandlePool<Context::PolyFn>* res_polys(int i) { Context* c = slot_ctx(i); return c ? &c->polys : nullptr; }
+static const bool g_hooks_set = [] {
+  HandlePool<Ciphertext>::resolver() = res_cts;
+  HandlePool<Plaintext>::resolver() = res_pts;
+  HandlePool<LinTrans>::resolver() = res_lts;
+  HandlePool<Context::PolyFn>::resolver() = res_polys;
+  HandlePool<Ciphertext>::hook() = [](int o, unsigned long long b) { foreign_order(o, b, true); };
+  HandlePool<Plaintext>::hook() = [](int o, unsigned long long b) { foreign_order(o, b, false); };
+  HandlePool<LinTrans>::hook() = [](int o, unsigned long long b) { foreign_order(o, b, false); };
+  HandlePool<Context::PolyFn>::hook() = [](int o, unsigned long long b) { foreign_order(o, b, false); };
+  HandlePool<Ciphertext>::check() = [](const Ciphertext& c) {
+    if (!c.poison.empty()) throw std::runtime_error(c.poison);
+  };
+  return true;
+}();
+
+// a new pipeline context (the caller holds no context lock)
+static Context* create_pipeline() {
+  std::lock_guard<std::mutex> lk(g_create_mu);
+  Context* s = scheme_ctx();
+  if (!s) throw std::runtime_error("scheme not initialised: call NewScheme first");
+  const int idx = g_nctx.load();
+  if (idx >= kMaxCtx) throw std::runtime_error("too many pipelines (" + std::to_string(kMaxCtx - 1) + " at most)");
+  std::lock_guard<std::recursive_mutex> sl(s->mu);  // the scheme's keys and transforms are read
+  if (t_dev != s->dev) {
+    HIPCHK(hipSetDevice(s->dev));
+    t_dev = s->dev;
+  }
+  // the scheme's transforms get their device plans now, so a pipeline only
+  // reads them; then every object born so far is complete once the queued
+  // work of every context has run
+  s->build_dirty_plans();
+  const unsigned long long stamp = g_birth.load();
+  for (int i = 0; i < idx; ++i) HIPCHK(hipStreamSynchronize(g_slot[i]->stream));
+  std::unique_ptr<Context> p(new Context());
+  p->index = idx;
+  p->dev = s->dev;
+  p->prng = Prng(g_seed ^ (0x9e3779b97f4a7c15ull * (u64)idx));
+  p->init_moduli(s->logN, s->mods, s->logQ_bits, s->logP_bits, s->logScale, s->h, s->ci);
+  p->adopt_keys(*s);
+  p->seed_encryption(g_seed + 0x9e3779b97f4a7c15ull * (u64)idx);
+  const int base = idx << kCtxShift;
+  p->pts.set_base(base), p->cts.set_base(base), p->lts.set_base(base), p->polys.set_base(base);
+  p->next_graph = base;
+  for (int j = 0; j < kMaxCtx; ++j) p->synced[j] = stamp;
+  Context* r = p.get();
+  g_slot[idx] = std::move(p);
+  g_nctx.store(idx + 1);
+  return r;
+}
+
+// the context the calling thread acts on (create: a thread's first call may
+// make its pipeline); nullptr without a scheme
+static Context* thread_ctx(bool create) {
+  Context* s = scheme_ctx();
+  if (!s) return nullptr;
+  const unsigned long long gen = g_scheme_gen.load();
+  if (t_bind.c && t_bind.gen == gen) return t_bind.c;
+  const int n = g_thread_pipes.load();
+  if (n <= 1 || std::this_thread::get_id() == g_scheme_thread) return s;
+  if (!create) return s;
+  Context* c = nullptr;
+  if (g_nctx.load() < n) {
+    c = create_pipeline();
+  } else {
+    const int np = g_nctx.load() - 1;
+    c = np > 0 ? g_slot[1 + (int)(g_rr.fetch_add(1) % (unsigned)np)].get() : s;
+  }
+  t_bind = ThreadBind{c, gen};
+  return c;
+}
+// the context of a handle (deletes and metadata go to the handle's own
+// context, whichever thread asks)
+static Context* handle_ctx(int id) {
+  Context* c = id >= 0 ? slot_ctx(id >> kCtxShift) : nullptr;
+  return c ? c : thread_ctx(false);
+}
+
+// one C-ABI call: the registry lock (outermost call only), the lock of the
+// context it acts on, and that context as the thread's acting one
+struct CallScope {
+  std::shared_lock<std::shared_mutex> rl;
+  std::unique_lock<std::recursive_mutex> cl;
+  Context* saved;
+  CallScope(bool reg = true) : saved(t_act) {
+    if (t_depth++ == 0 && reg) rl = std::shared_lock<std::shared_mutex>(g_reg);
+  }
+  void act(Context* c) {
+    if (!c) return;
+    cl = std::unique_lock<std::recursive_mutex>(c->mu);
+    t_act = c;
+    if (t_dev != c->dev) {
+      HIPCHK(hipSetDevice(c->dev));
+      t_dev = c->dev;
+    }
+  }
+  ~CallScope() {
+    t_act = saved;
+    --t_depth;
+  }
+};
 
 }  // namespace orion
 
@@ -3018,27 +3350,48 @@ static bool capture_ok(const char* fn) {
       "DeleteCiphertext", "DeletePlaintext", "SetCiphertextScale", "SetPlaintextScale", "GetCiphertextScale",
       "GetPlaintextScale", "GetCiphertextScaleF", "GetCiphertextLevel", "GetPlaintextLevel", "GetCiphertextSlots",
       "GetPlaintextSlots", "GetCiphertextDegree", "GetCiphertextBatch", "GetPlaintextBatch", "GetLiveCiphertexts",
-      "GetLivePlaintexts", "GetModuliChain", "GaloisElement", "OrionHipGraphEnd"};
+      "GetLivePlaintexts", "GetModuliChain", "GaloisElement", "OrionHipGraphEnd", "OrionHipGetStream",
+      "OrionHipCurrentPipeline"};
   return ok.count(fn) != 0;
 }
 // debugging switch ORION_DEBUG_SYNC=1: drain the library stream at the start
 // of every C-ABI call (separates an ordering race from an arithmetic fault)
 static const bool g_debug_sync = getenv("ORION_DEBUG_SYNC") && atoi(getenv("ORION_DEBUG_SYNC")) != 0;
 static void capture_guard(const char* fn) {
-  if (g && g->capturing && !capture_ok(fn))
+  Context* c = t_act;
+  if (c && c->capturing && !capture_ok(fn))
     throw std::runtime_error(std::string(fn) + " is not allowed while capturing a graph");
-  if (g_debug_sync && g && !g->capturing && g->stream) (void)hipStreamSynchronize(g->stream);
+  if (g_debug_sync && c && !c->capturing && c->stream) (void)hipStreamSynchronize(c->stream);
 }
 static int ct_ct_op(int i0, int i1, int op, bool inplace);
 // runs a deferred rotation (and the addition recorded after it) exactly as
-// the op-by-op calls would have (Context::Deferred)
+// the op-by-op calls would have (Context::Deferred).  If it fails, the
+// ciphertexts it should have written are poisoned: every later use of x
+// (which the AddCiphertext already reported as done) or r fails loudly with
+// this error, instead of reading a buffer that was never written
+static void poison_deferred(Context& c, const Context::Deferred& d, const char* what) {
+  const std::string msg = std::string("a deferred rotation by ") + std::to_string(d.k) + " failed (" + what +
+                          "): this ciphertext was never written";
+  for (int id : {d.r, d.kind == 2 ? d.x : -1}) {
+    if (id < 0) continue;
+    try {
+      c.cts.get(id).poison = msg;
+    } catch (const std::exception&) {
+    }
+  }
+}
 static void defer_flush() {
-  if (!g || !g->dfr.kind) return;
-  Context& c = *g;
+  if (!t_act || !t_act->dfr.kind) return;
+  Context& c = *t_act;
   const Context::Deferred d = c.dfr;
   c.dfr = Context::Deferred();
-  c.rotate_into(c.cts.get(d.x), d.k, c.cts.get(d.r));
-  if (d.kind == 2) ct_ct_op(d.x, d.r, EW_ADD, true);
+  try {
+    c.rotate_into(c.cts.get(d.x), d.k, c.cts.get(d.r));
+    if (d.kind == 2) ct_ct_op(d.x, d.r, EW_ADD, true);
+  } catch (const std::exception& e) {
+    poison_deferred(c, d, e.what());
+    throw;
+  }
 }
 // C-ABI calls that leave a pending rotation pending: host metadata reads
 // (the deferred result has its level, scale and batch already), error
@@ -3049,22 +3402,37 @@ static bool defer_keeps(const char* fn) {
       "AddCiphertext", "DeleteCiphertext", "DeletePlaintext", "GetCiphertextScale", "GetCiphertextScaleF",
       "GetCiphertextLevel", "GetCiphertextSlots", "GetCiphertextDegree", "GetCiphertextBatch", "GetPlaintextScale",
       "GetPlaintextLevel", "GetPlaintextSlots", "GetPlaintextBatch", "GetLiveCiphertexts", "GetLivePlaintexts",
-      "GetModuliChain", "GaloisElement", "OrionHipPeerSelect", "OrionHipPeerCount"};
+      "GetModuliChain", "GaloisElement", "OrionHipPeerSelect", "OrionHipPeerCount", "OrionHipGetStream",
+      "OrionHipCurrentPipeline"};
   return keep.count(fn) != 0;
 }
 static void defer_gate(const char* fn) {
-  if (!g || !g->dfr.kind) return;
-  if (!strcmp(fn, "NewScheme") || !strcmp(fn, "DeleteScheme")) {  // the scheme and its handles go away
-    g->dfr = Context::Deferred();
-    return;
-  }
+  if (!t_act || !t_act->dfr.kind) return;
   if (!defer_keeps(fn)) defer_flush();
 }
-#define API_BEGIN                                  \
-  std::lock_guard<std::recursive_mutex> lk_(g_mu); \
-  try {                                            \
-    capture_guard(__func__);                       \
+// a call acting on the calling thread's context
+#define API_BEGIN         \
+  CallScope cs_;          \
+  try {                   \
+    cs_.act(thread_ctx(true)); \
+    capture_guard(__func__); \
     defer_gate(__func__);
+// a call acting on the context of handle `id`
+#define API_BEGIN_HANDLE(id) \
+  CallScope cs_;             \
+  try {                      \
+    cs_.act(handle_ctx(id)); \
+    capture_guard(__func__); \
+    defer_gate(__func__);
+// a call acting on no context (or on several, one at a time)
+#define API_BEGIN_NOCTX \
+  CallScope cs_;        \
+  try {
+// NewScheme / DeleteScheme: every other call is kept out
+#define API_BEGIN_EXCL                                \
+  std::unique_lock<std::shared_mutex> xl_(g_reg);     \
+  CallScope cs_(false);                               \
+  try {
 // (a failed call's HIP error is read off here, so that it is reported once,
 // by this call, and not again by the next call's launch checks)
 #define API_END(errval)          \
@@ -3096,11 +3464,11 @@ const char* OrionHipLastError(void) { return g_last_error.c_str(); }
 void OrionHipClearError(void) { g_last_error.clear(); }
 
 static hipStream_t g_user_stream = nullptr;
-static unsigned long g_seed = 0x0123456789abcdefull;
 
 int OrionHipSetDevice(int device) {
-  API_BEGIN
+  API_BEGIN_NOCTX
   HIPCHK(hipSetDevice(device));
+  t_dev = device;
   return 0;
   API_END(-1)
 }
@@ -3108,39 +3476,46 @@ int OrionHipSetDevice(int device) {
 void OrionHipSetSeed(unsigned long seed) {
   API_BEGIN
   g_seed = seed;
-  if (g) {
-    g->prng = Prng(seed);
-    g->seed_encryption(seed);
+  if (t_act) {
+    t_act->prng = Prng(seed);
+    t_act->seed_encryption(seed);
   }
   API_END_VOID
 }
 
 void OrionHipSetStream(void* s) {
   API_BEGIN
-  g_user_stream = (hipStream_t)s;
-  if (g) {
+  Context* c = t_act;
+  if (!c || c->index == 0) g_user_stream = (hipStream_t)s;
+  if (c) {
     // the buffer pool hands freed buffers out again with no stream tracking:
     // drain the old stream so no kernel still reading or writing a pooled
     // buffer overlaps the first launches on the new one
-    if (g->stream) HIPCHK(hipStreamSynchronize(g->stream));
-    if (g->own_stream && g->stream) hipStreamDestroy(g->stream);
-    g->own_stream = false;
-    g->stream = (hipStream_t)s;
+    if (c->stream) HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    c->own_stream = false;
+    c->stream = (hipStream_t)s;
     if (!s) {
-      HIPCHK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
-      g->own_stream = true;
+      HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+      c->own_stream = true;
     }
-    for (auto& kv : g->btp_ctx) kv.second->stream = g->stream;
+    for (auto& kv : c->btp_ctx) kv.second->stream = c->stream;
   }
   API_END_VOID
 }
 
-void* OrionHipGetStream(void) { return g ? (void*)g->stream : nullptr; }
-
-int OrionHipSynchronize(void) {  // every context's stream (peer pipelines included)
+// the calling thread's context's stream (a thread's first call binds it to
+// its pipeline when thread pipelines are on)
+void* OrionHipGetStream(void) {
   API_BEGIN
-  ctx();
-  for (auto& p : g_ctxs) HIPCHK(hipStreamSynchronize(p->stream));
+  return t_act ? (void*)t_act->stream : nullptr;
+  API_END(nullptr)
+}
+
+int OrionHipSynchronize(void) {  // every context's stream (the pipelines' included)
+  API_BEGIN_NOCTX
+  if (!scheme_ctx()) throw std::runtime_error("scheme not initialised: call NewScheme first");
+  for (int i = 0; i < g_nctx.load(); ++i) HIPCHK(hipStreamSynchronize(g_slot[i]->stream));
   return 0;
   API_END(-1)
 }
@@ -3157,26 +3532,29 @@ int OrionHipGraphEnd(void) {
   return ctx().graph_end();
   API_END(-1)
 }
-int OrionHipGraphLaunch(int graph) {
-  API_BEGIN
+int OrionHipGraphLaunch(int graph) {  // on the stream of the context that captured it
+  API_BEGIN_HANDLE(graph)
   ctx().graph_launch(graph);
   return 0;
   API_END(-1)
 }
 void OrionHipGraphDestroy(int graph) {
-  API_BEGIN
+  API_BEGIN_HANDLE(graph)
   ctx().graph_destroy(graph);
   API_END_VOID
 }
 
-int OrionHipLogN(void) { return g ? g->logN : -1; }
-int OrionHipNumQ(void) { return g ? g->L : -1; }
-int OrionHipNumP(void) { return g ? g->K : -1; }
-unsigned long OrionHipModulus(int i) { return (g && i >= 0 && i < (int)g->mods.size()) ? g->mods[i] : 0; }
+int OrionHipLogN(void) { return scheme_ctx() ? scheme_ctx()->logN : -1; }
+int OrionHipNumQ(void) { return scheme_ctx() ? scheme_ctx()->L : -1; }
+int OrionHipNumP(void) { return scheme_ctx() ? scheme_ctx()->K : -1; }
+unsigned long OrionHipModulus(int i) {
+  Context* s = scheme_ctx();
+  return (s && i >= 0 && i < (int)s->mods.size()) ? s->mods[i] : 0;
+}
 
 void NewScheme(int logN, int* logQ, int lenQ, int* logP, int lenP, int logScale, int h, char* ringType,
                char* keysPath, char* ioMode) {
-  API_BEGIN
+  API_BEGIN_EXCL
   (void)keysPath;
   (void)ioMode;
   std::string rt = ringType ? ringType : "standard";
@@ -3191,58 +3569,70 @@ void NewScheme(int logN, int* logQ, int lenQ, int* logP, int lenP, int logScale,
   // the CI NTT folds/unfolds inside the one-pass kernels (N <= 2^15 per CU)
   if (ci && (logN < 13 || logN > 15))
     throw std::runtime_error("ConjugateInvariant ring: logN must be 13..15 in this build");
-  g = nullptr;
-  g_ctxs.clear();
-  g_ctxs.emplace_back(new Context());
-  g = g_ctxs[0].get();
-  g->stream = g_user_stream;
-  g->prng = Prng(g_seed);
-  g->setup(logN, std::vector<int>(logQ, logQ + lenQ), std::vector<int>(logP, logP + lenP), logScale, h, ci);
-  g->seed_encryption(g_seed);
+  for (int i = g_nctx.load() - 1; i >= 0; --i) g_slot[i].reset();  // pipelines first
+  g_nctx.store(0);
+  g_scheme_gen.fetch_add(1);
+  std::unique_ptr<Context> c(new Context());
+  c->index = 0;
+  HIPCHK(hipGetDevice(&c->dev));
+  t_dev = c->dev;
+  c->stream = g_user_stream;
+  c->prng = Prng(g_seed);
+  c->setup(logN, std::vector<int>(logQ, logQ + lenQ), std::vector<int>(logP, logP + lenP), logScale, h, ci);
+  c->seed_encryption(g_seed);
+  g_scheme_thread = std::this_thread::get_id();
+  t_bind = ThreadBind{c.get(), g_scheme_gen.load()};
+  g_slot[0] = std::move(c);
+  g_nctx.store(1);
   API_END_VOID
 }
 
 void DeleteScheme(void) {
-  API_BEGIN
-  g = nullptr;
-  while (!g_ctxs.empty()) g_ctxs.pop_back();  // peers first
+  API_BEGIN_EXCL
+  for (int i = g_nctx.load() - 1; i >= 0; --i) g_slot[i].reset();  // pipelines first
+  g_nctx.store(0);
+  g_scheme_gen.fetch_add(1);
   API_END_VOID
 }
 
-// A peer pipeline: a second context on the same chain with copies of the
-// scheme's keys (secret, public, relinearisation, Galois), its own stream,
-// buffer pool and handle heaps.  Ops issued to two contexts alternately run
-// concurrently on the GPU (their kernels share the CUs), which fills the
-// partial rounds and desynchronises the load and compute phases of the
-// one-limb-per-CU NTT.  Returns the peer's id (the scheme's context is 0).
+// Pipelines (see the registry above).  OrionHipPeerCreate makes one and
+// returns its index (the scheme's context is 0) without binding any thread;
+// OrionHipPeerSelect binds the calling thread to a context; with
+// OrionHipThreadPipelines(n > 1) threads are bound automatically.
 int OrionHipPeerCreate(void) {
-  API_BEGIN
-  if (g_ctxs.empty()) throw std::runtime_error("scheme not initialised: call NewScheme first");
-  Context& c0 = *g_ctxs[0];
-  std::unique_ptr<Context> p(new Context());
-  p->prng = Prng(c0.prng.next());
-  p->init_moduli(c0.logN, c0.mods, c0.logQ_bits, c0.logP_bits, c0.logScale, c0.h, c0.ci);
-  p->adopt_keys(c0);
-  p->seed_encryption(g_seed + 0x9e3779b97f4a7c15ull * g_ctxs.size());
-  const int base = (int)g_ctxs.size() << 20;
-  p->pts.set_base(base), p->cts.set_base(base), p->lts.set_base(base), p->polys.set_base(base);
-  p->next_graph = base;
-  g_ctxs.push_back(std::move(p));
-  return (int)g_ctxs.size() - 1;
+  API_BEGIN_NOCTX
+  return create_pipeline()->index;
   API_END(-1)
 }
 int OrionHipPeerSelect(int id) {
-  std::lock_guard<std::recursive_mutex> lk_(g_mu);
-  if (id < 0 || id >= (int)g_ctxs.size()) {
-    g_last_error = "no such peer context: " + std::to_string(id);
-    return -1;
-  }
-  g = g_ctxs[id].get();
+  API_BEGIN_NOCTX
+  Context* c = slot_ctx(id);
+  if (!c) throw std::runtime_error("no such pipeline context: " + std::to_string(id));
+  t_bind = ThreadBind{c, g_scheme_gen.load()};
   return 0;
+  API_END(-1)
 }
-int OrionHipPeerCount(void) { return (int)g_ctxs.size(); }
+int OrionHipPeerCount(void) { return g_nctx.load(); }
+// n > 1: every thread other than the scheme's gets a pipeline of its own at
+// its first call, up to n contexts in all (then round-robin); n <= 1: off.
+// Returns the previous setting.
+int OrionHipThreadPipelines(int n) { return g_thread_pipes.exchange(n); }
+// the index of the calling thread's context (binding it, as any call does)
+int OrionHipCurrentPipeline(void) {
+  API_BEGIN
+  return ctx().index;
+  API_END(-1)
+}
+// ORION_POOL_CAP_BYTES at run time (0: no cap; see DevicePool::alloc);
+// returns the previous cap
+double OrionHipPoolCap(double bytes) {
+  std::lock_guard<std::recursive_mutex> lk(DevicePool::mu());
+  const double prev = DevicePool::cap_bytes();
+  DevicePool::cap_ref() = bytes;
+  return prev;
+}
 int OrionHipPoolStats(double* out, int n) {
-  std::lock_guard<std::recursive_mutex> lk_(g_mu);
+  std::lock_guard<std::recursive_mutex> lk(DevicePool::mu());
   double cached = 0;
   for (DevicePool* q : DevicePool::registry()) cached += (double)q->cached();
   const double v[5] = {DevicePool::stats()[0], DevicePool::stats()[1], DevicePool::stats()[2], DevicePool::stats()[3],
@@ -3252,15 +3642,9 @@ int OrionHipPoolStats(double* out, int n) {
 }
 int OrionHipStreamWaitPeer(int peer) {
   API_BEGIN
-  if (peer < 0 || peer >= (int)g_ctxs.size()) throw std::runtime_error("no such peer context: " + std::to_string(peer));
-  Context& c = ctx();
-  Context& p = *g_ctxs[peer];
-  if (&p == &c) return 0;
-  hipEvent_t e;
-  HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  HIPCHK(hipEventRecord(e, p.stream));
-  HIPCHK(hipStreamWaitEvent(c.stream, e, 0));
-  HIPCHK(hipEventDestroy(e));  // (released once the wait has completed)
+  Context* p = slot_ctx(peer);
+  if (!p) throw std::runtime_error("no such pipeline context: " + std::to_string(peer));
+  wait_on(ctx(), *p);
   return 0;
   API_END(-1)
 }
@@ -3268,21 +3652,36 @@ int OrionHipStreamWaitPeer(int peer) {
 void FreeCArray(void* p) { free(p); }
 
 void DeletePlaintext(int id) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   ctx().pts.del(id);
   API_END_VOID
 }
 void DeleteCiphertext(int id) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   Context& c = ctx();
   const Context::Deferred d = c.dfr;
   if (d.kind && id == d.r) {
     c.dfr = Context::Deferred();
     // the rotation dies unread: kind 1 needs no work at all; kind 2 is
-    // x += Rotate(x, k) with the addition in the key switch's store
-    if (d.kind == 2) c.rotate_add_inplace(c.cts.get(d.x), d.k);
+    // x += Rotate(x, k) with the addition in the key switch's store.  The
+    // handle goes away whatever happens; if the key switch fails, x (which
+    // the AddCiphertext reported as done) is poisoned
+    if (d.kind == 2) {
+      try {
+        c.rotate_add_inplace(c.cts.get(d.x), d.k);
+      } catch (const std::exception& e) {
+        poison_deferred(c, d, e.what());
+        c.cts.del(id);
+        throw;
+      }
+    }
   } else if (d.kind && id == d.x) {
-    defer_flush();
+    try {
+      defer_flush();
+    } catch (const std::exception&) {
+      c.cts.del(id);
+      throw;
+    }
   }
   c.cts.del(id);
   API_END_VOID
@@ -3293,65 +3692,65 @@ static unsigned long scale_u64(long double s) {
   return (unsigned long)s;
 }
 unsigned long GetPlaintextScale(int id) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   return scale_u64(ctx().pts.get(id).scale);
   API_END(0)
 }
 unsigned long GetCiphertextScale(int id) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   return scale_u64(ctx().cts.get(id).scale);
   API_END(0)
 }
 double GetCiphertextScaleF(int id) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   return (double)ctx().cts.get(id).scale;
   API_END(0)
 }
 void SetPlaintextScale(int id, unsigned long s) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   ctx().pts.get(id).scale = (long double)s;
   API_END_VOID
 }
 void SetCiphertextScale(int id, unsigned long s) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   ctx().cts.get(id).scale = (long double)s;
   API_END_VOID
 }
 int GetPlaintextLevel(int id) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   return ctx().pts.get(id).level;
   API_END(-1)
 }
 int GetCiphertextLevel(int id) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   return ctx().cts.get(id).level;
   API_END(-1)
 }
 int GetPlaintextSlots(int id) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   ctx().pts.get(id);
   return ctx().slots;
   API_END(-1)
 }
 int GetCiphertextSlots(int id) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   ctx().cts.get(id);
   return ctx().slots;
   API_END(-1)
 }
 int GetCiphertextDegree(int id) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   ctx().cts.get(id);
   return 1;
   API_END(-1)
 }
 int GetCiphertextBatch(int id) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   return ctx().cts.get(id).poly.B;
   API_END(-1)
 }
 int GetPlaintextBatch(int id) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   return ctx().pts.get(id).poly.B;
   API_END(-1)
 }
@@ -3907,7 +4306,7 @@ int GenerateLinearTransform(int* diagIdx, int nIdx, float* data, int nData, int 
 }
 
 int GetLinearTransformN1(int id) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   return ctx().lts.get(id).N1;
   API_END(-1)
 }
@@ -3915,11 +4314,21 @@ int GetLinearTransformN1(int id) {
 int EvaluateLinearTransform(int tid, int cid) {
   API_BEGIN
   Context& c = ctx();
-  return c.cts.add(c.eval_lt(c.lts.get(tid), c.cts.get(cid)));
+  LinTrans& T = c.lts.get(tid);
+  Context* o = handle_ctx(tid);
+  if (T.plan_dirty && o && o != &c) {
+    // another context's transform whose plan is not built (its diagonals
+    // changed after the pipelines were made): its owner builds it, under its
+    // lock -- only a lower-index context may be waited on (lock order)
+    if (o->index > c.index) throw std::runtime_error("linear transform " + std::to_string(tid) + " of pipeline " + std::to_string(o->index) + " has no device plan yet: evaluate it there first");
+    std::lock_guard<std::recursive_mutex> lk(o->mu);
+    if (T.plan_dirty) o->build_plan(T);
+  }
+  return c.cts.add(c.eval_lt(T, c.cts.get(cid)));
   API_END(-1)
 }
 void DeleteLinearTransform(int id) {
-  API_BEGIN
+  API_BEGIN_HANDLE(id)
   ctx().lts.del(id);
   API_END_VOID
 }
@@ -4021,7 +4430,7 @@ void LoadRotationKey(char* data, unsigned long len, unsigned long galEl) {
     }
     // the whole key stays in host memory (as Lattigo keeps it,
     // lineartransform.go:143-159): a later use above tl uploads it whole
-    c.gk_host[galEl] = Context::HostKey{level, std::move(host)};
+    c.gk_host[galEl] = Context::HostKey{level, std::make_shared<const std::vector<u64>>(std::move(host))};
     host = std::move(sc);
   } else {
     c.gk_host.erase(galEl);
@@ -4167,19 +4576,44 @@ void NewBootstrapper(int* logPs, int n, int slots) {
 int Bootstrap(int ct, int slots) {
   API_BEGIN
   Context& c = ctx();
-  return c.cts.add(c.bootstrap(c.cts.get(ct), slots));
+  Context* s = scheme_ctx();
+  if (c.btps.count(slots) || !s || s == &c) return c.cts.add(c.bootstrap(c.cts.get(ct), slots));
+  // a pipeline bootstraps with the scheme's bootstrapper (one circuit and key
+  // set per process), on the scheme's stream under the scheme's lock: the
+  // scheme's stream waits for the input, the result is copied into a buffer
+  // of this pipeline's pool there, and this stream waits for the copy
+  const Ciphertext& in = c.cts.get(ct);
+  std::lock_guard<std::recursive_mutex> lk(s->mu);  // (a pipeline may wait on the scheme: index order)
+  wait_on(*s, c);
+  Ciphertext out;
+  {
+    Context* saved = t_act;
+    t_act = s;
+    try {
+      Ciphertext r = s->bootstrap(in, slots);
+      out = c.new_ct(r.level, r.poly.B, r.scale);
+      s->copy(s->lsq(out.poly, 0, 2, r.level), s->lsq(r.poly, 0, 2, r.level));
+    } catch (...) {
+      t_act = saved;
+      throw;
+    }
+    t_act = saved;
+  }
+  wait_on(c, *s);
+  return c.cts.add(std::move(out));
   API_END(-1)
 }
 void DeleteBootstrappers(void) {
   API_BEGIN
-  if (g) g->delete_bootstrappers();
+  if (t_act) t_act->delete_bootstrappers();
   API_END_VOID
 }
 // the bootstrapping chain of the circuit for `slots` (its Q primes, then its P primes)
 static Context* btp_context(int slots) {
-  if (!g) return nullptr;
-  auto it = g->btps.find(slots);
-  return it == g->btps.end() ? nullptr : it->second->bc;
+  Context* s = scheme_ctx();
+  if (!s) return nullptr;
+  auto it = s->btps.find(slots);
+  return it == s->btps.end() ? nullptr : it->second->bc;
 }
 int OrionHipBootstrapNumQ(int slots) {
   Context* b = btp_context(slots);
@@ -4444,7 +4878,11 @@ int ExportPublicKey(unsigned long* out, unsigned long n) {
   return export_poly(ctx().pk, out, n);
   API_END(-1)
 }
-unsigned int OrionHipEncryptionIndex(void) { return g ? g->enc_sampler.enc : 0; }
+unsigned int OrionHipEncryptionIndex(void) {
+  API_BEGIN
+  return t_act ? t_act->enc_sampler.enc : 0;
+  API_END(0)
+}
 int ExportRelinKey(unsigned long* out, unsigned long n) {
   API_BEGIN
   if (!ctx().have_rlk) throw std::runtime_error("no relinearization key");
@@ -4570,34 +5008,52 @@ int ImportKeyBundle(const void* dptr, unsigned long bytes) {
 }
 
 // ---- profiling ----
+// Profiling switches and counters cover every context of the scheme (the
+// pipelines' launches included); each context is locked on its own in turn.
+}  // extern "C"
+template <class F>
+static void each_ctx(F f) {
+  for (int i = 0; i < g_nctx.load(); ++i) {
+    Context* c = g_slot[i].get();
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    f(*c);
+  }
+}
+extern "C" {
 void OrionHipProfile(int enable) {
-  API_BEGIN
-  Context& c = ctx();
-  if (!enable) c.prof_flush();
-  c.prof = enable == 1 ? 0xffffffffu : (unsigned)enable;  // 1 = all categories, else a bit mask
+  API_BEGIN_NOCTX
+  each_ctx([&](Context& c) {
+    if (!enable) c.prof_flush();
+    c.prof = enable == 1 ? 0xffffffffu : (unsigned)enable;  // 1 = all categories, else a bit mask
+  });
   API_END_VOID
 }
-// the reference of the union timing: recorded on the current context's
-// stream; the intervals collected so far are dropped
+// the reference of the union timing: recorded on the scheme's stream once
+// every context is drained; the intervals collected so far are dropped
 void OrionHipProfileClock(void) {
-  API_BEGIN
-  Context& c = ctx();
-  for (auto& p : g_ctxs) p->prof_flush();
+  API_BEGIN_NOCTX
+  Context* s = scheme_ctx();
+  if (!s) throw std::runtime_error("scheme not initialised: call NewScheme first");
+  each_ctx([](Context& c) { c.prof_flush(); });
+  std::lock_guard<std::mutex> lk(g_prof_mu);
   g_prof_iv.clear();
   if (!g_prof_ref) HIPCHK(hipEventCreate(&g_prof_ref));
-  HIPCHK(hipEventRecord(g_prof_ref, c.stream));
+  HIPCHK(hipEventRecord(g_prof_ref, s->stream));
   HIPCHK(hipEventSynchronize(g_prof_ref));
   API_END_VOID
 }
 // the union of the wall-clock intervals of every context's profiled launches
 // of the categories in `mask` since OrionHipProfileClock (ms): e.g. the time
-// at least one NTT ran while two pipelines interleave
+// at least one NTT ran while pipelines overlap
 double OrionHipProfileUnion(unsigned mask) {
-  API_BEGIN
-  for (auto& p : g_ctxs) p->prof_flush();
+  API_BEGIN_NOCTX
+  each_ctx([](Context& c) { c.prof_flush(); });
   std::vector<std::pair<float, float>> iv;
-  for (const ProfIv& r : g_prof_iv)
-    if (mask & (1u << r.cat)) iv.push_back({r.t0, r.t1});
+  {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    for (const ProfIv& r : g_prof_iv)
+      if (mask & (1u << r.cat)) iv.push_back({r.t0, r.t1});
+  }
   std::sort(iv.begin(), iv.end());
   double tot = 0;
   float b = 0, e = 0;
@@ -4620,33 +5076,42 @@ void OrionHipLogMark(const char* tag) {
   if (FILE* f = ntt_log_file()) fprintf(f, "# %s\n", tag ? tag : "");
 }
 void OrionHipProfileReset(void) {
-  API_BEGIN
-  Context& c = ctx();
-  c.prof_flush();
-  for (int i = 0; i < P_NCAT; ++i) c.prof_launch[i] = c.prof_ms[i] = c.prof_bytes[i] = c.prof_strict[i] = 0;
+  API_BEGIN_NOCTX
+  each_ctx([](Context& c) {
+    c.prof_flush();
+    for (int i = 0; i < P_NCAT; ++i) c.prof_launch[i] = c.prof_ms[i] = c.prof_bytes[i] = c.prof_strict[i] = 0;
+  });
   API_END_VOID
 }
+// counters summed over every context
 int OrionHipProfileRead(char* names, long* launches, double* ms, double* bytes, int max) {
-  API_BEGIN
-  Context& c = ctx();
-  c.prof_flush();
+  API_BEGIN_NOCTX
   int n = std::min(max, (int)P_NCAT);
   for (int i = 0; i < n; ++i) {
     strncpy(names + 32 * i, kProfNames[i], 31);
     names[32 * i + 31] = 0;
-    launches[i] = (long)c.prof_launch[i];
-    ms[i] = c.prof_ms[i];
-    bytes[i] = c.prof_bytes[i];
+    launches[i] = 0;
+    ms[i] = bytes[i] = 0;
   }
+  each_ctx([&](Context& c) {
+    c.prof_flush();
+    for (int i = 0; i < n; ++i) {
+      launches[i] += (long)c.prof_launch[i];
+      ms[i] += c.prof_ms[i];
+      bytes[i] += c.prof_bytes[i];
+    }
+  });
   return n;
   API_END(-1)
 }
 int OrionHipProfileReadStrict(double* strict, int max) {
-  API_BEGIN
-  Context& c = ctx();
-  c.prof_flush();
+  API_BEGIN_NOCTX
   int n = std::min(max, (int)P_NCAT);
-  for (int i = 0; i < n; ++i) strict[i] = c.prof_strict[i];
+  for (int i = 0; i < n; ++i) strict[i] = 0;
+  each_ctx([&](Context& c) {
+    c.prof_flush();
+    for (int i = 0; i < n; ++i) strict[i] += c.prof_strict[i];
+  });
   return n;
   API_END(-1)
 }

@@ -19,9 +19,18 @@ Every other call goes through its own C-ABI entry, in the stream's order: the
 rotate-and-add fusion of `out += out.roll(k)` (RotateNew, AddCiphertext,
 DeleteCiphertext) and RescaleNew's copy-on-write result happen inside the
 library, behind the unchanged calls (backend.hip Context::Deferred, alias).
+
+Concurrency is the frontend's own: several threads each call forward() of the
+same compiled stream on ciphertexts they encrypted themselves (Pipelines).
+With thread pipelines on (OrionHipThreadPipelines) the library gives each
+thread a context of its own -- the scheme's keys and compiled objects, its own
+HIP stream, pool and handles -- so the threads' kernels overlap on the GPU.
+forward() keeps its state in locals, so it is reentrant across threads.
 """
 import json
 import os
+import queue
+import threading
 
 import numpy as np
 
@@ -63,38 +72,22 @@ _NEW_CT = ("EvaluateLinearTransform", "EvaluatePolynomial", "Bootstrap", "Negate
 class OrionStream:
     """A compiled Orion model as an op stream bound to one HipLibrary."""
 
-    def __init__(self, name, lib=None, seed=2024, device=None, root=GOLDEN, synthetic_diagonals=False,
-                 peer_of=None):
-        """peer_of: another OrionStream whose scheme (and keys) this one shares
-        as a peer pipeline (OrionHipPeerCreate): its own stream, buffer pool
-        and handles, so the two can run concurrently (forward_interleaved)."""
+    def __init__(self, name, lib=None, seed=2024, device=None, root=GOLDEN, synthetic_diagonals=False):
         self.name = name
         self.trace, self.arrays = load_stream(name, root)
         self.meta = self.trace["meta"]
         cfg = self.meta["config"]
-        if peer_of is not None:
-            self.lib = peer_of.lib
-            self.ctx_id = self.lib._chk(self.lib.OrionHipPeerCreate(), "OrionHipPeerCreate")
-        else:
-            self.lib = lib or HipLibrary()
-            self.lib.new_scheme(cfg["logn"], cfg["logq"], cfg["logp"], cfg["logscale"], h=cfg["h"], seed=seed,
-                                device=device, ringtype=cfg.get("ringtype", "standard"))
-            self.ctx_id = 0
-        self.use()
+        self.lib = lib or HipLibrary()
+        self.lib.new_scheme(cfg["logn"], cfg["logq"], cfg["logp"], cfg["logscale"], h=cfg["h"], seed=seed,
+                            device=device, ringtype=cfg.get("ringtype", "standard"))
         self.slots = self.meta["slots"]
         self.synthetic = synthetic_diagonals
         self.pt_map, self.ct_map, self.lt_map, self.poly_map = {}, {}, {}, {}
         self.input_level = self.meta["input_level"]
         self._events = self.trace["events"]
 
-    def use(self):
-        """Make this pipeline's context the one the library's calls act on."""
-        if self.lib.OrionHipPeerCount() > 1 or self.ctx_id:
-            self.lib._chk(self.lib.OrionHipPeerSelect(self.ctx_id), "OrionHipPeerSelect")
-
     # -- setup: keys + evaluator (key_generator.py:10-15, evaluator.py:2-6) ---
     def keygen(self, with_po2=True):
-        self.use()
         lib = self.lib
         lib.NewKeyGenerator()
         lib.GenerateSecretKey()
@@ -111,7 +104,6 @@ class OrionStream:
 
     # -- compile phase: bias plaintexts + linear transforms + their keys --------
     def compile(self, gen_keys=True):
-        self.use()
         lib = self.lib
         rng = np.random.default_rng(7)
         for ev in self._events:
@@ -151,7 +143,6 @@ class OrionStream:
     def encrypt_batch(self, images):
         """images: (B, ...) array; each image flattened into the slots the way
         orion's encoder pads it (encoder.py:29-42)."""
-        self.use()
         imgs = np.asarray(images, dtype=np.float32).reshape(len(images), -1)
         enc = [e for e in self.input_events() if e["op"] == "Encode"][0]
         level, scale = enc["args"][1], enc["args"][2]
@@ -170,45 +161,12 @@ class OrionStream:
         """hook(event, handle): called after every replayed op (debugging).
         stop_after: index of a forward event; the handle that event produced is
         returned (the stream's other temporaries are deleted)."""
-        self.use()
         it = self.forward_iter(ct_in, hook, stop_after)
         while True:
             try:
                 next(it)
             except StopIteration as e:
                 return e.value
-
-    @staticmethod
-    def forward_interleaved(pairs, lag=0):
-        """Run the forward passes of several pipelines [(stream, ct_in), ...]
-        (peer contexts of one scheme) op by op in turn, so their kernels run
-        concurrently on the GPU; returns their outputs in order.  lag > 0:
-        pipeline i starts once pipeline 0 has issued i * lag ops, and its
-        stream first waits on the GPU for the work pipeline 0 has enqueued by
-        then (OrionHipStreamWaitPeer), so the pipelines run phase-shifted."""
-        its = [(st, st.forward_iter(ct)) for st, ct in pairs]
-        outs = [None] * len(its)
-        live = list(range(len(its)))
-        issued = 0  # pipeline 0's ops so far
-        started = set([0]) if lag > 0 else set(range(len(its)))
-        while live:
-            for i in list(live):
-                st, it = its[i]
-                if i not in started:
-                    if issued < i * lag and 0 in live:
-                        continue
-                    st.use()
-                    st.lib.OrionHipStreamWaitPeer(pairs[0][0].ctx_id)
-                    started.add(i)
-                st.use()
-                if i == 0:
-                    issued += 1
-                try:
-                    next(it)
-                except StopIteration as e:
-                    outs[i] = e.value
-                    live.remove(i)
-        return outs
 
     def forward_iter(self, ct_in, hook=None, stop_after=None):
         """forward() one op at a time: yields after every library call that
@@ -272,7 +230,6 @@ class OrionStream:
         re-runs every kernel of the pass on ct_in's current contents and
         rewrites the output handle; the clone keeps in-place ops off ct_in.
         Run forward() once first (keys, tables and LT plans are made then)."""
-        self.use()
         lib = self.lib
         lib.OrionHipGraphBegin()
         try:
@@ -290,7 +247,6 @@ class OrionStream:
 
     def decrypt_output(self, ct, n_out=None):
         """Decrypt + decode a batch output; returns (B, n_out) floats."""
-        self.use()
         lib = self.lib
         B = lib.GetCiphertextBatch(ct)
         pt = lib.Decrypt(ct)
@@ -306,3 +262,62 @@ class OrionStream:
                                                           "DeleteCiphertext"):
                 c[e["op"]] = c.get(e["op"], 0) + 1
         return c
+
+
+class Pipelines:
+    """n worker threads, each bound by the library to a pipeline context of its
+    own at its first call (OrionHipThreadPipelines(n + 1): the scheme's context
+    plus n).  run(fns) runs fns[i] on thread i and returns the results in
+    order; a worker's exception is raised in the caller.  The threads keep
+    their contexts (and the handles made there) across run() calls."""
+
+    def __init__(self, lib, n, device=None):
+        self.lib, self.n = lib, n
+        self.prev = lib.thread_pipelines(n + 1)
+        self._tasks = [queue.Queue() for _ in range(n)]
+        self._done = queue.Queue()
+        self._threads = [threading.Thread(target=self._work, args=(i, device), daemon=True) for i in range(n)]
+        for t in self._threads:
+            t.start()
+        self.contexts = self.run([self.lib.OrionHipCurrentPipeline] * n)
+
+    def _work(self, i, device):
+        if device is not None:
+            import torch
+            torch.cuda.set_device(device)
+        while True:
+            fn = self._tasks[i].get()
+            if fn is None:
+                return
+            try:
+                self._done.put((i, True, fn()))
+            except BaseException as e:  # reported by run()
+                self._done.put((i, False, e))
+
+    def run(self, fns):
+        assert len(fns) == self.n
+        for q, fn in zip(self._tasks, fns):
+            q.put(fn)
+        out, err = [None] * self.n, None
+        for _ in range(self.n):
+            i, ok, v = self._done.get()
+            if ok:
+                out[i] = v
+            elif err is None:
+                err = v
+        if err is not None:
+            raise err
+        return out
+
+    def run_one(self, i, fn):
+        """fn on thread i alone (the others idle)."""
+        fns = [(lambda: None)] * self.n
+        fns[i] = fn
+        return self.run(fns)[i]
+
+    def close(self):
+        for q in self._tasks:
+            q.put(None)
+        for t in self._threads:
+            t.join()
+        self.lib.thread_pipelines(self.prev)

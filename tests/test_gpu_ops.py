@@ -245,7 +245,7 @@ def test_lola_n15_matches_cpu_oracle_replay(torch_cuda):
     _replay_gpu_vs_cpu("lola_n15", seed=32)
 
 
-@pytest.mark.parametrize("B", [6, 64])
+@pytest.mark.parametrize("B", [6, 32, 64])
 def test_lola_n15_batch_invariance(torch_cuda, B):
     """Full-size property: a batch of B copies of one ciphertext (every kernel
     launched at batch B) gives, image by image, exactly the single-image run.
@@ -405,61 +405,173 @@ def test_library_deferral_matches_undeferred(torch_cuda, monkeypatch):
         assert np.array_equal(outs[0], outs[1]), name
 
 
-def test_peer_pipelines_interleaved(torch_cuda):
-    """Peer pipelines (OrionHipPeerCreate / OrionHipPeerSelect): a second
-    context on the scheme's chain with copies of its keys, its own stream,
-    pool and handles.  Two pipelines replayed op by op in turn
-    (OrionStream.forward_interleaved, their kernels concurrent on the GPU)
-    give, for the same input ciphertext, exactly the single pipeline's output
-    -- LoLA N=2^13 at batch 3 and N=2^15 at batch 4, also with the peer
-    started 3 ops behind; a peer's handles are unknown to context 0;
-    DeleteScheme removes the peers."""
+def test_thread_pipelines_small(torch_cuda):
+    """Thread-affine pipelines (OrionHipThreadPipelines): two frontend threads
+    each run the unchanged op stream's forward() (one compiled stream: the
+    scheme's keys and transforms) on a ciphertext they imported themselves; the
+    library binds each thread to a context of its own (own stream, pool,
+    handle range), and each output equals the scheme thread's single run bit
+    for bit -- LoLA N=2^13 at batch 3.  Handles are unique across contexts:
+    the main thread reads and deletes the pipelines' outputs; an in-place op
+    on another context's ciphertext is refused; DeleteScheme removes the
+    pipelines."""
     import numpy as np
-    from orion_amd.replay import OrionStream
-    for name, B in (("lola_n13", 3), ("lola_n15", 4)):
-        st = OrionStream(name, seed=91)
-        st.keygen()
-        st.compile()
-        st2 = OrionStream(name, peer_of=st)
-        st2.compile()
-        lib = st.lib
-        assert lib.OrionHipPeerCount() == 2 and st2.ctx_id == 1
-        rng = np.random.default_rng(92)
-        imgs = rng.standard_normal((B,) + np.asarray(st.reference_input()).shape[1:]).astype(np.float32)
-        ct = st.encrypt_batch(imgs)
-        x, scale = lib.export_ciphertext(ct), lib.GetCiphertextScaleF(ct)
-        st2.use()
-        ct2 = lib.import_ciphertext(x, scale)
-        st.use()
-        ref = lib.export_ciphertext(st.forward(lib.CloneCiphertext(ct)))
-        # phase-shifted: the peer starts 3 ops behind, its stream waiting on the
-        # GPU for context 0's work so far (OrionHipStreamWaitPeer)
-        ca = lib.CloneCiphertext(ct)
-        st2.use()
-        cb = lib.CloneCiphertext(ct2)
-        outs_lag = OrionStream.forward_interleaved([(st, ca), (st2, cb)], lag=3)
-        st.use()
-        assert np.array_equal(lib.export_ciphertext(outs_lag[0]), ref), name
-        lib.DeleteCiphertext(outs_lag[0])
-        st2.use()
-        assert np.array_equal(lib.export_ciphertext(outs_lag[1]), ref), name
-        lib.DeleteCiphertext(outs_lag[1])
-        outs = OrionStream.forward_interleaved([(st, ct), (st2, ct2)])
-        st.use()
-        got0 = lib.export_ciphertext(outs[0])
-        st2.use()
-        got1 = lib.export_ciphertext(outs[1])
-        assert np.array_equal(got0, ref) and np.array_equal(got1, ref), name
-        # each context's handles live in a range of their own: a peer's handle
-        # passed to context 0 is unknown there, never another ciphertext
-        assert outs[0] < 1 << 20 <= outs[1] < 2 << 20, (outs, name)
-        st.use()
-        with pytest.raises(RuntimeError, match="handle not found"):
-            lib.GetCiphertextLevel(outs[1])
-        # the peer decrypts with its copy of the secret
-        dec = st2.decrypt_output(outs[1])
-        exp = st.arrays["expected_output"].reshape(-1)
+    from orion_amd.replay import OrionStream, Pipelines
+    st = OrionStream("lola_n13", seed=91)
+    st.keygen()
+    st.compile()
+    lib = st.lib
+    B = 3
+    rng = np.random.default_rng(92)
+    imgs = rng.standard_normal((B,) + np.asarray(st.reference_input()).shape[1:]).astype(np.float32)
+    ct = st.encrypt_batch(imgs)
+    x, scale = lib.export_ciphertext(ct), lib.GetCiphertextScaleF(ct)
+    ref = lib.export_ciphertext(st.forward(lib.CloneCiphertext(ct)))
+    pipes = Pipelines(lib, 2, device=0)
+    try:
+        assert sorted(pipes.contexts) == [1, 2] and lib.OrionHipPeerCount() == 3
+        assert lib.OrionHipCurrentPipeline() == 0  # the scheme's thread keeps the scheme's context
+        cts = pipes.run([lambda: lib.import_ciphertext(x, scale)] * 2)
+        for i, c in enumerate(cts):
+            assert c >> 20 == pipes.contexts[i]
+        for _ in range(2):  # twice: the second pass reuses each pipeline's pooled buffers
+            outs = pipes.run([(lambda c=c: st.forward(c)) for c in cts])
+            for o in outs:
+                assert np.array_equal(lib.export_ciphertext(o), ref)  # read from the main thread
+                lib.DeleteCiphertext(o)  # deleted on its own context
+        with pytest.raises(RuntimeError, match="changed only by the context"):
+            lib.Rescale(cts[0])
+        dec = pipes.run_one(1, lambda: st.decrypt_output(cts[1]))  # the pipelines share the scheme's secret
         assert dec.shape[0] == B
-        st.use()
-        lib.DeleteScheme()
-        assert lib.OrionHipPeerCount() == 0
+    finally:
+        pipes.close()
+    lib.DeleteScheme()
+    assert lib.OrionHipPeerCount() == 0
+
+
+def test_thread_pipelines_lola_n15_timed_config(torch_cuda):
+    """The bench's timed configuration, bit for bit: LoLA N=2^15, two frontend
+    threads with 32 images each on their own pipeline contexts (bench.py
+    --pipelines 2, batch 64).  64 different images are encrypted once; every
+    image's output from the threads equals the single-image run of that
+    image's ciphertext on the scheme's context (the batch-1 path that
+    test_lola_n15_matches_cpu_oracle_replay checks against the CPU oracle)."""
+    import numpy as np
+    from orion_amd.replay import OrionStream, Pipelines
+    st = OrionStream("lola_n15", seed=33)
+    st.keygen()
+    st.compile()
+    lib = st.lib
+    rng = np.random.default_rng(5)
+    imgs = rng.standard_normal((64,) + np.asarray(st.reference_input()).shape[1:]).astype(np.float32)
+    imgs[0] = np.asarray(st.reference_input()).reshape(imgs.shape[1:])
+    ct = st.encrypt_batch(imgs)
+    x, scale = lib.export_ciphertext(ct), lib.GetCiphertextScaleF(ct)
+    lib.DeleteCiphertext(ct)
+    pipes = Pipelines(lib, 2, device=0)
+    try:
+        cts = pipes.run([(lambda i=i: lib.import_ciphertext(x[32 * i:32 * (i + 1)], scale)) for i in range(2)])
+        pipes.run([(lambda c=c: lib.DeleteCiphertext(st.forward(lib.CloneCiphertext(c)))) for c in cts])  # warm
+        outs = pipes.run([(lambda c=c: st.forward(c)) for c in cts])
+        got = np.concatenate([lib.export_ciphertext(o) for o in outs])
+    finally:
+        pipes.close()
+    assert got.shape[0] == 64
+    for b in range(64):
+        one = lib.import_ciphertext(x[b:b + 1], scale)
+        assert np.array_equal(lib.export_ciphertext(st.forward(one))[0], got[b]), b
+    res = st.decrypt_output(lib.import_ciphertext(got[:1], lib.GetCiphertextScaleF(outs[0])))[0]
+    assert np.abs(res - st.arrays["expected_output"].reshape(-1)).mean() < 0.005
+    lib.DeleteScheme()
+
+
+def test_pool_cap_forces_trim_and_retry(torch_cuda):
+    """The failed-allocation path (the a6cfbba fix): under a
+    pool byte cap (OrionHipPoolCap, = ORION_POOL_CAP_BYTES) an allocation past
+    the cap releases every pool's cache and retries once.  A chain whose
+    buffer sizes are new, run with the cap at the bytes held (cache full of
+    other sizes), forces that trim, leaves no stale HIP error for the next
+    call, and gives the uncapped run's output bit for bit; a cap below the
+    live bytes fails the call with a clear error, and the scheme works again
+    once the cap is lifted."""
+    import numpy as np
+    from orion_amd.backend import HipLibrary
+    lib = HipLibrary().new_scheme(13, [55, 40, 40, 40, 40, 40], [60, 60], 40, h=192, seed=7, device=0)
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    lib.AddRotationKey(5)
+    rng = np.random.default_rng(0)
+
+    def enc(B):
+        return lib.Encrypt(lib.encode_batch(rng.standard_normal((B, 4096)).astype(np.float32), 5, 1 << 40))
+
+    def chain(ct):
+        a = lib.MulRelinCiphertextNew(ct, ct)
+        b = lib.RotateNew(a, 5)
+        lib.Rescale(b)
+        c = lib.AddCiphertextNew(b, b)
+        out = lib.export_ciphertext(c)
+        for h in (a, b, c):
+            lib.DeleteCiphertext(h)
+        return out
+
+    ct16, ct32 = enc(16), enc(32)
+    chain(enc(4))
+    # the cache fills with buffers of a size the chain at batch 16 never takes
+    junk = [lib.encode_batch(np.zeros((64, 4096), np.float32), 5, 1 << 40) for _ in range(16)]
+    for h in junk:
+        lib.DeletePlaintext(h)
+    st1 = lib.pool_stats()
+    live = st1["held_bytes"] - st1["cached_bytes"]
+    assert st1["cached_bytes"] > 300e6, st1
+    prev = lib.pool_cap(st1["held_bytes"])
+    try:
+        got = chain(ct16)  # its first new-size allocation is past the cap: trim, retry
+        st2 = lib.pool_stats()
+        assert st2["trims"] > st1["trims"], (st1, st2)
+        assert st2["held_bytes"] <= st1["held_bytes"], (st1, st2)
+        assert lib.GetCiphertextLevel(ct16) == 5  # the next call sees no stale error
+        lib.pool_cap(live * 0.5)
+        with pytest.raises(RuntimeError, match="device memory exhausted"):
+            chain(ct32)
+        assert lib.GetCiphertextLevel(ct32) == 5
+    finally:
+        lib.pool_cap(prev)
+    assert np.array_equal(chain(ct16), got)  # uncapped: the same bits
+    chain(ct32)
+    lib.DeleteScheme()
+
+
+def test_deferred_rotation_failure_poisons(torch_cuda):
+    """a deferred rotate-and-add whose key switch fails when it runs
+    (DeleteCiphertext of the rotation, here an allocation past the pool cap)
+    reports the failure, deletes the rotation's handle, and poisons the
+    ciphertext the AddCiphertext had reported as updated: every later use of
+    it fails loudly instead of reading a buffer that was never written."""
+    import numpy as np
+    from orion_amd.backend import HipLibrary
+    lib = HipLibrary().new_scheme(13, [55, 40, 40, 40, 40, 40], [60, 60], 40, h=192, seed=7, device=0)
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    lib.AddRotationKey(1)
+    vals = np.random.default_rng(1).standard_normal((2, 4096)).astype(np.float32)
+    x = lib.Encrypt(lib.encode_batch(vals, 5, 1 << 40))
+    live0 = lib.GetLiveCiphertexts()
+    r = lib.RotateNew(x, 1)
+    assert lib.AddCiphertext(x, r) == x
+    st = lib.pool_stats()
+    lib.pool_cap(st["held_bytes"] - st["cached_bytes"])  # nothing new fits
+    try:
+        with pytest.raises(RuntimeError, match="device memory exhausted"):
+            lib.DeleteCiphertext(r)
+    finally:
+        lib.pool_cap(0)
+    assert lib.GetLiveCiphertexts() == live0  # r is gone
+    with pytest.raises(RuntimeError, match="deferred rotation by 1 failed"):
+        lib.GetCiphertextLevel(x)
+    lib.DeleteCiphertext(x)
+    y = lib.Encrypt(lib.encode_batch(vals, 5, 1 << 40))  # the scheme still works
+    assert lib.GetCiphertextLevel(lib.RotateNew(y, 1)) == 5
+    lib.DeleteScheme()
