@@ -106,39 +106,63 @@ class DevicePool {
     return c;
   }
   static double cap_bytes() { return cap_ref(); }
+  // A cached buffer is reused for a request of up to its size when the
+  // request is at least 7/8 of it (best fit): the limb counts of a chain's
+  // levels make many nearby sizes, and exact-size classes alone left memory
+  // cached in sizes no request took (ResNet-20 N=2^16 at batch 8 thrashed).
   void* alloc(size_t bytes) {
     std::lock_guard<std::recursive_mutex> lk(mu());
     void* p = nullptr;
-    auto it = free_.find(bytes);
-    if (it != free_.end() && !it->second.empty()) {
+    auto it = free_.lower_bound(bytes);
+    if (it != free_.end() && it->first - bytes <= it->first / 8) {
       p = it->second.back();
       it->second.pop_back();
+      if (it->second.empty()) free_.erase(it);
     } else {
       const bool over = cap_bytes() > 0 && stats()[0] + (double)bytes > cap_bytes();
       hipError_t e = over ? hipErrorOutOfMemory : hipMalloc(&p, bytes);
       if (e != hipSuccess) {
-        // release the caches of every pool on the device (the scheme's,
-        // its pipelines' and the bootstrappers' contexts) and retry -- not
-        // while capturing: trim synchronises.  The failed call's error is
-        // cleared: HIP keeps it as the thread's last error, and a later launch
-        // check (hipGetLastError) would report it
+        // release cached buffers of every pool on the device (the scheme's,
+        // its pipelines' and the bootstrappers' contexts), the largest first,
+        // until the request fits; then, if it still does not, every cache --
+        // not while capturing: a trim synchronises.  The failed call's error
+        // is cleared: HIP keeps it as the thread's last error, and a later
+        // launch check (hipGetLastError) would report it
         (void)hipGetLastError();
         for (DevicePool* q : registry())
           if (q->tracking_) throw std::runtime_error("device memory exhausted during graph capture");
         stats()[3] += 1;  // one forced trim per failed allocation, whatever the number of pools
-        for (DevicePool* q : registry()) q->trim();
-        if (cap_bytes() > 0 && stats()[0] + (double)bytes > cap_bytes())
-          throw std::runtime_error("device memory exhausted: " + std::to_string(bytes) + " more bytes exceed the pool cap (ORION_POOL_CAP_BYTES) with every cache released");
-        e = hipMalloc(&p, bytes);
-        if (e != hipSuccess) {
+        // first, the smallest cached buffer of any pool that is large enough
+        // is taken over as it is (no free, no allocation: under memory
+        // pressure a larger buffer serves the request); the device is drained
+        // first, since another context's stream may still use its cache
+        hipDeviceSynchronize();
+        p = adopt_cached(bytes);
+        if (p) {
+          if (tracking_) touched_[p] = bytes;
+          return p;
+        }
+        for (int pass = 0; pass < 2; ++pass) {
+          // pass 0: twice the request (at least 1 GiB) from the largest
+          // cached buffers; pass 1: everything
+          trim_largest(pass == 0 ? std::max<size_t>(2 * bytes, (size_t)1 << 30) : SIZE_MAX);
+          if (cap_bytes() > 0 && stats()[0] + (double)bytes > cap_bytes()) {
+            if (pass == 0) continue;
+            throw std::runtime_error("device memory exhausted: " + std::to_string(bytes) +
+                                     " more bytes exceed the pool cap (ORION_POOL_CAP_BYTES) with every cache released");
+          }
+          e = hipMalloc(&p, bytes);
+          if (e == hipSuccess) break;
           (void)hipGetLastError();
-          throw std::runtime_error("device memory exhausted: hipMalloc of " + std::to_string(bytes) +
-                                   " bytes failed with every pool's cache released (" +
-                                   std::to_string((long long)stats()[0]) + " bytes held by live objects)");
+          if (pass == 1)
+            throw std::runtime_error("device memory exhausted: hipMalloc of " + std::to_string(bytes) +
+                                     " bytes failed with every pool's cache released (" +
+                                     std::to_string((long long)stats()[0]) + " bytes held by live objects)");
         }
       }
       stats()[2] += 1;
       held_ += bytes;
+      real_[p] = bytes;
       add_held((double)bytes);
     }
     if (tracking_) touched_[p] = bytes;
@@ -150,8 +174,14 @@ class DevicePool {
     }
     return p;
   }
+  // a pointer's allocated size (>= the bytes its holder asked for)
+  size_t real(void* p) const {
+    auto it = real_.find(p);
+    return it == real_.end() ? 0 : it->second;
+  }
   void release(void* p, size_t bytes) {
     std::lock_guard<std::recursive_mutex> lk(mu());
+    bytes = real(p);  // cached by its allocated size
     if (pins_.count(p)) {
       parked_[p] = bytes;
       return;
@@ -173,7 +203,7 @@ class DevicePool {
       if (pins_.count(pb.first)) continue;
       auto pk = parked_.find(pb.first);
       if (pk != parked_.end()) {
-        free_[pk->second].push_back(pk->first);
+        free_[real(pk->first)].push_back(pk->first);
         parked_.erase(pk);
       }
     }
@@ -183,8 +213,53 @@ class DevicePool {
     std::lock_guard<std::recursive_mutex> lk(mu());
     hipDeviceSynchronize();
     for (auto& kv : free_)
-      for (void* p : kv.second) hipFree(p), held_ -= kv.first, add_held(-(double)kv.first);
+      for (void* p : kv.second) free_one(p);
     free_.clear();
+  }
+  // the smallest cached buffer of at least `bytes` in any pool, moved into
+  // this pool (nullptr: none); the caller has drained the device
+  void* adopt_cached(size_t bytes) {
+    DevicePool* best = nullptr;
+    size_t bsz = SIZE_MAX;
+    for (DevicePool* q : registry()) {
+      auto it = q->free_.lower_bound(bytes);
+      if (it != q->free_.end() && it->first < bsz) best = q, bsz = it->first;
+    }
+    if (!best) return nullptr;
+    auto it = best->free_.find(bsz);
+    void* p = it->second.back();
+    it->second.pop_back();
+    if (it->second.empty()) best->free_.erase(it);
+    if (best != this) {
+      best->real_.erase(p);
+      best->held_ -= bsz;
+      real_[p] = bsz;
+      held_ += bsz;
+    }
+    return p;
+  }
+  // free cached buffers of every pool, the largest first, until `need` bytes
+  // are freed (or every cache is empty)
+  static void trim_largest(size_t need) {
+    std::lock_guard<std::recursive_mutex> lk(mu());
+    hipDeviceSynchronize();
+    std::vector<std::pair<size_t, DevicePool*>> sizes;
+    for (DevicePool* q : registry())
+      for (auto& kv : q->free_)
+        if (!kv.second.empty()) sizes.push_back({kv.first, q});
+    std::sort(sizes.begin(), sizes.end(), [](const std::pair<size_t, DevicePool*>& x,
+                                              const std::pair<size_t, DevicePool*>& y) { return x.first > y.first; });
+    size_t freed = 0;
+    for (auto& sq : sizes) {
+      auto it = sq.second->free_.find(sq.first);
+      while (freed < need && it != sq.second->free_.end() && !it->second.empty()) {
+        sq.second->free_one(it->second.back());
+        it->second.pop_back();
+        freed += sq.first;
+      }
+      if (it != sq.second->free_.end() && it->second.empty()) sq.second->free_.erase(it);
+      if (freed >= need) break;
+    }
   }
   DevicePool() {
     std::lock_guard<std::recursive_mutex> lk(mu());
@@ -232,14 +307,17 @@ class DevicePool {
     std::lock_guard<std::recursive_mutex> lk(mu());
     for (auto& pb : v) {
       if (pins_[pb.first]++) continue;
-      auto& fl = free_[pb.second];  // released during the capture: park it
+      auto fit = free_.find(real(pb.first));  // released during the capture: park it
+      if (fit == free_.end()) continue;
+      auto& fl = fit->second;
       for (size_t i = 0; i < fl.size(); ++i)
         if (fl[i] == pb.first) {
           fl[i] = fl.back();
           fl.pop_back();
-          parked_[pb.first] = pb.second;
+          parked_[pb.first] = real(pb.first);
           break;
         }
+      if (fl.empty()) free_.erase(fit);
     }
   }
   void unpin(const std::vector<std::pair<void*, size_t>>& v) {
@@ -250,14 +328,14 @@ class DevicePool {
       pins_.erase(it);
       auto pk = parked_.find(pb.first);
       if (pk != parked_.end()) {
-        free_[pk->second].push_back(pk->first);
+        free_[real(pk->first)].push_back(pk->first);
         parked_.erase(pk);
       }
     }
   }
   ~DevicePool() {
     std::lock_guard<std::recursive_mutex> lk(mu());
-    for (auto& kv : parked_) free_[kv.second].push_back(kv.first);
+    for (auto& kv : parked_) free_[real(kv.first)].push_back(kv.first);
     parked_.clear();
     trim();
     stats()[0] -= (double)held_;  // (buffers still handed out are released with their owners)
@@ -266,8 +344,16 @@ class DevicePool {
   }
 
  private:
+  void free_one(void* p) {
+    const size_t b = real(p);
+    hipFree(p);
+    held_ -= b;
+    add_held(-(double)b);
+    real_.erase(p);
+  }
   size_t held_ = 0;
-  std::unordered_map<size_t, std::vector<void*>> free_;
+  std::map<size_t, std::vector<void*>> free_;  // allocated size -> cached buffers
+  std::unordered_map<void*, size_t> real_;     // every buffer this pool allocated -> its size
   bool tracking_ = false;
   std::unordered_map<void*, size_t> touched_, parked_;
   std::unordered_map<void*, int> pins_;

@@ -971,6 +971,12 @@ int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const LimbSet& own
     if ((G.logN != 15 && G.logN != 16) || N != (1 << G.logN) || ngroup != 1) return -1;
     if (G.fwd_rows) {
       if (beta > 16 || G.d_gstride) return -1;
+      // (4 + 2 beta) x 2 KiB of LDS: up to 72 KiB at beta = 16, past the
+      // 64 KiB a launch gets without the attribute (set once, for the largest)
+      static const bool lds_attr = hipFuncSetAttribute((const void*)ks_mac_full_kernel,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (4 + 2 * 16) * 256 * 8) == hipSuccess;
+      if (!lds_attr) return -1;
       hipLaunchKernelGGL(ks_mac_full_kernel, ew_grid(N, rows), dim3(256), (size_t)(4 + 2 * beta) * 256 * 8, st, out, D,
                          own, G, beta, tb, N);
       return 0;

@@ -14,17 +14,22 @@ __device__ __forceinline__ void buf_ld2(__amdgpu_buffer_rsrc_t r, u64& x, u64& y
   x = ((u64)v[1] << 32) | v[0];
   y = ((u64)v[3] << 32) | v[2];
 }
+// timing switch: the cache-policy bits of the one-pass kernels' output
+// stores (2 = non-temporal); 0 in the product
+#ifndef NTT_ST_AUX
+#define NTT_ST_AUX 0
+#endif
 __device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, u64 x, u64 y, int voff, int soff) {
   __attribute__((ext_vector_type(4))) unsigned v = {(unsigned)x, (unsigned)(x >> 32), (unsigned)y,
                                                    (unsigned)(y >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, NTT_ST_AUX);
 }
 __device__ __forceinline__ u64 buf_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, u64 v, int voff, int soff) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), r,
-                                        voff, soff, 0);
+                                        voff, soff, NTT_ST_AUX);
 }
 
 #define NTT_FENCE() __builtin_amdgcn_sched_barrier(0)

@@ -842,6 +842,38 @@ def test_basis_extension_modes(torch_cuda, oracle_mod):
     lib.DeleteScheme()
 
 
+def test_one_prime_gadget_wide_fused_mac(torch_cuda, oracle_mod, monkeypatch):
+    """one P prime (K = 1) makes one gadget digit per Q limb, so a
+    16-limb chain has beta = 16; with the INTT fusion unlimited
+    (ORION_NTT_IFUSE_MAXR=1000) the key switch takes ks_mac_full_kernel, whose
+    LDS is (4 + 2 beta) x 2 KiB = 72 KiB -- past the default 64 KiB a launch
+    gets without its attribute.  mul_relin -> rescale at N = 2^15, batch 1
+    and 2, bit-exact vs the oracle."""
+    monkeypatch.setenv("ORION_NTT_IFUSE_MAXR", "1000")
+    from orion_amd.backend import HipLibrary
+    logq, logp = [60] + [40] * 15, [61]
+    lib = HipLibrary().new_scheme(15, logq, logp, 40, h=192, seed=717)
+    mods = lib.moduli()
+    orc = oracle_mod.Oracle(15, mods, len(logq), len(logp))
+    lib.GenerateSecretKey()
+    lib.GeneratePublicKey()
+    lib.GenerateRelinearizationKey()
+    rlk = lib.export_relin_key()
+    rng = np.random.default_rng(7171)
+    level = len(logq) - 1
+    for B in (1, 2):
+        x = rand_ct(rng, mods, level, orc.N, B=B)
+        ct = lib.import_ciphertext(x, 2.0 ** 40)
+        cc = lib.MulRelinCiphertextNew(ct, ct)
+        lib.Rescale(cc)
+        got = lib.export_ciphertext(cc)
+        for b in range(B):
+            assert np.array_equal(got[b], orc.rescale(orc.mul_relin(x[b], x[b], rlk, level), level)), (B, b)
+        lib.DeleteCiphertext(cc)
+        lib.DeleteCiphertext(ct)
+    lib.DeleteScheme()
+
+
 @pytest.mark.parametrize("env", [{}, {"ORION_NTT_TAILSPLIT": "1"}, {"ORION_NTT_IFUSE": "0"},
                                  {"ORION_NTT_AUT_FUSE": "0"}, {"ORION_BEXT_MODES": "0", "ORION_NTT_IFUSE_MAXR": "1000"}])
 @pytest.mark.parametrize("B", [2, 12, 40])

@@ -98,8 +98,9 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
 
     def log_window(name, tag):
         """[c0, c1): the calls between the log's last "# <tag> begin" and
-        "# <tag> end" markers (bench.py: "timed" = the timed steps, "solo" =
-        the profiled step of the whole batch on one pipeline), or None."""
+        "# <tag> end" markers (bench.py: "timed" = the timed steps, "single" =
+        the timed steps of the whole batch on one pipeline, "solo" = one fully
+        profiled step of it), or None."""
         p = os.path.join(d, f"ntt_log_{name}.txt")
         if not os.path.exists(p):
             return None
@@ -169,7 +170,9 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
         if log is None:
             continue
         cnt = "FETCH_SIZE" if name == "pmc_fetch" else "WRITE_SIZE"
-        sw = log_window(name, "solo")  # the single-pipeline step the bench's roofline is taken on
+        # the single-pipeline window the bench's roofline is taken on: "single"
+        # (round 6: the K timed steps on one context), else "solo" (one profiled step)
+        sw = log_window(name, "single") or log_window(name, "solo")
         for call, drs, alg, jobs in priced(order, log):
             if jobs < 64:
                 continue
@@ -200,7 +203,8 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
     n_us = n_b = n_s = 0.0
     klog = ntt_log("kt")
     win = log_window("kt", "timed")
-    swin = log_window("kt", "solo")
+    swin = log_window("kt", "single") or log_window("kt", "solo")
+    rwin = "single" if log_window("kt", "single") else "solo"
     w_iv, w_b, w_s, w_l = [], 0.0, 0.0, 0
     s_us, s_b, s_s, s_l = 0.0, 0.0, 0.0, 0
     if klog is not None:
@@ -282,7 +286,7 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
              "frac_fused": n_b / (n_us * 1e-6) / 1e9 / 8000.0 if n_us else None,
              "frac_strict": n_s / (n_us * 1e-6) / 1e9 / 8000.0 if n_us else None,
              "timed_window": timed,
-             "solo_window": {"calls": s_l, "avg_launch_us": s_us / s_l if s_l else None,
+             "solo_window": {"window": rwin, "calls": s_l, "avg_launch_us": s_us / s_l if s_l else None,
                              "strict_bytes_per_launch": s_s / s_l if s_l else None,
                              "frac_strict": s_s / (s_us * 1e-6) / 1e9 / 8000.0 if s_us else None,
                              "frac_fused": s_b / (s_us * 1e-6) / 1e9 / 8000.0 if s_us else None}
