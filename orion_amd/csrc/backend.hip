@@ -472,7 +472,7 @@ class HandlePool {  // lowest-free-id reuse (minheap.go:46-64)
     } else {
       id = next_++;
     }
-    map_[id] = Entry{std::make_unique<T>(std::move(v)), g_birth.fetch_add(1)};
+    map_[id] = Entry{std::make_unique<T>(std::move(v)), g_birth.fetch_add(1), false};
     if (born) born->insert(id);
     return id;
   }
@@ -488,7 +488,7 @@ class HandlePool {  // lowest-free-id reuse (minheap.go:46-64)
       HandlePool* o = resolver() ? resolver()(own) : nullptr;
       if (!o || o == this) throw std::runtime_error("handle not found: " + std::to_string(id));
       unsigned long long birth = 0;
-      T& v = o->get_local(id, &birth);
+      T& v = o->get_local(id, &birth, true);
       if (check()) check()(v);
       if (hook()) hook()(own, birth);
       return v;
@@ -518,10 +518,21 @@ class HandlePool {  // lowest-free-id reuse (minheap.go:46-64)
     HandlePool* o = resolver() ? resolver()(own) : nullptr;
     return o ? o : this;
   }
+  // an object another context has read goes only once the device has drained:
+  // that context's kernels may still read its buffer, which the owner's pool
+  // would otherwise hand out again in the owner's stream order only
   void del(int id) {
     HandlePool* o = owner_pool(id);
-    std::lock_guard<std::mutex> lk(o->mu_);
-    if (o->map_.erase(id)) o->free_.insert(id);
+    std::unique_ptr<T> dead;
+    {
+      std::lock_guard<std::mutex> lk(o->mu_);
+      auto it = o->map_.find(id);
+      if (it == o->map_.end()) return;
+      if (it->second.foreign) (void)hipDeviceSynchronize();
+      dead = std::move(it->second.obj);
+      o->map_.erase(it);
+      o->free_.insert(id);
+    }
   }
   void reset() {
     std::lock_guard<std::mutex> lk(mu_);
@@ -548,12 +559,14 @@ class HandlePool {  // lowest-free-id reuse (minheap.go:46-64)
   struct Entry {
     std::unique_ptr<T> obj;
     unsigned long long birth = 0;
+    bool foreign = false;  // read by another context
   };
-  T& get_local(int id, unsigned long long* birth) {
+  T& get_local(int id, unsigned long long* birth, bool foreign = false) {
     std::lock_guard<std::mutex> lk(mu_);
     auto it = map_.find(id);
     if (it == map_.end()) throw std::runtime_error("handle not found: " + std::to_string(id));
     if (birth) *birth = it->second.birth;
+    if (foreign) it->second.foreign = true;
     return *it->second.obj;
   }
   mutable std::mutex mu_;
