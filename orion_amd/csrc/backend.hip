@@ -457,6 +457,13 @@ class HandlePool {  // lowest-free-id reuse (minheap.go:46-64)
     static Hook h = nullptr;
     return h;
   }
+  // run on every foreign object get() returns (a capture on the acting
+  // context keeps that object's device buffers alive with its graph)
+  using Hold = void (*)(const T&);
+  static Hold& hold() {
+    static Hold h = nullptr;
+    return h;
+  }
   // run on every object get() returns (a poisoned ciphertext throws)
   using Check = void (*)(const T&);
   static Check& check() {
@@ -491,6 +498,7 @@ class HandlePool {  // lowest-free-id reuse (minheap.go:46-64)
       T& v = o->get_local(id, &birth, true);
       if (check()) check()(v);
       if (hook()) hook()(own, birth);
+      if (hold()) hold()(v);
       return v;
     }
     T& v = get_local(id, nullptr);
@@ -675,6 +683,9 @@ struct Context {
     std::vector<std::shared_ptr<void>> holds;
   };
   std::set<int> capture_born;  // ciphertext ids created inside the open capture
+  // buffers of other contexts' objects read inside the open capture (a
+  // pipeline's graph reads the scheme's transforms and plaintexts)
+  std::vector<std::shared_ptr<void>> capture_holds;
   std::map<int, GraphRec> graphs;
   int next_graph = 0;
   bool capturing = false;
@@ -788,6 +799,7 @@ struct Context {
     prof = 0;
     pool.begin_track();
     capture_born.clear();
+    capture_holds.clear();
     cts.born = &capture_born;
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
     capturing = true;
@@ -830,6 +842,8 @@ struct Context {
     pool.pin(touched);
     r.pins = std::move(touched);
     r.holds = graph_holds();
+    r.holds.insert(r.holds.end(), capture_holds.begin(), capture_holds.end());
+    capture_holds.clear();
     const int id = next_graph++;
     graphs[id] = std::move(r);
     return id;
@@ -3340,6 +3354,20 @@ static const bool g_hooks_set = [] {
   HandlePool<Context::PolyFn>::hook() = [](int o, unsigned long long b) { foreign_order(o, b, false); };
   HandlePool<Ciphertext>::check() = [](const Ciphertext& c) {
     if (!c.poison.empty()) throw std::runtime_error(c.poison);
+  };
+  HandlePool<Ciphertext>::hold() = [](const Ciphertext& c) {
+    if (t_act && t_act->capturing && c.poly.buf) t_act->capture_holds.push_back(c.poly.buf);
+  };
+  HandlePool<Plaintext>::hold() = [](const Plaintext& p) {
+    if (t_act && t_act->capturing && p.poly.buf) t_act->capture_holds.push_back(p.poly.buf);
+  };
+  HandlePool<LinTrans>::hold() = [](const LinTrans& t) {
+    if (!t_act || !t_act->capturing) return;
+    for (auto& kv : t.diags)
+      if (kv.second.poly.buf) t_act->capture_holds.push_back(kv.second.poly.buf);
+    for (auto& kv : t.sdiags)
+      if (kv.second.buf) t_act->capture_holds.push_back(kv.second.buf);
+    if (t.plan) t_act->capture_holds.push_back(t.plan);
   };
   return true;
 }();

@@ -13,26 +13,22 @@ def main():
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"] for r in rows]
-    # the pass length: the smallest period P under which the middle half of
-    # the trace repeats; the timed passes are the run of STEPS periods ending
-    # where the repetition stops
+    # the pass length: the smallest period P under which the last quarter of
+    # the trace repeats (bench.py ends with the timed passes, the same passes
+    # on one context, and one fully profiled pass; the setup's launches --
+    # keygen, the transforms' diagonal encodes -- come first); the timed
+    # passes are the STEPS periods before the final (profiled) one
     n = len(names)
     per = None
-    # (the window starts at n/4, or at n/2 when the setup's launches fill the
-    # first half of the trace)
-    for start in (n // 4, n // 2):
-        for P in range(20, n // 4):
-            lo, hi = start, 3 * n // 4 - P
-            if hi > lo and sum(names[i] == names[i + P] for i in range(lo, hi)) >= 0.995 * (hi - lo):
-                per = P
-                break
-        if per is not None:
+    lo = n - n // 4
+    for P in range(20, n // 6):
+        hi = n - P
+        if hi > lo and sum(names[i] == names[i + P] for i in range(lo, hi)) >= 0.995 * (hi - lo):
+            per = P
             break
     if per is None:
         raise SystemExit("no period found")
-    end = 3 * n // 4
-    while end + per < n and names[end] == names[end - per]:
-        end += 1
+    end = n - per
     last = rows[end - per * steps:end]
     t0, t1 = int(last[0]["Start_Timestamp"]), int(last[-1]["End_Timestamp"])
     busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in last)
