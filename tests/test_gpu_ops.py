@@ -439,6 +439,16 @@ def test_thread_pipelines_small(torch_cuda):
             for o in outs:
                 assert np.array_equal(lib.export_ciphertext(o), ref)  # read from the main thread
                 lib.DeleteCiphertext(o)  # deleted on its own context
+        # a pipeline captures its pass into a hipGraph (the scheme's compiled
+        # transforms held by the graph); any thread launches it on the
+        # pipeline's stream (graph ids route like handles)
+        gid, gout = pipes.run_one(0, lambda: st.capture(cts[0]))
+        assert gid >> 20 == pipes.contexts[0]
+        lib.OrionHipGraphLaunch(gid)
+        lib.OrionHipSynchronize()
+        assert np.array_equal(lib.export_ciphertext(gout), ref)
+        lib.OrionHipGraphDestroy(gid)
+        lib.DeleteCiphertext(gout)
         with pytest.raises(RuntimeError, match="changed only by the context"):
             lib.Rescale(cts[0])
         dec = pipes.run_one(1, lambda: st.decrypt_output(cts[1]))  # the pipelines share the scheme's secret
@@ -608,3 +618,76 @@ def test_thread_pipeline_bootstrap_and_polynomials(torch_cuda):
     finally:
         pipes.close()
     lib.DeleteScheme()
+
+
+def test_thread_pipelines_stress_cross_context(torch_cuda):
+    """Four frontend threads on their own pipeline contexts hammer the C-ABI at
+    once (the LoLA N=2^13 op stream -- linear transforms, rotate-and-adds,
+    mul_relin, rescales -- then mul_relin + rotation on its output), each
+    also reading the other threads' ciphertexts (AddCiphertextNew across
+    contexts, ordered after the owner's queued work) and deleting handles
+    another thread made (routed to the owner's context).  Every result equals the one computed by the scheme thread
+    alone; no handle leaks; the thread-local last error of one thread is not
+    seen by another."""
+    import numpy as np
+    from orion_amd.replay import OrionStream, Pipelines
+    st = OrionStream("lola_n13", seed=55)
+    st.keygen()
+    st.compile()
+    lib = st.lib
+    lib.AddRotationKey(7)
+    rng = np.random.default_rng(56)
+    imgs = rng.standard_normal((8,) + np.asarray(st.reference_input()).shape[1:]).astype(np.float32)
+    ct = st.encrypt_batch(imgs)
+    x, scale = lib.export_ciphertext(ct), lib.GetCiphertextScaleF(ct)
+    shards = [x[2 * i:2 * i + 2] for i in range(4)]
+
+    def chain(h):
+        out = st.forward(h)
+        lib.DeleteCiphertext(h)
+        sq = lib.MulRelinCiphertextNew(out, out)  # (the stream ends at level 0: no rescale)
+        r = lib.RotateNew(sq, 7)
+        res = lib.export_ciphertext(r)
+        for k in (out, sq, r):
+            lib.DeleteCiphertext(k)
+        return res
+
+    ref = [chain(lib.import_ciphertext(s, scale)) for s in shards]
+    live0 = set(lib.GetLiveCiphertexts())
+    pipes = Pipelines(lib, 4, device=0)
+    try:
+        ins = pipes.run([(lambda s=s: lib.import_ciphertext(s, scale)) for s in shards])
+        for rep in range(3):
+            outs = pipes.run([(lambda h=h: chain(lib.CloneCiphertext(h))) for h in ins])
+            for i in range(4):
+                assert np.array_equal(outs[i], ref[i]), (rep, i)
+        # cross-context reads: thread i adds thread (i+1)'s input into a new ciphertext of its own
+        sums = pipes.run([(lambda i=i: lib.AddCiphertextNew(ins[i], ins[(i + 1) % 4])) for i in range(4)])
+        for i in range(4):
+            got = lib.export_ciphertext(sums[i])
+            qs = np.array(lib.moduli()[:got.shape[2]], dtype=np.uint64)[None, None, :, None]
+            a = shards[i].astype(object)
+            b = shards[(i + 1) % 4].astype(object)
+            assert np.array_equal(got, ((a + b) % qs.astype(object)).astype(np.uint64)), i
+        # an in-place op on another thread's ciphertext is refused; each
+        # thread's error stays its own
+        errs = pipes.run([(lambda i=i: _try(lambda: lib.Rescale(ins[(i + 1) % 4]))) for i in range(4)])
+        assert all("changed only by the context" in e for e in errs), errs
+        assert lib.lib.OrionHipLastError() == b""
+        # deletes from other threads go to the owner's context
+        pipes.run([(lambda i=i: lib.DeleteCiphertext(sums[(i + 2) % 4])) for i in range(4)])
+        pipes.run([(lambda i=i: lib.DeleteCiphertext(ins[(i + 3) % 4])) for i in range(4)])
+        left = pipes.run([lambda: lib.GetLiveCiphertexts()] * 4)
+        assert all(len(v) == 0 for v in left), left
+    finally:
+        pipes.close()
+    assert set(lib.GetLiveCiphertexts()) == live0
+    lib.DeleteScheme()
+
+
+def _try(fn):
+    try:
+        fn()
+    except RuntimeError as e:
+        return str(e)
+    return ""
