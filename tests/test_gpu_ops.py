@@ -405,19 +405,22 @@ def test_library_deferral_matches_undeferred(torch_cuda, monkeypatch):
         assert np.array_equal(outs[0], outs[1]), name
 
 
-def test_thread_pipelines_small(torch_cuda):
+@pytest.mark.parametrize("name", ["lola_n13", "lola_n13_ci", "mlp_n14"])
+def test_thread_pipelines_small(torch_cuda, name):
     """Thread-affine pipelines (OrionHipThreadPipelines): two frontend threads
     each run the unchanged op stream's forward() (one compiled stream: the
     scheme's keys and transforms) on a ciphertext they imported themselves; the
     library binds each thread to a context of its own (own stream, pool,
     handle range), and each output equals the scheme thread's single run bit
-    for bit -- LoLA N=2^13 at batch 3.  Handles are unique across contexts:
+    for bit -- at batch 3, LoLA N=2^13 on the Standard and the
+    ConjugateInvariant ring (configs/lola.yml) and the MLP at N=2^14
+    (BASELINE C2).  Handles are unique across contexts:
     the main thread reads and deletes the pipelines' outputs; an in-place op
     on another context's ciphertext is refused; DeleteScheme removes the
     pipelines."""
     import numpy as np
     from orion_amd.replay import OrionStream, Pipelines
-    st = OrionStream("lola_n13", seed=91)
+    st = OrionStream(name, seed=91)
     st.keygen()
     st.compile()
     lib = st.lib
