@@ -4,11 +4,13 @@ Metric (BASELINE.json): encrypted images/sec (LoLA, N=2^15) + NTT achieved
 HBM GB/s vs peak.  A "step" is one FHE forward pass `net(ct)` of the LoLA op
 stream (the exact backend-call sequence the reference frontend emits, see
 orion_amd/replay.py) over one batch of B images per GPU, every ciphertext
-already resident in HBM.  Multi-GPU: one process per GPU, independent image
+already resident in HBM, run as --pipelines frontend threads of B/P images
+(each on a pipeline context of its own); the same steps on one context are
+timed right after (value_single_pipeline, and the roofline).  Multi-GPU: one process per GPU, independent image
 shards (weak scaling), evaluation keys generated on rank 0 and broadcast over
 RCCL/xGMI once before timing; no collective inside the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--pipelines P]
 
 --gpus N without a torch.distributed.run environment starts N rank processes
 itself (one per GPU, fresh interpreters, before anything touches the GPU);
@@ -85,8 +87,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("ORION_BENCH_BATCH", 64)))
-    # the GPU's batch as P concurrent pipelines of batch/P images each (peer
-    # contexts sharing the keys, their ops interleaved on P HIP streams)
+    # the GPU's batch as P frontend threads of batch/P images each, every
+    # thread on a pipeline context of its own (the scheme's keys and compiled
+    # transforms, its own HIP stream): their kernels run concurrently
     ap.add_argument("--pipelines", type=int, default=int(os.environ.get("ORION_BENCH_PIPELINES", 2)))
     ap.add_argument("--workload", default="lola_n15")
     ap.add_argument("--no-cpu-baseline", action="store_true")

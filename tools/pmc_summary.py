@@ -195,7 +195,7 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
     # duration = the dispatches' summed time, priced with the logged
     # limb-transform counts; setup calls (keygen, < 64 jobs) are excluded
     kt = os.path.join(d, "kt_kernel_trace.csv")
-    # issue order (Dispatch_Id): with peer pipelines the kernels of two streams
+    # issue order (Dispatch_Id): with pipeline threads the kernels of two streams
     # start out of call order, but they are dispatched in it
     tr = sorted(rows(kt), key=lambda r: int(r["Dispatch_Id"])) if os.path.exists(kt) else []
     tr = [r for r in tr if "ntt" in r["Kernel_Name"]]
@@ -229,7 +229,7 @@ def main(tag, workload="lola_n15", batch=64, logn=15, resnet=False, out=None):
                 n_b += alg
                 n_s += 16.0 * N * jobs
     # the timed window: the wall-clock union of its NTT dispatch intervals (the
-    # bench line's definition with peer pipelines) and their summed durations
+    # bench line's definition with pipeline threads) and their summed durations
     timed = None
     if w_iv:
         w_iv.sort()
