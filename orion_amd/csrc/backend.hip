@@ -4584,6 +4584,7 @@ ArrayResultByte SerializeDiagonal(int tid, int diagIdx) {
   T.diags.erase(it);
   T.sdiags.erase(key);
   T.plan_dirty = true;
+  c.lts.touch(tid);  // (a pipeline reading it waits for this context's work again)
   return to_bytes(bytes);
   API_END(r)
 }
@@ -4605,6 +4606,7 @@ void LoadPlaintextDiagonal(char* data, unsigned long len, int tid, unsigned long
   c.upload(p.poly, host);
   T.diags[(int)diagIdx & (c.slots - 1)] = p;
   T.plan_dirty = true;
+  c.lts.touch(tid);
   API_END_VOID
 }
 void RemovePlaintextDiagonals(int tid) {
@@ -4612,6 +4614,7 @@ void RemovePlaintextDiagonals(int tid) {
   ctx().lts.get(tid).diags.clear();
   ctx().lts.get(tid).sdiags.clear();
   ctx().lts.get(tid).plan_dirty = true;
+  ctx().lts.touch(tid);
   API_END_VOID
 }
 void RemoveRotationKeys(void) {
