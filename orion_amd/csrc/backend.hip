@@ -5147,6 +5147,8 @@ static void each_ctx(F f) {
     Context* c = g_slot[i].get();
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     f(*c);
+    // the bootstrapping contexts the context owns (their launches run under its lock)
+    for (auto& kv : c->btp_ctx) f(*kv.second);
   }
 }
 extern "C" {

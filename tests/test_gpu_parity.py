@@ -509,6 +509,14 @@ def test_bootstrap_functional(torch_cuda, h):
     out = lib.Bootstrap(ct, n)
     assert lib.GetCiphertextLevel(out) == len(BTP_LOGQ) - 1
     assert lib.GetCiphertextScaleF(out) == 2.0 ** 40
+    # the bootstrapping context's launches are in the profile counters (its
+    # CoeffsToSlots / SlotsToCoeffs transforms run lt_bsgs; none run outside it here)
+    lib.OrionHipProfileReset()
+    lib.OrionHipProfile(1)
+    lib.DeleteCiphertext(lib.Bootstrap(ct, n))
+    lib.OrionHipProfile(0)
+    prof = lib.profile_read()
+    assert prof["lt_bsgs"]["launches"] > 0 and prof["ntt_fwd"]["ms"] > 0, prof
     dec = lib.decode_f64(lib.Decrypt(out))
     err = np.abs(dec - vals.astype(np.float64))
     # Lattigo's default message ratio (2^8) and degree-30 CosDiscrete cosine:

@@ -65,6 +65,19 @@ def main():
                           "mae_vs_cleartext": mae, "argmax_ok": bool(np.argmax(res[0]) == np.argmax(exp)),
                           "setup_s": round(setup, 1), "pools": st.lib.pool_stats()}), flush=True)
         st.lib.DeleteCiphertext(out)
+        if os.environ.get("PROF") == "1":
+            # one more forward with HIP events around every launch: per-category
+            # kernel ms and algorithmic GB/s (profiling serialises the host a little)
+            st.lib.OrionHipProfileReset()
+            st.lib.OrionHipProfile(1)
+            st.lib.DeleteCiphertext(st.forward(ct))
+            st.lib.OrionHipSynchronize()
+            st.lib.OrionHipProfile(0)
+            br = st.lib.profile_read()
+            print(json.dumps({"batch": B, "kernel_ms": {k: round(v["ms"], 2) for k, v in br.items()},
+                              "launches": {k: v["launches"] for k, v in br.items()},
+                              "algorithmic_gbs": {k: round(v["bytes"] / v["ms"] / 1e6, 1)
+                                                  for k, v in br.items() if v["ms"] > 0}}), flush=True)
         st.lib.DeleteCiphertext(ct)
 
 
