@@ -729,6 +729,10 @@ struct Context {
       hipEventDestroy(r.e1);
     }
     for (auto e : ev_free) hipEventDestroy(e);
+    for (auto e : cs_ev)
+      if (e) hipEventDestroy(e);
+    for (auto s : cs_stream)
+      if (s) hipStreamDestroy(s);
     if (own_stream && stream) hipStreamDestroy(stream);
   }
 
@@ -1083,6 +1087,36 @@ struct Context {
   // job of every other CU in persistent launches of >= ntt_stagger_min rounds
   int ntt_stagger = getenv("ORION_NTT_STAGGER") ? atoi(getenv("ORION_NTT_STAGGER")) : 0;
   int ntt_stagger_min = getenv("ORION_NTT_STAGGER_MIN") ? atoi(getenv("ORION_NTT_STAGGER_MIN")) : 2;
+  // co-split (timing switch): a one-pass launch of >= ntt_cosplit_min jobs
+  // gives the fraction ntt_cosplit of its jobs (its tail: the float64 limbs
+  // under job order 2) to the two-pass kernels, run concurrently on a
+  // disjoint set of CUs: the one-pass kernel is bound by one job per CU with
+  // serialised phases (~45% of HBM streaming), the two-pass kernels by HBM
+  // (86-89%), so the two can share the chip.  ntt_cosplit_q quarters of every
+  // XCD's CUs take the one-pass part (CU-masked streams, joined to the
+  // context's stream by events)
+  double ntt_cosplit = getenv("ORION_NTT_COSPLIT") ? atof(getenv("ORION_NTT_COSPLIT")) : 0.0;
+  int ntt_cosplit_min = getenv("ORION_NTT_COSPLIT_MIN") ? atoi(getenv("ORION_NTT_COSPLIT_MIN")) : 512;
+  int ntt_cosplit_q = getenv("ORION_NTT_COSPLIT_Q") ? atoi(getenv("ORION_NTT_COSPLIT_Q")) : 2;
+  hipStream_t cs_stream[2] = {nullptr, nullptr};
+  hipEvent_t cs_ev[3] = {nullptr, nullptr, nullptr};
+  int cs_cus = 0;  // CUs of the one-pass side
+  void cosplit_init() {
+    if (cs_stream[0]) return;
+    const int n = cus(), words = (n + 31) / 32;
+    // bit i in the one-pass set when (i / 8) % 4 < q: a quarter-granular share
+    // of every XCD whether the mask's CUs are numbered XCD-major or interleaved
+    std::vector<uint32_t> ma(words, 0), mb(words, 0);
+    cs_cus = 0;
+    for (int i = 0; i < n; ++i) {
+      const bool a = (i / 8) % 4 < ntt_cosplit_q;
+      (a ? ma : mb)[i / 32] |= 1u << (i % 32);
+      cs_cus += a;
+    }
+    HIPCHK(hipExtStreamCreateWithCUMask(&cs_stream[0], words, ma.data()));
+    HIPCHK(hipExtStreamCreateWithCUMask(&cs_stream[1], words, mb.data()));
+    for (auto& e : cs_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   // ORION_NTT_LOG=path: one line per NTT call ("<dispatches> <jobs> <epi> <inv>
   // <pro> <intjobs> <family>": dispatches = kernel launches of the call (1 or
   // 2); epi = the epilogue (NTT_EPI_*); pro = the prologue; intjobs =
@@ -1280,6 +1314,39 @@ struct Context {
     }
     if (io.ifuse) throw std::runtime_error("NTT: a fused INTT columns pass needs the latency kernels");
     cus();
+    if (ntt_cosplit > 0 && logN == 15 && !ci && io.jobs >= ntt_cosplit_min && !capturing) {
+      // jobs [0, j1) on the one-pass kernel (one persistent workgroup per CU
+      // of its share), jobs [j1, jobs) on the two-pass kernels through a
+      // compact scratch, concurrently on the two CU-masked streams
+      cosplit_init();
+      const int j2 = std::min(io.jobs - 1, std::max(1, (int)lround(io.jobs * ntt_cosplit))), j1 = io.jobs - j2;
+      Scope sc(this, cat, per * io.jobs, strict * io.jobs);
+      Poly scratch = alloc(1, 1, j2);
+      NttIO a = io;
+      a.njob = j1;
+      a.grid = cs_cus;
+      NttIO b = io;
+      b.mid = ls(scratch, 0, 1, {0}, {0});
+      b.mid_compact = 1;
+      b.job0 = j1;
+      b.njob = j2;
+      HIPCHK(hipEventRecord(cs_ev[0], stream));
+      HIPCHK(hipStreamWaitEvent(cs_stream[0], cs_ev[0], 0));
+      HIPCHK(hipStreamWaitEvent(cs_stream[1], cs_ev[0], 0));
+      if (orion_launch_ntt_io(logN, a, d_tb, inv, cs_stream[0])) throw std::runtime_error("NTT launch failed");
+      const bool small = j2 <= ntt2s_below;
+      if (small ? orion_launch_ntt2s(logN, b, d_tb, inv, cs_stream[1]) : orion_launch_ntt2(logN, b, d_tb, inv, cs_stream[1]))
+        throw std::runtime_error("NTT launch failed");
+      HIPCHK(hipEventRecord(cs_ev[1], cs_stream[0]));
+      HIPCHK(hipEventRecord(cs_ev[2], cs_stream[1]));
+      HIPCHK(hipStreamWaitEvent(stream, cs_ev[1], 0));
+      HIPCHK(hipStreamWaitEvent(stream, cs_ev[2], 0));
+      a.jobs = j1;
+      b.jobs = j2;
+      log_ntt(1, a, inv);
+      log_ntt(small ? 3 : 2, b, inv);
+      return;
+    }
     const int tail = io.jobs % n_cu;
     if (ntt_tailsplit && logN == 15 && !ci && io.jobs > n_cu && tail > 0 && tail <= ntt_tailsplit_max) {
       // the whole rounds on the one-pass kernel, the partial last round (the

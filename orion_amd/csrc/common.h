@@ -600,6 +600,7 @@ struct NttIO {
   // mid is a compact scratch of njob rows (row = job - job0), reused by every
   // chunk so the intermediate can stay in the Infinity Cache
   int job0, njob, mid_compact;
+  int grid;  // one-pass persistent launch: workgroups (0 = one per CU), e.g. a CU-masked co-split share
   u64 s[ORION_MAXLIMB], ss[ORION_MAXLIMB];
   unsigned char lord[ORION_MAXLIMB];  // order 2: dispatch order of dst's limbs
   // NTT_PRO_BEXT: the basis-extension tables, and per dst limb its table and

@@ -443,7 +443,8 @@ int launch_ntt_ring(const NttIO& io, const DeviceTables* tb, bool inverse, hipSt
   if (io.jobs != total || io.njob < 0 || io.njob > total || io.job0 != 0) return -1;
   const int jobs = io.njob > 0 ? io.njob : total;  // njob: the first njob jobs only (a split launch)
   const size_t lds = (size_t)(N + N / 32) * sizeof(u32);
-  const dim3 g(g_ntt_grid > 0 && jobs > g_ntt_grid ? g_ntt_grid : jobs), blk(NttGeom<LOGN>::T);
+  const int gmax = io.grid > 0 ? io.grid : g_ntt_grid;
+  const dim3 g(gmax > 0 && jobs > gmax ? gmax : jobs), blk(NttGeom<LOGN>::T);
   if (inverse) {
     if (io.pro != NTT_PRO_LOAD || io.epi != NTT_EPI_STORE) return -1;
     hipLaunchKernelGGL((ntt_inv_kernel<LOGN, CI>), g, blk, lds, st, io, tb);
