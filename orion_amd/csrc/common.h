@@ -557,6 +557,112 @@ __device__ __forceinline__ void bext_target2(const BextTarget* __restrict__ R, i
   o0 = a0 >= q ? a0 - q : a0;
   o1 = a1 >= q ? a1 - q : a1;
 }
+// A load through the constant address space: with a wave-uniform address it
+// is a scalar (SMEM) load into SGPRs, issued where it is written
+template <class T>
+__device__ __forceinline__ T cload(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)p;
+}
+// The constants of an extension of at most 2 sources to one target, for a
+// kernel that forms several coefficients late in its run (the fused INTT
+// columns + forward kernel, ntt2s_ifwd_cols_p): loaded once, at the start,
+// through the scalar cache -- read where bext_prep / bext_target_sel read
+// them, the table fields were a chain of dependent vector loads per
+// coefficient after the INTT half.  bext2_apply is their arithmetic, bit for
+// bit (bext_prep<2> then bext_target_sel<2>: the centered, BEXT_NARROW and
+// BEXT_LAZY cases).
+struct Bext2 {
+  u64 chalf, sq[2], qhi[2], qhis[2];
+  double qinv_f[2], qf[2];
+  u64 q, vS0, vS1, vS2, qh[2], qhs[2], nS;
+  double tinv, tinv32, qd;
+  int centered, ns, mode;
+};
+__device__ __forceinline__ Bext2 bext2_load(const BasisExtTable* T, int ti) {  // T, ti wave-uniform
+  Bext2 c;
+  c.centered = cload(&T->centered);
+  c.ns = cload(&T->ns);
+  c.chalf = cload(&T->chalf);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    c.sq[i] = cload(&T->sq[i]);
+    c.qhi[i] = cload(&T->qhatinv[i]);
+    c.qhis[i] = cload(&T->qhatinv_s[i]);
+    c.qinv_f[i] = cload(&T->qinv_f[i]);
+    c.qf[i] = cload(&T->qf[i]);
+  }
+  const BextTarget* R = T->tgt + ti;
+  c.mode = cload(&R->mode);
+  c.q = cload(&R->q);
+  c.vS0 = cload(&R->vS[0]);
+  c.vS1 = cload(&R->vS[1]);
+  c.vS2 = cload(&R->vS[2]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    c.qh[i] = cload(&R->qh[i]);
+    c.qhs[i] = cload(&R->qhs[i]);
+  }
+  c.nS = cload(&R->nS);
+  c.tinv = cload(&R->tinv);
+  c.tinv32 = cload(&R->tinv32);
+  c.qd = cload(&R->qd);
+  return c;
+}
+// source side, source i (not centered): y_i = x_i qhatinv_i mod s_i and its
+// term of the float quotient
+__device__ __forceinline__ u64 bext2_src(const Bext2& c, int i, u64 x, double& f) {
+  const u64 y = shoup_mul(x, c.qhi[i], c.qhis[i], c.sq[i]);
+  const double yd = (double)y, rc = c.qinv_f[i];
+  const double q0 = __dmul_rn(yd, rc);
+  const double r = __builtin_fma(-q0, c.qf[i], yd);
+  f = __builtin_fma(r, rc, q0);
+  return y;
+}
+// v from the sources' float terms (summed in source order) or the centered test
+__device__ __forceinline__ u64 bext2_v(const Bext2& c, u64 y0, double f0, double f1) {
+  if (c.centered) return y0 >= c.chalf ? 1 : 0;
+  double vf = __dadd_rn(0.0, f0);
+  if (c.ns > 1) vf = __dadd_rn(vf, f1);
+  return (u64)vf;
+}
+// target side: sum_i y_i (S/s_i mod t) - v S mod t
+__device__ __forceinline__ u64 bext2_tgt(const Bext2& c, u64 y0, u64 y1, u64 v) {
+  const u64 y[2] = {y0, y1};
+  if (c.mode == BEXT_NARROW) {  // bext_target_sel's narrow sum and bext_narrow_red
+    u64 acc = (u64)(u32)v * (u32)c.nS;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (i >= c.ns) break;
+      acc += (u64)(u32)y[i] * (u32)c.qh[i];
+    }
+    u32 hw = (u32)(acc >> 32);
+    asm volatile("" : "+v"(hw));
+    const double ah = (double)hw, al = (double)(u32)acc;
+    const double k = __builtin_rint(__builtin_fma(ah, c.tinv32, al * c.tinv));
+    double r = __builtin_fma(-k, c.qd, ah * 0x1p32) + al;
+    r = r < 0.0 ? r + c.qd : r;
+    return (u64)(u32)r;
+  }
+  const u64 q = c.q, q2 = q << 1, nq = 0 - q;
+  // v in {0, 1, 2} selects vS_v, by masks: as selects between the fields the
+  // compiler made one load from a selected address, which put the struct in scratch
+  const u64 m1 = 0 - (u64)(v == 1), m2 = 0 - (u64)(v == 2);
+  u64 acc = (c.vS0 & ~(m1 | m2)) | (c.vS1 & m1) | (c.vS2 & m2);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if (i >= c.ns) break;
+    acc += shoup_lazy_nq(y[i], c.qh[i], c.qhs[i], nq);
+    acc = acc >= q2 ? acc - q2 : acc;
+  }
+  return acc >= q ? acc - q : acc;
+}
+__device__ __forceinline__ u64 bext2_apply(const Bext2& c, u64 x0, u64 x1) {
+  if (c.centered) return bext2_tgt(c, x0, 0, bext2_v(c, x0, 0.0, 0.0));
+  double f0 = 0.0, f1 = 0.0;
+  const u64 y0 = bext2_src(c, 0, x0, f0);
+  const u64 y1 = c.ns > 1 ? bext2_src(c, 1, x1, f1) : 0;
+  return bext2_tgt(c, y0, y1, bext2_v(c, y0, f0, f1));
+}
 // ---------------------------------------------------------------------------
 // NTT launch descriptor: transform + fused producer (prologue) / consumer
 // (epilogue).  Job j = (c, l, b) over dst's (ncomp, nlimb, nbatch); the limb's

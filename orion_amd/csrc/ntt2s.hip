@@ -30,6 +30,12 @@ namespace {
 #ifndef NTT2S_RW
 #define NTT2S_RW 4
 #endif
+// timing-only ablation (tools/build_ablation.py; 0 in the product): bit 0 =
+// no inverse columns butterflies, bit 1 = no basis-extension / rescale
+// prologue arithmetic in ntt2s_ifwd_cols_p, bit 2 = no forward columns butterflies
+#ifndef NTT2S_ABLATE
+#define NTT2S_ABLATE 0
+#endif
 // 1: ntt2s_ifwd_cols_p fetches its forward twiddles before the INTT half
 #ifndef NTT2S_FWD_PREFETCH
 #define NTT2S_FWD_PREFETCH 0
@@ -357,7 +363,7 @@ __device__ __forceinline__ void s_fwd_cols4_run(const NttIO& io, int job, int c,
       x[2] = from_bits<typename A::T>(lds[e2 * CW + cl]);
       x[3] = from_bits<typename A::T>(lds[e3 * CW + cl]);
     }
-    ct4(ar, x, wa[st], wb[st], wc[st]);
+    if (!(NTT2S_ABLATE & 4)) ct4(ar, x, wa[st], wb[st], wc[st]);
     if (st == 1)  // after 4 stages (float64: |x| stays below 16q)
       for (int i = 0; i < 4; ++i) x[i] = ar.reduce_round(x[i]);
     if (st < NS - 1 || (R & 1)) {
@@ -371,8 +377,8 @@ __device__ __forceinline__ void s_fwd_cols4_run(const NttIO& io, int job, int c,
   if (R & 1) {  // the last stage (bit 0): pairs (4j, 4j + 1), (4j + 2, 4j + 3)
 #pragma unroll
     for (int i = 0; i < 4; ++i) x[i] = from_bits<typename A::T>(lds[(4 * j + i) * CW + cl]);
-    ar.ct(x[0], x[1], wl[0]);
-    ar.ct(x[2], x[3], wl[1]);
+    if (!(NTT2S_ABLATE & 4)) ar.ct(x[0], x[1], wl[0]);
+    if (!(NTT2S_ABLATE & 4)) ar.ct(x[2], x[3], wl[1]);
   }
   u64* mid = mid_row_s(io, job, c, l, b);
 #pragma unroll
@@ -403,8 +409,24 @@ __device__ __forceinline__ void s_fwd_cols4(const NttIO& io, int job, int c, int
   constexpr int R = S2<LOGN>::R, CW = S2<LOGN>::CW, Q = 1 << (R - 2);
   const int t = threadIdx.x, cl = t % CW, j = t / CW, col = tile * CW + cl;
   typename A::T x[4];
+  if constexpr (PRO == NTT_PRO_BEXT) {
+    // the extension's constants once per thread, through the scalar cache (bext2_load)
+    const int k = arg_byte(io.bx_tab, l), ti = arg_byte(io.bx_t, l), s0 = arg_byte(io.bx_s0, k);
+    const Bext2 bc = bext2_load(io.bx + k, ti);
+    const u64* p0 = row_ptr(io.src, c, s0, b);
+    const u64* p1 = row_ptr(io.src, c, s0 + (bc.ns > 1 ? 1 : 0), b);
+    u64 x0[4], x1[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) x[i] = fwd_load<A, PRO>(io, c, l, b, col + ((j + i * Q) << 8), mc, ar, tb);
+    for (int i = 0; i < 4; ++i) {
+      x0[i] = p0[col + ((j + i * Q) << 8)];
+      x1[i] = bc.ns > 1 ? p1[col + ((j + i * Q) << 8)] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = ar.from_u64(bext2_apply(bc, x0[i], x1[i]));
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = fwd_load<A, PRO>(io, c, l, b, col + ((j + i * Q) << 8), mc, ar, tb);
+  }
   s_fwd_cols4_core<A, LOGN>(io, job, c, l, b, tile, x, ar, tw, lds, (int)threadIdx.x);
 }
 
@@ -507,8 +529,10 @@ __device__ __forceinline__ void s_inv_cols4_src(const u64* m0, const u64* m1, co
         if (TWO) y[i] = from_bits<typename A1::T>(l1[e[i] * CW + cl]);
       }
     }
-    gs4(a0, x, wa0[st], wb0[st], wc0[st], false, true);
-    if (TWO) gs4(a1, y, wa1[st], wb1[st], wc1[st], false, true);
+    if (!(NTT2S_ABLATE & 1)) {
+      gs4(a0, x, wa0[st], wb0[st], wc0[st], false, true);
+      if (TWO) gs4(a1, y, wa1[st], wb1[st], wc1[st], false, true);
+    }
     if (st < NS - 1 || (R & 1)) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -524,9 +548,9 @@ __device__ __forceinline__ void s_inv_cols4_src(const u64* m0, const u64* m1, co
       x[i] = from_bits<typename A0::T>(l0[(j + i * Q) * CW + cl]);
       if (TWO) y[i] = from_bits<typename A1::T>(l1[(j + i * Q) * CW + cl]);
     }
-    a0.gs(x[0], x[2], wl0, ((R - 1) & 1) == 1);
-    a0.gs(x[1], x[3], wl0, ((R - 1) & 1) == 1);
-    if (TWO) {
+    if (!(NTT2S_ABLATE & 1)) a0.gs(x[0], x[2], wl0, ((R - 1) & 1) == 1);
+    if (!(NTT2S_ABLATE & 1)) a0.gs(x[1], x[3], wl0, ((R - 1) & 1) == 1);
+    if (TWO && !(NTT2S_ABLATE & 1)) {
       a1.gs(y[0], y[2], wl1, ((R - 1) & 1) == 1);
       a1.gs(y[1], y[3], wl1, ((R - 1) & 1) == 1);
     }
@@ -587,6 +611,8 @@ __global__ void __launch_bounds__(NTT2S_R4 ? S2<LOGN>::CT4 : S2<LOGN>::CT)
     T = io.bx + kt;
     ns = T->ns;
   }
+  [[maybe_unused]] Bext2 bc;  // the extension's constants, before the INTT half (bext2_load)
+  if constexpr (PRO == NTT_PRO_BEXT) bc = bext2_load(T, ti);
   const int m0 = arg_byte(io.src.mod, sl0), m1 = ns > 1 ? arg_byte(io.src.mod, sl0 + 1) : m0;
   const u64* p0 = row_ptr(io.imid, c, sl0, b);
   const u64* p1 = ns > 1 ? row_ptr(io.imid, c, sl0 + 1, b) : p0;
@@ -617,9 +643,7 @@ __global__ void __launch_bounds__(NTT2S_R4 ? S2<LOGN>::CT4 : S2<LOGN>::CT)
 #pragma unroll
   for (int i = 0; i < NE; ++i) {
     if constexpr (PRO == NTT_PRO_BEXT) {
-      u64 x[2] = {v[0][i], ns > 1 ? v[1][i] : 0}, y[2];
-      const u64 vv = bext_prep<2>(T, x, y);
-      o[i] = bext_target_sel<2>(T->tgt + ti, ns, y, vv);
+      o[i] = bext2_apply(bc, v[0][i], ns > 1 ? v[1][i] : 0);
     } else {  // NTT_PRO_RESCALE: ((x + h) mod q_L) mod q_l - (h mod q_l)
       const u64 qL = tb->mc[io.modL].q, h = qL >> 1;
       const u64 hm = barrett128(0, h, mc);
@@ -663,6 +687,9 @@ __global__ void __launch_bounds__(G * S2<LOGN>::CT4) ntt2s_ifwd_cols_p(NttIO io,
   constexpr int CT = S2<LOGN>::CT4, REG = S2<LOGN>::CW << S2<LOGN>::R;  // LDS words per group
   __shared__ u64 lds[G * REG + 2 * 4 * CT];
   u64* const sb = lds + G * REG;  // the sources' INTT values, [source][element][thread]
+  // BEXT: the sources' y_i (in sb) and float-quotient terms, formed once per
+  // source in phase 1 instead of once per target in phase 2
+  [[maybe_unused]] __shared__ double sf[PRO == NTT_PRO_BEXT ? 2 * 4 * CT : 1];
   const int grp = threadIdx.x / CT, t = threadIdx.x % CT;  // (group-uniform, so wave-uniform)
   const int tile = blockIdx.x % S2<LOGN>::CTILES, q = blockIdx.x / S2<LOGN>::CTILES;
   const int seg = q % io.ntg, row = q / io.ntg;
@@ -678,6 +705,9 @@ __global__ void __launch_bounds__(G * S2<LOGN>::CT4) ntt2s_ifwd_cols_p(NttIO io,
     T = io.bx + kt;
     ns = T->ns;
   }
+  // the extension's constants, in SGPRs before the INTT half (bext2_load)
+  [[maybe_unused]] Bext2 bc;
+  if constexpr (PRO == NTT_PRO_BEXT) bc = bext2_load(T, ti);
   const int mod = arg_byte(io.dst.mod, l);
   const ModConst mc = tb->mc[mod];
   // NTT2S_FWD_PREFETCH: the forward stages' twiddles are fetched before the
@@ -708,7 +738,17 @@ __global__ void __launch_bounds__(G * S2<LOGN>::CT4) ntt2s_ifwd_cols_p(NttIO io,
       typename A::T x[4], y[4];
       s_inv_cols4_src<A, A, LOGN, false>(p, p, ar, ar, tw, tw, lds + grp * REG, x, y, t, tile);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sb[(grp * 4 + i) * CT + t] = ar.final_inv(x[i]);
+      for (int i = 0; i < 4; ++i) {
+        u64 xv = ar.final_inv(x[i]);
+        if constexpr (PRO == NTT_PRO_BEXT && !(NTT2S_ABLATE & 2)) {
+          if (!bc.centered) {  // (grp wave-uniform: constant table indices on each branch)
+            double f;
+            xv = __builtin_amdgcn_readfirstlane(grp) == 0 ? bext2_src(bc, 0, xv, f) : bext2_src(bc, 1, xv, f);
+            sf[(grp * 4 + i) * CT + t] = f;
+          }
+        }
+        sb[(grp * 4 + i) * CT + t] = xv;
+      }
     };
     if (mcs.f64)
       inv(F64Arith(mcs), twr_s(tb->inv_d[ms], 8 << LOGN));
@@ -722,10 +762,13 @@ __global__ void __launch_bounds__(G * S2<LOGN>::CT4) ntt2s_ifwd_cols_p(NttIO io,
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const u64 v0 = sb[i * CT + t];
-    if constexpr (PRO == NTT_PRO_BEXT) {
-      u64 x[2] = {v0, ns > 1 ? sb[(4 + i) * CT + t] : 0}, y[2];
-      const u64 vv = bext_prep<2>(T, x, y);
-      o[i] = bext_target_sel<2>(T->tgt + ti, ns, y, vv);
+    if constexpr (NTT2S_ABLATE & 2) {
+      o[i] = v0 + (ns > 1 ? sb[(4 + i) * CT + t] : 0);
+    } else if constexpr (PRO == NTT_PRO_BEXT) {
+      const u64 y1 = ns > 1 ? sb[(4 + i) * CT + t] : 0;
+      const double f0 = bc.centered ? 0.0 : sf[i * CT + t];
+      const double f1 = (bc.centered || ns < 2) ? 0.0 : sf[(4 + i) * CT + t];
+      o[i] = bext2_tgt(bc, v0, y1, bext2_v(bc, v0, f0, f1));
     } else {  // NTT_PRO_RESCALE
       const u64 qL = tb->mc[io.modL].q, h = qL >> 1;
       const u64 hm = barrett128(0, h, mc);
