@@ -261,7 +261,7 @@ __global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, c
 // decomposition, group stride own_gstride) instead of D, so the decomposition
 // never copies them.  out comps 0/1 of group g at out.p + g*out_gstride.
 // key layout [digit][2][klvl+1+K][N] (common.h key_pos).
-template <bool ROWS, bool FR = false>
+template <bool ROWS, bool FR = false, bool PRE = false>
 __device__ __forceinline__ void ks_mac_body(LimbSet& out, LimbSet& D, LimbSet& own, MacGroups& G, int beta,
                                             const DeviceTables* __restrict__ tb, int N, u64* lds) {
   const int row = blockIdx.y;
@@ -301,6 +301,24 @@ __device__ __forceinline__ void ks_mac_body(LimbSet& out, LimbSet& D, LimbSet& o
   // forward rows pass here, 4 rows at a time (groups past the last row keep
   // the barriers on their own LDS row), into fr = [digit][2 rows][256]
   [[maybe_unused]] const u64* fr = nullptr;
+  // FR with at most 4 digits (the batch-1 key switches): the key words and the
+  // own digit's words are loaded before the rows pass, so their latency
+  // overlaps it instead of following it
+  // (PRE: an instantiation of its own, so the other launches keep their registers)
+  constexpr bool pre = FR && PRE;
+  [[maybe_unused]] ulonglong2 pkb[4], pka[4], pown = make_ulonglong2(0, 0);
+  if constexpr (pre) {
+    {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (u < beta) {
+          pkb[u] = *(const ulonglong2*)(kp + (2 * u + 0) * kstride);
+          pka[u] = *(const ulonglong2*)(kp + (2 * u + 1) * kstride);
+        }
+      }
+      if (owndigit >= 0) pown = *(const ulonglong2*)(own.p + g * G.own_gstride + row_off(own, 0, l, bi) + n);
+    }
+  }
   if constexpr (FR) {
     u64* const frw = lds + 4 * 256;
     const int t = threadIdx.x, rr = t >> 6, kk = t & 63;
@@ -336,7 +354,31 @@ __device__ __forceinline__ void ks_mac_body(LimbSet& out, LimbSet& D, LimbSet& o
   const bool small = KS_MAC_ACC && mc.bar_k <= 52 && beta <= 120;
   MacAcc s0x, s0y, s1x, s1y;
   mac_zero(s0x), mac_zero(s0y), mac_zero(s1x), mac_zero(s1y);
-  for (int i0 = 0; i0 < beta; i0 += KS_CH) {  // chunks of KS_CH digits: 3 KS_CH loads in flight
+  if constexpr (pre) {
+    {  // the preloaded words, in chunks of 2 digits as below
+      const int lt = 2 * (int)threadIdx.x;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (u < beta) {
+          const ulonglong2 d = u == owndigit ? pown
+                                             : make_ulonglong2(fr[(2 * u + (lt >> 8)) * 256 + (lt & 255)],
+                                                               fr[(2 * u + (lt >> 8)) * 256 + (lt & 255) + 1]);
+          mac_add(s0x, d.x, pkb[u].x);
+          mac_add(s0y, d.y, pkb[u].y);
+          mac_add(s1x, d.x, pka[u].x);
+          mac_add(s1y, d.y, pka[u].y);
+        }
+        if ((u & 1) && u - 1 < beta) {
+          r0.x = add_mod(r0.x, mac_reduce(s0x, mc), q);
+          r0.y = add_mod(r0.y, mac_reduce(s0y, mc), q);
+          r1.x = add_mod(r1.x, mac_reduce(s1x, mc), q);
+          r1.y = add_mod(r1.y, mac_reduce(s1y, mc), q);
+          mac_zero(s0x), mac_zero(s0y), mac_zero(s1x), mac_zero(s1y);
+        }
+      }
+    }
+  }
+  for (int i0 = 0; i0 < (pre ? 0 : beta); i0 += KS_CH) {  // chunks of KS_CH digits: 3 KS_CH loads in flight
     ulonglong2 d[KS_CH], kb[KS_CH], ka[KS_CH];
 #pragma unroll
     for (int u = 0; u < KS_CH; ++u) {
@@ -421,10 +463,11 @@ __global__ void __launch_bounds__(256) ks_mac_rows_kernel(LimbSet out, LimbSet D
 }
 // the same, and before the products the decomposition's forward rows pass
 // (MacGroups.fwd_rows; dynamic LDS: (4 + 2 beta) rows of 256 words)
+template <bool PRE>
 __global__ void __launch_bounds__(256) ks_mac_full_kernel(LimbSet out, LimbSet D, LimbSet own, MacGroups G, int beta,
                                                           const DeviceTables* __restrict__ tb, int N) {
   extern __shared__ u64 lds_dyn[];
-  ks_mac_body<true, true>(out, D, own, G, beta, tb, N, lds_dyn);
+  ks_mac_body<true, true, PRE>(out, D, own, G, beta, tb, N, lds_dyn);
 }
 
 // NTT-domain automorphism: o[j] = a[idx[j]]  (optionally o += a[idx[j]])
@@ -973,12 +1016,15 @@ int orion_launch_ks_mac(const LimbSet& out, const LimbSet& D, const LimbSet& own
       if (beta > 16 || G.d_gstride) return -1;
       // (4 + 2 beta) x 2 KiB of LDS: up to 72 KiB at beta = 16, past the
       // 64 KiB a launch gets without the attribute (set once, for the largest)
-      static const bool lds_attr = hipFuncSetAttribute((const void*)ks_mac_full_kernel,
+      static const bool lds_attr = hipFuncSetAttribute((const void*)ks_mac_full_kernel<false>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        (4 + 2 * 16) * 256 * 8) == hipSuccess;
       if (!lds_attr) return -1;
-      hipLaunchKernelGGL(ks_mac_full_kernel, ew_grid(N, rows), dim3(256), (size_t)(4 + 2 * beta) * 256 * 8, st, out, D,
-                         own, G, beta, tb, N);
+      const size_t lds = (size_t)(4 + 2 * beta) * 256 * 8;
+      if (beta <= 4)  // the key words loaded before the rows pass (12 KiB of LDS at most)
+        hipLaunchKernelGGL(ks_mac_full_kernel<true>, ew_grid(N, rows), dim3(256), lds, st, out, D, own, G, beta, tb, N);
+      else
+        hipLaunchKernelGGL(ks_mac_full_kernel<false>, ew_grid(N, rows), dim3(256), lds, st, out, D, own, G, beta, tb, N);
       return 0;
     }
     hipLaunchKernelGGL(ks_mac_rows_kernel, ew_grid(N, rows), dim3(256), 0, st, out, D, own, G, beta, tb, N);
