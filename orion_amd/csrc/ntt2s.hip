@@ -439,28 +439,41 @@ __device__ __forceinline__ void s_fwd_rows4(const NttIO& io, int job, int c, int
   typename A::T x[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) x[i] = from_bits<typename A::T>(mid[kk + 64 * i]);
-  fwd_rows4_core<A, LOGN>(x, row, kk, ar, tw, lds + rr * 256);
+  typename A::W wa[4], wb[4], wc[4];
+  fwd_rows4_tw<A, LOGN>(row, kk, ar, tw, wa, wb, wc);
+  // the epilogue's operands are loaded before the steps, so their latency
+  // overlaps them: ex, the scatter index and (_ACC) the words at aut[e] (aut
+  // is a permutation: no other thread of the launch writes them)
+  [[maybe_unused]] ulonglong2 e01, e23;
+  [[maybe_unused]] uint4 ix;
+  [[maybe_unused]] u64 dv[4];
+  if constexpr (EPI != NTT_EPI_STORE) {
+    const u64* ex = row_ptr(io.ex, c, l, b) + (row << 8) + 4 * kk;
+    e01 = *(const ulonglong2*)ex, e23 = *(const ulonglong2*)(ex + 2);
+  }
+  u64* const d = row_ptr(io.dst, c, l, b);
+  if constexpr (epi_aut(EPI)) {
+    ix = *(const uint4*)(io.aut + (row << 8) + 4 * kk);
+    if constexpr (EPI == NTT_EPI_SUBSCALE_AUT_ACC) dv[0] = d[ix.x], dv[1] = d[ix.y], dv[2] = d[ix.z], dv[3] = d[ix.w];
+  }
+  fwd_rows4_run<A>(x, kk, ar, wa, wb, wc, lds + rr * 256);
   // the last step's elements: columns 4kk .. 4kk + 3
-  u64* dst = row_ptr(io.dst, c, l, b) + (row << 8) + 4 * kk;
+  u64* dst = d + (row << 8) + 4 * kk;
   u64 o[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) o[i] = ar.final_fwd(x[i]);
   if constexpr (EPI != NTT_EPI_STORE) {  // dst = (ex - y) * s_l
-    const u64* ex = row_ptr(io.ex, c, l, b) + (row << 8) + 4 * kk;
-    const ulonglong2 e01 = *(const ulonglong2*)ex, e23 = *(const ulonglong2*)(ex + 2);
     const u64 ev[4] = {e01.x, e01.y, e23.x, e23.y};
     const u64 s = io.s[l], ss = io.ss[l];
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = shoup_mul(sub_mod(ev[i], o[i], mc.q), s, ss, mc.q);
   }
   if constexpr (epi_aut(EPI)) {  // element e to position aut[e] (added to the word there for _ACC)
-    const uint4 ix = *(const uint4*)(io.aut + (row << 8) + 4 * kk);
-    u64* d = row_ptr(io.dst, c, l, b);
     if constexpr (EPI == NTT_EPI_SUBSCALE_AUT_ACC) {
-      o[0] = add_mod(o[0], d[ix.x], mc.q);
-      o[1] = add_mod(o[1], d[ix.y], mc.q);
-      o[2] = add_mod(o[2], d[ix.z], mc.q);
-      o[3] = add_mod(o[3], d[ix.w], mc.q);
+      o[0] = add_mod(o[0], dv[0], mc.q);
+      o[1] = add_mod(o[1], dv[1], mc.q);
+      o[2] = add_mod(o[2], dv[2], mc.q);
+      o[3] = add_mod(o[3], dv[3], mc.q);
     }
     d[ix.x] = o[0];
     d[ix.y] = o[1];

@@ -36,11 +36,12 @@ __device__ __forceinline__ void gs4(const A& ar, typename A::T (&x)[4], const ty
 // one 256-element row: x holds the intermediate's elements kk + 64 i on entry
 // and the last step's elements 4 kk .. 4 kk + 3 (lazy range) on return; lr is
 // the row's 256 words of LDS (one barrier per step but the last)
+// (split in its twiddle loads and its steps, so a caller can issue more loads
+// between the two: fwd_rows4_tw, fwd_rows4_run)
 template <class A, int LOGN>
-__device__ __forceinline__ void fwd_rows4_core(typename A::T (&x)[4], int row, int kk, const A& ar,
-                                               __amdgpu_buffer_rsrc_t tw, u64* lr) {
+__device__ __forceinline__ void fwd_rows4_tw(int row, int kk, const A& ar, __amdgpu_buffer_rsrc_t tw,
+                                             typename A::W (&wa)[4], typename A::W (&wb)[4], typename A::W (&wc)[4]) {
   constexpr int N = 1 << LOGN;
-  typename A::W wa[4], wb[4], wc[4];
 #pragma unroll
   for (int st = 0; st < 4; ++st) {
     const int hb = 7 - 2 * st, g = kk >> (hb - 1);
@@ -48,6 +49,10 @@ __device__ __forceinline__ void fwd_rows4_core(typename A::T (&x)[4], int row, i
     wb[st] = ar.tw(tw, (row << (8 - hb)) | (2 * g), N >> hb);
     wc[st] = ar.tw(tw, (row << (8 - hb)) | (2 * g + 1), N >> hb);
   }
+}
+template <class A>
+__device__ __forceinline__ void fwd_rows4_run(typename A::T (&x)[4], int kk, const A& ar, const typename A::W (&wa)[4],
+                                              const typename A::W (&wb)[4], const typename A::W (&wc)[4], u64* lr) {
 #pragma unroll
   for (int st = 0; st < 4; ++st) {
     const int hb = 7 - 2 * st, lb = hb - 1;
@@ -69,6 +74,13 @@ __device__ __forceinline__ void fwd_rows4_core(typename A::T (&x)[4], int row, i
       __syncthreads();
     }
   }
+}
+template <class A, int LOGN>
+__device__ __forceinline__ void fwd_rows4_core(typename A::T (&x)[4], int row, int kk, const A& ar,
+                                               __amdgpu_buffer_rsrc_t tw, u64* lr) {
+  typename A::W wa[4], wb[4], wc[4];
+  fwd_rows4_tw<A, LOGN>(row, kk, ar, tw, wa, wb, wc);
+  fwd_rows4_run<A>(x, kk, ar, wa, wb, wc, lr);
 }
 
 // the inverse rows pass (the first pass of the two-pass INTT, ntt2s.hip) of
