@@ -67,6 +67,12 @@
 
 namespace {
 
+// the workgroup size of every kernel in this file (launch_bounds and launches:
+// 256).  As a constant, not blockDim.x: HIP reads blockDim.x from the
+// dispatch's implicit arguments (the remainder for a partial last block) with
+// a 16-bit vector load and waits for it before any address is formed
+constexpr int kBlk = 256;
+
 // p[i] through a global-address-space pointer: for a pointer read from device
 // memory (a plan's diagonal table) the compiler cannot infer the address
 // space and emits a flat load, whose completion is only trackable with
@@ -107,7 +113,7 @@ __global__ void __launch_bounds__(256) ew_kernel(LimbSet o, LimbSet a, LimbSet b
   const int r = row / o.nbatch;
   const int l = r % o.nlimb;
   const int c = r / o.nlimb;
-  const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  const int n = (blockIdx.x * kBlk + threadIdx.x) * 2;
   if (n >= N) return;
   const ModConst mc = tb->mc[arg_byte(o.mod, l)];
   const u64 q = mc.q;
@@ -155,7 +161,7 @@ __global__ void __launch_bounds__(256) tensor_kernel(LimbSet d, LimbSet a, LimbS
   const int row = blockIdx.y;
   const int bi = row % d.nbatch;
   const int l = row / d.nbatch;
-  const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  const int n = (blockIdx.x * kBlk + threadIdx.x) * 2;
   if (n >= N) return;
   const ModConst mc = tb->mc[arg_byte(d.mod, l)];
   const u64 q = mc.q;
@@ -183,7 +189,7 @@ __global__ void __launch_bounds__(256) basis_ext_kernel(LimbSet out, LimbSet in,
   const int row = blockIdx.y;  // (comp, image)
   const int bi = row % out.nbatch;
   const int c = row / out.nbatch;
-  const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  const int n = (blockIdx.x * kBlk + threadIdx.x) * 2;
   if (n >= N) return;
   const int ns = T->ns, nt = T->nt;
   u64 x0[MS], x1[MS], y0[MS], y1[MS];
@@ -218,7 +224,7 @@ __global__ void __launch_bounds__(256) modup_all_kernel(LimbSet D, LimbSet in, c
   const int r = row / D.nbatch;
   const int i = r % beta;
   const int c = r / beta;
-  const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  const int n = (blockIdx.x * kBlk + threadIdx.x) * 2;
   if (n >= N) return;
   const BasisExtTable* __restrict__ T = Ts + i;
   const int ns = T->ns, lo = i * K;
@@ -269,7 +275,7 @@ __device__ __forceinline__ void ks_mac_body(LimbSet& out, LimbSet& D, LimbSet& o
   const int r = row / out.nbatch;
   const int l = r % out.nlimb;
   const int g = r / out.nlimb;
-  const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  const int n = (blockIdx.x * kBlk + threadIdx.x) * 2;
   if (n >= N) return;
   const int m = arg_byte(out.mod, l);
   const ModConst mc = tb->mc[m];
@@ -478,7 +484,7 @@ __global__ void __launch_bounds__(256) automorph_kernel(LimbSet o, LimbSet a, co
   const int r = row / o.nbatch;
   const int l = r % o.nlimb;
   const int c = r / o.nlimb;
-  const int n = (blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  const int n = (blockIdx.x * kBlk + threadIdx.x) * 2;
   if (n >= N) return;
   const u64 q = tb->mc[arg_byte(o.mod, l)].q;
   const u64* src = a.p + row_off(a, c, l, bi);
@@ -571,7 +577,7 @@ __device__ __forceinline__ void lt_bsgs_body(LimbSet& t0, LimbSet& t1, const Lim
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   if (Bb.xcd) lt_xcd_decode(bx, by, bz);
   const int bi = bx;
-  const int n = by * blockDim.x + threadIdx.x;
+  const int n = by * kBlk + threadIdx.x;
   const int l = z0 + bz;
   if (n >= N) return;
   const int m = arg_byte(t0.mod, l);
@@ -762,7 +768,7 @@ __global__ void __launch_bounds__(256) lt_giant_kernel(LimbSet acc, LimbSet D, L
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   if (G.xcd) lt_xcd_decode(bx, by, bz);
   const int b0 = bx * IB;
-  const int n = by * blockDim.x + threadIdx.x;
+  const int n = by * kBlk + threadIdx.x;
   const int l = bz;
   if (n >= N) return;
   const int nb = acc.nbatch - b0 < IB ? acc.nbatch - b0 : IB;  // uniform
