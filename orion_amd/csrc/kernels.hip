@@ -325,6 +325,27 @@ __device__ __forceinline__ void ks_mac_body(LimbSet& out, LimbSet& D, LimbSet& o
       if (owndigit >= 0) pown = *(const ulonglong2*)(own.p + g * G.own_gstride + row_off(own, 0, l, bi) + n);
     }
   }
+  // ... and a P limb's inverse-rows twiddles (the ROWS epilogue below), raw
+  [[maybe_unused]] ulonglong2 itw[12];
+  if constexpr (pre && ROWS) {
+    if (l >= G.rows_from) {  // (block-uniform)
+      const int t = threadIdx.x, rr = t >> 6, kk = t & 63, row = 2 * blockIdx.x + (rr & 1);
+      auto tws = [&](const auto& ar, __amdgpu_buffer_rsrc_t tw) {
+        using A = std::decay_t<decltype(ar)>;
+        typename A::W wa[4], wb[4], wc[4];
+        if (G.logN == 15)
+          inv_rows4_tw<A, 15>(row, kk, ar, tw, wa, wb, wc);
+        else
+          inv_rows4_tw<A, 16>(row, kk, ar, tw, wa, wb, wc);
+#pragma unroll
+        for (int st = 0; st < 4; ++st) itw[st] = w_raw(wa[st]), itw[4 + st] = w_raw(wb[st]), itw[8 + st] = w_raw(wc[st]);
+      };
+      if (mc.f64)
+        tws(F64Arith(mc), twr_s(tb->inv_d[m], 8 * N));
+      else
+        tws(IntArith(mc), twr_s(tb->inv[m], 16 * N));
+    }
+  }
   if constexpr (FR) {
     u64* const frw = lds + 4 * 256;
     const int t = threadIdx.x, rr = t >> 6, kk = t & 63;
@@ -442,10 +463,17 @@ __device__ __forceinline__ void ks_mac_body(LimbSet& out, LimbSet& D, LimbSet& o
         typename A::T x[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) x[i] = ar.from_u64(lr[4 * kk + i]);
-        if (G.logN == 15)
+        if constexpr (pre) {  // the twiddles fetched at the start
+          typename A::W wa[4], wb[4], wc[4];
+#pragma unroll
+          for (int st = 0; st < 4; ++st)
+            wa[st] = w_of<A>(itw[st]), wb[st] = w_of<A>(itw[4 + st]), wc[st] = w_of<A>(itw[8 + st]);
+          inv_rows4_run<A>(x, kk, ar, wa, wb, wc, lr, mid);
+        } else if (G.logN == 15) {
           inv_rows4_core<A, 15>(x, row, kk, ar, tw, lr, mid);
-        else
+        } else {
           inv_rows4_core<A, 16>(x, row, kk, ar, tw, lr, mid);
+        }
       };
       if (mc.f64)
         rows(F64Arith(mc), twr_s(tb->inv_d[m], 8 * N));

@@ -393,15 +393,6 @@ __device__ __forceinline__ void s_fwd_cols4_core(const NttIO& io, int job, int c
   s_fwd_cols4_tw<A, LOGN>(ar, tw, t / S2<LOGN>::CW, wa, wb, wc, wl);
   s_fwd_cols4_run<A, LOGN>(io, job, c, l, b, tile, x, ar, wa, wb, wc, wl, lds, t);
 }
-// a twiddle word kept as two u64 (the float64 path's double in .x), so the
-// forward twiddles of either arithmetic can be fetched before the INTT half
-__device__ __forceinline__ ulonglong2 w_raw(double w) { return make_ulonglong2(__builtin_bit_cast(u64, w), 0); }
-__device__ __forceinline__ ulonglong2 w_raw(ulonglong2 w) { return w; }
-template <class A>
-__device__ __forceinline__ typename A::W w_of(ulonglong2 r) {
-  if constexpr (std::is_same_v<typename A::W, double>) return __builtin_bit_cast(double, r.x);
-  else return r;
-}
 template <class A, int LOGN, int PRO>
 __device__ __forceinline__ void s_fwd_cols4(const NttIO& io, int job, int c, int l, int b, int tile,
                                             const ModConst& mc, const A& ar, __amdgpu_buffer_rsrc_t tw, u64* lds,

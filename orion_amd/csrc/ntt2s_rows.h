@@ -2,6 +2,7 @@
 // (ntt2s.hip) and the kernels that end in an inverse rows pass of their own
 // output (kernels.hip: ks_mac's P limbs).  Device code only.
 #pragma once
+#include <type_traits>
 #include "common.h"
 #include "ntt_arith.h"
 
@@ -89,11 +90,11 @@ __device__ __forceinline__ void fwd_rows4_core(typename A::T (&x)[4], int row, i
 // one barrier per step, and none before the first), mid the row's
 // intermediate (element kk + 64 i of the last step).  row: the row's index in
 // the limb (the twiddles of its groups)
+// (split like the forward: inv_rows4_tw, inv_rows4_run)
 template <class A, int LOGN>
-__device__ __forceinline__ void inv_rows4_core(typename A::T (&x)[4], int row, int kk, const A& ar,
-                                               __amdgpu_buffer_rsrc_t tw, u64* lr, u64* mid, bool store = true) {
+__device__ __forceinline__ void inv_rows4_tw(int row, int kk, const A& ar, __amdgpu_buffer_rsrc_t tw,
+                                             typename A::W (&wa)[4], typename A::W (&wb)[4], typename A::W (&wc)[4]) {
   constexpr int N = 1 << LOGN;
-  typename A::W wa[4], wb[4], wc[4];
 #pragma unroll
   for (int st = 0; st < 4; ++st) {
     const int lb = 2 * st, g = kk >> lb;
@@ -101,6 +102,11 @@ __device__ __forceinline__ void inv_rows4_core(typename A::T (&x)[4], int row, i
     wb[st] = ar.tw(tw, (row << (7 - lb)) | (2 * g + 1), N >> (lb + 1));
     wc[st] = ar.tw(tw, (row << (6 - lb)) | g, N >> (lb + 2));
   }
+}
+template <class A>
+__device__ __forceinline__ void inv_rows4_run(typename A::T (&x)[4], int kk, const A& ar, const typename A::W (&wa)[4],
+                                              const typename A::W (&wb)[4], const typename A::W (&wc)[4], u64* lr,
+                                              u64* mid, bool store = true) {
 #pragma unroll
   for (int st = 0; st < 4; ++st) {
     const int lb = 2 * st, hb = lb + 1;
@@ -124,6 +130,22 @@ __device__ __forceinline__ void inv_rows4_core(typename A::T (&x)[4], int row, i
 #pragma unroll
     for (int i = 0; i < 4; ++i) mid[kk + 64 * i] = to_bits(ar.reduce_round(x[i]));
   }
+}
+template <class A, int LOGN>
+__device__ __forceinline__ void inv_rows4_core(typename A::T (&x)[4], int row, int kk, const A& ar,
+                                               __amdgpu_buffer_rsrc_t tw, u64* lr, u64* mid, bool store = true) {
+  typename A::W wa[4], wb[4], wc[4];
+  inv_rows4_tw<A, LOGN>(row, kk, ar, tw, wa, wb, wc);
+  inv_rows4_run<A>(x, kk, ar, wa, wb, wc, lr, mid, store);
+}
+// a twiddle word kept as two u64 (the float64 path's double in .x), so that
+// twiddles of either arithmetic can be fetched early into one register array
+__device__ __forceinline__ ulonglong2 w_raw(double w) { return make_ulonglong2(__builtin_bit_cast(u64, w), 0); }
+__device__ __forceinline__ ulonglong2 w_raw(ulonglong2 w) { return w; }
+template <class A>
+__device__ __forceinline__ typename A::W w_of(ulonglong2 r) {
+  if constexpr (std::is_same_v<typename A::W, double>) return __builtin_bit_cast(double, r.x);
+  else return r;
 }
 
 }  // namespace
