@@ -789,8 +789,12 @@ lt_bsgs_kernel16(LimbSet t0, LimbSet t1, LimbSet D, LimbSet ct, LtBabies Bb, con
 // Each thread takes one coefficient of IB images: the automorphism index, the
 // key words and every pointer step are shared by the IB images, so the key
 // reads from L2 and the scalar address work per product drop IB-fold.
+#ifndef LT_GIANT_WAVES
+#define LT_GIANT_WAVES 0  // timing switch: minimum waves per SIMD for lt_giant (0: the compiler's choice)
+#endif
 template <int IB, bool ROWS>
-__global__ void __launch_bounds__(256) lt_giant_kernel(LimbSet acc, LimbSet D, LimbSet own, LimbSet t0, LimbSet z,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LT_GIANT_WAVES > 0 ? LT_GIANT_WAVES : 1)))
+lt_giant_kernel(LimbSet acc, LimbSet D, LimbSet own, LimbSet t0, LimbSet z,
                                                        LtGiants G, const DeviceTables* __restrict__ tb, int N) {
   constexpr int CH = LT_GIANT_CH > 0 ? LT_GIANT_CH : (IB >= 4 ? 2 : 4);  // digits per load chunk
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
