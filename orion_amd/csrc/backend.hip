@@ -1140,6 +1140,7 @@ struct Context {
   bool two_pass(int jobs, bool inv, int pro, int epi, bool inplace_sub) {
     if (logN == 16) return true;
     if (logN != 15 || ci) return false;
+    if (md_force) return true;
     if (ntt_impl == 2 || jobs < ntt2_below) return true;
     const bool plain = (pro == NTT_PRO_LOAD || pro == NTT_PRO_BEXT) && epi == NTT_EPI_STORE;
     return (inv || (ntt2_tail_fwd == 1 && plain) || (ntt2_tail_fwd == 2 && !inplace_sub) ||
@@ -1160,8 +1161,22 @@ struct Context {
   // so it is kept to small launches (bext_fuse_below limb-transforms)
   bool fuse_bext(int jobs, int ns, int epi) {
     if (!bext_fuse || ns > 2 || ci) return false;
-    return bext_fuse == 2 || (jobs <= bext_fuse_below && two_pass(jobs, false, NTT_PRO_BEXT, epi, false));
+    return bext_fuse == 2 || ((md_force || jobs <= bext_fuse_below) && two_pass(jobs, false, NTT_PRO_BEXT, epi, false));
   }
+  // timing switch ORION_MODDOWN_LAT=1: every ModDown takes the fused latency
+  // path whatever its size (the gadget product's rows pass of the P limbs'
+  // INTT, their columns pass + the extension + the Q limbs' forward columns in
+  // ntt2s_ifwd_cols_p, the Q rows pass with the subtract-and-scale), instead of
+  // the one-pass INTT, basis_ext and one-pass NTT of large batches.  md_force
+  // holds while a ModDown (or its fusability test) decides its launches
+  int moddown_lat = getenv("ORION_MODDOWN_LAT") ? atoi(getenv("ORION_MODDOWN_LAT")) : 0;
+  bool md_force = false;
+  struct MdForce {
+    Context* c;
+    bool old;
+    explicit MdForce(Context* c_) : c(c_), old(c_->md_force) { c->md_force = c->moddown_lat != 0 && !c->ci; }
+    ~MdForce() { c->md_force = old; }
+  };
   int bext_fuse_below = getenv("ORION_BEXT_FUSE_BELOW") ? atoi(getenv("ORION_BEXT_FUSE_BELOW")) : 64;
   // src_per_job: NTT_PRO_BEXT launches, the mean source limbs read per
   // limb-transform (their algorithmic bytes are (src_per_job + 1) 8 N, + 8 N
@@ -1203,7 +1218,7 @@ struct Context {
   // workgroup, the sources' columns redone for each (ntt2s_ifwd_cols)
   int ntt_ifuse_p = getenv("ORION_NTT_IFUSE_P") ? atoi(getenv("ORION_NTT_IFUSE_P")) : 2;
   bool on_ntt2s(int jobs, bool inv, int pro, int epi, bool inplace_sub) {
-    return (logN == 15 || logN == 16) && !ci && jobs <= ntt2s_below &&
+    return (logN == 15 || logN == 16) && !ci && (md_force || jobs <= ntt2s_below) &&
            two_pass(jobs, inv, pro, epi, inplace_sub);
   }
   // the INTT iio (load prologue, store epilogue) and then the forward fio whose
@@ -1305,7 +1320,7 @@ struct Context {
         io.mid = ls(scratch, 0, io.dst.ncomp, iota(0, io.dst.nlimb), std::vector<int>(io.dst.mod, io.dst.mod + io.dst.nlimb));
       }
       Scope sc(this, cat, per * io.jobs, strict * io.jobs);
-      const bool small = io.jobs <= ntt2s_below;
+      const bool small = md_force || io.jobs <= ntt2s_below;
       if (io.ifuse && !small) throw std::runtime_error("NTT: a fused INTT columns pass needs the latency kernels");
       if (small ? orion_launch_ntt2s(logN, io, d_tb, inv, stream) : orion_launch_ntt2(logN, io, d_tb, inv, stream))
         throw std::runtime_error("NTT launch failed");
@@ -2084,7 +2099,7 @@ struct Context {
   bool aut_epi_ok(int jobs, int pro) {
     if (ci || ntt_tailsplit) return false;
     if (!two_pass(jobs, false, pro, NTT_EPI_SUBSCALE_AUT, false)) return logN <= 15 && pro == NTT_PRO_LOAD;
-    if (jobs <= ntt2s_below) return NTT2S_R4;
+    if (md_force || jobs <= ntt2s_below) return NTT2S_R4;
     return pro == NTT_PRO_LOAD && ntt2_tail_aut;  // the large two-pass kernels (ntt2.hip), load prologue
   }
   u64 galois_inverse(u64 g) const {
@@ -2106,6 +2121,7 @@ struct Context {
   // after the INTT's rows pass (keyswitch, ks_mac_rows_kernel)
   bool moddown_rows_fusable(const LimbSet& x, int level, const LimbSet& out, u64 aut_g, bool aut_acc) {
     if (!mac_rows || (logN != 15 && logN != 16) || !NTT2S_R4) return false;
+    MdForce mf(this);
     const int nc = x.ncomp, B = x.nbatch, jobs = nc * B * (level + 1);
     if (!fuse_bext(jobs, K, NTT_EPI_SUBSCALE)) return false;
     const bool scatter = aut_g && ntt_aut_fuse && aut_epi_ok(jobs, NTT_PRO_BEXT);
@@ -2127,6 +2143,7 @@ struct Context {
   int lt_xcd = getenv("ORION_LT_XCD") ? atoi(getenv("ORION_LT_XCD")) : 1;
   void moddown(const LimbSet& x, int level, const LimbSet& out, u64 aut_g = 0, bool aut_acc = false,
                bool rows_done = false) {
+    MdForce mf(this);
     const int nc = x.ncomp, B = x.nbatch, jobs = nc * B * (level + 1);
     LimbSet xp = limbs(x, level + 1, K);
     const bool fused = fuse_bext(jobs, K, NTT_EPI_SUBSCALE);
