@@ -1163,7 +1163,7 @@ struct Context {
     if (!bext_fuse || ns > 2 || ci) return false;
     return bext_fuse == 2 || ((md_force || jobs <= bext_fuse_below) && two_pass(jobs, false, NTT_PRO_BEXT, epi, false));
   }
-  // timing switch ORION_MODDOWN_LAT=1: every ModDown takes the fused latency
+  // timing switch ORION_MODDOWN_LAT=1 (2: rotations only): every ModDown takes the fused latency
   // path whatever its size (the gadget product's rows pass of the P limbs'
   // INTT, their columns pass + the extension + the Q limbs' forward columns in
   // ntt2s_ifwd_cols_p, the Q rows pass with the subtract-and-scale), instead of
@@ -1174,7 +1174,10 @@ struct Context {
   struct MdForce {
     Context* c;
     bool old;
-    explicit MdForce(Context* c_) : c(c_), old(c_->md_force) { c->md_force = c->moddown_lat != 0 && !c->ci; }
+    // (2: only the rotations' ModDowns, whose one-pass scatter-store NTT is the slowest class)
+    MdForce(Context* c_, bool aut) : c(c_), old(c_->md_force) {
+      c->md_force = !c->ci && (c->moddown_lat == 1 || (c->moddown_lat == 2 && aut));
+    }
     ~MdForce() { c->md_force = old; }
   };
   int bext_fuse_below = getenv("ORION_BEXT_FUSE_BELOW") ? atoi(getenv("ORION_BEXT_FUSE_BELOW")) : 64;
@@ -2121,7 +2124,7 @@ struct Context {
   // after the INTT's rows pass (keyswitch, ks_mac_rows_kernel)
   bool moddown_rows_fusable(const LimbSet& x, int level, const LimbSet& out, u64 aut_g, bool aut_acc) {
     if (!mac_rows || (logN != 15 && logN != 16) || !NTT2S_R4) return false;
-    MdForce mf(this);
+    MdForce mf(this, aut_g != 0);
     const int nc = x.ncomp, B = x.nbatch, jobs = nc * B * (level + 1);
     if (!fuse_bext(jobs, K, NTT_EPI_SUBSCALE)) return false;
     const bool scatter = aut_g && ntt_aut_fuse && aut_epi_ok(jobs, NTT_PRO_BEXT);
@@ -2143,7 +2146,7 @@ struct Context {
   int lt_xcd = getenv("ORION_LT_XCD") ? atoi(getenv("ORION_LT_XCD")) : 1;
   void moddown(const LimbSet& x, int level, const LimbSet& out, u64 aut_g = 0, bool aut_acc = false,
                bool rows_done = false) {
-    MdForce mf(this);
+    MdForce mf(this, aut_g != 0);
     const int nc = x.ncomp, B = x.nbatch, jobs = nc * B * (level + 1);
     LimbSet xp = limbs(x, level + 1, K);
     const bool fused = fuse_bext(jobs, K, NTT_EPI_SUBSCALE);
