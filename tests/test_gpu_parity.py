@@ -884,15 +884,17 @@ def test_one_prime_gadget_wide_fused_mac(torch_cuda, oracle_mod, monkeypatch):
 
 @pytest.mark.parametrize("env", [{}, {"ORION_NTT_TAILSPLIT": "1"}, {"ORION_NTT_IFUSE": "0"},
                                  {"ORION_NTT_AUT_FUSE": "0"}, {"ORION_BEXT_MODES": "0", "ORION_NTT_IFUSE_MAXR": "1000"},
-                                 {"ORION_NTT_COSPLIT": "0.5", "ORION_NTT_COSPLIT_MIN": "200"}])
+                                 {"ORION_NTT_COSPLIT": "0.5", "ORION_NTT_COSPLIT_MIN": "200"},
+                                 {"ORION_MODDOWN_LAT": "1"}])
 @pytest.mark.parametrize("B", [2, 12, 40])
 def test_runtime_switch_parity(torch_cuda, oracle_mod, env, B, monkeypatch):
     """The default environment and the non-default NTT / basis-extension
     paths behind the runtime switches stay bit-exact: the partial-round split (B=40 at
     N=2^15 leaves 144- and 80-job tails), the unfused INTT + prologue NTT,
     the lazy-only basis extension, the INTT fusion with no redundancy limit,
-    the rotation's automorphism as its own launch, and the one-pass launches
-    co-split with the two-pass kernels on CU-masked streams; and the fused
+    the rotation's automorphism as its own launch, the one-pass launches
+    co-split with the two-pass kernels on CU-masked streams, and every ModDown
+    on the fused latency path whatever its size; and the fused
     rotate-and-add (OrionHipRotateAdd) on each of those paths.  B=12 gives
     120-job latency-kernel launches, with more rows-pass workgroups than the
     chip holds at once: a scattering rows pass that stored into rows another
