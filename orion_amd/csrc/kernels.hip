@@ -50,6 +50,9 @@
 #ifndef LT_GIANT_IB
 #define LT_GIANT_IB 4
 #endif
+#ifndef LT_GIANT_B1
+#define LT_GIANT_B1 1  // 1: one-image launches take lt_giant_kernel<1, ...>
+#endif
 #ifndef LT_GIANT_CH
 #define LT_GIANT_CH 0  // lt_giant digits per load chunk (0: 2 at IB >= 4, else 4)
 #endif
@@ -1102,10 +1105,21 @@ int orion_launch_lt_bsgs(const LimbSet& t0, const LimbSet& t1, const LimbSet& D,
 int orion_launch_lt_giant(const LimbSet& acc, const LimbSet& D, const LimbSet& own, const LimbSet& t0,
                           const LimbSet& z, const LtGiants& G, const DeviceTables* tb, int N, hipStream_t st) {
   if (G.ng > ORION_MAXGROUP) return -1;
+  if (G.rows_from > 0 && ((G.logN != 15 && G.logN != 16) || N != (1 << G.logN))) return -1;
+  // one image (batch 1): the one-image instantiation, whose registers are a
+  // quarter of IB = 4's (more waves per SIMD, more loads in flight per CU)
+  const bool one = acc.nbatch == 1 && LT_GIANT_B1;
+  if (one) {
+    const dim3 g(1, (N + 255) / 256, acc.nlimb);
+    if (G.rows_from > 0)
+      hipLaunchKernelGGL((lt_giant_kernel<1, true>), g, dim3(256), 0, st, acc, D, own, t0, z, G, tb, N);
+    else
+      hipLaunchKernelGGL((lt_giant_kernel<1, false>), g, dim3(256), 0, st, acc, D, own, t0, z, G, tb, N);
+    return 0;
+  }
   constexpr int IB = LT_GIANT_IB;
   dim3 g((acc.nbatch + IB - 1) / IB, (N + 255) / 256, acc.nlimb);
   if (G.rows_from > 0) {
-    if ((G.logN != 15 && G.logN != 16) || N != (1 << G.logN)) return -1;
     hipLaunchKernelGGL((lt_giant_kernel<IB, true>), g, dim3(256), 0, st, acc, D, own, t0, z, G, tb, N);
     return 0;
   }
