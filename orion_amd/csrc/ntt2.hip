@@ -325,8 +325,12 @@ struct N2 {
   static constexpr int R = LOGN - 8, ATHREADS = 16 << (R - 4), BTILES = 1 << (R - 4);
 };
 
+#ifndef NTT2_COLS_WAVES
+#define NTT2_COLS_WAVES 0  // minimum waves per SIMD for the forward columns pass (0: the compiler's choice)
+#endif
 template <int LOGN, int PRO>
-__global__ void __launch_bounds__(N2<LOGN>::ATHREADS) ntt2_fwd_cols(NttIO io, const DeviceTables* __restrict__ tb) {
+__global__ void __launch_bounds__(N2<LOGN>::ATHREADS) __attribute__((amdgpu_waves_per_eu(NTT2_COLS_WAVES > 0 ? NTT2_COLS_WAVES : 1)))
+ntt2_fwd_cols(NttIO io, const DeviceTables* __restrict__ tb) {
   __shared__ u64 lds[(1 << N2<LOGN>::R) * A_STRIDE];
   int c, l, b;
   const int job = io.job0 + (blockIdx.x >> 4);
